@@ -1,0 +1,50 @@
+# bedops_amd build: libbedgpu (HIP, gfx950) + C front-ends + tools + CPU oracle.
+# Everything is built in-tree so the artefacts travel to the GPU box with the repo.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CC ?= gcc
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-value -Wno-unused-result
+CFLAGS ?= -O2 -std=gnu11 -Wall -Wno-unused-result
+
+SRC := bedops_amd/csrc
+OBJ := build/obj
+LIB := bedops_amd/lib/libbedgpu.so
+BIN := bedops_amd/bin
+HIPSRCS := $(wildcard $(SRC)/*.hip)
+HIPOBJS := $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIPSRCS))
+CLIS := $(BIN)/bedops $(BIN)/bedmap
+
+all: lib cli tools oracle
+
+lib: $(LIB)
+cli: $(CLIS)
+tools: tools/build/libbedgen.so tools/build/bedgen
+
+$(OBJ)/%.o: $(SRC)/%.hip $(SRC)/bg_internal.h include/bedgpu.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIPOBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -Wl,-rpath,/opt/rocm/lib
+
+$(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h include/bedgpu.h $(LIB)
+	@mkdir -p $(BIN)
+	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
+
+tools/build/libbedgen.so: tools/bedgen.c
+	@mkdir -p tools/build
+	$(CC) -O3 -fopenmp -shared -fPIC -o $@ $<
+
+tools/build/bedgen: tools/bedgen.c
+	@mkdir -p tools/build
+	$(CC) -O3 -fopenmp -DBEDGEN_MAIN -o $@ $<
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build bedops_amd/lib bedops_amd/bin tools/build
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib cli tools oracle clean

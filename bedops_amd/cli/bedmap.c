@@ -1,0 +1,157 @@
+/*
+ * bedmap — drop-in front-end for `bedmap [options] <ops> <ref-file> [map-file]`,
+ * computing the per-reference overlap aggregates on an MI355X through libbedgpu.
+ *
+ * argv grammar follows applications/bed/bedmap/src/Input.hpp:75-367 (options start
+ * with "--", the last one or two arguments are files, --delim/--prec/--sci/
+ * --skip-unmapped/--bp-ovr/--chrom/--ec/--header/--faster/--sweep-all); output per
+ * reference row is the operations' values in command-line order joined by --delim
+ * (MultiVisitor.hpp:83-98). GPU path: --count and --mean with the default overlap
+ * rule (--bp-ovr N); other operations and overlap criteria are reported as not
+ * available in this build.
+ */
+#include "cli_common.h"
+
+static const char* PROG = "bedmap";
+
+static void usage(FILE* f) {
+  fprintf(f,
+          "bedmap\n  version:  %s\n\n"
+          " USAGE: bedmap [process-flags] [overlap-option] <operation(s)...> <ref-file> [map-file]\n"
+          "     Any input file must be sorted per the sort-bed utility.\n\n"
+          "    Process Flags:\n"
+          "      --chrom <chromosome>  Jump to and process data only for <chromosome>.\n"
+          "      --delim <delim>       Change output delimiter from '|' to <delim> between columns.\n"
+          "      --ec / --header       Error check / accept header lines.\n"
+          "      --prec <int>          Change the post-decimal precision of scores to <int>.\n"
+          "      --skip-unmapped       Print no output for a row with no mapped elements.\n\n"
+          "    Overlap Options:\n"
+          "      --bp-ovr <int>        Require <int> bp overlap (default 1).\n\n"
+          "    Operations (GPU path):\n"
+          "      --count               The number of overlapping elements in <map-file>.\n"
+          "      --mean                The average score from overlapping elements in <map-file>.\n",
+          BEDOPS_AMD_VERSION);
+}
+
+static void arg_error(const char* msg) { die_msg(PROG, msg); }
+
+int main(int argc, char** argv) {
+  if (argc <= 1) {
+    usage(stderr);
+    return EXIT_FAILURE;
+  }
+  bg_map_opts o;
+  memset(&o, 0, sizeof(o));
+  o.overlap_bp = 1;
+  o.precision = 6;
+  strcpy(o.delim, "|");
+  int ec = 0, need5 = 0, set_prec = 0, set_delim = 0;
+  const char* chrom = NULL;
+  int a = 1;
+  while (a < argc) {
+    const char* nx = argv[a++];
+    if (strncmp(nx, "--", 2) != 0 && argc - a < 2) { --a; break; }
+    if (strncmp(nx, "--", 2) != 0) {
+      char b[512];
+      snprintf(b, sizeof(b), "Option %s does not start with '--'", nx);
+      arg_error(b);
+    }
+    const char* k = nx + 2;
+    if (!strcmp(k, "help")) { usage(stdout); return EXIT_SUCCESS; }
+    else if (!strcmp(k, "version")) { printf("bedmap\n  version:  %s\n", BEDOPS_AMD_VERSION); return EXIT_SUCCESS; }
+    else if (!strcmp(k, "ec") || !strcmp(k, "header")) ec = 1;
+    else if (!strcmp(k, "faster") || !strcmp(k, "sweep-all")) {}
+    else if (!strcmp(k, "delim")) {
+      if (set_delim) arg_error("--delim specified multiple times");
+      if (a >= argc) arg_error("No output delimiter given");
+      if (strlen(argv[a]) >= sizeof(o.delim)) arg_error("--delim value too long for this build");
+      strcpy(o.delim, argv[a++]);
+      set_delim = 1;
+    } else if (!strcmp(k, "chrom")) {
+      if (a >= argc) arg_error("No chromosome name given");
+      chrom = argv[a++];
+      if (!strcmp(chrom, "all")) chrom = NULL;
+    } else if (!strcmp(k, "skip-unmapped")) o.skip_unmapped = 1;
+    else if (!strcmp(k, "sci")) o.scientific = 1;
+    else if (!strcmp(k, "prec")) {
+      if (a >= argc) arg_error("No precision value given");
+      if (set_prec) arg_error("--prec specified multiple times.");
+      const char* v = argv[a++];
+      if (strspn(v, "0123456789") != strlen(v)) {
+        char b[512];
+        snprintf(b, sizeof(b), "Non-positive-integer argument: %s for --prec", v);
+        arg_error(b);
+      }
+      o.precision = atoi(v);
+      set_prec = 1;
+    } else if (!strcmp(k, "bp-ovr")) {
+      if (a >= argc) arg_error("No arg for --bp-ovr");
+      const char* v = argv[a++];
+      if (strspn(v, "0123456789") != strlen(v)) {
+        char b[512];
+        snprintf(b, sizeof(b), "Non-positive-integer argument: %s for --bp-ovr", v);
+        arg_error(b);
+      }
+      o.overlap_bp = strtoull(v, NULL, 10);
+      if (o.overlap_bp == 0) arg_error("--bp-ovr value must be > 0");
+    } else if (!strcmp(k, "count")) {
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.ops[o.n_ops++] = BG_MAP_COUNT;
+    } else if (!strcmp(k, "mean")) {
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.ops[o.n_ops++] = BG_MAP_MEAN;
+      need5 = 1;
+    } else {
+      char b[512];
+      snprintf(b, sizeof(b), "--%s is not available in this build (GPU path: --count --mean, --bp-ovr)", k);
+      arg_error(b);
+    }
+  }
+  if (o.n_ops == 0) arg_error("No processing option specified (ie; --count).");
+  int nf = argc - a;
+  if (nf < 1 || nf > 2) arg_error("Need one or two input files");
+  for (int i = a; i < argc; ++i) {
+    if (strcmp(argv[i], "-") && access(argv[i], R_OK) != 0) {
+      char b[1024];
+      snprintf(b, sizeof(b), "Unable to find file: %s", argv[i]);
+      arg_error(b);
+    }
+  }
+  if (nf == 2 && !strcmp(argv[a], "-") && !strcmp(argv[a + 1], "-")) arg_error("Cannot have both input files set to '-'");
+
+  bg_ctx* ctx = NULL;
+  int rc = bg_open(&ctx, env_device());
+  if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
+  text_buf_t tr = {0}, tm = {0};
+  if (read_text(argv[a], &tr)) arg_error("Unable to read the reference file");
+  if (ec) apply_ec_header(&tr);
+  bg_input in[2];
+  in[0].data = tr.data;
+  in[0].nbytes = tr.n;
+  in[0].on_device = 0;
+  in[0].kind = BG_BED3;
+  if (nf == 2) {
+    if (read_text(argv[a + 1], &tm)) arg_error("Unable to read the map file");
+    if (ec) apply_ec_header(&tm);
+    in[1].data = tm.data;
+    in[1].nbytes = tm.n;
+  } else { /* single-file mode: the reference file is also the map file */
+    in[1].data = tr.data;
+    in[1].nbytes = tr.n;
+  }
+  in[1].on_device = 0;
+  in[1].kind = need5 ? BG_BED5 : BG_BED3;
+  bg_set* set = NULL;
+  if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
+  free_text(&tr);
+  free_text(&tm);
+  if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
+  bg_result* res = NULL;
+  if ((rc = bg_map(ctx, set, 0, 1, &o, &res))) die_ctx(PROG, ctx, rc);
+  if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
+  maybe_stats(ctx);
+  bg_result_free(res);
+  bg_set_free(set);
+  bg_close(ctx);
+  return EXIT_SUCCESS;
+}

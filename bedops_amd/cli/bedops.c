@@ -1,0 +1,259 @@
+/*
+ * bedops — drop-in front-end for the BEDOPS set-operation CLI, running the sweep on
+ * an MI355X through libbedgpu.
+ *
+ * argv grammar follows applications/bed/bedops/src/Input.hpp:57-298 (process flags,
+ * one operation, long->short option map :422-433, minimum file counts :389-420, the
+ * -e/-n overlap spec :171-206 and :344-382, '-' for stdin :271-287); output and exit
+ * behaviour follow Bedops.cpp:81-127. Operations on the GPU path: --merge,
+ * --intersect, --difference, --element-of, --not-element-of. The
+ * other operations (complement, symmdiff, everything, partition, chop) and --range
+ * are reported as not available in this build instead of being approximated.
+ */
+#include <ctype.h>
+
+#include "cli_common.h"
+
+static const char* PROG = "bedops";
+
+static void usage(FILE* f) {
+  fprintf(f,
+          "bedops\n  version:  %s\n\n"
+          "      USAGE: bedops [process-flags] <operation> <File(s)>*\n\n"
+          "          Every input file must be sorted per the sort-bed utility.\n"
+          "          May use '-' for a file to indicate reading from standard input.\n\n"
+          "      Process Flags:\n"
+          "          --chrom <chromosome> Process data for given <chromosome> only.\n"
+          "          --ec                 Error check input files.\n"
+          "          --header             Accept headers (browser/track/#/@) in input files.\n"
+          "          --help               Print this message and exit successfully.\n"
+          "          --version            Print program information.\n\n"
+          "      Operations (GPU path): choose one of\n"
+          "          -d, --difference ReferenceFile File2 [File]*\n"
+          "          -e, --element-of [bp | percentage] ReferenceFile File2 [File]*\n"
+          "          -i, --intersect File1 File2 [File]*\n"
+          "          -m, --merge File1 [File]*\n"
+          "          -n, --not-element-of [bp | percentage] ReferenceFile File2 [File]*\n",
+          BEDOPS_AMD_VERSION);
+}
+
+static void bad_input(const char* msg) {
+  char buf[1024];
+  snprintf(buf, sizeof(buf), "Bad Input\n%s", msg);
+  die_msg(PROG, buf);
+}
+
+static const char* long_to_short(const char* s) {
+  static const char* map[][2] = {{"--complement", "-c"}, {"--difference", "-d"}, {"--element-of", "-e"},
+                                 {"--intersect", "-i"},  {"--merge", "-m"},      {"--not-element-of", "-n"},
+                                 {"--partition", "-p"},  {"--symmdiff", "-s"},   {"--everything", "-u"},
+                                 {"--chop", "-w"}};
+  for (size_t k = 0; k < sizeof(map) / sizeof(map[0]); ++k)
+    if (strcmp(s, map[k][0]) == 0) return map[k][1];
+  return NULL;
+}
+
+static int all_chars_in(const char* s, const char* set) {
+  for (; *s; ++s)
+    if (!strchr(set, *s)) return 0;
+  return 1;
+}
+
+/* -e/-n overlap spec (Input.hpp:344-382) */
+static void set_subset(const char* str, double* thres, int* use_pct) {
+  const char* pct = strchr(str, '%');
+  if (pct) {
+    if (pct[1] != '\0') bad_input("Bad placement of %");
+    char val[128];
+    size_t n = (size_t)(pct - str);
+    if (n >= sizeof(val)) bad_input("Bad % value");
+    memcpy(val, str, n);
+    val[n] = 0;
+    const char* v = val;
+    if (!*v) bad_input("Bad % value");
+    if (*v == '-') {
+      ++v;
+      if (!*v) bad_input("Bad % value");
+    }
+    if (!all_chars_in(v, ".1234567890")) bad_input("Bad: % value");
+    double d = strtod(v, NULL) / 100.0;
+    if (d > 1) bad_input("Expect percentage less than or equal to 100%");
+    *thres = d;
+    *use_pct = 1;
+    if (d == 0) { *thres = 1; *use_pct = 0; }
+  } else if (all_chars_in(str, "1234567890")) {
+    *thres = atoi(str);
+    *use_pct = 0;
+  } else if (str[0] && all_chars_in(str + 1, "1234567890")) {
+    *thres = atoi(str + 1);
+    *use_pct = 0;
+  } else if (all_chars_in(str, ".1234567890")) {
+    bad_input("Fractional amounts require a '%' symbol (e.g.; 5.4% not 5.4 base-pair)");
+  } else {
+    char b[512];
+    snprintf(b, sizeof(b), "Unknown arg: %s", str);
+    bad_input(b);
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc <= 1) {
+    usage(stderr);
+    return EXIT_FAILURE;
+  }
+  int ec = 0, has_op = 0, has_chrom = 0;
+  char mode = 0;
+  const char* chrom = NULL;
+  double thres = 1.0;
+  int use_pct = 1, minfiles = 1;
+  int a = 1;
+  while (a < argc) {
+    const char* nx = argv[a];
+    if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) {
+      ec = 1;
+    } else if (!strcmp(nx, "--chrom")) {
+      if (has_chrom) bad_input("--chrom specified multiple times.");
+      if (++a >= argc) bad_input("No value for --chrom given.");
+      chrom = argv[a];
+      has_chrom = strcmp(chrom, "all") != 0;
+      if (!has_chrom) chrom = NULL;
+    } else if (!strcmp(nx, "--range")) {
+      die_msg(PROG, "--range is not available in this build (GPU path: -m -i -d -e -n)");
+    } else if (!strcmp(nx, "--help") || !strncmp(nx, "--help-", 7)) {
+      usage(stdout);
+      return EXIT_SUCCESS;
+    } else if (!strcmp(nx, "--version")) {
+      printf("bedops\n  version:  %s\n", BEDOPS_AMD_VERSION);
+      return EXIT_SUCCESS;
+    } else if (nx[0] != '-') {
+      break;
+    } else if (strlen(nx) > 1) {
+      if (strspn(nx, "-") == strlen(nx)) {
+        char b[512];
+        snprintf(b, sizeof(b), "Bad option: %s", nx);
+        bad_input(b);
+      }
+      if (has_op) {
+        char b[512];
+        snprintf(b, sizeof(b), "More than one operation specified: %s", nx);
+        bad_input(b);
+      }
+      has_op = 1;
+      const char* op = nx;
+      if (!strncmp(nx, "--", 2)) {
+        op = long_to_short(nx);
+        if (!op) {
+          char b[512];
+          snprintf(b, sizeof(b), "Unknown operation: %s", nx);
+          bad_input(b);
+        }
+      }
+      if (strlen(op) != 2) {
+        char b[512];
+        snprintf(b, sizeof(b), "Unknown operation: %s", op);
+        bad_input(b);
+      }
+      mode = (char)tolower((unsigned char)op[1]);
+      switch (mode) {
+        case 'm': minfiles = 1; break;
+        case 'i': case 'd': case 'e': case 'n': minfiles = 2; break;
+        case 'c': case 's': case 'u': case 'p': case 'w': {
+          char b[256];
+          snprintf(b, sizeof(b), "operation %s is not available in this build (GPU path: -m -i -d -e -n)", nx);
+          die_msg(PROG, b);
+        }
+        default: {
+          char b[512];
+          snprintf(b, sizeof(b), "Unknown operation: -%c", op[1]);
+          bad_input(b);
+        }
+      }
+      if (mode == 'e' || mode == 'n') { /* optional overlap spec (Input.hpp:171-206) */
+        if (a + 1 < argc) {
+          const char* q = argv[a + 1];
+          size_t sz = strlen(q);
+          if ((q[0] == '-' && sz > 1) || all_chars_in(q, "1234567890") || strchr(q, '%')) {
+            if (!strstr(q, "--")) {
+              if (access(q, F_OK) != 0) {
+                set_subset(q, &thres, &use_pct);
+                ++a;
+              } else if (all_chars_in(q, "0123456789")) {
+                fprintf(stderr,
+                        "Warning: interpreting argument '%s' as a file input and not as an overlap spec,\n"
+                        "         since the file exists.\n"
+                        "You can use the legacy syntax '-%s' if you want to use it as an overlap criterion.\n",
+                        q, q);
+              }
+            }
+          }
+        }
+      }
+    } else {
+      break; /* "-" = stdin */
+    }
+    ++a;
+  }
+  if (a >= argc) bad_input("No input file given.");
+  if (!has_op) bad_input("No operation argument given.");
+  int nf = argc - a, stdin_seen = 0;
+  for (int i = a; i < argc; ++i) {
+    if (!strcmp(argv[i], "-")) {
+      if (stdin_seen) bad_input("Too many '-'");
+      stdin_seen = 1;
+    } else {
+      char b[1024];
+      if (argv[i][0] == '-') {
+        snprintf(b, sizeof(b), "Bad option: %s", argv[i]);
+        bad_input(b);
+      }
+      if (access(argv[i], R_OK) != 0) {
+        snprintf(b, sizeof(b), "Cannot find %s", argv[i]);
+        bad_input(b);
+      }
+    }
+  }
+  if (nf < minfiles) bad_input("Not enough files");
+
+  bg_ctx* ctx = NULL;
+  int rc = bg_open(&ctx, env_device());
+  if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
+  text_buf_t* tx = (text_buf_t*)calloc((size_t)nf, sizeof(text_buf_t));
+  bg_input* in = (bg_input*)calloc((size_t)nf, sizeof(bg_input));
+  for (int i = 0; i < nf; ++i) {
+    if (read_text(argv[a + i], &tx[i])) {
+      char b[1024];
+      snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
+      die_msg(PROG, b);
+    }
+    if (ec) apply_ec_header(&tx[i]);
+    in[i].data = tx[i].data;
+    in[i].nbytes = tx[i].n;
+    in[i].on_device = 0;
+    /* element-of keeps all columns of the reference file (Bedops.cpp:412-421) */
+    in[i].kind = ((mode == 'e' || mode == 'n') && i == 0) ? BG_BED3_REST : BG_BED3;
+  }
+  bg_set* set = NULL;
+  if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);
+  for (int i = 0; i < nf; ++i) free_text(&tx[i]);
+  if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
+  int* idx = (int*)calloc((size_t)nf, sizeof(int));
+  for (int i = 0; i < nf; ++i) idx[i] = i;
+  bg_result* res = NULL;
+  switch (mode) {
+    case 'm': rc = bg_merge(ctx, set, idx, nf, &res); break;
+    case 'i': rc = bg_intersect(ctx, set, idx, nf, &res); break;
+    case 'd': rc = bg_difference(ctx, set, 0, idx + 1, nf - 1, &res); break;
+    case 'e': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 0, &res); break;
+    case 'n': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 1, &res); break;
+  }
+  if (rc) die_ctx(PROG, ctx, rc);
+  if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
+  maybe_stats(ctx);
+  bg_result_free(res);
+  bg_set_free(set);
+  bg_close(ctx);
+  free(idx);
+  free(in);
+  free(tx);
+  return EXIT_SUCCESS;
+}

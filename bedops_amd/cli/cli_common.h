@@ -1,0 +1,123 @@
+/*
+ * cli_common.h — shared host-side plumbing of the bedops_amd front-ends (C).
+ *
+ * Input files are read whole into pinned host memory and handed to libbedgpu, which
+ * parses them on the GPU. '-' reads stdin (at most one per command line, as in
+ * applications/bed/bedops/src/Input.hpp:271-287). Error text and exit codes follow
+ * the reference front-ends: "May use <prog> --help for more help.\n\nError: <msg>"
+ * on stderr and EXIT_FAILURE (applications/bed/bedops/src/Bedops.cpp:117-126).
+ */
+#ifndef BEDOPS_AMD_CLI_COMMON_H
+#define BEDOPS_AMD_CLI_COMMON_H
+
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "../../include/bedgpu.h"
+
+#define BEDOPS_AMD_VERSION "2.4.26 (bedops_amd MI355X engine)"
+
+typedef struct {
+  char* data;     /* pinned host buffer */
+  uint64_t n;     /* bytes of BED text */
+  int pinned;
+} text_buf_t;
+
+static void die_msg(const char* prog, const char* msg) {
+  fprintf(stderr, "May use %s --help for more help.\n\nError: %s\n", prog, msg);
+  exit(EXIT_FAILURE);
+}
+
+static void die_ctx(const char* prog, bg_ctx* ctx, int rc) {
+  char msg[1024];
+  snprintf(msg, sizeof(msg), "%s", ctx ? bg_last_error(ctx) : "");
+  if (!msg[0]) snprintf(msg, sizeof(msg), "GPU engine failure (code %d)", rc);
+  die_msg(prog, msg);
+}
+
+/* read a whole file (or stdin for "-") into a pinned buffer */
+static int read_text(const char* path, text_buf_t* out) {
+  int fd = strcmp(path, "-") == 0 ? 0 : open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  uint64_t cap = 1 << 20;
+  if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) cap = (uint64_t)st.st_size + 1;
+  char* buf = (char*)bg_host_alloc(cap + 16);
+  int pinned = 1;
+  if (!buf) { buf = (char*)malloc(cap + 16); pinned = 0; }
+  if (!buf) return -1;
+  uint64_t n = 0;
+  for (;;) {
+    if (n == cap) { /* grow (pipes / stdin) */
+      uint64_t nc = cap * 2;
+      char* nb = (char*)malloc(nc + 16);
+      if (!nb) return -1;
+      memcpy(nb, buf, n);
+      if (pinned) bg_host_free(buf); else free(buf);
+      buf = nb;
+      pinned = 0;
+      cap = nc;
+    }
+    ssize_t r = read(fd, buf + n, (size_t)(cap - n));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    if (r == 0) break;
+    n += (uint64_t)r;
+  }
+  if (fd != 0) close(fd);
+  out->data = buf;
+  out->n = n;
+  out->pinned = pinned;
+  return 0;
+}
+
+static void free_text(text_buf_t* t) {
+  if (!t->data) return;
+  if (t->pinned) bg_host_free(t->data); else free(t->data);
+  t->data = NULL;
+}
+
+/* --header / --ec: drop leading UCSC/VCF/SAM header lines ("browser", "track", '#',
+ * '@'; BedCheckIterator.hpp:315-350) and keep an unterminated final line (the error
+ * checking reader keeps it, the plain reader drops it). */
+static void apply_ec_header(text_buf_t* t) {
+  uint64_t p = 0;
+  for (;;) {
+    uint64_t e = p;
+    while (e < t->n && t->data[e] != '\n') ++e;
+    if (e >= t->n) break;
+    const char* l = t->data + p;
+    uint64_t len = e - p;
+    int hdr = (len > 0 && (l[0] == '#' || l[0] == '@')) ||
+              (len >= 5 && strncasecmp(l, "track", 5) == 0 && (len == 5 || l[5] == ' ' || l[5] == '\t')) ||
+              (len >= 7 && strncasecmp(l, "browser", 7) == 0 && (len == 7 || l[7] == ' ' || l[7] == '\t'));
+    if (!hdr) break;
+    p = e + 1;
+  }
+  if (p) {
+    memmove(t->data, t->data + p, t->n - p);
+    t->n -= p;
+  }
+  if (t->n > 0 && t->data[t->n - 1] != '\n') t->data[t->n++] = '\n'; /* capacity has +16 */
+}
+
+static int env_device(void) {
+  const char* d = getenv("BEDGPU_DEVICE");
+  return d ? atoi(d) : 0;
+}
+
+static void maybe_stats(bg_ctx* ctx) {
+  const char* s = getenv("BEDGPU_STATS");
+  if (!s || !*s || strcmp(s, "0") == 0) return;
+  char buf[4096];
+  if (bg_stats(ctx, buf, sizeof(buf)) == 0) fputs(buf, stderr);
+}
+
+#endif

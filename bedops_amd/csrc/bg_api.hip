@@ -1,0 +1,265 @@
+// bg_api.hip — libbedgpu context, caching allocator, errors, result plumbing.
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <unordered_map>
+
+#include "bg_internal.h"
+
+namespace {
+struct LiveMap {
+  std::unordered_map<void*, size_t> m;
+};
+std::unordered_map<bg_ctx*, LiveMap> g_live;  // one entry per context
+}  // namespace
+
+int bg_fail(bg_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int bg_hip_fail(bg_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string("HIP error: ") + hipGetErrorString(e) + " in " + what;
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return bg_fail(c, BG_E_NOMEM, m);
+  return bg_fail(c, BG_E_HIP, m);
+}
+
+void* bg_alloc(bg_ctx* c, size_t bytes) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  if (bytes == 0) bytes = 256;
+  // best fit among cached blocks no larger than 2x the request
+  size_t best = (size_t)-1;
+  for (size_t k = 0; k < c->free_list.size(); ++k) {
+    const size_t b = c->free_list[k].bytes;
+    if (b >= bytes && b <= 2 * bytes && (best == (size_t)-1 || b < c->free_list[best].bytes)) best = k;
+  }
+  void* p = nullptr;
+  size_t got = bytes;
+  if (best != (size_t)-1) {
+    p = c->free_list[best].p;
+    got = c->free_list[best].bytes;
+    c->free_list.erase(c->free_list.begin() + best);
+  } else {
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      // drop the cache and retry once
+      hipStreamSynchronize(c->stream);
+      for (auto& b : c->free_list) hipFree(b.p);
+      c->free_list.clear();
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        bg_fail(c, BG_E_NOMEM, "device allocation of " + std::to_string(bytes) + " bytes failed");
+        return nullptr;
+      }
+    }
+  }
+  g_live[c].m[p] = got;
+  return p;
+}
+
+void bg_release(bg_ctx* c, void* p) {
+  if (!c || !p) return;
+  auto& L = g_live[c].m;
+  auto it = L.find(p);
+  if (it == L.end()) return;
+  c->free_list.push_back({p, it->second});
+  L.erase(it);
+}
+
+void bg_mark(bg_ctx* c, const char* name) {
+  if (!c->stats) return;
+  hipEvent_t ev;
+  if (hipEventCreate(&ev) != hipSuccess) return;
+  hipEventRecord(ev, c->stream);
+  c->marks.emplace_back(name, ev);
+}
+
+extern "C" int bg_open(bg_ctx** out, int device) {
+  if (!out) return BG_E_ARG;
+  *out = nullptr;
+  bg_ctx* c = new bg_ctx();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete c;
+    return BG_E_HIP;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess ||
+      hipHostMalloc(&c->hstat, sizeof(bg_dstatus), hipHostMallocDefault) != hipSuccess) {
+    delete c;
+    return BG_E_HIP;
+  }
+  const char* st = getenv("BEDGPU_STATS");
+  c->stats = st && *st && strcmp(st, "0") != 0;
+  bg_mark(c, "open");
+  *out = c;
+  return 0;
+}
+
+extern "C" void bg_close(bg_ctx* c) {
+  if (!c) return;
+  hipStreamSynchronize(c->stream);
+  for (auto& b : c->free_list) hipFree(b.p);
+  for (auto& kv : g_live[c].m) hipFree(kv.first);
+  g_live.erase(c);
+  for (auto& m : c->marks) hipEventDestroy(m.second);
+  hipFree(c->dstat);
+  hipHostFree(c->hstat);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" const char* bg_last_error(const bg_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+extern "C" int bg_sync(bg_ctx* c) {
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" void* bg_stream(bg_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int bg_stats(const bg_ctx* cc, char* buf, uint64_t cap) {
+  bg_ctx* c = const_cast<bg_ctx*>(cc);
+  if (!c || !buf || !cap) return BG_E_ARG;
+  std::string s;
+  hipStreamSynchronize(c->stream);
+  for (size_t k = 1; k < c->marks.size(); ++k) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->marks[k - 1].second, c->marks[k].second);
+    char line[128];
+    snprintf(line, sizeof(line), "bedgpu stage %-12s %10.3f ms\n", c->marks[k].first.c_str(), ms);
+    s += line;
+  }
+  snprintf(buf, cap, "%s", s.c_str());
+  return 0;
+}
+
+extern "C" int bg_set_restrict_chrom(bg_ctx* c, bg_set* s, const char* chrom) {
+  if (!c || !s || !chrom) return BG_E_ARG;
+  for (bg_table* T : s->t) {
+    uint64_t a = 0, b = 0;
+    for (size_t k = 0; k + 1 < T->run_row0.size(); ++k)
+      if (T->run_name[k] == chrom) { a = T->run_row0[k]; b = T->run_row0[k + 1]; }
+    const uint64_t n = b - a;
+    auto sub = [&](void* p, size_t w) -> void* {
+      if (!p) return nullptr;
+      void* q = bg_alloc(c, w * (n ? n : 1));
+      if (q && n) hipMemcpyAsync(q, (char*)p + w * a, w * n, hipMemcpyDeviceToDevice, c->stream);
+      bg_release(c, p);
+      return q;
+    };
+    T->ks = (int64_t*)sub(T->ks, 8);
+    T->ke = (int64_t*)sub(T->ke, 8);
+    T->rest_off = (uint64_t*)sub(T->rest_off, 8);
+    T->rest_len = (uint32_t*)sub(T->rest_len, 4);
+    T->score = (double*)sub(T->score, 8);
+    T->n = n;
+    T->run_row0.assign({0, n});
+    T->run_name.assign({std::string(chrom)});
+    if (!T->ks || !T->ke) return BG_E_NOMEM;
+  }
+  return 0;
+}
+
+extern "C" int bg_result_rows(const bg_result* r, uint64_t* rows) {
+  if (!r || !rows) return BG_E_ARG;
+  *rows = r->n;
+  return 0;
+}
+
+extern "C" int bg_result_text_device(const bg_result* r, const char** dptr, uint64_t* nbytes) {
+  if (!r || !dptr || !r->formatted) return BG_E_ARG;
+  *dptr = r->text;
+  if (nbytes) *nbytes = r->nbytes;
+  return 0;
+}
+
+extern "C" int bg_result_copy_text(bg_ctx* c, bg_result* r, char* host, uint64_t cap) {
+  uint64_t n = 0;
+  int rc = bg_result_format(c, r, &n);
+  if (rc) return rc;
+  if (cap < n) return bg_fail(c, BG_E_ARG, "host buffer too small");
+  if (n) BG_HIP(c, hipMemcpyAsync(host, r->text, n, hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+static int write_all(int fd, const char* p, uint64_t n) {
+  while (n) {
+    ssize_t w = write(fd, p, n > (1u << 30) ? (1u << 30) : n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    p += w;
+    n -= (uint64_t)w;
+  }
+  return 0;
+}
+
+// formats on the device, then streams the text to fd through two pinned buffers so
+// the D2H copy of chunk k+1 overlaps write(2) of chunk k
+extern "C" int bg_result_write(bg_ctx* c, bg_result* r, int fd) {
+  uint64_t n = 0;
+  int rc = bg_result_format(c, r, &n);
+  if (rc) return rc;
+  if (n == 0) return 0;
+  const uint64_t CH = 64ull << 20;
+  char* hb[2] = {nullptr, nullptr};
+  hipEvent_t ev[2];
+  for (int k = 0; k < 2; ++k) {
+    BG_HIP(c, hipHostMalloc((void**)&hb[k], CH, hipHostMallocDefault));
+    BG_HIP(c, hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+  }
+  const uint64_t nch = (n + CH - 1) / CH;
+  auto issue = [&](uint64_t k) -> int {
+    const uint64_t off = k * CH, len = std::min(CH, n - off);
+    BG_HIP(c, hipMemcpyAsync(hb[k & 1], r->text + off, len, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipEventRecord(ev[k & 1], c->stream));
+    return 0;
+  };
+  if ((rc = issue(0))) return rc;
+  for (uint64_t k = 0; k < nch; ++k) {
+    BG_HIP(c, hipEventSynchronize(ev[k & 1]));
+    if (k + 1 < nch && (rc = issue(k + 1))) return rc;
+    const uint64_t off = k * CH, len = std::min(CH, n - off);
+    if (write_all(fd, hb[k & 1], len)) {
+      rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
+      break;
+    }
+  }
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < 2; ++k) {
+    hipHostFree(hb[k]);
+    hipEventDestroy(ev[k]);
+  }
+  bg_mark(c, "write");
+  return rc;
+}
+
+extern "C" void* bg_host_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+extern "C" void bg_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+extern "C" void bg_result_free(bg_result* r) {
+  if (!r) return;
+  bg_ctx* c = r->ctx;
+  bg_release(c, r->s);
+  bg_release(c, r->e);
+  bg_release(c, r->rows);
+  bg_release(c, r->cnt);
+  bg_release(c, r->isum);
+  bg_release(c, r->text);
+  delete r;
+}

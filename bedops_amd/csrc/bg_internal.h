@@ -1,0 +1,248 @@
+// bg_internal.h — shared internals of libbedgpu (host structs + gfx950 device helpers).
+//
+// Data layout in HBM: every parsed input is two int64 SoA columns
+//   ks[i] = (chrom_id << 40) | start_i,   ke[i] = (chrom_id << 40) | end_i
+// with chrom_id the rank of the chromosome name in strcmp order over the union of
+// the inputs (the order every reference comparator uses: BedCompare.hpp:42-43).
+// Coordinates are <= 999,999,999,999 < 2^40 (BEDOPS.Constants.hpp:36), so keyed
+// intervals of different chromosomes never overlap or touch, and a whole
+// multi-chromosome file is ONE sorted array: every sweep is a single global
+// scan / merge-path pass with no per-chromosome segmentation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/bedgpu.h"
+
+#define BG_KEY_SHIFT 40
+#define BG_COORD_MASK ((1LL << BG_KEY_SHIFT) - 1)
+#define BG_MAX_COORD 999999999999ULL
+#define BG_CHR_MAX 127
+
+// ---------------------------------------------------------------------------------
+// device status word: first error as (row << 8 | code), run-record counters
+// ---------------------------------------------------------------------------------
+struct bg_dstatus {
+  unsigned long long first_bad;  // min over errors of (row << 8) | code; ~0 if none
+  unsigned long long nruns;      // chromosome-run records appended by the parser
+  unsigned long long nblank;     // blank lines seen
+  unsigned long long flags;      // bit0: non-integer score, bit1: zero-length row, bit2: |sum|>=2^53
+  long long maxlen;              // max (end - start) seen (bedmap window)
+  unsigned long long pad[3];
+};
+
+enum { ERR_PARSE = 1, ERR_CHROM = 2, ERR_RANGE = 3, ERR_UNSORTED = 4, ERR_BLANK = 5, ERR_SCORE = 6 };
+
+// ---------------------------------------------------------------------------------
+// host-side objects
+// ---------------------------------------------------------------------------------
+struct bg_buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct bg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bg_dstatus* dstat = nullptr;  // device
+  bg_dstatus* hstat = nullptr;  // pinned host mirror
+  // caching allocator: free blocks by size
+  std::vector<bg_buf> free_list;
+  std::vector<bg_buf> live;
+  // stage timing
+  bool stats = false;
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::string stats_text;
+};
+
+struct bg_table {
+  uint64_t n = 0;
+  int kind = BG_BED3;
+  int64_t* ks = nullptr;  // keyed starts (raw coordinates until keyed)
+  int64_t* ke = nullptr;  // keyed ends
+  // kept for BG_BED3_REST output: text + remainder span per row
+  const char* text = nullptr;  // device text
+  uint64_t nbytes = 0;
+  char* own_text = nullptr;  // when the library copied host text in
+  uint64_t* rest_off = nullptr;
+  uint32_t* rest_len = nullptr;
+  double* score = nullptr;  // BG_BED5
+  bool score_int = true;     // every score is an integer (exact sums)
+  bool has_zero_len = false; // some row has end == start
+  // chromosome runs (host, sorted by row): rows [row0[k], row0[k+1]) are chrom names[k]
+  std::vector<uint64_t> run_row0;
+  std::vector<std::string> run_name;
+};
+
+struct bg_set {
+  bg_ctx* ctx = nullptr;
+  std::vector<bg_table*> t;
+  std::vector<std::string> names;  // global chromosome dictionary, strcmp order
+  char* d_names = nullptr;         // packed names on device
+  uint32_t* d_name_off = nullptr;  // offset of name g
+  uint32_t* d_name_len = nullptr;
+  uint32_t max_name_len = 0;
+};
+
+enum { RES_IVL = 0, RES_ROWS = 1, RES_MAP = 2 };
+
+struct bg_result {
+  bg_ctx* ctx = nullptr;
+  bg_set* set = nullptr;
+  int kind = RES_IVL;
+  uint64_t n = 0;
+  // RES_IVL: keyed intervals
+  int64_t* s = nullptr;
+  int64_t* e = nullptr;
+  // RES_ROWS: selected row indices of table `tab`
+  uint64_t* rows = nullptr;
+  int tab = -1;
+  // RES_MAP: per reference row columns
+  int32_t* cnt = nullptr;
+  int64_t* isum = nullptr;
+  bg_map_opts mopts;
+  // rendered text
+  char* text = nullptr;
+  uint64_t nbytes = 0;
+  bool formatted = false;
+};
+
+// allocator / error helpers (bg_api.cpp)
+void* bg_alloc(bg_ctx* c, size_t bytes);
+void bg_release(bg_ctx* c, void* p);
+int bg_fail(bg_ctx* c, int code, const std::string& msg);
+int bg_hip_fail(bg_ctx* c, hipError_t e, const char* what);
+void bg_mark(bg_ctx* c, const char* name);
+
+#define BG_HIP(c, expr)                                  \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return bg_hip_fail((c), _e, #expr); \
+  } while (0)
+
+// device-wide helpers (bg_scan.hip)
+// exclusive prefix sum of n uint64 values (in may alias out); *total (device ptr,
+// optional) receives the sum.
+int bg_scan_sum_u64(bg_ctx* c, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* d_total);
+// exclusive prefix max of n int64 values with identity `init`
+int bg_scan_max_i64(bg_ctx* c, const int64_t* in, int64_t* out, uint64_t n, int64_t init);
+// copy one device uint64 to host (synchronises the stream)
+int bg_fetch_u64(bg_ctx* c, const uint64_t* d, uint64_t* h);
+
+// ---------------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------------
+#define BG_NT 256  // threads per workgroup (4 waves of 64)
+
+__device__ __forceinline__ int bg_lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ int bg_wave() { return threadIdx.x >> 6; }
+
+// inclusive wave (64-lane) scan
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T v, Op op) {
+  const int lane = bg_lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T u = __shfl_up(v, d, 64);
+    if (lane >= d) v = op(v, u);
+  }
+  return v;
+}
+
+struct OpSum {
+  template <typename T>
+  __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
+};
+struct OpMax {
+  template <typename T>
+  __device__ __forceinline__ T operator()(T a, T b) const { return a > b ? a : b; }
+};
+
+// Block (BG_NT threads) exclusive scan. `sh` must hold BG_NT/64 + 1 elements.
+// Returns the exclusive prefix of this thread; *total gets the block aggregate.
+template <typename T, typename Op>
+__device__ __forceinline__ T block_excl_scan(T v, Op op, T identity, T* sh, T* total) {
+  const int lane = bg_lane(), w = bg_wave();
+  T inc = wave_incl_scan(v, op);
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = identity;
+#pragma unroll
+    for (int i = 0; i < BG_NT / 64; ++i) {
+      T x = sh[i];
+      sh[i] = run;
+      run = op(run, x);
+    }
+    sh[BG_NT / 64] = run;
+  }
+  __syncthreads();
+  T wpre = sh[w];
+  T excl = __shfl_up(inc, 1, 64);
+  excl = (lane == 0) ? wpre : op(wpre, excl);
+  *total = sh[BG_NT / 64];
+  __syncthreads();  // sh may be reused by the caller
+  return excl;
+}
+
+__device__ __forceinline__ bool bg_isws(uint8_t c) {
+  // C-locale isspace minus '\n' (lines are split on '\n' first)
+  return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
+}
+
+// number of elements of X among the first d of merge(X, Y) when X[i] goes first
+// only if X[i] < Y[j] strictly (ties: Y first). X, Y sorted ascending.
+__device__ __forceinline__ uint64_t merge_path_ystrict(const int64_t* X, uint64_t nx,
+                                                       const int64_t* Y, uint64_t ny,
+                                                       uint64_t d) {
+  uint64_t lo = d > ny ? d - ny : 0, hi = d < nx ? d : nx;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (X[mid] < Y[d - 1 - mid]) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// same with X first on ties (X[i] <= Y[j])
+__device__ __forceinline__ uint64_t merge_path_xfirst(const int64_t* X, uint64_t nx,
+                                                      const int64_t* Y, uint64_t ny,
+                                                      uint64_t d) {
+  uint64_t lo = d > ny ? d - ny : 0, hi = d < nx ? d : nx;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (X[mid] <= Y[d - 1 - mid]) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// first index k in [0,n) with A[k] >= v (A sorted ascending); n if none
+__device__ __forceinline__ uint64_t lower_bound_i64(const int64_t* A, uint64_t n, int64_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (A[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// first index k with A[k] > v
+__device__ __forceinline__ uint64_t upper_bound_i64(const int64_t* A, uint64_t n, int64_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (A[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void bg_report(bg_dstatus* st, uint64_t row, int code) {
+  atomicMin(&st->first_bad, (unsigned long long)((row << 8) | (uint64_t)code));
+}
+
+static inline unsigned bg_blocks(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }

@@ -1,0 +1,534 @@
+// bg_setops.hip — K1..K4: the bedops sweep kernels on keyed SoA intervals.
+//
+// The reference walks the inputs with pull readers and strcmp on every comparison
+// (applications/bed/bedops/src/Bedops.cpp:792-1243). Here every operation is a
+// scan, a merge-path pass or a binary search over whole sorted arrays:
+//
+//  components(X)        = running-max merge of one start-sorted array: row i opens a
+//                         component iff ks[i] > max(ke[0..i-1]); touching rows merge
+//                         (mergeOverlap's `p1.end >= p2.start`, Bedops.cpp:864-886;
+//                         nextMergeAllLines, :1186-1243)
+//  merge_sorted(X, Y)   = stable merge path of two start-sorted arrays (k-way union)
+//  intersect2(X, Y)     = every element of merge(X,Y) (ties: Y first) emits at most one
+//                         piece: [x.s, min(x.e, y.e)) with y the last Y starting <= x.s,
+//                         [y.s, min(y.e, x.e)) with x the last X starting < y.s; pieces
+//                         of length 0 are never emitted (nextIntersectLine :1105-1181)
+//  difference(R, O)     = merge of R by start with O by end (ties: O first): r emits
+//                         [r.s, min(r.e, q.s)) unless covered, q = first O ending after
+//                         r.s; o emits [o.e, min(r.e, next.s)) inside the last R starting
+//                         before o.e. This reproduces nextDifferenceLine (:950-1018)
+//                         including its zero-length-row behaviour.
+//  element_of(rows, O)  = exact covered bp by two binary searches + prefix sums of
+//                         component lengths, then the reference's double-precision
+//                         test (:1094-1096)
+// Count pass and write pass share one device function per kernel (reduce-then-scan
+// between them), so outputs are deterministic and exactly sized.
+#include <climits>
+
+#include "bg_internal.h"
+
+#define CT_ITEMS 16
+#define CT_TILE (BG_NT * CT_ITEMS)
+#define MP_ITEMS 8
+#define MP_TILE (BG_NT * MP_ITEMS)
+
+// ------------------------------- components ---------------------------------------
+__global__ void __launch_bounds__(BG_NT) k_tile_max(const int64_t* __restrict__ E, uint64_t n,
+                                                    int64_t* __restrict__ tmax) {
+  __shared__ int64_t sh[BG_NT / 64 + 1];
+  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE + (uint64_t)threadIdx.x * CT_ITEMS;
+  int64_t m = LLONG_MIN;
+#pragma unroll
+  for (int k = 0; k < CT_ITEMS; ++k)
+    if (base + k < n) m = max(m, E[base + k]);
+  int64_t tot;
+  (void)block_excl_scan(m, OpMax(), (int64_t)LLONG_MIN, sh, &tot);
+  if (threadIdx.x == 0) tmax[blockIdx.x] = tot;
+}
+
+template <bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_components(
+    const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
+    const int64_t* __restrict__ carry, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+    int64_t* __restrict__ CS, int64_t* __restrict__ CE) {
+  __shared__ int64_t shm[BG_NT / 64 + 1];
+  __shared__ uint32_t shc[BG_NT / 64 + 1];
+  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE + (uint64_t)threadIdx.x * CT_ITEMS;
+  int64_t vs[CT_ITEMS], ve[CT_ITEMS];
+  int64_t lm = LLONG_MIN;
+#pragma unroll
+  for (int k = 0; k < CT_ITEMS; ++k) {
+    const bool in = base + k < n;
+    vs[k] = in ? S[base + k] : LLONG_MAX;
+    ve[k] = in ? E[base + k] : LLONG_MIN;
+    lm = max(lm, ve[k]);
+  }
+  int64_t tot;
+  int64_t run = block_excl_scan(lm, OpMax(), (int64_t)LLONG_MIN, shm, &tot);
+  run = max(run, carry[blockIdx.x]);
+  uint32_t flags = 0, c = 0;
+  int64_t incl[CT_ITEMS];
+#pragma unroll
+  for (int k = 0; k < CT_ITEMS; ++k) {
+    const bool in = base + k < n;
+    if (in && vs[k] > run) { flags |= 1u << k; ++c; }
+    run = max(run, ve[k]);
+    incl[k] = run;
+  }
+  uint32_t btot;
+  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  if (!WRITE) {
+    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    return;
+  }
+  uint64_t q = off[blockIdx.x] + o;  // components opened before this thread's rows
+#pragma unroll
+  for (int k = 0; k < CT_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i >= n) break;
+    if (flags & (1u << k)) CS[q++] = vs[k];
+    bool next_opens;
+    if (i + 1 >= n) next_opens = true;
+    else if (k + 1 < CT_ITEMS) next_opens = (flags >> (k + 1)) & 1u;
+    else next_opens = S[i + 1] > incl[k];
+    if (next_opens) CE[q - 1] = incl[k];
+  }
+}
+
+// ------------------------------- merge (union of two lists) -----------------------
+__global__ void __launch_bounds__(BG_NT) k_merge_sorted(const int64_t* __restrict__ XS,
+                                                        const int64_t* __restrict__ XE, uint64_t nx,
+                                                        const int64_t* __restrict__ YS,
+                                                        const int64_t* __restrict__ YE, uint64_t ny,
+                                                        int64_t* __restrict__ ZS,
+                                                        int64_t* __restrict__ ZE) {
+  const uint64_t d0 = ((uint64_t)blockIdx.x * BG_NT + threadIdx.x) * MP_ITEMS;
+  const uint64_t nz = nx + ny;
+  if (d0 >= nz) return;
+  uint64_t i = merge_path_xfirst(XS, nx, YS, ny, d0), j = d0 - i;
+  for (int k = 0; k < MP_ITEMS && d0 + k < nz; ++k) {
+    const bool takex = i < nx && (j >= ny || XS[i] <= YS[j]);
+    if (takex) { ZS[d0 + k] = XS[i]; ZE[d0 + k] = XE[i]; ++i; }
+    else { ZS[d0 + k] = YS[j]; ZE[d0 + k] = YE[j]; ++j; }
+  }
+}
+
+// ------------------------------- intersect ----------------------------------------
+template <bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_intersect2(
+    const int64_t* __restrict__ XS, const int64_t* __restrict__ XE, uint64_t nx,
+    const int64_t* __restrict__ YS, const int64_t* __restrict__ YE, uint64_t ny,
+    uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, int64_t* __restrict__ OS,
+    int64_t* __restrict__ OE) {
+  __shared__ uint32_t shc[BG_NT / 64 + 1];
+  const uint64_t d0 = ((uint64_t)blockIdx.x * BG_NT + threadIdx.x) * MP_ITEMS;
+  const uint64_t nz = nx + ny;
+  int64_t ps[MP_ITEMS], pe[MP_ITEMS];
+  uint32_t c = 0;
+  if (d0 < nz) {
+    uint64_t i = merge_path_ystrict(XS, nx, YS, ny, d0), j = d0 - i;
+    int64_t lastx_e = i > 0 ? XE[i - 1] : LLONG_MIN;
+    int64_t lasty_e = j > 0 ? YE[j - 1] : LLONG_MIN;
+    for (int k = 0; k < MP_ITEMS && d0 + k < nz; ++k) {
+      const bool takex = i < nx && (j >= ny || XS[i] < YS[j]);
+      int64_t s, e, pend;
+      if (takex) {
+        s = XS[i]; e = XE[i]; pend = lasty_e; lastx_e = e; ++i;
+      } else {
+        s = YS[j]; e = YE[j]; pend = lastx_e; lasty_e = e; ++j;
+      }
+      const int64_t hi = min(e, pend);
+      if (hi > s) { ps[c] = s; pe[c] = hi; ++c; }
+    }
+  }
+  uint32_t btot;
+  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  if (!WRITE) {
+    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    return;
+  }
+  const uint64_t q = off[blockIdx.x] + o;
+  for (uint32_t k = 0; k < c; ++k) { OS[q + k] = ps[k]; OE[q + k] = pe[k]; }
+}
+
+// ------------------------------- difference ---------------------------------------
+// R: reference components (by start); O: other components, merged against R by END.
+template <bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_difference(
+    const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
+    const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
+    uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, int64_t* __restrict__ DS,
+    int64_t* __restrict__ DE) {
+  __shared__ uint32_t shc[BG_NT / 64 + 1];
+  const uint64_t d0 = ((uint64_t)blockIdx.x * BG_NT + threadIdx.x) * MP_ITEMS;
+  const uint64_t nz = nr + no;
+  int64_t ps[MP_ITEMS], pe[MP_ITEMS];
+  uint32_t c = 0;
+  if (d0 < nz) {
+    uint64_t i = merge_path_ystrict(RS, nr, OE_, no, d0), j = d0 - i;
+    for (int k = 0; k < MP_ITEMS && d0 + k < nz; ++k) {
+      const bool taker = i < nr && (j >= no || RS[i] < OE_[j]);
+      if (taker) {
+        const int64_t a = RS[i], b = RE[i];
+        if (j >= no || OS_[j] >= b) { ps[c] = a; pe[c] = b; ++c; }
+        else if (OS_[j] > a) { ps[c] = a; pe[c] = OS_[j]; ++c; }
+        ++i;
+      } else {
+        if (i > 0) {
+          const int64_t oe = OE_[j], rb = RE[i - 1];
+          if (rb > oe) {
+            const int64_t nxt = (j + 1 < no) ? min(rb, OS_[j + 1]) : rb;
+            ps[c] = oe; pe[c] = nxt; ++c;
+          }
+        }
+        ++j;
+      }
+    }
+  }
+  uint32_t btot;
+  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  if (!WRITE) {
+    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    return;
+  }
+  const uint64_t q = off[blockIdx.x] + o;
+  for (uint32_t k = 0; k < c; ++k) { DS[q + k] = ps[k]; DE[q + k] = pe[k]; }
+}
+
+// ------------------------------- element-of ---------------------------------------
+__global__ void __launch_bounds__(BG_NT) k_lengths(const int64_t* __restrict__ S,
+                                                   const int64_t* __restrict__ E, uint64_t n,
+                                                   uint64_t* __restrict__ L) {
+  const uint64_t i = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (i < n) L[i] = (uint64_t)(E[i] - S[i]);
+}
+
+__global__ void __launch_bounds__(BG_NT) k_element_flags(
+    const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
+    const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
+    const uint64_t* __restrict__ P, double thres, int use_pct, int invert,
+    uint8_t* __restrict__ flag) {
+  const uint64_t r = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (r >= nr) return;
+  const int64_t s = RS[r], e = RE[r];
+  const uint64_t lo = upper_bound_i64(OE_, no, s);  // first component ending after s
+  bool keep;
+  if (lo >= no) {
+    keep = invert;  // nothing left to be an element of (Bedops.cpp:1044-1048)
+  } else {
+    const uint64_t hi = lower_bound_i64(OS_, no, e);  // first component starting at/after e
+    uint64_t ov = 0;
+    if (lo < hi) {
+      ov = P[hi] - P[lo];
+      if (s > OS_[lo]) ov -= (uint64_t)(s - OS_[lo]);
+      if (OE_[hi - 1] > e) ov -= (uint64_t)(OE_[hi - 1] - e);
+    }
+    const double rov = (double)ov, range = (double)(e - s);
+    const bool is_el = use_pct ? (rov / range >= thres) : (rov >= thres);
+    keep = invert ? !is_el : is_el;
+  }
+  flag[r] = keep ? 1 : 0;
+}
+
+#define CF_ITEMS 16
+#define CF_TILE (BG_NT * CF_ITEMS)
+template <bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_compact_flags(const uint8_t* __restrict__ flag,
+                                                         uint64_t n, uint64_t* __restrict__ cnt,
+                                                         const uint64_t* __restrict__ off,
+                                                         uint64_t* __restrict__ rows) {
+  __shared__ uint32_t shc[BG_NT / 64 + 1];
+  const uint64_t base = (uint64_t)blockIdx.x * CF_TILE + (uint64_t)threadIdx.x * CF_ITEMS;
+  uint32_t f = 0, c = 0;
+#pragma unroll
+  for (int k = 0; k < CF_ITEMS; ++k)
+    if (base + k < n && flag[base + k]) { f |= 1u << k; ++c; }
+  uint32_t btot;
+  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  if (!WRITE) {
+    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    return;
+  }
+  uint64_t q = off[blockIdx.x] + o;
+  while (f) {
+    int k = __ffs(f) - 1;
+    rows[q++] = base + k;
+    f &= f - 1;
+  }
+}
+
+// =====================================================================================
+// host drivers
+// =====================================================================================
+struct Ivl {
+  int64_t* s = nullptr;
+  int64_t* e = nullptr;
+  uint64_t n = 0;
+  bool owned = false;
+};
+
+static void ivl_free(bg_ctx* c, Ivl& v) {
+  if (v.owned) { bg_release(c, v.s); bg_release(c, v.e); }
+  v = Ivl();
+}
+
+static int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
+  v.n = n;
+  v.s = (int64_t*)bg_alloc(c, 8 * (n ? n : 1));
+  v.e = (int64_t*)bg_alloc(c, 8 * (n ? n : 1));
+  v.owned = true;
+  return (v.s && v.e) ? 0 : BG_E_NOMEM;
+}
+
+// count pass -> scan -> allocate exact output -> write pass
+template <typename CountFn, typename WriteFn>
+static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint64_t* total,
+                            uint64_t** off_out) {
+  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
+  uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
+  if (!cnt || !d_tot) return BG_E_NOMEM;
+  if (nb) {
+    cf(cnt);
+    BG_HIP(c, hipGetLastError());
+  }
+  int rc = bg_scan_sum_u64(c, cnt, cnt, nb, d_tot);
+  if (rc) return rc;
+  if ((rc = bg_fetch_u64(c, d_tot, total))) return rc;
+  bg_release(c, d_tot);
+  if ((rc = wf(cnt, *total))) return rc;
+  BG_HIP(c, hipGetLastError());
+  if (off_out) *off_out = cnt;
+  else bg_release(c, cnt);
+  return 0;
+}
+
+static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
+  const uint64_t n = in.n;
+  if (n == 0) return ivl_alloc(c, out, 0);
+  const unsigned nb = bg_blocks(n, CT_TILE);
+  int64_t* carry = (int64_t*)bg_alloc(c, 8ull * nb);
+  if (!carry) return BG_E_NOMEM;
+  hipLaunchKernelGGL(k_tile_max, dim3(nb), dim3(BG_NT), 0, c->stream, in.e, n, carry);
+  BG_HIP(c, hipGetLastError());
+  int rc = bg_scan_max_i64(c, carry, carry, nb, LLONG_MIN);
+  if (rc) return rc;
+  uint64_t total = 0;
+  rc = count_scan_write(
+      c, nb,
+      [&](uint64_t* cnt) {
+        hipLaunchKernelGGL(k_components<false>, dim3(nb), dim3(BG_NT), 0, c->stream, in.s, in.e, n,
+                           carry, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
+                           (int64_t*)nullptr);
+      },
+      [&](uint64_t* off, uint64_t tot) -> int {
+        int r = ivl_alloc(c, out, tot);
+        if (r) return r;
+        hipLaunchKernelGGL(k_components<true>, dim3(nb), dim3(BG_NT), 0, c->stream, in.s, in.e, n,
+                           carry, (uint64_t*)nullptr, off, out.s, out.e);
+        return 0;
+      },
+      &total, nullptr);
+  bg_release(c, carry);
+  return rc;
+}
+
+static int merge_sorted(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& z) {
+  int rc = ivl_alloc(c, z, x.n + y.n);
+  if (rc) return rc;
+  if (x.n + y.n == 0) return 0;
+  hipLaunchKernelGGL(k_merge_sorted, dim3(bg_blocks(x.n + y.n, MP_TILE)), dim3(BG_NT), 0,
+                     c->stream, x.s, x.e, x.n, y.s, y.e, y.n, z.s, z.e);
+  BG_HIP(c, hipGetLastError());
+  return 0;
+}
+
+static int intersect2(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out) {
+  const uint64_t nz = x.n + y.n;
+  const unsigned nb = bg_blocks(nz, MP_TILE);
+  uint64_t total = 0;
+  return count_scan_write(
+      c, nb,
+      [&](uint64_t* cnt) {
+        hipLaunchKernelGGL(k_intersect2<false>, dim3(nb), dim3(BG_NT), 0, c->stream, x.s, x.e, x.n,
+                           y.s, y.e, y.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
+                           (int64_t*)nullptr);
+      },
+      [&](uint64_t* off, uint64_t tot) -> int {
+        int r = ivl_alloc(c, out, tot);
+        if (r) return r;
+        if (nb)
+          hipLaunchKernelGGL(k_intersect2<true>, dim3(nb), dim3(BG_NT), 0, c->stream, x.s, x.e,
+                             x.n, y.s, y.e, y.n, (uint64_t*)nullptr, off, out.s, out.e);
+        return 0;
+      },
+      &total, nullptr);
+}
+
+static int difference2(bg_ctx* c, const Ivl& r, const Ivl& o, Ivl& out) {
+  const uint64_t nz = r.n + o.n;
+  const unsigned nb = bg_blocks(nz, MP_TILE);
+  uint64_t total = 0;
+  return count_scan_write(
+      c, nb,
+      [&](uint64_t* cnt) {
+        hipLaunchKernelGGL(k_difference<false>, dim3(nb), dim3(BG_NT), 0, c->stream, r.s, r.e, r.n,
+                           o.s, o.e, o.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
+                           (int64_t*)nullptr);
+      },
+      [&](uint64_t* off, uint64_t tot) -> int {
+        int rr = ivl_alloc(c, out, tot);
+        if (rr) return rr;
+        if (nb)
+          hipLaunchKernelGGL(k_difference<true>, dim3(nb), dim3(BG_NT), 0, c->stream, r.s, r.e,
+                             r.n, o.s, o.e, o.n, (uint64_t*)nullptr, off, out.s, out.e);
+        return 0;
+      },
+      &total, nullptr);
+}
+
+static Ivl table_ivl(bg_table* T) {
+  Ivl v;
+  v.s = T->ks;
+  v.e = T->ke;
+  v.n = T->n;
+  v.owned = false;
+  return v;
+}
+
+// components of the union of the given tables
+static int union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out) {
+  Ivl acc;
+  int rc = components(c, table_ivl(set->t[files[0]]), acc);
+  if (rc) return rc;
+  for (int k = 1; k < nf; ++k) {
+    Ivl ck, z, m;
+    if ((rc = components(c, table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = merge_sorted(c, acc, ck, z))) return rc;
+    ivl_free(c, acc);
+    ivl_free(c, ck);
+    if ((rc = components(c, z, m))) return rc;
+    ivl_free(c, z);
+    acc = m;
+  }
+  out = acc;
+  return 0;
+}
+
+static bg_result* new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
+  bg_result* r = new bg_result();
+  r->ctx = c;
+  r->set = set;
+  r->kind = RES_IVL;
+  r->n = v.n;
+  r->s = v.s;
+  r->e = v.e;
+  v.owned = false;
+  return r;
+}
+
+static int check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf) {
+  if (!c || !set || !files || nf < minf) return BG_E_ARG;
+  for (int k = 0; k < nf; ++k)
+    if (files[k] < 0 || files[k] >= (int)set->t.size()) return BG_E_ARG;
+  return 0;
+}
+
+extern "C" int bg_merge(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
+  int rc = check_files(c, set, files, nf, 1);
+  if (rc) return rc;
+  Ivl m;
+  if ((rc = union_components(c, set, files, nf, m))) return rc;
+  *out = new_ivl_result(c, set, m);
+  bg_mark(c, "merge");
+  return 0;
+}
+
+extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
+  int rc = check_files(c, set, files, nf, 2);
+  if (rc) return rc;
+  Ivl acc;
+  if ((rc = components(c, table_ivl(set->t[files[0]]), acc))) return rc;
+  for (int k = 1; k < nf; ++k) {
+    Ivl ck, p;
+    if ((rc = components(c, table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = intersect2(c, acc, ck, p))) return rc;
+    ivl_free(c, acc);
+    ivl_free(c, ck);
+    acc = p;
+  }
+  *out = new_ivl_result(c, set, acc);
+  bg_mark(c, "intersect");
+  return 0;
+}
+
+extern "C" int bg_difference(bg_ctx* c, bg_set* set, int ref, const int* others, int no,
+                             bg_result** out) {
+  int rc = check_files(c, set, others, no, 1);
+  if (rc) return rc;
+  if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
+  Ivl r, o, d;
+  if ((rc = components(c, table_ivl(set->t[ref]), r))) return rc;
+  if ((rc = union_components(c, set, others, no, o))) return rc;
+  if ((rc = difference2(c, r, o, d))) return rc;
+  ivl_free(c, r);
+  ivl_free(c, o);
+  *out = new_ivl_result(c, set, d);
+  bg_mark(c, "difference");
+  return 0;
+}
+
+extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others, int no,
+                             double thres, int use_pct, int invert, bg_result** out) {
+  int rc = check_files(c, set, others, no, 1);
+  if (rc) return rc;
+  if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
+  bg_table* R = set->t[ref];
+  Ivl o;
+  if ((rc = union_components(c, set, others, no, o))) return rc;
+  uint64_t* P = (uint64_t*)bg_alloc(c, 8 * (o.n + 1));
+  uint8_t* flag = (uint8_t*)bg_alloc(c, R->n ? R->n : 1);
+  if (!P || !flag) return BG_E_NOMEM;
+  if (o.n) {
+    hipLaunchKernelGGL(k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), 0, c->stream, o.s, o.e,
+                       o.n, P);
+    BG_HIP(c, hipGetLastError());
+  }
+  if ((rc = bg_scan_sum_u64(c, P, P, o.n, P + o.n))) return rc;
+  if (R->n) {
+    hipLaunchKernelGGL(k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT), 0, c->stream,
+                       R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
+    BG_HIP(c, hipGetLastError());
+  }
+  const unsigned nb = bg_blocks(R->n, CF_TILE);
+  uint64_t total = 0;
+  uint64_t* rows = nullptr;
+  rc = count_scan_write(
+      c, nb,
+      [&](uint64_t* cnt) {
+        hipLaunchKernelGGL(k_compact_flags<false>, dim3(nb), dim3(BG_NT), 0, c->stream, flag, R->n,
+                           cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
+      },
+      [&](uint64_t* off, uint64_t tot) -> int {
+        rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
+        if (!rows) return BG_E_NOMEM;
+        if (nb)
+          hipLaunchKernelGGL(k_compact_flags<true>, dim3(nb), dim3(BG_NT), 0, c->stream, flag,
+                             R->n, (uint64_t*)nullptr, off, rows);
+        return 0;
+      },
+      &total, nullptr);
+  if (rc) return rc;
+  bg_release(c, P);
+  bg_release(c, flag);
+  ivl_free(c, o);
+  bg_result* res = new bg_result();
+  res->ctx = c;
+  res->set = set;
+  res->kind = RES_ROWS;
+  res->n = total;
+  res->rows = rows;
+  res->tab = ref;
+  *out = res;
+  bg_mark(c, "element-of");
+  return 0;
+}

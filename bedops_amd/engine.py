@@ -1,0 +1,291 @@
+"""ctypes binding of libbedgpu (include/bedgpu.h) — the Python side of the C ABI.
+
+Mirrors the reference front-ends' operations (applications/bed/bedops/src/Input.hpp
+modes, applications/bed/bedmap/src/Input.hpp visitors). Errors raise BedgpuError with
+the library's message; nothing here computes intervals on the CPU.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+BED3, BED3_REST, BED5 = 0, 1, 2
+MAP_COUNT, MAP_MEAN = 1, 2
+
+ERRORS = {-1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
+          -7: "NOMEM", -8: "UNSUPPORTED", -9: "CHROM", -10: "IO"}
+
+# exported symbols of include/bedgpu.h (checked by tests/test_abi.py)
+SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_load",
+           "bg_set_rows", "bg_set_restrict_chrom", "bg_set_free", "bg_merge", "bg_intersect",
+           "bg_difference", "bg_element_of", "bg_map", "bg_result_rows", "bg_result_format",
+           "bg_result_text_device", "bg_result_copy_text", "bg_result_write", "bg_result_free",
+           "bg_stats", "bg_host_alloc", "bg_host_free"]
+
+
+def lib_path():
+    return os.path.join(HERE, "lib", "libbedgpu.so")
+
+
+class BedgpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"bedgpu {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class _Input(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("nbytes", ctypes.c_uint64),
+                ("on_device", ctypes.c_int), ("kind", ctypes.c_int)]
+
+
+class _MapOpts(ctypes.Structure):
+    _fields_ = [("overlap_bp", ctypes.c_uint64), ("n_ops", ctypes.c_int),
+                ("ops", ctypes.c_int * 16), ("precision", ctypes.c_int),
+                ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
+                ("delim", ctypes.c_char * 16)]
+
+
+_LIB = None
+
+
+def load_library():
+    """Load libbedgpu.so (fails loudly: there is no fallback path)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    p = lib_path()
+    if not os.path.exists(p):
+        raise BedgpuError(-6, f"{p} not built (run `make lib` or __graft_entry__.build())")
+    L = ctypes.CDLL(p)
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    L.bg_open.argtypes = [ctypes.POINTER(vp), i32]
+    L.bg_close.argtypes = [vp]
+    L.bg_close.restype = None
+    L.bg_last_error.argtypes = [vp]
+    L.bg_last_error.restype = ctypes.c_char_p
+    L.bg_sync.argtypes = [vp]
+    L.bg_stream.argtypes = [vp]
+    L.bg_stream.restype = vp
+    L.bg_load.argtypes = [vp, i32, ctypes.POINTER(_Input), ctypes.POINTER(vp)]
+    L.bg_set_rows.argtypes = [vp, i32, ctypes.POINTER(u64)]
+    L.bg_set_restrict_chrom.argtypes = [vp, vp, ctypes.c_char_p]
+    L.bg_set_free.argtypes = [vp]
+    L.bg_set_free.restype = None
+    L.bg_merge.argtypes = [vp, vp, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.bg_intersect.argtypes = [vp, vp, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.bg_difference.argtypes = [vp, vp, i32, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.bg_element_of.argtypes = [vp, vp, i32, ctypes.POINTER(i32), i32, ctypes.c_double, i32,
+                                i32, ctypes.POINTER(vp)]
+    L.bg_map.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_MapOpts), ctypes.POINTER(vp)]
+    L.bg_result_rows.argtypes = [vp, ctypes.POINTER(u64)]
+    L.bg_result_format.argtypes = [vp, vp, ctypes.POINTER(u64)]
+    L.bg_result_text_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    L.bg_result_copy_text.argtypes = [vp, vp, ctypes.c_char_p, u64]
+    L.bg_result_write.argtypes = [vp, vp, i32]
+    L.bg_result_free.argtypes = [vp]
+    L.bg_result_free.restype = None
+    L.bg_stats.argtypes = [vp, ctypes.c_char_p, u64]
+    L.bg_host_alloc.argtypes = [u64]
+    L.bg_host_alloc.restype = vp
+    L.bg_host_free.argtypes = [vp]
+    L.bg_host_free.restype = None
+    _LIB = L
+    return L
+
+
+def parse_overlap_spec(spec):
+    """-e/-n argument -> (threshold, use_percent) (Input.hpp:344-382)."""
+    if spec is None:
+        return 1.0, 1
+    s = str(spec)
+    if s.endswith("%"):
+        v = s[:-1].lstrip("-")
+        d = float(v) / 100.0
+        if d > 1:
+            raise BedgpuError(-6, "Expect percentage less than or equal to 100%")
+        return (1.0, 0) if d == 0 else (d, 1)
+    return float(int(s.lstrip("-"))), 0
+
+
+class Result:
+    def __init__(self, eng, handle):
+        self.eng, self.h = eng, handle
+
+    def rows(self):
+        n = ctypes.c_uint64()
+        self.eng._check(self.eng.L.bg_result_rows(self.h, ctypes.byref(n)))
+        return n.value
+
+    def format(self):
+        n = ctypes.c_uint64()
+        self.eng._check(self.eng.L.bg_result_format(self.eng.ctx, self.h, ctypes.byref(n)))
+        return n.value
+
+    def device_text(self):
+        """(device pointer, nbytes) of the rendered text (formats first)."""
+        self.format()
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        self.eng._check(self.eng.L.bg_result_text_device(self.h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+    def text(self):
+        n = self.format()
+        buf = ctypes.create_string_buffer(max(n, 1))
+        self.eng._check(self.eng.L.bg_result_copy_text(self.eng.ctx, self.h, buf, n))
+        return buf.raw[:n]
+
+    def free(self):
+        if self.h:
+            self.eng.L.bg_result_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class InputSet:
+    def __init__(self, eng, handle, keep):
+        self.eng, self.h, self._keep = eng, handle, keep
+
+    def rows(self, i):
+        n = ctypes.c_uint64()
+        self.eng._check(self.eng.L.bg_set_rows(self.h, i, ctypes.byref(n)))
+        return n.value
+
+    def restrict_chrom(self, chrom):
+        self.eng._check(self.eng.L.bg_set_restrict_chrom(self.eng.ctx, self.h, chrom.encode()))
+
+    def free(self):
+        if self.h:
+            self.eng.L.bg_set_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One libbedgpu context (one device, one HIP stream)."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        self.ctx = ctypes.c_void_p()
+        rc = self.L.bg_open(ctypes.byref(self.ctx), int(device))
+        if rc:
+            raise BedgpuError(rc, "bg_open failed (no usable GPU?)")
+
+    def _check(self, rc):
+        if rc:
+            raise BedgpuError(rc, self.L.bg_last_error(self.ctx).decode(errors="replace"))
+
+    def close(self):
+        if self.ctx:
+            self.L.bg_close(self.ctx)
+            self.ctx = None
+
+    def stream(self):
+        return self.L.bg_stream(self.ctx)
+
+    def sync(self):
+        self._check(self.L.bg_sync(self.ctx))
+
+    # -------------------------------------------------------------- loading
+    def load(self, inputs):
+        """inputs: list of (data, kind) where data is bytes (host) or (devptr, nbytes)."""
+        n = len(inputs)
+        arr = (_Input * n)()
+        keep = []
+        for i, (data, kind) in enumerate(inputs):
+            if isinstance(data, tuple):
+                arr[i].data, arr[i].nbytes, arr[i].on_device = data[0], data[1], 1
+            else:
+                b = ctypes.create_string_buffer(bytes(data), len(data) + 1)
+                keep.append(b)
+                arr[i].data = ctypes.cast(b, ctypes.c_void_p)
+                arr[i].nbytes, arr[i].on_device = len(data), 0
+            arr[i].kind = kind
+        h = ctypes.c_void_p()
+        self._check(self.L.bg_load(self.ctx, n, arr, ctypes.byref(h)))
+        return InputSet(self, h, keep)
+
+    # -------------------------------------------------------------- bedops
+    def op(self, mode, s, files, spec=None):
+        """Run one bedops operation on loaded set `s` over file indices `files`."""
+        h = ctypes.c_void_p()
+        idx = (ctypes.c_int * len(files))(*files)
+        L = self.L
+        if mode in ("-m", "--merge"):
+            self._check(L.bg_merge(self.ctx, s.h, idx, len(files), ctypes.byref(h)))
+        elif mode in ("-i", "--intersect"):
+            self._check(L.bg_intersect(self.ctx, s.h, idx, len(files), ctypes.byref(h)))
+        elif mode in ("-d", "--difference"):
+            rest = (ctypes.c_int * (len(files) - 1))(*files[1:])
+            self._check(L.bg_difference(self.ctx, s.h, files[0], rest, len(files) - 1,
+                                        ctypes.byref(h)))
+        elif mode in ("-e", "--element-of", "-n", "--not-element-of"):
+            thr, pct = parse_overlap_spec(spec)
+            inv = 1 if mode in ("-n", "--not-element-of") else 0
+            rest = (ctypes.c_int * (len(files) - 1))(*files[1:])
+            self._check(L.bg_element_of(self.ctx, s.h, files[0], rest, len(files) - 1, thr, pct,
+                                        inv, ctypes.byref(h)))
+        else:
+            raise BedgpuError(-8, f"operation {mode} is not on the GPU path")
+        return Result(self, h)
+
+    def bedops(self, mode, texts, spec=None, chrom=None):
+        """bedops <mode> [spec] file1 file2 ... on in-memory BED texts -> output bytes."""
+        keep_rest = mode in ("-e", "--element-of", "-n", "--not-element-of")
+        s = self.load([(t, BED3_REST if (keep_rest and i == 0) else BED3)
+                       for i, t in enumerate(texts)])
+        try:
+            if chrom:
+                s.restrict_chrom(chrom)
+            r = self.op(mode, s, list(range(len(texts))), spec)
+            try:
+                return r.text()
+            finally:
+                r.free()
+        finally:
+            s.free()
+
+    # -------------------------------------------------------------- bedmap
+    def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
+               skip_unmapped=False, chrom=None):
+        names = {"count": MAP_COUNT, "mean": MAP_MEAN}
+        need5 = "mean" in ops
+        s = self.load([(ref_text, BED3), (map_text if map_text is not None else ref_text,
+                                          BED5 if need5 else BED3)])
+        try:
+            if chrom:
+                s.restrict_chrom(chrom)
+            o = _MapOpts()
+            o.overlap_bp = overlap_bp
+            o.n_ops = len(ops)
+            for k, op in enumerate(ops):
+                o.ops[k] = names[op]
+            o.precision = precision
+            o.scientific = 0
+            o.skip_unmapped = 1 if skip_unmapped else 0
+            o.delim = delim.encode()
+            h = ctypes.c_void_p()
+            self._check(self.L.bg_map(self.ctx, s.h, 0, 1, ctypes.byref(o), ctypes.byref(h)))
+            r = Result(self, h)
+            try:
+                return r.text()
+            finally:
+                r.free()
+        finally:
+            s.free()
+
+    def stats(self):
+        buf = ctypes.create_string_buffer(8192)
+        self._check(self.L.bg_stats(self.ctx, buf, 8192))
+        return buf.value.decode()

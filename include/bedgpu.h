@@ -1,0 +1,121 @@
+/*
+ * bedgpu.h — C ABI of libbedgpu, the MI355X (gfx950) engine behind the drop-in
+ * `bedops` / `bedmap` / `closest-features` front-ends of bedops_amd.
+ *
+ * BEDOPS has no library API: its only boundary is the process (argv, BED text on
+ * stdin/files, BED text on stdout). This ABI is the seam that
+ * replaces the reference's internal sweep entry points. Each entry point below
+ * names the reference function it replaces:
+ *
+ *   bg_load .............. Bed readers + per-line parse
+ *                          (interfaces/general-headers/data/bed/AllocateIterator_BED_starch.hpp:47-230,
+ *                           Bed.hpp:244-255 BED3, :277-383 BED3+rest, :829-860 BED5)
+ *   bg_merge ............. doMerge / nextMergeAllLines  (applications/bed/bedops/src/Bedops.cpp:593-606, :1186-1243)
+ *   bg_intersect ......... doIntersection / nextIntersectLine (Bedops.cpp:575-587, :1105-1181)
+ *   bg_difference ........ doDifference / nextDifferenceLine (Bedops.cpp:500-524, :950-1018)
+ *   bg_element_of ........ doElementOf / nextElementOfLine (Bedops.cpp:538-566, :1023-1100)
+ *   bg_map ............... WindowSweep::sweep overload 2 + MultiVisitor{Count,Average}
+ *                          (interfaces/src/algorithm/sweep/WindowSweepImpl.cpp:168-256,
+ *                           algorithm/visitors/other/MultiVisitor.hpp:45-129)
+ *   bg_closest ........... FeatDist::findDistances + PrintShortest
+ *                          (applications/bed/closestfeats/src/ClosestFeature.cpp:260-413, Printers.hpp:104-205)
+ *   bg_result_format /
+ *   bg_result_write ...... record() -> printf("%s\t%lu\t%lu\n") (Bedops.cpp:148-152, Bed.hpp:228-232,321-325),
+ *                          visitor printing ("%d", "%.6lf", "NAN": Formats.hpp:31-50, NaN.cpp:26)
+ *
+ * Conventions: plain pointers and sizes only. Every call returns 0 on success or a
+ * negative BG_E* code, never aborts; bg_last_error() gives the message. One context
+ * per device, not thread-safe; all device work is ordered on the context's stream.
+ * Handles are owned by the caller and released with the matching bg_*_free().
+ */
+#ifndef BEDGPU_H
+#define BEDGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BG_OK 0
+#define BG_E_HIP (-1)         /* HIP runtime failure */
+#define BG_E_PARSE (-2)       /* malformed BED line */
+#define BG_E_UNSORTED (-3)    /* input not sorted per sort-bed (strcmp chrom, start) */
+#define BG_E_RANGE (-4)       /* coordinate > 999999999999 or end < start */
+#define BG_E_BLANK (-5)       /* blank line inside the data */
+#define BG_E_ARG (-6)         /* bad argument */
+#define BG_E_NOMEM (-7)       /* device or host allocation failed */
+#define BG_E_UNSUPPORTED (-8) /* input/option outside the GPU path (message says which) */
+#define BG_E_CHROM (-9)       /* chromosome name longer than 127 bytes */
+#define BG_E_IO (-10)         /* read/write failure */
+
+/* kinds of input, decided by the operation (Bedops.cpp:402-429, Bedmap.cpp:643-654) */
+#define BG_BED3 0      /* chrom start end; remainder ignored            (Bed::B3NoRest) */
+#define BG_BED3_REST 1 /* remainder after `end` kept verbatim for output (Bed::B3Rest)  */
+#define BG_BED5 2      /* chrom start end id score; score parsed         (Bed::B5Rest)  */
+
+typedef struct bg_ctx bg_ctx;
+typedef struct bg_set bg_set;       /* N parsed inputs sharing one chromosome dictionary */
+typedef struct bg_result bg_result; /* an operation's output, resident on the device   */
+
+typedef struct bg_input {
+  const void* data;   /* BED text */
+  uint64_t nbytes;
+  int on_device;      /* 0: host memory (copied to HBM); 1: device pointer (16-B aligned) */
+  int kind;           /* BG_BED3 / BG_BED3_REST / BG_BED5 */
+} bg_input;
+
+typedef struct bg_map_opts {
+  uint64_t overlap_bp; /* --bp-ovr (default 1)                                  */
+  int n_ops;           /* number of entries in ops[]                            */
+  int ops[16];         /* BG_MAP_COUNT / BG_MAP_MEAN, in command-line order     */
+  int precision;       /* --prec (default 6)                                    */
+  int scientific;      /* --sci                                                 */
+  int skip_unmapped;   /* --skip-unmapped                                       */
+  char delim[16];      /* --delim (default "|")                                 */
+} bg_map_opts;
+#define BG_MAP_COUNT 1
+#define BG_MAP_MEAN 2
+
+/* context */
+int bg_open(bg_ctx** ctx, int device);
+void bg_close(bg_ctx* ctx);
+const char* bg_last_error(const bg_ctx* ctx);
+int bg_sync(bg_ctx* ctx);
+void* bg_stream(bg_ctx* ctx); /* the hipStream_t all work of this context runs on */
+
+/* loading: parse N BED texts into device-resident keyed SoA columns */
+int bg_load(bg_ctx* ctx, int n, const bg_input* inputs, bg_set** out);
+int bg_set_rows(const bg_set* set, int i, uint64_t* rows);
+int bg_set_restrict_chrom(bg_ctx* ctx, bg_set* set, const char* chrom); /* --chrom */
+void bg_set_free(bg_set* set);
+
+/* operations (file indices refer to the set) */
+int bg_merge(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
+int bg_intersect(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
+int bg_difference(bg_ctx* ctx, bg_set* set, int ref, const int* others, int nothers,
+                  bg_result** out);
+int bg_element_of(bg_ctx* ctx, bg_set* set, int ref, const int* others, int nothers,
+                  double threshold, int use_percent, int invert, bg_result** out);
+int bg_map(bg_ctx* ctx, bg_set* set, int ref, int map, const bg_map_opts* opts,
+           bg_result** out);
+
+/* results */
+int bg_result_rows(const bg_result* res, uint64_t* rows);
+int bg_result_format(bg_ctx* ctx, bg_result* res, uint64_t* nbytes); /* text in HBM */
+int bg_result_text_device(const bg_result* res, const char** dptr, uint64_t* nbytes);
+int bg_result_copy_text(bg_ctx* ctx, bg_result* res, char* host, uint64_t cap);
+int bg_result_write(bg_ctx* ctx, bg_result* res, int fd); /* format + stream to fd */
+void bg_result_free(bg_result* res);
+
+/* per-stage device timings of the last call sequence (ms), for BEDGPU_STATS */
+int bg_stats(const bg_ctx* ctx, char* buf, uint64_t cap);
+
+/* pinned host buffers for input text (faster H2D); NULL on failure */
+void* bg_host_alloc(uint64_t bytes);
+void bg_host_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

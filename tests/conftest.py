@@ -1,0 +1,40 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP library)")
+    config.addinivalue_line("markers", "slow: large-input parity (minutes)")
+
+
+def _make(*targets):
+    subprocess.run(["make", "-s", "-j8", *targets], cwd=ROOT, check=True,
+                   stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture(scope="session")
+def oracle_bin():
+    _make("oracle")
+    return {"bedops": os.path.join(ROOT, "oracle", "build", "bedops_oracle"),
+            "bedmap": os.path.join(ROOT, "oracle", "build", "bedmap_oracle")}
+
+
+@pytest.fixture(scope="session")
+def gpu_bin():
+    """The drop-in front-ends (C, linked to libbedgpu.so)."""
+    _make("lib", "cli")
+    return {"bedops": os.path.join(ROOT, "bedops_amd", "bin", "bedops"),
+            "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap")}
+
+
+@pytest.fixture(scope="session")
+def bedgen():
+    _make("tools")
+    return os.path.join(ROOT, "tools", "build", "bedgen")

@@ -1,0 +1,190 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's own known-answer tests. Bit-exact byte comparison everywhere."""
+import hashlib
+import os
+import random
+import subprocess
+import tempfile
+
+import pytest
+
+import randbed
+import testplan_runner
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from bedops_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def run_oracle(binary, args, texts, tmpdir):
+    paths = []
+    for i, t in enumerate(texts):
+        p = os.path.join(tmpdir, f"in{i}.bed")
+        with open(p, "wb") as f:
+            f.write(t if isinstance(t, bytes) else t.encode())
+        paths.append(p)
+    r = subprocess.run([binary] + args + paths, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       check=True)
+    return r.stdout
+
+
+# ---------------------------------------------------------------------------------
+# reference KATs (applications/bed/bedops/test/TestPlan.xml) through the C front-end
+# ---------------------------------------------------------------------------------
+def test_testplan_kats_gpu_cli(gpu_bin, tmp_path):
+    res = testplan_runner.run_testplan([gpu_bin["bedops"]], str(tmp_path),
+                                       modes={"m", "i", "d", "e", "n"})
+    bad = [r for r in res if not r[2]]
+    assert len(res) == 28
+    assert not bad, bad
+
+
+# ---------------------------------------------------------------------------------
+# randomized differential tests against the oracle
+# ---------------------------------------------------------------------------------
+CASES = [("-m", 1), ("-m", 2), ("-m", 3), ("-i", 2), ("-i", 3), ("-d", 2), ("-d", 3),
+         ("-e", 2), ("-n", 2), ("-e", 3)]
+SPECS = {"-e": [None, "1", "3", "50%", "100%", "0%"], "-n": [None, "1", "25%"]}
+
+
+@pytest.mark.parametrize("zero_frac", [0.0, 0.06])
+@pytest.mark.parametrize("mode,nfiles", CASES)
+def test_random_bedops_vs_oracle(eng, oracle_bin, mode, nfiles, zero_frac):
+    rng = random.Random(hash((mode, nfiles, zero_frac)) & 0xffffffff)
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(12):
+            n = rng.choice([0, 1, 2, 5, 30, 200, 1500])
+            texts = []
+            for f in range(nfiles):
+                rs = randbed.rows(rng, n if f == 0 else rng.choice([0, 3, 40, 300, 1200]),
+                                  span=rng.choice([50, 400, 3000]), maxlen=rng.choice([5, 40, 150]),
+                                  zero_frac=zero_frac)
+                rest = "cols" if (f == 0 and mode in ("-e", "-n")) else None
+                texts.append(randbed.text(rs, rest=rest, rng=rng).encode())
+            for spec in SPECS.get(mode, [None]):
+                args = [mode] + ([spec] if spec else [])
+                want = run_oracle(oracle_bin["bedops"], args, texts, td)
+                got = eng.bedops(mode, texts, spec=spec)
+                assert got == want, (mode, spec, trial, n)
+
+
+@pytest.mark.parametrize("ovr,prec,skip", [(1, 6, False), (5, 6, False), (1, 3, True), (2, 0, False)])
+def test_random_bedmap_vs_oracle(eng, oracle_bin, ovr, prec, skip):
+    rng = random.Random(ovr * 100 + prec)
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(10):
+            ref = randbed.rows(rng, rng.choice([0, 1, 20, 400, 2000]), span=rng.choice([300, 3000]),
+                               maxlen=rng.choice([10, 80, 300]))
+            mp = randbed.rows(rng, rng.choice([0, 1, 50, 800, 4000]), span=rng.choice([300, 3000]),
+                              maxlen=rng.choice([10, 80, 300]))
+            rt = randbed.text(ref).encode()
+            mt = randbed.text(mp, rest="bed5", rng=rng).encode()
+            for ops in (["count"], ["mean"], ["count", "mean"], ["mean", "count"]):
+                args = [f"--{o}" for o in ops] + ["--bp-ovr", str(ovr), "--prec", str(prec)]
+                if skip:
+                    args.append("--skip-unmapped")
+                want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                got = eng.bedmap(ops, rt, mt, overlap_bp=ovr, precision=prec, skip_unmapped=skip)
+                assert got == want, (ops, trial)
+
+
+# ---------------------------------------------------------------------------------
+# I/O edge cases (Appendix B of SURVEY.md)
+# ---------------------------------------------------------------------------------
+EDGE = [
+    b"",                                                  # empty file
+    b"chr1\t5\t10\n",                                     # single row
+    b"chr1\t5\t10\nchr1\t20\t30",                         # unterminated last line: dropped
+    b"chr1 5 10\nchr1  7   12\n",                         # spaces as separators
+    b"chr1\t5\t10\r\nchr1\t11\t12\r\n",                   # CRLF
+    b"chr1\t005\t010\tx\ty\n",                            # leading zeros, extra columns
+    b"chr1\t5\t5\nchr1\t5\t10\n",                         # zero-length then real row
+    b"chr1\t10\t20\nchr1\t20\t30\n",                      # touching rows
+    b"  chr1\t1\t2\n",                                    # leading whitespace
+    b"chrVeryLongName_" + b"x" * 100 + b"\t1\t9\n",       # long chrom name
+]
+
+
+@pytest.mark.parametrize("k", range(len(EDGE)))
+@pytest.mark.parametrize("mode", ["-m", "-i", "-e", "-d"])
+def test_io_edge_cases(eng, oracle_bin, k, mode):
+    a = EDGE[k]
+    b = b"chr1\t4\t8\nchr1\t9\t25\nchr2\t0\t5\n"
+    texts = [a] if mode == "-m" else [a, b]
+    spec = "1" if mode == "-e" else None
+    with tempfile.TemporaryDirectory() as td:
+        want = run_oracle(oracle_bin["bedops"], [mode] + ([spec] if spec else []), texts, td)
+    assert eng.bedops(mode, texts, spec=spec) == want
+
+
+def test_unsorted_input_is_an_error(eng):
+    from bedops_amd import BedgpuError
+    for bad in (b"chr1\t50\t60\nchr1\t5\t10\n", b"chr2\t1\t2\nchr1\t1\t2\n",
+                b"chr1\t1\t2\nchr2\t1\t2\nchr1\t3\t4\n"):
+        with pytest.raises(BedgpuError) as ei:
+            eng.bedops("-m", [bad])
+        assert ei.value.code == -3
+
+
+def test_malformed_line_is_an_error(eng):
+    from bedops_amd import BedgpuError
+    for bad in (b"chr1\t5\n", b"chr1\tx\t10\n", b"chr1\t5\t2\n", b"chr1\t1\t2\n\nchr1\t3\t4\n"):
+        with pytest.raises(BedgpuError):
+            eng.bedops("-m", [bad])
+
+
+def test_chrom_restriction(eng, oracle_bin):
+    rng = random.Random(7)
+    a = randbed.text(randbed.rows(rng, 500)).encode()
+    b = randbed.text(randbed.rows(rng, 500)).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for ch in ("chr10", "chrX", "chrNone"):
+            want = run_oracle(oracle_bin["bedops"], ["--chrom", ch, "-i"], [a, b], td)
+            assert eng.bedops("-i", [a, b], chrom=ch) == want
+
+
+# ---------------------------------------------------------------------------------
+# full-size pinned hashes (produced by the reference binaries)
+# ---------------------------------------------------------------------------------
+def _gen(bedgen, n, seed, *flags):
+    return subprocess.run([bedgen, str(n), str(seed), *flags], stdout=subprocess.PIPE,
+                          check=True).stdout
+
+
+def _h(b):
+    return hashlib.sha256(b).hexdigest()[:16]
+
+
+def test_merge_m1M_reference_hash(eng, bedgen):
+    m = _gen(bedgen, 1000000, 1, "--chr1")
+    out = eng.bedops("-m", [m])
+    assert out.count(b"\n") == 847748 and len(out) == 20437351
+    assert _h(out) == "5356e0cdf191310c"
+
+
+@pytest.mark.slow
+def test_bedmap_R5M_M50M_reference_hash(eng, bedgen):
+    r = _gen(bedgen, 5000000, 7)
+    m = _gen(bedgen, 50000000, 8, "--bed5")
+    out = eng.bedmap(["count", "mean"], r, m)
+    assert out.count(b"\n") == 4999998 and len(out) == 54515904
+    assert _h(out) == "899ec7973e166e2d"
+
+
+@pytest.mark.slow
+def test_intersect_and_element_of_100M_reference_hash(eng, bedgen):
+    a = _gen(bedgen, 100000000, 42)
+    b = _gen(bedgen, 100000000, 43)
+    out = eng.bedops("-i", [a, b])
+    assert out.count(b"\n") == 38507974 and len(out) == 917848625
+    assert _h(out) == "2495074965b49d74"
+    del out
+    out = eng.bedops("-e", [a, b], spec="1")
+    assert out.count(b"\n") == 90223158 and len(out) == 2150489515
+    assert _h(out) == "98a8a1c8a72bf6f5"
