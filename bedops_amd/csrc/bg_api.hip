@@ -78,6 +78,74 @@ void bg_mark(bg_ctx* c, const char* name) {
   c->marks.emplace_back(name, ev);
 }
 
+bool bg_prof_on(bg_ctx* c, const char* name) {
+  if (c->prof_filter.empty()) return false;
+  return c->prof_filter == "*" || c->prof_filter == name;
+}
+
+hipEvent_t bg_prof_event(bg_ctx* c) {
+  if (!c->prof_events.empty()) {
+    hipEvent_t e = c->prof_events.back();
+    c->prof_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void bg_prof_push(bg_ctx* c, const char* name, hipEvent_t a, hipEvent_t b) {
+  c->prof_pending.push_back({name, a, b});
+  if (c->prof_pending.size() > 4096) {  // bound the number of live events
+    (void)hipStreamSynchronize(c->stream);
+    char tmp[8];
+    bg_prof_read(c, tmp, 0);
+  }
+}
+
+static void prof_drain(bg_ctx* c) {
+  if (c->prof_pending.empty()) return;
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& p : c->prof_pending) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    size_t k = 0;
+    while (k < c->prof.size() && c->prof[k].first != p.name) ++k;
+    if (k == c->prof.size()) c->prof.push_back({p.name, bg_ctx::KStat()});
+    c->prof[k].second.ms += ms;
+    c->prof[k].second.calls += 1;
+    c->prof_events.push_back(p.a);
+    c->prof_events.push_back(p.b);
+  }
+  c->prof_pending.clear();
+}
+
+// filter: NULL or "" disables, "*" profiles every kernel, else one kernel name.
+// Enabling clears the accumulated statistics.
+extern "C" int bg_prof_enable(bg_ctx* c, const char* filter) {
+  if (!c) return BG_E_ARG;
+  prof_drain(c);
+  c->prof.clear();
+  c->prof_filter = filter ? filter : "";
+  return 0;
+}
+
+// "name calls total_ms" lines, one per kernel, in first-launch order
+extern "C" int bg_prof_read(bg_ctx* c, char* buf, uint64_t cap) {
+  if (!c) return BG_E_ARG;
+  prof_drain(c);
+  if (!buf || cap == 0) return 0;
+  std::string s;
+  for (auto& kv : c->prof) {
+    char line[256];
+    snprintf(line, sizeof(line), "%s %llu %.6f\n", kv.first.c_str(),
+             (unsigned long long)kv.second.calls, kv.second.ms);
+    s += line;
+  }
+  snprintf(buf, cap, "%s", s.c_str());
+  return 0;
+}
+
 extern "C" int bg_open(bg_ctx** out, int device) {
   if (!out) return BG_E_ARG;
   *out = nullptr;
@@ -108,6 +176,8 @@ extern "C" void bg_close(bg_ctx* c) {
   for (auto& kv : g_live[c].m) hipFree(kv.first);
   g_live.erase(c);
   for (auto& m : c->marks) hipEventDestroy(m.second);
+  for (auto& p : c->prof_pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
+  for (auto e : c->prof_events) hipEventDestroy(e);
   hipFree(c->dstat);
   hipHostFree(c->hstat);
   hipStreamDestroy(c->stream);
@@ -261,5 +331,6 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->cnt);
   bg_release(c, r->isum);
   bg_release(c, r->text);
+  bg_release(c, r->toff);
   delete r;
 }

@@ -247,6 +247,8 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.rest_off = T->rest_off;
     A.rest_len = T->rest_len;
   } else {
+    A.s = s->t[r->tab]->ks;  // reference rows (chromosome spans)
+    A.e = s->t[r->tab]->ke;
     A.cnt = r->cnt;
     A.isum = r->isum;
     A.nops = r->mopts.n_ops;
@@ -274,7 +276,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!tb || !d_tot) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   if (nb) {
-    hipLaunchKernelGGL(k_fmt_count, dim3(nb), dim3(BG_NT), 0, c->stream, A, tb, c->dstat);
+    BG_LAUNCH(c, "k_fmt_count", k_fmt_count, dim3(nb), dim3(BG_NT), A, tb, c->dstat);
     BG_HIP(c, hipGetLastError());
   }
   int rc = bg_scan_sum_u64(c, tb, tb, nb, d_tot);
@@ -287,14 +289,77 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   r->text = (char*)bg_alloc(c, total + 16);
   if (!r->text) return BG_E_NOMEM;
   if (nb) {
-    hipLaunchKernelGGL(k_fmt_write, dim3(nb), dim3(BG_NT), 0, c->stream, A, tb, r->text);
+    BG_LAUNCH(c, "k_fmt_write", k_fmt_write, dim3(nb), dim3(BG_NT), A, tb, r->text);
     BG_HIP(c, hipGetLastError());
   }
-  bg_release(c, tb);
+  r->toff = tb;
   bg_release(c, d_tot);
   r->nbytes = total;
   r->formatted = true;
   if (nbytes) *nbytes = total;
   bg_mark(c, "format");
+  return 0;
+}
+
+// Byte offset of the first output line of every chromosome g of the set's dictionary;
+// out[nchroms] = total bytes, so chromosome g's lines are text[out[g], out[g+1]).
+// Used to reassemble per-GPU shards in strcmp chromosome order (multi-GPU path).
+__global__ void k_chrom_spans(FmtArgs A, const uint64_t* __restrict__ toff, uint32_t nchroms,
+                              uint64_t nbytes, uint64_t* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > nchroms) return;
+  if (g == nchroms) { out[g] = nbytes; return; }
+  const int64_t key = (int64_t)g << BG_KEY_SHIFT;
+  uint64_t lo = 0, hi = A.n;  // first output row whose chromosome is >= g
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint64_t r = A.rows ? A.rows[mid] : mid;
+    if (A.s[r] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo >= A.n) { out[g] = nbytes; return; }
+  const uint64_t t = lo / FT_TILE;
+  CountOut co;
+  for (uint64_t j = t * FT_TILE; j < lo; ++j) render(A, j, co);
+  out[g] = toff[t] + co.n;
+}
+
+extern "C" int bg_result_chrom_spans(bg_ctx* c, bg_result* r, uint64_t* offsets, uint32_t cap) {
+  if (!c || !r || !offsets) return BG_E_ARG;
+  const uint32_t nc = (uint32_t)r->set->names.size();
+  if (cap < nc + 1) return bg_fail(c, BG_E_ARG, "offsets buffer needs nchroms+1 entries");
+  int rc = bg_result_format(c, r, nullptr);
+  if (rc) return rc;
+  FmtArgs A;
+  fill_args(r, A);
+  uint64_t* d = (uint64_t*)bg_alloc(c, 8ull * (nc + 1));
+  if (!d) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_chrom_spans", k_chrom_spans, dim3(bg_blocks(nc + 1, 64)), dim3(64), A, r->toff,
+            nc, r->nbytes, d);
+  BG_HIP(c, hipGetLastError());
+  BG_HIP(c, hipMemcpyAsync(offsets, d, 8ull * (nc + 1), hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  bg_release(c, d);
+  return 0;
+}
+
+extern "C" int bg_set_chroms(const bg_set* s, uint32_t* n) {
+  if (!s || !n) return BG_E_ARG;
+  *n = (uint32_t)s->names.size();
+  return 0;
+}
+
+extern "C" const char* bg_set_chrom_name(const bg_set* s, uint32_t g) {
+  if (!s || g >= s->names.size()) return nullptr;
+  return s->names[g].c_str();
+}
+
+extern "C" int bg_result_copy_text_device(bg_ctx* c, bg_result* r, void* dst, uint64_t cap) {
+  uint64_t n = 0;
+  int rc = bg_result_format(c, r, &n);
+  if (rc) return rc;
+  if (cap < n) return bg_fail(c, BG_E_ARG, "device buffer too small");
+  if (n) BG_HIP(c, hipMemcpyAsync(dst, r->text, n, hipMemcpyDeviceToDevice, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
   return 0;
 }

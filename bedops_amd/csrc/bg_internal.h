@@ -57,6 +57,13 @@ struct bg_ctx {
   bool stats = false;
   std::vector<std::pair<std::string, hipEvent_t>> marks;
   std::string stats_text;
+  // kernel profiling
+  std::string prof_filter;  // "" off, "*" all, else exact kernel name
+  struct Pend { std::string name; hipEvent_t a, b; };
+  std::vector<Pend> prof_pending;
+  std::vector<hipEvent_t> prof_events;  // recycled
+  struct KStat { double ms = 0; uint64_t calls = 0; };
+  std::vector<std::pair<std::string, KStat>> prof;
 };
 
 struct bg_table {
@@ -109,6 +116,7 @@ struct bg_result {
   char* text = nullptr;
   uint64_t nbytes = 0;
   bool formatted = false;
+  uint64_t* toff = nullptr;  // byte offset of each 1024-row format tile (kept for spans)
 };
 
 // allocator / error helpers (bg_api.cpp)
@@ -117,6 +125,22 @@ void bg_release(bg_ctx* c, void* p);
 int bg_fail(bg_ctx* c, int code, const std::string& msg);
 int bg_hip_fail(bg_ctx* c, hipError_t e, const char* what);
 void bg_mark(bg_ctx* c, const char* name);
+
+// kernel profiling (bg_prof_enable): HIP events on the context stream around launches
+// whose name matches the filter ("*" = all)
+bool bg_prof_on(bg_ctx* c, const char* name);
+void bg_prof_push(bg_ctx* c, const char* name, hipEvent_t a, hipEvent_t b);
+hipEvent_t bg_prof_event(bg_ctx* c);
+
+#define BG_LAUNCH(c, name, kern, grid, block, ...)                           \
+  do {                                                                       \
+    const bool _p = bg_prof_on((c), (name));                                 \
+    hipEvent_t _a = nullptr, _b = nullptr;                                   \
+    if (_p) { _a = bg_prof_event(c); hipEventRecord(_a, (c)->stream); }      \
+    hipLaunchKernelGGL(kern, grid, block, 0, (c)->stream, __VA_ARGS__);      \
+    if (_p) { _b = bg_prof_event(c); hipEventRecord(_b, (c)->stream);        \
+              bg_prof_push((c), (name), _a, _b); }                           \
+  } while (0)
 
 #define BG_HIP(c, expr)                                  \
   do {                                                   \

@@ -378,14 +378,25 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
   T->nbytes = in.nbytes;
   const uint64_t nb = in.nbytes;
   const unsigned ntiles = nb ? bg_blocks(nb, TXT_TILE) : 0;
-  if (ntiles == 0) { T->n = 0; return 0; }
+  if (ntiles == 0) {  // empty input: valid, zero rows; keep every column non-null
+    T->n = 0;
+    T->ks = (int64_t*)bg_alloc(c, 8);
+    T->ke = (int64_t*)bg_alloc(c, 8);
+    if (in.kind == BG_BED3_REST) {
+      T->rest_off = (uint64_t*)bg_alloc(c, 8);
+      T->rest_len = (uint32_t*)bg_alloc(c, 4);
+    }
+    if (in.kind == BG_BED5) T->score = (double*)bg_alloc(c, 8);
+    T->run_row0.assign(1, 0);
+    return 0;
+  }
   uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * ntiles);
   uint64_t* row0 = (uint64_t*)bg_alloc(c, 8ull * ntiles);
   int64_t* lastnl = (int64_t*)bg_alloc(c, 8ull * ntiles);
   int64_t* prevnl = (int64_t*)bg_alloc(c, 8ull * ntiles);
   uint64_t* d_rows = (uint64_t*)bg_alloc(c, 8);
   if (!cnt || !row0 || !lastnl || !prevnl || !d_rows) return BG_E_NOMEM;
-  hipLaunchKernelGGL(k_nl_count, dim3(ntiles), dim3(BG_NT), 0, c->stream, txt, nb, cnt, lastnl);
+  BG_LAUNCH(c, "k_nl_count", k_nl_count, dim3(ntiles), dim3(BG_NT), txt, nb, cnt, lastnl);
   BG_HIP(c, hipGetLastError());
   int rc = bg_scan_sum_u64(c, cnt, row0, ntiles, d_rows);
   if (rc) return rc;
@@ -414,7 +425,7 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   if (rows) {
-    hipLaunchKernelGGL(k_parse, dim3(ntiles), dim3(BG_NT), 0, c->stream, txt, nb, cnt, row0,
+    BG_LAUNCH(c, "k_parse", k_parse, dim3(ntiles), dim3(BG_NT), txt, nb, cnt, row0,
                        prevnl, in.kind, (uint64_t*)T->ks, (uint64_t*)T->ke, T->rest_off,
                        T->rest_len, T->score, run_row, run_tok, run_len, c->dstat);
     BG_HIP(c, hipGetLastError());
@@ -432,7 +443,7 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
   if (nr) {
     char* d_names = (char*)bg_alloc(c, nr * 128);
     if (!d_names) return BG_E_NOMEM;
-    hipLaunchKernelGGL(k_gather_tokens, dim3(bg_blocks(nr, 256)), dim3(256), 0, c->stream, txt,
+    BG_LAUNCH(c, "k_gather_tokens", k_gather_tokens, dim3(bg_blocks(nr, 256)), dim3(256), txt,
                        run_tok, run_len, nr, d_names);
     BG_HIP(c, hipGetLastError());
     BG_HIP(c, hipMemcpyAsync(rr.data(), run_row, 8 * nr, hipMemcpyDeviceToHost, c->stream));
@@ -517,7 +528,7 @@ int bg_key_tables(bg_ctx* c, bg_set* s) {
     // copies are from pageable vectors: make them synchronous w.r.t. the host below
     BG_HIP(c, hipMemcpyAsync(d_r0, T->run_row0.data(), 8ull * (nr + 1), hipMemcpyHostToDevice, c->stream));
     BG_HIP(c, hipMemcpyAsync(d_g, g.data(), 4ull * nr, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_key, dim3(bg_blocks(T->n, BG_NT)), dim3(BG_NT), 0, c->stream, T->ks, T->ke,
+    BG_LAUNCH(c, "k_key", k_key, dim3(bg_blocks(T->n, BG_NT)), dim3(BG_NT), T->ks, T->ke,
                        T->n, d_r0, d_g, nr, c->dstat);
     BG_HIP(c, hipGetLastError());
     BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));

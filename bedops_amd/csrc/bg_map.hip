@@ -81,7 +81,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean yet");
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
   if (M->n)
-    hipLaunchKernelGGL(k_max_len, dim3(bg_blocks(M->n, BG_NT * 16)), dim3(BG_NT), 0, c->stream,
+    BG_LAUNCH(c, "k_max_len", k_max_len, dim3(bg_blocks(M->n, BG_NT * 16)), dim3(BG_NT),
                        M->ks, M->ke, M->n, c->dstat);
   BG_HIP(c, hipGetLastError());
   int32_t* cnt = (int32_t*)bg_alloc(c, 4 * (R->n ? R->n : 1));
@@ -91,7 +91,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   BG_HIP(c, hipStreamSynchronize(c->stream));
   const int64_t L = c->hstat->maxlen > 0 ? c->hstat->maxlen : 1;
   if (R->n)
-    hipLaunchKernelGGL(k_map_count_sum, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT), 0, c->stream,
+    BG_LAUNCH(c, "k_map_count_sum", k_map_count_sum, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
                        R->ks, R->ke, R->n, M->ks, M->ke, need_score ? M->score : nullptr, M->n, L,
                        (int64_t)opts->overlap_bp, cnt, isum, c->dstat);
   BG_HIP(c, hipGetLastError());

@@ -55,19 +55,19 @@ static int scan_impl(bg_ctx* c, const T* in, T* out, uint64_t n, Op op, T identi
   }
   unsigned nb = bg_blocks(n, SCAN_TILE);
   if (nb == 1) {
-    hipLaunchKernelGGL((k_tile_scan<T, Op>), dim3(1), dim3(BG_NT), 0, c->stream, in, out, n,
+    BG_LAUNCH(c, "k_tile_scan", (k_tile_scan<T, Op>), dim3(1), dim3(BG_NT), in, out, n,
                        (const T*)nullptr, op, identity, d_total);
     BG_HIP(c, hipGetLastError());
     return 0;
   }
   T* part = (T*)bg_alloc(c, sizeof(T) * nb);
   if (!part) return BG_E_NOMEM;
-  hipLaunchKernelGGL((k_tile_reduce<T, Op>), dim3(nb), dim3(BG_NT), 0, c->stream, in, n, part,
+  BG_LAUNCH(c, "k_tile_reduce", (k_tile_reduce<T, Op>), dim3(nb), dim3(BG_NT), in, n, part,
                      op, identity);
   BG_HIP(c, hipGetLastError());
   int rc = scan_impl<T, Op>(c, part, part, nb, op, identity, (T*)nullptr);
   if (rc) return rc;
-  hipLaunchKernelGGL((k_tile_scan<T, Op>), dim3(nb), dim3(BG_NT), 0, c->stream, in, out, n,
+  BG_LAUNCH(c, "k_tile_scan", (k_tile_scan<T, Op>), dim3(nb), dim3(BG_NT), in, out, n,
                      (const T*)part, op, identity, d_total);
   BG_HIP(c, hipGetLastError());
   bg_release(c, part);

@@ -308,7 +308,7 @@ static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
   const unsigned nb = bg_blocks(n, CT_TILE);
   int64_t* carry = (int64_t*)bg_alloc(c, 8ull * nb);
   if (!carry) return BG_E_NOMEM;
-  hipLaunchKernelGGL(k_tile_max, dim3(nb), dim3(BG_NT), 0, c->stream, in.e, n, carry);
+  BG_LAUNCH(c, "k_tile_max", k_tile_max, dim3(nb), dim3(BG_NT), in.e, n, carry);
   BG_HIP(c, hipGetLastError());
   int rc = bg_scan_max_i64(c, carry, carry, nb, LLONG_MIN);
   if (rc) return rc;
@@ -316,14 +316,14 @@ static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
   rc = count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        hipLaunchKernelGGL(k_components<false>, dim3(nb), dim3(BG_NT), 0, c->stream, in.s, in.e, n,
+        BG_LAUNCH(c, "k_components_count", k_components<false>, dim3(nb), dim3(BG_NT), in.s, in.e, n,
                            carry, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
                            (int64_t*)nullptr);
       },
       [&](uint64_t* off, uint64_t tot) -> int {
         int r = ivl_alloc(c, out, tot);
         if (r) return r;
-        hipLaunchKernelGGL(k_components<true>, dim3(nb), dim3(BG_NT), 0, c->stream, in.s, in.e, n,
+        BG_LAUNCH(c, "k_components_write", k_components<true>, dim3(nb), dim3(BG_NT), in.s, in.e, n,
                            carry, (uint64_t*)nullptr, off, out.s, out.e);
         return 0;
       },
@@ -336,8 +336,7 @@ static int merge_sorted(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& z) {
   int rc = ivl_alloc(c, z, x.n + y.n);
   if (rc) return rc;
   if (x.n + y.n == 0) return 0;
-  hipLaunchKernelGGL(k_merge_sorted, dim3(bg_blocks(x.n + y.n, MP_TILE)), dim3(BG_NT), 0,
-                     c->stream, x.s, x.e, x.n, y.s, y.e, y.n, z.s, z.e);
+  BG_LAUNCH(c, "k_merge_sorted", k_merge_sorted, dim3(bg_blocks(x.n + y.n, MP_TILE)), dim3(BG_NT), x.s, x.e, x.n, y.s, y.e, y.n, z.s, z.e);
   BG_HIP(c, hipGetLastError());
   return 0;
 }
@@ -349,7 +348,7 @@ static int intersect2(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out) {
   return count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        hipLaunchKernelGGL(k_intersect2<false>, dim3(nb), dim3(BG_NT), 0, c->stream, x.s, x.e, x.n,
+        BG_LAUNCH(c, "k_intersect2_count", k_intersect2<false>, dim3(nb), dim3(BG_NT), x.s, x.e, x.n,
                            y.s, y.e, y.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
                            (int64_t*)nullptr);
       },
@@ -357,7 +356,7 @@ static int intersect2(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out) {
         int r = ivl_alloc(c, out, tot);
         if (r) return r;
         if (nb)
-          hipLaunchKernelGGL(k_intersect2<true>, dim3(nb), dim3(BG_NT), 0, c->stream, x.s, x.e,
+          BG_LAUNCH(c, "k_intersect2_write", k_intersect2<true>, dim3(nb), dim3(BG_NT), x.s, x.e,
                              x.n, y.s, y.e, y.n, (uint64_t*)nullptr, off, out.s, out.e);
         return 0;
       },
@@ -371,7 +370,7 @@ static int difference2(bg_ctx* c, const Ivl& r, const Ivl& o, Ivl& out) {
   return count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        hipLaunchKernelGGL(k_difference<false>, dim3(nb), dim3(BG_NT), 0, c->stream, r.s, r.e, r.n,
+        BG_LAUNCH(c, "k_difference_count", k_difference<false>, dim3(nb), dim3(BG_NT), r.s, r.e, r.n,
                            o.s, o.e, o.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
                            (int64_t*)nullptr);
       },
@@ -379,7 +378,7 @@ static int difference2(bg_ctx* c, const Ivl& r, const Ivl& o, Ivl& out) {
         int rr = ivl_alloc(c, out, tot);
         if (rr) return rr;
         if (nb)
-          hipLaunchKernelGGL(k_difference<true>, dim3(nb), dim3(BG_NT), 0, c->stream, r.s, r.e,
+          BG_LAUNCH(c, "k_difference_write", k_difference<true>, dim3(nb), dim3(BG_NT), r.s, r.e,
                              r.n, o.s, o.e, o.n, (uint64_t*)nullptr, off, out.s, out.e);
         return 0;
       },
@@ -446,6 +445,16 @@ extern "C" int bg_merge(bg_ctx* c, bg_set* set, const int* files, int nf, bg_res
 extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
   int rc = check_files(c, set, files, nf, 2);
   if (rc) return rc;
+  // Zero-length rows (end == start; rejected by the reference's own --ec checker,
+  // BedCheckIterator.hpp:619-620) make nextIntersectLine's output depend on its
+  // stream state (a zero-length piece is emitted only when reached while skipping
+  // a stale head); that is not reproduced here, so such inputs are refused.
+  for (int k = 0; k < nf; ++k)
+    if (set->t[files[k]]->has_zero_len)
+      return bg_fail(c, BG_E_UNSUPPORTED,
+                     "zero-length elements (end == start) are not supported by --intersect on "
+                     "the GPU path (BEDOPS --ec rejects them: End coordinates must be greater "
+                     "than start coordinates)");
   Ivl acc;
   if ((rc = components(c, table_ivl(set->t[files[0]]), acc))) return rc;
   for (int k = 1; k < nf; ++k) {
@@ -489,13 +498,13 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   uint8_t* flag = (uint8_t*)bg_alloc(c, R->n ? R->n : 1);
   if (!P || !flag) return BG_E_NOMEM;
   if (o.n) {
-    hipLaunchKernelGGL(k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), 0, c->stream, o.s, o.e,
+    BG_LAUNCH(c, "k_lengths", k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), o.s, o.e,
                        o.n, P);
     BG_HIP(c, hipGetLastError());
   }
   if ((rc = bg_scan_sum_u64(c, P, P, o.n, P + o.n))) return rc;
   if (R->n) {
-    hipLaunchKernelGGL(k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT), 0, c->stream,
+    BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
                        R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
     BG_HIP(c, hipGetLastError());
   }
@@ -505,14 +514,14 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   rc = count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        hipLaunchKernelGGL(k_compact_flags<false>, dim3(nb), dim3(BG_NT), 0, c->stream, flag, R->n,
+        BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag, R->n,
                            cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
       },
       [&](uint64_t* off, uint64_t tot) -> int {
         rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
         if (!rows) return BG_E_NOMEM;
         if (nb)
-          hipLaunchKernelGGL(k_compact_flags<true>, dim3(nb), dim3(BG_NT), 0, c->stream, flag,
+          BG_LAUNCH(c, "k_compact_flags_write", k_compact_flags<true>, dim3(nb), dim3(BG_NT), flag,
                              R->n, (uint64_t*)nullptr, off, rows);
         return 0;
       },

@@ -21,7 +21,9 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_set_rows", "bg_set_restrict_chrom", "bg_set_free", "bg_merge", "bg_intersect",
            "bg_difference", "bg_element_of", "bg_map", "bg_result_rows", "bg_result_format",
            "bg_result_text_device", "bg_result_copy_text", "bg_result_write", "bg_result_free",
-           "bg_stats", "bg_host_alloc", "bg_host_free"]
+           "bg_stats", "bg_host_alloc", "bg_host_free", "bg_prof_enable", "bg_prof_read",
+           "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
+           "bg_set_chrom_name"]
 
 
 def lib_path():
@@ -91,6 +93,13 @@ def load_library():
     L.bg_host_alloc.restype = vp
     L.bg_host_free.argtypes = [vp]
     L.bg_host_free.restype = None
+    L.bg_prof_enable.argtypes = [vp, ctypes.c_char_p]
+    L.bg_prof_read.argtypes = [vp, ctypes.c_char_p, u64]
+    L.bg_result_copy_text_device.argtypes = [vp, vp, vp, u64]
+    L.bg_result_chrom_spans.argtypes = [vp, vp, ctypes.POINTER(u64), ctypes.c_uint32]
+    L.bg_set_chroms.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+    L.bg_set_chrom_name.argtypes = [vp, ctypes.c_uint32]
+    L.bg_set_chrom_name.restype = ctypes.c_char_p
     _LIB = L
     return L
 
@@ -130,6 +139,15 @@ class Result:
         self.eng._check(self.eng.L.bg_result_text_device(self.h, ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
 
+    def copy_to_device(self, dst_ptr, cap):
+        self.eng._check(self.eng.L.bg_result_copy_text_device(self.eng.ctx, self.h, dst_ptr, cap))
+
+    def chrom_spans(self, nchroms):
+        """byte offset of each chromosome's first line (+ total) in the rendered text"""
+        arr = (ctypes.c_uint64 * (nchroms + 1))()
+        self.eng._check(self.eng.L.bg_result_chrom_spans(self.eng.ctx, self.h, arr, nchroms + 1))
+        return list(arr)
+
     def text(self):
         n = self.format()
         buf = ctypes.create_string_buffer(max(n, 1))
@@ -156,6 +174,11 @@ class InputSet:
         n = ctypes.c_uint64()
         self.eng._check(self.eng.L.bg_set_rows(self.h, i, ctypes.byref(n)))
         return n.value
+
+    def chroms(self):
+        n = ctypes.c_uint32()
+        self.eng._check(self.eng.L.bg_set_chroms(self.h, ctypes.byref(n)))
+        return [self.eng.L.bg_set_chrom_name(self.h, g).decode() for g in range(n.value)]
 
     def restrict_chrom(self, chrom):
         self.eng._check(self.eng.L.bg_set_restrict_chrom(self.eng.ctx, self.h, chrom.encode()))
@@ -284,6 +307,19 @@ class Engine:
                 r.free()
         finally:
             s.free()
+
+    def prof_enable(self, filt):
+        self._check(self.L.bg_prof_enable(self.ctx, filt.encode() if filt else None))
+
+    def prof_read(self):
+        """{kernel: (launches, total_ms)} measured with HIP events on the engine stream"""
+        buf = ctypes.create_string_buffer(1 << 16)
+        self._check(self.L.bg_prof_read(self.ctx, buf, 1 << 16))
+        out = {}
+        for ln in buf.value.decode().splitlines():
+            name, calls, ms = ln.split()
+            out[name] = (int(calls), float(ms))
+        return out
 
     def stats(self):
         buf = ctypes.create_string_buffer(8192)

@@ -106,10 +106,23 @@ int bg_result_format(bg_ctx* ctx, bg_result* res, uint64_t* nbytes); /* text in 
 int bg_result_text_device(const bg_result* res, const char** dptr, uint64_t* nbytes);
 int bg_result_copy_text(bg_ctx* ctx, bg_result* res, char* host, uint64_t cap);
 int bg_result_write(bg_ctx* ctx, bg_result* res, int fd); /* format + stream to fd */
+int bg_result_copy_text_device(bg_ctx* ctx, bg_result* res, void* dst, uint64_t cap);
+/* offsets[g] = byte offset of chromosome g's first output line (g in the set's strcmp-
+ * ordered dictionary), offsets[nchroms] = total bytes; used to reassemble per-GPU
+ * chromosome shards in sorted order */
+int bg_result_chrom_spans(bg_ctx* ctx, bg_result* res, uint64_t* offsets, uint32_t cap);
+int bg_set_chroms(const bg_set* set, uint32_t* n);
+const char* bg_set_chrom_name(const bg_set* set, uint32_t g);
 void bg_result_free(bg_result* res);
 
 /* per-stage device timings of the last call sequence (ms), for BEDGPU_STATS */
 int bg_stats(const bg_ctx* ctx, char* buf, uint64_t cap);
+
+/* kernel timing with HIP events on the context stream: filter NULL/"" = off, "*" = all
+ * kernels, else one kernel name (e.g. "k_parse"); bg_prof_read returns lines
+ * "<kernel> <launches> <total_ms>" accumulated since bg_prof_enable */
+int bg_prof_enable(bg_ctx* ctx, const char* filter);
+int bg_prof_read(bg_ctx* ctx, char* buf, uint64_t cap);
 
 /* pinned host buffers for input text (faster H2D); NULL on failure */
 void* bg_host_alloc(uint64_t bytes);

@@ -74,10 +74,26 @@ typedef struct {
   uint16_t* score;   /* BED5 only */
 } cgen_t;
 
+/* Number of contigs and their names/lengths (for sharding by chromosome). */
+int bedgen_ncontigs(void) { return 25; }
+const char* bedgen_contig_name(int c) { return (c >= 0 && c < 25) ? HG38[c].name : ""; }
+uint64_t bedgen_contig_len(int c) { return (c >= 0 && c < 25) ? HG38[c].len : 0; }
+
+/* Generate the rows of the contigs selected by `mask` (bit c = contig c) of the
+ * file described by (N, seed, mode, chr1_only): identical bytes to the matching
+ * contig sections of the full file, thanks to the jump-ahead stream. */
+int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uint64_t mask,
+                         char** out, uint64_t* out_len, uint64_t* out_rows);
+
 /* Generate a whole file into a malloc'ed buffer. mode: 3 = BED3, 5 = BED5.
  * Returns 0 on success; *out must be freed with bedgen_free(). */
 int bedgen_buffer(uint64_t N, uint64_t seed, int mode, int chr1_only,
                   char** out, uint64_t* out_len, uint64_t* out_rows) {
+  return bedgen_buffer_subset(N, seed, mode, chr1_only, ~0ULL, out, out_len, out_rows);
+}
+
+int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uint64_t mask,
+                         char** out, uint64_t* out_len, uint64_t* out_rows) {
   int nc = chr1_only ? 1 : 25;
   double total = 0;
   for (int c = 0; c < nc; ++c) total += (double)HG38[c].len;
@@ -88,6 +104,9 @@ int bedgen_buffer(uint64_t N, uint64_t seed, int mode, int chr1_only,
     g[c].c = c;
     g[c].n = (uint64_t)((double)N * ((double)HG38[c].len / total) + 0.5);
     base[c + 1] = base[c] + g[c].n * (mode == 5 ? 3 : 2);
+  }
+  for (int c = 0; c < nc; ++c) { /* unselected contigs keep their draw offsets, emit nothing */
+    if (!((mask >> c) & 1ULL)) g[c].n = 0;
     rows += g[c].n;
   }
   /* draws + sorting, one contig per task */
