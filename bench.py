@@ -178,8 +178,8 @@ def main():
     tb_ = to_device(torch, L, pb, nb, dev)
     A_bytes = B_bytes = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        A_bytes = ctypes.string_at(pa, na)
-        B_bytes = ctypes.string_at(pb, nb)
+        A_bytes = bytes((ctypes.c_char * na).from_address(pa.value))
+        B_bytes = bytes((ctypes.c_char * nb).from_address(pb.value))
     L.bedgen_free(pa)
     L.bedgen_free(pb)
     torch.cuda.synchronize(dev)
