@@ -15,8 +15,7 @@ def from_db(path):
     db = sqlite3.connect(path)
     rows = db.execute("select name, total_calls, total_duration, average, percentage "
                       "from top_kernels").fetchall()
-    # rocprofv3 durations in the db are nanoseconds
-    return [(n.split("(")[0], int(c), t / 1e3, a / 1e3, p) for n, c, t, a, p in rows]
+    return [(n.split("(")[0], int(c), t, a, p) for n, c, t, a, p in rows]  # top_kernels view: microseconds
 
 
 def from_csv(path):
