@@ -177,10 +177,12 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
 __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __restrict__ tb,
                                                      bg_dstatus* st) {
   __shared__ uint64_t sh[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + (uint64_t)threadIdx.x * FT_ROWS;
+  const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + threadIdx.x;  // rows striped
   CountOut co;
-  for (int k = 0; k < FT_ROWS; ++k)
-    if (base + k < A.n && !render(A, base + k, co)) bg_report(st, base + k, ERR_RANGE);
+  for (int k = 0; k < FT_ROWS; ++k) {
+    const uint64_t row = base + (uint64_t)k * BG_NT;
+    if (row < A.n && !render(A, row, co)) bg_report(st, row, ERR_RANGE);
+  }
   uint64_t tot;
   (void)block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &tot);
   if (threadIdx.x == 0) tb[blockIdx.x] = tot;
@@ -190,22 +192,33 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
                                                      char* __restrict__ out) {
   __shared__ uint64_t sh[BG_NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) char buf[FT_LDS];
-  const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + (uint64_t)threadIdx.x * FT_ROWS;
-  CountOut co;
-  for (int k = 0; k < FT_ROWS; ++k)
-    if (base + k < A.n) render(A, base + k, co);
-  uint64_t tot;
-  const uint64_t my = block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &tot);
+  // rows are striped over the threads (coalesced column reads); a row's byte offset
+  // in the tile = all bytes of the previous stripes + its prefix inside its stripe
+  const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + threadIdx.x;
+  uint64_t my[FT_ROWS];
+  uint64_t tot = 0;
+  for (int k = 0; k < FT_ROWS; ++k) {
+    const uint64_t row = base + (uint64_t)k * BG_NT;
+    CountOut co;
+    if (row < A.n) render(A, row, co);
+    uint64_t st;
+    my[k] = tot + block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &st);
+    tot += st;
+  }
   const uint64_t dst0 = toff[blockIdx.x];
   if (tot > FT_LDS) {  // oversized tile (long names / rests): render straight to HBM
-    LdsOut o{out + dst0 + my};
-    for (int k = 0; k < FT_ROWS; ++k)
-      if (base + k < A.n) render(A, base + k, o);
+    for (int k = 0; k < FT_ROWS; ++k) {
+      const uint64_t row = base + (uint64_t)k * BG_NT;
+      LdsOut o{out + dst0 + my[k]};
+      if (row < A.n) render(A, row, o);
+    }
     return;
   }
-  LdsOut o{buf + my};
-  for (int k = 0; k < FT_ROWS; ++k)
-    if (base + k < A.n) render(A, base + k, o);
+  for (int k = 0; k < FT_ROWS; ++k) {
+    const uint64_t row = base + (uint64_t)k * BG_NT;
+    LdsOut o{buf + my[k]};
+    if (row < A.n) render(A, row, o);
+  }
   __syncthreads();
   // stream buf[0, tot) -> out[dst0, dst0 + tot)
   const uint64_t a0 = dst0, a1 = dst0 + tot;

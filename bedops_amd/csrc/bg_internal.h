@@ -185,6 +185,14 @@ struct OpMax {
   template <typename T>
   __device__ __forceinline__ T operator()(T a, T b) const { return a > b ? a : b; }
 };
+struct OpMin {
+  template <typename T>
+  __device__ __forceinline__ T operator()(T a, T b) const { return a < b ? a : b; }
+};
+
+static inline int bg_hip_ok(bg_ctx* c, hipError_t e) {
+  return e == hipSuccess ? 0 : bg_hip_fail(c, e, "HIP runtime call");
+}
 
 // Block (BG_NT threads) exclusive scan. `sh` must hold BG_NT/64 + 1 elements.
 // Returns the exclusive prefix of this thread; *total gets the block aggregate.

@@ -1,4 +1,4 @@
-// bg_load.hip — K0: BED text in HBM -> keyed int64 SoA columns.
+// bg_load.hip — K0: BED text in HBM -> keyed int64 SoA columns, one text pass.
 //
 // Replaces the reference's per-line readers (fscanf "%s\t%lu\t%lu%*[^\n]s\n" + fgetc,
 // interfaces/general-headers/data/bed/Bed.hpp:244-255,270-272; B3Rest :277-383;
@@ -11,24 +11,34 @@
 // line: !feof check). Lines outside the grammar are reported as BG_E_PARSE with the
 // line number instead of reproducing fscanf's cross-line behaviour on garbage.
 //
-// Pipeline (per input):
-//   k_nl_count   tiles of 4 KiB: '\n' count + last '\n' offset per tile   (text read 1x)
-//   scans        row0[t] = sum of counts before t; prevnl[t] = last '\n' before t
-//   k_parse      per tile: text (+256 B halo) staged in LDS, '\n' offsets found
-//                with a wave/block scan, one thread per line parses
-//                chrom/start/end(/id/score), writes raw start/end, records
-//                chromosome-change rows and sort-order violations   (text read 1x)
-//   host         chromosome dictionary (strcmp order over all inputs), run checks
-//   k_key        ks/ke = (chrom_id << 40) | coordinate, in place, range checks
+// Pipeline per input (tiles of 8 KiB; a tile owns the lines that START in it):
+//   k_scout      '\n' count per tile + hash of the chromosome token of the tile's
+//                first line                                        (text read 1x)
+//   scan         row0[t] = '\n' before the tile = row index of its first owned line
+//   k_boundary   tiles whose first token differs from the next tile's hold every
+//                chromosome change; k_tile_runs lists the token changes inside them
+//   host         run list per input (position, name), strcmp order check, global
+//                dictionary over all inputs -> chromosome id per run
+//   k_parse      per tile: text + halos staged in LDS, '\n' offsets by a block scan,
+//                one thread per line: SWAR field masks + 8-digit SWAR decimal
+//                conversion (bg_parse.h; byte path for anything else), run by
+//                position, token hash check against the run, keys
+//                ks = (chrom_id << 40) | start, ke = (chrom_id << 40) | end written
+//                directly, in-tile sort check                     (text read 1x)
+//   k_check_bounds  sort check across tile boundaries
 #include <algorithm>
 #include <cstring>
 #include <map>
 
 #include "bg_internal.h"
+#include "bg_parse.h"
 
-#define TXT_TILE 4096
-#define TXT_HALO 256
-#define RUN_CAP (1u << 20)
+#define TT 8192   // tile bytes
+#define HB 16     // halo before (we need the byte before the tile)
+#define HA 256    // halo after (the tail of the tile's last line)
+#define LBUF (HB + TT + HA + 32)
+#define LCAP 1536  // lines per tile on the LDS path (>= TT / 6: shortest valid line)
+#define REC_CAP (1u << 20)
 
 __device__ __forceinline__ uint32_t nl_mask4(uint32_t w) {
   // bit 7 of each byte set iff that byte == '\n' (exact, no borrow artefacts)
@@ -37,69 +47,245 @@ __device__ __forceinline__ uint32_t nl_mask4(uint32_t w) {
   return ~nz & 0x80808080u;
 }
 
-// guarded 16-byte load of txt[base, base+16) (bytes >= nbytes read as 0)
-__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ txt, uint64_t base,
+// guarded 16-byte load of txt[base, base+16) (bytes outside [0, nbytes) read as 0)
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ txt, int64_t base,
                                         uint64_t nbytes) {
-  if (base + 16 <= nbytes) return *reinterpret_cast<const uint4*>(txt + base);
+  if (base >= 0 && (uint64_t)base + 16 <= nbytes) return *reinterpret_cast<const uint4*>(txt + base);
   uint32_t w[4] = {0, 0, 0, 0};
   for (int k = 0; k < 16; ++k)
-    if (base + k < nbytes) w[k >> 2] |= (uint32_t)txt[base + k] << (8 * (k & 3));
+    if (base + k >= 0 && (uint64_t)(base + k) < nbytes)
+      w[k >> 2] |= (uint32_t)txt[base + k] << (8 * (k & 3));
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__global__ void __launch_bounds__(BG_NT) k_nl_count(const uint8_t* __restrict__ txt,
-                                                    uint64_t nbytes, uint64_t* __restrict__ cnt,
-                                                    int64_t* __restrict__ lastnl) {
-  __shared__ uint64_t shc[BG_NT / 64 + 1];
-  __shared__ int64_t shm[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * TXT_TILE + (uint64_t)threadIdx.x * 16;
-  uint4 v = load16(txt, base, nbytes);
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint64_t c = 0;
-  int64_t last = -1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t m = nl_mask4(w[k]);
-    c += __popc(m);
-    if (m) last = (int64_t)(base + 4 * k + (31 - __clz(m)) / 8);
-  }
-  uint64_t tc;
-  int64_t tm;
-  (void)block_excl_scan(c, OpSum(), (uint64_t)0, shc, &tc);
-  (void)block_excl_scan(last, OpMax(), (int64_t)-1, shm, &tm);
-  if (threadIdx.x == 0) {
-    cnt[blockIdx.x] = tc;
-    lastnl[blockIdx.x] = tm;
-  }
-}
-
-// byte view of one tile: LDS copy of [lo, hi), global memory elsewhere
+// byte view of one tile: LDS copy of [lo, hi), global memory elsewhere (< nbytes)
 struct TileText {
   const uint8_t* g;
   const uint8_t* l;
   int64_t lo, hi;
+  uint64_t nb;
   __device__ __forceinline__ uint8_t at(int64_t p) const {
     return (p >= lo && p < hi) ? l[p - lo] : g[p];
   }
 };
 
-struct LineFields {
-  int64_t tok;     // chrom token offset
-  int32_t toklen;
-  uint64_t start, end;
-  int64_t rest;    // offset of the first byte after the end digits
-  double score;
-  int32_t err;     // 0 ok, ERR_*
-  int32_t scoreint;
+// Stage [t0-HB, t0+TT+HA) into LDS (zeros outside the text). Each thread also returns
+// its 32 tile bytes in registers.
+__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ txt, uint64_t nb,
+                                           int64_t t0, uint8_t* buf, uint4& v0, uint4& v1) {
+  const int64_t b = t0 + (int64_t)threadIdx.x * 32;
+  v0 = load16(txt, b, nb);
+  v1 = load16(txt, b + 16, nb);
+  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32]) = v0;
+  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32 + 16]) = v1;
+  if (threadIdx.x < (HA + 32) / 16)
+    *reinterpret_cast<uint4*>(&buf[HB + TT + threadIdx.x * 16]) =
+        load16(txt, t0 + TT + (int64_t)threadIdx.x * 16, nb);
+  if (threadIdx.x == BG_NT - 1) *reinterpret_cast<uint4*>(&buf[0]) = load16(txt, t0 - HB, nb);
+}
+
+// token [tok, tok+len) of the line starting at p (leading ws skipped, stops at ws or
+// '\n'); returns its hash; blank line -> len 0
+__device__ __forceinline__ uint64_t line_token(const TileText& T, int64_t p, int64_t& tok,
+                                               uint32_t& len) {
+  while ((uint64_t)p < T.nb) {
+    uint8_t ch = T.at(p);
+    if (!bg_isws(ch)) break;
+    ++p;
+  }
+  tok = p;
+  uint64_t h = BGP_FNV_OFF;
+  uint32_t n = 0;
+  while ((uint64_t)p < T.nb) {
+    uint8_t ch = T.at(p);
+    if (ch == '\n' || bg_isws(ch)) break;
+    h = bgp_hash_step(h, ch);
+    ++n;
+    ++p;
+  }
+  len = n;
+  return bgp_hash_final(h, n);
+}
+
+// -------------------------------------------------------------------------------------
+// k_scout: newline count per tile + first owned line and its chromosome token
+// -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                 uint64_t* __restrict__ cnt,
+                                                 int64_t* __restrict__ fls,
+                                                 uint64_t* __restrict__ fhash) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
+  __shared__ uint64_t shc[BG_NT / 64 + 1];
+  __shared__ uint32_t shm[BG_NT / 64 + 1];
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  uint4 v0, v1;
+  stage_tile(txt, nb, t0, buf, v0, v1);
+  uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint64_t c = 0;
+  uint32_t first = TT;
+#pragma unroll
+  for (int k = 7; k >= 0; --k) {
+    uint32_t m = nl_mask4(w[k]);
+    c += __popc(m);
+    if (m) first = threadIdx.x * 32 + 4 * k + (__ffs(m) - 1) / 8;
+  }
+  uint64_t tc;
+  (void)block_excl_scan(c, OpSum(), (uint64_t)0, shc, &tc);
+  uint32_t fmin;
+  (void)block_excl_scan(first, OpMin(), (uint32_t)TT, shm, &fmin);
+  if (threadIdx.x == 0) {
+    cnt[blockIdx.x] = tc;
+    int64_t ls = -1;
+    if (t0 == 0 || buf[HB - 1] == '\n') ls = t0;
+    else if (fmin + 1 < TT) ls = t0 + fmin + 1;
+    if (ls >= 0 && (uint64_t)ls >= nb) ls = -1;
+    uint64_t h = 0;
+    if (ls >= 0) {
+      TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
+      int64_t tok;
+      uint32_t len;
+      h = line_token(T, ls, tok, len);
+    }
+    fls[blockIdx.x] = ls;
+    fhash[blockIdx.x] = h;
+  }
+}
+
+// tile t may hold a chromosome change iff its first token differs from the next
+// tile's (or either has no line start); tile 0 and the last tile always qualify
+__global__ void k_boundary(const int64_t* __restrict__ fls, const uint64_t* __restrict__ fhash,
+                           uint32_t ntiles, uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  bool b = (t == 0) || (t + 1 == ntiles) || fls[t] < 0 || fls[t + 1] < 0 || fhash[t] != fhash[t + 1];
+  if (b) list[atomicAdd(nlist, 1u)] = t;
+}
+
+// line starts of the tile (local offsets) -> LDS; returns the number of lines.
+// has0: a line starts at the tile's first byte. Lines are the starts t0+ls[k].
+__device__ __forceinline__ uint32_t tile_line_starts(const uint4& v0, const uint4& v1,
+                                                     const uint8_t* buf, int64_t t0,
+                                                     uint16_t* ls, uint32_t cap,
+                                                     uint32_t* shs, bool& has0) {
+  has0 = (t0 == 0) || buf[HB - 1] == '\n';
+  uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t m[8], c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m[k] = nl_mask4(w[k]);
+    // a '\n' on the tile's last byte starts a line in the next tile
+    if (threadIdx.x == BG_NT - 1 && k == 7) m[k] &= 0x00808080u;
+    c += __popc(m[k]);
+  }
+  uint32_t tot;
+  uint32_t o = block_excl_scan(c, OpSum(), 0u, shs, &tot) + (has0 ? 1u : 0u);
+  if (threadIdx.x == 0 && has0) ls[0] = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t mm = m[k];
+    while (mm) {
+      const int bit = __ffs(mm) - 1;
+      if (o < cap) ls[o] = (uint16_t)(threadIdx.x * 32 + 4 * k + bit / 8 + 1);
+      ++o;
+      mm &= mm - 1;
+    }
+  }
+  __syncthreads();
+  return tot + (has0 ? 1u : 0u);
+}
+
+// end ('\n' position) of the line starting at p, searching from `from`; -1 if none
+__device__ __forceinline__ int64_t find_nl(const TileText& T, int64_t from) {
+  for (int64_t q = from; (uint64_t)q < T.nb; ++q)
+    if (T.at(q) == '\n') return q;
+  return -1;
+}
+
+// k_tile_runs: records (position, token hash, token span) of every line in a boundary
+// tile whose token differs from the previous line's, plus the tile's first line and the
+// next tile's first line
+__global__ void __launch_bounds__(BG_NT) k_tile_runs(
+    const uint8_t* __restrict__ txt, uint64_t nb, const uint32_t* __restrict__ tiles,
+    const int64_t* __restrict__ fls, const uint64_t* __restrict__ fhash, uint32_t ntiles,
+    int64_t* __restrict__ rpos, uint64_t* __restrict__ rhash, int64_t* __restrict__ rtok,
+    uint32_t* __restrict__ rlen, uint32_t* __restrict__ nrec) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
+  __shared__ uint16_t lst[TT + 1];
+  __shared__ uint32_t shs[BG_NT / 64 + 1];
+  const uint32_t t = tiles[blockIdx.x];
+  const int64_t t0 = (int64_t)t * TT;
+  uint4 v0, v1;
+  stage_tile(txt, nb, t0, buf, v0, v1);
+  __syncthreads();
+  bool has0;
+  const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, TT + 1, shs, has0);
+  TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
+  for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
+    const int64_t p = t0 + lst[k];
+    if ((uint64_t)p >= nb) continue;
+    int64_t tok;
+    uint32_t len;
+    const uint64_t h = line_token(T, p, tok, len);
+    bool rec = (k == 0);
+    if (!rec) {
+      int64_t ptok;
+      uint32_t plen;
+      rec = line_token(T, t0 + lst[k - 1], ptok, plen) != h;
+    }
+    if (rec) {
+      const uint32_t q = atomicAdd(nrec, 1u);
+      if (q < REC_CAP) { rpos[q] = p; rhash[q] = h; rtok[q] = tok; rlen[q] = len; }
+    }
+  }
+  if (threadIdx.x == 0) {  // first line of the next tile that has one
+    uint32_t u = t + 1;
+    while (u < ntiles && fls[u] < 0) ++u;
+    if (u < ntiles) {
+      int64_t tok;
+      uint32_t len;
+      const uint64_t h = line_token(T, fls[u], tok, len);
+      const uint32_t q = atomicAdd(nrec, 1u);
+      if (q < REC_CAP) { rpos[q] = fls[u]; rhash[q] = h; rtok[q] = tok; rlen[q] = len; }
+    }
+  }
+}
+
+// gather the chromosome tokens of run records into fixed 128-byte slots
+__global__ void k_gather_tokens(const uint8_t* __restrict__ txt, const int64_t* rtok,
+                                const uint32_t* rlen, uint32_t n, char* out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t len = rlen[k];
+  for (uint32_t i = 0; i < 128; ++i) out[k * 128ull + i] = (i < len) ? (char)txt[rtok[k] + i] : 0;
+}
+
+// -------------------------------------------------------------------------------------
+// k_parse
+// -------------------------------------------------------------------------------------
+struct RunTable {
+  const int64_t* pos;    // byte position of each run's first line, ascending
+  const uint64_t* hash;  // token hash of the run
+  const int32_t* gid;    // global chromosome id
+  uint64_t* row;         // out: row index of each run's first line
+  uint32_t n;
 };
 
-__device__ __forceinline__ bool parse_u64(const TileText& T, int64_t& p, int64_t le,
-                                          uint64_t& v) {
+__device__ __forceinline__ uint32_t run_of(const RunTable& R, int64_t p, uint32_t lo, uint32_t hi) {
+  // last k in [lo, hi] with pos[k] <= p
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (R.pos[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ bool parse_u64(const TileText& T, int64_t& p, int64_t le, uint64_t& v) {
   if (p < le && T.at(p) == '+') ++p;
   int nd = 0;
   uint64_t x = 0;
   while (p < le) {
-    uint8_t ch = T.at(p);
+    const uint8_t ch = T.at(p);
     if (ch < '0' || ch > '9') break;
     if (nd < 19) x = x * 10 + (ch - '0');
     ++nd;
@@ -110,7 +296,7 @@ __device__ __forceinline__ bool parse_u64(const TileText& T, int64_t& p, int64_t
 }
 
 // strtod subset, exact where it claims to be: [+-]digits[.digits] with <= 19
-// significant digits; integers are flagged (scoreint). Anything else -> ERR_SCORE.
+// significant digits; integers are flagged. Anything else -> ERR_SCORE.
 __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64_t le,
                                             double& out, int& isint) {
   bool neg = false;
@@ -119,7 +305,7 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
   int nd = 0, frac = 0, sig = 0;
   bool dot = false, fracnz = false;
   while (p < le) {
-    uint8_t ch = T.at(p);
+    const uint8_t ch = T.at(p);
     if (ch == '.' && !dot) { dot = true; ++p; continue; }
     if (ch < '0' || ch > '9') break;
     ++nd;
@@ -136,23 +322,33 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
   if (p < le && !bg_isws(T.at(p))) return false;  // exponent / junk: not on the GPU path
   isint = !fracnz;
   if (!fracnz) {
-    // drop the zero fraction digits, value is m / 10^frac exactly an integer
     for (int k = 0; k < frac; ++k) m /= 10;
     if (m > (1ULL << 53)) return false;
     out = neg ? -(double)m : (double)m;
     return true;
   }
-  // Clinger fast path: exact when m < 2^53 and 10^frac exactly representable
-  if (m > (1ULL << 53) || frac > 22) return false;
-  double d = (double)m, s = 1.0;
-  for (int k = 0; k < frac; ++k) s *= 10.0;  // exact for frac <= 22
-  out = d / s;
+  if (m > (1ULL << 53) || frac > 22) return false;  // Clinger fast path: exact
+  double s = 1.0;
+  for (int k = 0; k < frac; ++k) s *= 10.0;
+  out = (double)m / s;
   if (neg) out = -out;
   return true;
 }
 
-__device__ __forceinline__ void parse_line(const TileText& T, int64_t ls, int64_t le, int kind,
-                                           LineFields& L) {
+struct Line {
+  int64_t tok;
+  uint32_t toklen;
+  uint64_t hash;
+  uint64_t start, end;
+  int64_t rest;
+  double score;
+  int err;
+  int scoreint;
+};
+
+// full grammar, byte by byte (fallback path and error reporting)
+__device__ __forceinline__ void parse_line_slow(const TileText& T, int64_t ls, int64_t le, int kind,
+                                             Line& L) {
   L.err = 0;
   L.scoreint = 1;
   L.score = 0;
@@ -160,18 +356,21 @@ __device__ __forceinline__ void parse_line(const TileText& T, int64_t ls, int64_
   while (p < le && bg_isws(T.at(p))) ++p;
   if (p == le) { L.err = ERR_BLANK; return; }
   L.tok = p;
-  while (p < le && !bg_isws(T.at(p))) ++p;
-  L.toklen = (int32_t)(p - L.tok);
+  uint64_t h = BGP_FNV_OFF;
+  while (p < le && !bg_isws(T.at(p))) { h = bgp_hash_step(h, T.at(p)); ++p; }
+  L.toklen = (uint32_t)(p - L.tok);
+  L.hash = bgp_hash_final(h, L.toklen);
   if (L.toklen > BG_CHR_MAX) { L.err = ERR_CHROM; return; }
   while (p < le && bg_isws(T.at(p))) ++p;
   if (!parse_u64(T, p, le, L.start)) { L.err = ERR_PARSE; return; }
+  if (p < le && !bg_isws(T.at(p))) { L.err = ERR_PARSE; return; }
   while (p < le && bg_isws(T.at(p))) ++p;
   if (!parse_u64(T, p, le, L.end)) { L.err = ERR_PARSE; return; }
   L.rest = p;
   if (kind == BG_BED5) {
     if (p == le || !bg_isws(T.at(p))) { L.err = ERR_PARSE; return; }
     while (p < le && bg_isws(T.at(p))) ++p;
-    int64_t id = p;
+    const int64_t id = p;
     while (p < le && !bg_isws(T.at(p))) ++p;
     if (p == id) { L.err = ERR_PARSE; return; }
     while (p < le && bg_isws(T.at(p))) ++p;
@@ -181,161 +380,137 @@ __device__ __forceinline__ void parse_line(const TileText& T, int64_t ls, int64_
   }
 }
 
-// chrom token + start of the line [ls, le) (used for the previous-line comparison)
-__device__ __forceinline__ int parse_head(const TileText& T, int64_t ls, int64_t le,
-                                          int64_t& tok, int32_t& toklen, uint64_t& start) {
-  int64_t p = ls;
-  while (p < le && bg_isws(T.at(p))) ++p;
-  if (p == le) return ERR_BLANK;
-  tok = p;
-  while (p < le && !bg_isws(T.at(p))) ++p;
-  toklen = (int32_t)(p - tok);
-  while (p < le && bg_isws(T.at(p))) ++p;
-  if (!parse_u64(T, p, le, start)) return ERR_PARSE;
-  return 0;
+// 16 bytes of LDS starting at byte offset q (q + 20 <= LBUF)
+__device__ __forceinline__ void lds16(const uint8_t* buf, uint32_t q, uint64_t& lo, uint64_t& hi) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (q & ~3u));
+  const uint32_t o = q & 3u;
+  const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+  lo = (uint64_t)bgp_align(x0, x1, o) | ((uint64_t)bgp_align(x1, x2, o) << 32);
+  hi = (uint64_t)bgp_align(x2, x3, o) | ((uint64_t)bgp_align(x3, x4, o) << 32);
+}
+
+// fast path: fields from the line's first 32 bytes (LDS) -> true if decided
+__device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const TileText& T, int64_t ls,
+                                                int64_t le, Line& L) {
+  if (ls < T.lo || ls + 52 > T.hi + 32) return false;
+  const uint32_t q = (uint32_t)(ls - T.lo);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (q & ~3u));
+  const uint32_t o = q & 3u;
+  uint32_t x[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) x[i] = d[i];
+  uint32_t W[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) W[i] = bgp_align(x[i], x[i + 1], o);
+  BgpFields F;
+  const int r = bgp_fields(W, (uint32_t)(le - ls), F);
+  if (r != 1) return false;  // blank lines and errors take the byte path (messages)
+  const uint32_t toklen = F.a1 - F.a0;
+  if (toklen > BG_CHR_MAX) return false;
+  uint64_t lo, hi;
+  lds16(buf, q + F.s0, lo, hi);
+  L.start = bgp_digits(lo, hi, (int)(F.s1 - F.s0));
+  lds16(buf, q + F.e0, lo, hi);
+  L.end = bgp_digits(lo, hi, (int)(F.e1 - F.e0));
+  if (F.s1 - F.s0 > 13) L.start = ~0ULL;
+  if (F.e1 - F.e0 > 13) L.end = ~0ULL;
+  L.tok = ls + F.a0;
+  L.toklen = toklen;
+  uint64_t h = BGP_FNV_OFF;
+  for (uint32_t i = 0; i < toklen; ++i) h = bgp_hash_step(h, buf[q + F.a0 + i]);
+  L.hash = bgp_hash_final(h, toklen);
+  L.rest = ls + F.e1;
+  L.err = 0;
+  L.score = 0;
+  L.scoreint = 1;
+  return true;
 }
 
 __global__ void __launch_bounds__(BG_NT) k_parse(
-    const uint8_t* __restrict__ txt, uint64_t nbytes, const uint64_t* __restrict__ cnt,
-    const uint64_t* __restrict__ row0, const int64_t* __restrict__ prevnl, int kind,
-    uint64_t* __restrict__ S, uint64_t* __restrict__ E, uint64_t* __restrict__ rest_off,
-    uint32_t* __restrict__ rest_len, double* __restrict__ score, uint64_t* __restrict__ run_row,
-    uint64_t* __restrict__ run_tok, uint32_t* __restrict__ run_len, bg_dstatus* st) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[TXT_HALO + TXT_TILE];
-  __shared__ uint16_t nlpos[TXT_TILE];
+    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
+    int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
+    uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
+    bg_dstatus* st) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
+  __shared__ uint16_t lst[LCAP + 1];
+  __shared__ int64_t lkey[LCAP];
   __shared__ uint32_t shs[BG_NT / 64 + 1];
-  const uint64_t t = blockIdx.x;
-  const int64_t t0 = (int64_t)(t * TXT_TILE);
-  const uint64_t lines = cnt[t];
-  if (lines == 0) return;  // uniform per block
-  const int64_t lo = t0 >= TXT_HALO ? t0 - TXT_HALO : 0;
-  // stage [lo, t0 + TILE) in LDS
-  {
-    const uint64_t b = (uint64_t)t0 + (uint64_t)threadIdx.x * 16;
-    uint4 v = load16(txt, b, nbytes);
-    *reinterpret_cast<uint4*>(&buf[TXT_HALO + threadIdx.x * 16]) = v;
-    if (threadIdx.x < TXT_HALO / 16 && t0 >= TXT_HALO) {
-      uint4 h = load16(txt, (uint64_t)lo + threadIdx.x * 16, nbytes);
-      *reinterpret_cast<uint4*>(&buf[threadIdx.x * 16]) = h;
-    }
-    // newline offsets of this thread's 16 bytes, compacted by a block scan
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t m[4], c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      m[k] = nl_mask4(w[k]);
-      c += __popc(m[k]);
-    }
-    uint32_t tot;
-    uint32_t o = block_excl_scan(c, OpSum(), 0u, shs, &tot);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t mm = m[k];
-      while (mm) {
-        int bit = __ffs(mm) - 1;
-        nlpos[o++] = (uint16_t)(threadIdx.x * 16 + 4 * k + bit / 8);
-        mm &= mm - 1;
+  __shared__ uint32_t runlo, runhi;
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  uint4 v0, v1;
+  stage_tile(txt, nb, t0, buf, v0, v1);
+  if (threadIdx.x == 0) {  // runs that can occur in this tile
+    runlo = run_of(R, t0, 0, R.n - 1);
+    runhi = run_of(R, t0 + TT - 1, 0, R.n - 1);
+  }
+  __syncthreads();
+  bool has0;
+  const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, LCAP + 1, shs, has0);
+  const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1);  // row of the first owned line
+  if (L > LCAP) {  // > LCAP lines in 8 KiB: some line is shorter than any valid record
+    if (threadIdx.x == 0) bg_report(st, r0, ERR_PARSE);
+    return;
+  }
+  TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
+  const uint32_t rl = runlo, rh = runhi;
+  for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
+    const int64_t ls = t0 + lst[k];
+    const uint64_t r = r0 + k;
+    lkey[k] = LLONG_MIN;
+    if (r >= nrows) continue;  // unterminated last line (dropped like the reference)
+    const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : find_nl(T, ls);
+    if (le < 0) continue;
+    Line Ln;
+    if (kind == BG_BED5 || !parse_line_fast(buf, T, ls, le, Ln)) {
+      parse_line_slow(T, ls, le, kind, Ln);
+      if (Ln.err) {
+        if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
+        bg_report(st, r, Ln.err);
+        KS[r] = KE[r] = 0;
+        continue;
       }
+    }
+    const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+    if (Ln.hash != R.hash[run]) {  // a chromosome outside the run order: unsorted input
+      bg_report(st, r, ERR_UNSORTED);
+      continue;
+    }
+    if (R.pos[run] == ls) R.row[run] = r;
+    if (Ln.end > BG_MAX_COORD || Ln.start > Ln.end) bg_report(st, r, ERR_RANGE);
+    if (Ln.start == Ln.end) atomicOr(&st->flags, 2ULL);
+    const int64_t g = (int64_t)R.gid[run] << BG_KEY_SHIFT;
+    const int64_t ks = g | (int64_t)(Ln.start & BG_COORD_MASK);
+    KS[r] = ks;
+    KE[r] = g | (int64_t)(Ln.end & BG_COORD_MASK);
+    lkey[k] = ks;
+    if (rest_off) {
+      rest_off[r] = (uint64_t)Ln.rest;
+      rest_len[r] = (uint32_t)(le - Ln.rest);
+    }
+    if (score) {
+      score[r] = Ln.score;
+      if (!Ln.scoreint) atomicOr(&st->flags, 1ULL);
     }
   }
   __syncthreads();
-  TileText T;
-  T.g = txt;
-  T.l = (t0 >= TXT_HALO) ? buf : buf + TXT_HALO;
-  T.lo = lo;
-  T.hi = t0 + TXT_TILE;
-  const int64_t pnl = prevnl[t];  // '\n' before this tile (-1: none)
-  const uint64_t r0 = row0[t];
-  for (uint64_t j = threadIdx.x; j < lines; j += BG_NT) {
-    const int64_t le = t0 + nlpos[j];
-    const int64_t ls = (j == 0 ? pnl : t0 + (int64_t)nlpos[j - 1]) + 1;
-    const uint64_t r = r0 + j;
-    LineFields L;
-    parse_line(T, ls, le, kind, L);
-    if (L.err) {
-      if (L.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
-      bg_report(st, r, L.err);
-      S[r] = E[r] = 0;
-      continue;
-    }
-    S[r] = L.start;
-    E[r] = L.end;
-    if (rest_off) {
-      rest_off[r] = (uint64_t)L.rest;
-      rest_len[r] = (uint32_t)(le - L.rest);
-    }
-    if (score) {
-      score[r] = L.score;
-      if (!L.scoreint) atomicOr(&st->flags, 1ULL);
-    }
-    bool newrun = (r == 0);
-    if (r > 0) {
-      const int64_t ple = ls - 1;  // previous line's '\n'
-      int64_t pls;
-      if (j >= 2) pls = t0 + (int64_t)nlpos[j - 2] + 1;
-      else if (j == 1) pls = pnl + 1;
-      else {
-        int64_t q = ple - 1;
-        while (q >= 0 && T.at(q) != '\n') --q;
-        pls = q + 1;
-      }
-      int64_t ptok = 0;
-      int32_t ptoklen = 0;
-      uint64_t pstart = 0;
-      int perr = parse_head(T, pls, ple, ptok, ptoklen, pstart);
-      if (perr) {
-        newrun = true;  // the previous line is itself reported
-      } else {
-        bool same = (ptoklen == L.toklen);
-        for (int32_t k = 0; same && k < L.toklen; ++k) same = T.at(ptok + k) == T.at(L.tok + k);
-        if (!same) newrun = true;
-        else if (L.start < pstart) bg_report(st, r, ERR_UNSORTED);
-      }
-    }
-    if (newrun) {
-      unsigned long long k = atomicAdd(&st->nruns, 1ULL);
-      if (k < RUN_CAP) {
-        run_row[k] = r;
-        run_tok[k] = (uint64_t)L.tok;
-        run_len[k] = (uint32_t)L.toklen;
-      }
-    }
-  }
+  for (uint32_t k = threadIdx.x + 1; k < L; k += BG_NT)
+    if (lkey[k] != LLONG_MIN && lkey[k - 1] != LLONG_MIN && lkey[k] < lkey[k - 1])
+      bg_report(st, r0 + k, ERR_UNSORTED);
 }
 
-// gather the chromosome tokens of the run records into fixed 128-byte slots
-__global__ void k_gather_tokens(const uint8_t* __restrict__ txt, const uint64_t* run_tok,
-                                const uint32_t* run_len, uint64_t nruns, char* out) {
-  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nruns) return;
-  uint32_t n = run_len[k];
-  for (uint32_t i = 0; i < 128; ++i) out[k * 128 + i] = (i < n) ? (char)txt[run_tok[k] + i] : 0;
+// sort order across tile boundaries: the first rows of each tile vs their predecessors
+__global__ void k_check_bounds(const int64_t* __restrict__ KS, const uint64_t* __restrict__ row0,
+                               uint32_t ntiles, uint64_t nrows, bg_dstatus* st) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t r = row0[t];
+  for (uint64_t q = r; q < r + 2 && q < nrows; ++q)
+    if (q > 0 && KS[q] < KS[q - 1]) bg_report(st, q, ERR_UNSORTED);
 }
 
-// ks/ke: raw -> (gid << 40) | coord, in place; run_row0 has nruns+1 entries
-__global__ void __launch_bounds__(BG_NT) k_key(int64_t* __restrict__ S, int64_t* __restrict__ E,
-                                               uint64_t n, const uint64_t* __restrict__ run_row0,
-                                               const int32_t* __restrict__ run_gid,
-                                               uint32_t nruns, bg_dstatus* st) {
-  const uint64_t r = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (r >= n) return;
-  uint32_t lo = 0, hi = nruns;  // last k with run_row0[k] <= r
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (run_row0[mid] <= r) lo = mid;
-    else hi = mid;
-  }
-  const int64_t g = (int64_t)run_gid[lo] << BG_KEY_SHIFT;
-  const uint64_t s = (uint64_t)S[r], e = (uint64_t)E[r];
-  if (e > BG_MAX_COORD || s > e) bg_report(st, r, ERR_RANGE);
-  if (s == e) atomicOr(&st->flags, 2ULL);
-  S[r] = g | (int64_t)(s & BG_COORD_MASK);
-  E[r] = g | (int64_t)(e & BG_COORD_MASK);
-}
-
-// ---------------------------------------------------------------------------------
+// -------------------------------------------------------------------------------------
 // host side
-// ---------------------------------------------------------------------------------
+// -------------------------------------------------------------------------------------
 static const char* kind_name(int k) {
   return k == BG_BED5 ? "BED5" : (k == BG_BED3_REST ? "BED3+rest" : "BED3");
 }
@@ -360,9 +535,19 @@ static int report_status(bg_ctx* c, int file, const bg_dstatus& h) {
   return bg_fail(c, rc, msg);
 }
 
-static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
+// per-input loader state between the passes
+struct LoadState {
+  const uint8_t* txt = nullptr;
+  uint64_t nb = 0;
+  uint32_t ntiles = 0;
+  uint64_t* row0 = nullptr;  // tile row offsets (device)
+  std::vector<int64_t> run_pos;
+  std::vector<uint64_t> run_hash;
+};
+
+// pass 1: text to HBM, scout, row offsets, chromosome runs
+static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S) {
   T->kind = in.kind;
-  // text into HBM
   const uint8_t* txt;
   if (in.on_device) {
     if (((uintptr_t)in.data & 15) != 0) return bg_fail(c, BG_E_ARG, "device text must be 16-byte aligned");
@@ -376,36 +561,133 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
   }
   T->text = (const char*)txt;
   T->nbytes = in.nbytes;
-  const uint64_t nb = in.nbytes;
-  const unsigned ntiles = nb ? bg_blocks(nb, TXT_TILE) : 0;
-  if (ntiles == 0) {  // empty input: valid, zero rows; keep every column non-null
-    T->n = 0;
-    T->ks = (int64_t*)bg_alloc(c, 8);
-    T->ke = (int64_t*)bg_alloc(c, 8);
-    if (in.kind == BG_BED3_REST) {
-      T->rest_off = (uint64_t*)bg_alloc(c, 8);
-      T->rest_len = (uint32_t*)bg_alloc(c, 4);
-    }
-    if (in.kind == BG_BED5) T->score = (double*)bg_alloc(c, 8);
-    T->run_row0.assign(1, 0);
-    return 0;
-  }
-  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * ntiles);
-  uint64_t* row0 = (uint64_t*)bg_alloc(c, 8ull * ntiles);
-  int64_t* lastnl = (int64_t*)bg_alloc(c, 8ull * ntiles);
-  int64_t* prevnl = (int64_t*)bg_alloc(c, 8ull * ntiles);
-  uint64_t* d_rows = (uint64_t*)bg_alloc(c, 8);
-  if (!cnt || !row0 || !lastnl || !prevnl || !d_rows) return BG_E_NOMEM;
-  BG_LAUNCH(c, "k_nl_count", k_nl_count, dim3(ntiles), dim3(BG_NT), txt, nb, cnt, lastnl);
+  S.txt = txt;
+  S.nb = in.nbytes;
+  S.ntiles = in.nbytes ? bg_blocks(in.nbytes, TT) : 0;
+  if (S.ntiles == 0) return 0;
+  const uint32_t nt = S.ntiles;
+  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
+  S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
+  int64_t* fls = (int64_t*)bg_alloc(c, 8ull * nt);
+  uint64_t* fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
+  uint32_t* blist = (uint32_t*)bg_alloc(c, 4ull * nt);
+  // small counters block: [0] rows, [1] nboundary (u32), [2] nrec (u32)
+  uint64_t* ctr = (uint64_t*)bg_alloc(c, 64);
+  const uint32_t RC = std::min<uint32_t>(REC_CAP, 4 * nt + 16);
+  int64_t* rpos = (int64_t*)bg_alloc(c, 8ull * RC);
+  uint64_t* rhash = (uint64_t*)bg_alloc(c, 8ull * RC);
+  int64_t* rtok = (int64_t*)bg_alloc(c, 8ull * RC);
+  uint32_t* rlen = (uint32_t*)bg_alloc(c, 4ull * RC);
+  if (!cnt || !S.row0 || !fls || !fhash || !blist || !ctr || !rpos || !rhash || !rtok || !rlen)
+    return BG_E_NOMEM;
+  BG_HIP(c, hipMemsetAsync(ctr, 0, 64, c->stream));
+  BG_LAUNCH(c, "k_scout", k_scout, dim3(nt), dim3(BG_NT), txt, S.nb, cnt, fls, fhash);
   BG_HIP(c, hipGetLastError());
-  int rc = bg_scan_sum_u64(c, cnt, row0, ntiles, d_rows);
+  int rc = bg_scan_sum_u64(c, cnt, S.row0, nt, &ctr[0]);
   if (rc) return rc;
-  rc = bg_scan_max_i64(c, lastnl, prevnl, ntiles, -1);
-  if (rc) return rc;
-  uint64_t rows = 0;
-  if ((rc = bg_fetch_u64(c, d_rows, &rows))) return rc;
-  T->n = rows;
-  const uint64_t na = rows ? rows : 1;
+  uint32_t* nbound = reinterpret_cast<uint32_t*>(&ctr[1]);
+  uint32_t* nrec = reinterpret_cast<uint32_t*>(&ctr[2]);
+  BG_LAUNCH(c, "k_boundary", k_boundary, dim3(bg_blocks(nt, 256)), dim3(256), fls, fhash, nt, blist,
+            nbound);
+  BG_HIP(c, hipGetLastError());
+  uint64_t hc[3];
+  BG_HIP(c, hipMemcpyAsync(hc, ctr, 24, hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  T->n = hc[0];
+  const uint32_t nbd = (uint32_t)hc[1];
+  if (nbd) {
+    BG_LAUNCH(c, "k_tile_runs", k_tile_runs, dim3(nbd), dim3(BG_NT), txt, S.nb, blist, fls, fhash,
+              nt, rpos, rhash, rtok, rlen, nrec);
+    BG_HIP(c, hipGetLastError());
+  }
+  uint32_t nr = 0;
+  BG_HIP(c, hipMemcpyAsync(&nr, nrec, 4, hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  if (nr > RC) return bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input");
+  std::vector<int64_t> pos(nr), tok(nr);
+  std::vector<uint64_t> hs(nr);
+  std::vector<uint32_t> len(nr);
+  if (nr) {
+    BG_HIP(c, hipMemcpyAsync(pos.data(), rpos, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipMemcpyAsync(hs.data(), rhash, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  // runs: records by position, consecutive duplicates removed
+  std::vector<uint32_t> ord(nr);
+  for (uint32_t k = 0; k < nr; ++k) ord[k] = k;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return pos[a] < pos[b]; });
+  std::vector<uint32_t> keep;
+  for (uint32_t k : ord) {
+    if (!keep.empty() && pos[keep.back()] == pos[k]) continue;
+    if (!keep.empty() && hs[keep.back()] == hs[k]) continue;
+    keep.push_back(k);
+  }
+  // names of the runs
+  const uint32_t nk = (uint32_t)keep.size();
+  std::vector<char> names(128ull * (nk ? nk : 1));
+  if (nk) {
+    std::vector<int64_t> ktok(nk);
+    std::vector<uint32_t> klen(nk);
+    // record spans are on the device; gather them by index
+    std::vector<int64_t> all_tok(nr);
+    std::vector<uint32_t> all_len(nr);
+    BG_HIP(c, hipMemcpyAsync(all_tok.data(), rtok, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipMemcpyAsync(all_len.data(), rlen, 4ull * nr, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < nk; ++i) {
+      ktok[i] = all_tok[keep[i]];
+      klen[i] = all_len[keep[i]];
+      if (klen[i] > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
+    }
+    int64_t* d_tok = (int64_t*)bg_alloc(c, 8ull * nk);
+    uint32_t* d_len = (uint32_t*)bg_alloc(c, 4ull * nk);
+    char* d_names = (char*)bg_alloc(c, 128ull * nk);
+    if (!d_tok || !d_len || !d_names) return BG_E_NOMEM;
+    BG_HIP(c, hipMemcpyAsync(d_tok, ktok.data(), 8ull * nk, hipMemcpyHostToDevice, c->stream));
+    BG_HIP(c, hipMemcpyAsync(d_len, klen.data(), 4ull * nk, hipMemcpyHostToDevice, c->stream));
+    BG_LAUNCH(c, "k_gather_tokens", k_gather_tokens, dim3(bg_blocks(nk, 256)), dim3(256), txt,
+              d_tok, d_len, nk, d_names);
+    BG_HIP(c, hipGetLastError());
+    BG_HIP(c, hipMemcpyAsync(names.data(), d_names, 128ull * nk, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipStreamSynchronize(c->stream));
+    bg_release(c, d_tok);
+    bg_release(c, d_len);
+    bg_release(c, d_names);
+  }
+  T->run_name.clear();
+  S.run_pos.clear();
+  S.run_hash.clear();
+  for (uint32_t i = 0; i < nk; ++i) {
+    const uint32_t k = keep[i];
+    S.run_pos.push_back(pos[k]);
+    S.run_hash.push_back(hs[k]);
+    T->run_name.emplace_back(&names[128ull * i], strnlen(&names[128ull * i], 128));
+  }
+  for (size_t k = 1; k < T->run_name.size(); ++k) {
+    if (strcmp(T->run_name[k - 1].c_str(), T->run_name[k].c_str()) >= 0) {
+      char msg[400];
+      snprintf(msg, sizeof(msg),
+               "input %d: chromosome '%s' follows '%s' (%s input is not sorted per sort-bed)",
+               idx + 1, T->run_name[k].c_str(), T->run_name[k - 1].c_str(), kind_name(in.kind));
+      return bg_fail(c, BG_E_UNSORTED, msg);
+    }
+  }
+  bg_release(c, cnt);
+  bg_release(c, fls);
+  bg_release(c, fhash);
+  bg_release(c, blist);
+  bg_release(c, ctr);
+  bg_release(c, rpos);
+  bg_release(c, rhash);
+  bg_release(c, rtok);
+  bg_release(c, rlen);
+  return 0;
+}
+
+// pass 2: keyed parse with the global dictionary
+static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S,
+                     const std::map<std::string, int32_t>& gid) {
+  const uint64_t na = T->n ? T->n : 1;
   T->ks = (int64_t*)bg_alloc(c, 8 * na);
   T->ke = (int64_t*)bg_alloc(c, 8 * na);
   if (!T->ks || !T->ke) return BG_E_NOMEM;
@@ -418,73 +700,58 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T) {
     T->score = (double*)bg_alloc(c, 8 * na);
     if (!T->score) return BG_E_NOMEM;
   }
-  uint64_t* run_row = (uint64_t*)bg_alloc(c, 8ull * RUN_CAP);
-  uint64_t* run_tok = (uint64_t*)bg_alloc(c, 8ull * RUN_CAP);
-  uint32_t* run_len = (uint32_t*)bg_alloc(c, 4ull * RUN_CAP);
-  if (!run_row || !run_tok || !run_len) return BG_E_NOMEM;
-  BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
-  BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
-  if (rows) {
-    BG_LAUNCH(c, "k_parse", k_parse, dim3(ntiles), dim3(BG_NT), txt, nb, cnt, row0,
-                       prevnl, in.kind, (uint64_t*)T->ks, (uint64_t*)T->ke, T->rest_off,
-                       T->rest_len, T->score, run_row, run_tok, run_len, c->dstat);
-    BG_HIP(c, hipGetLastError());
+  const uint32_t nr = (uint32_t)S.run_pos.size();
+  T->run_row0.assign(1, 0);
+  if (S.ntiles == 0 || T->n == 0 || nr == 0) {
+    T->run_row0.assign(1, 0);
+    T->run_name.clear();
+    return 0;
   }
+  std::vector<int32_t> g(nr);
+  for (uint32_t k = 0; k < nr; ++k) g[k] = gid.at(T->run_name[k]);
+  int64_t* d_pos = (int64_t*)bg_alloc(c, 8ull * nr);
+  uint64_t* d_hash = (uint64_t*)bg_alloc(c, 8ull * nr);
+  int32_t* d_gid = (int32_t*)bg_alloc(c, 4ull * nr);
+  uint64_t* d_row = (uint64_t*)bg_alloc(c, 8ull * nr);
+  if (!d_pos || !d_hash || !d_gid || !d_row) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(d_pos, S.run_pos.data(), 8ull * nr, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemcpyAsync(d_hash, S.run_hash.data(), 8ull * nr, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemcpyAsync(d_gid, g.data(), 4ull * nr, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemsetAsync(d_row, 0xff, 8ull * nr, c->stream));
+  RunTable R{d_pos, d_hash, d_gid, d_row, nr};
+  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0,
+            in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, c->dstat);
+  BG_HIP(c, hipGetLastError());
+  BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
+            S.row0, S.ntiles, T->n, c->dstat);
+  BG_HIP(c, hipGetLastError());
+  std::vector<uint64_t> rows(nr);
+  BG_HIP(c, hipMemcpyAsync(rows.data(), d_row, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
-  bg_dstatus h = *c->hstat;
-  if ((rc = report_status(c, idx, h))) return rc;
-  if (h.nruns > RUN_CAP) return bg_fail(c, BG_E_UNSUPPORTED, "more than 2^20 chromosome runs in one input");
-  if (in.kind == BG_BED5 && (h.flags & 1ULL)) T->score_int = false;
-  // fetch run records
-  const uint64_t nr = h.nruns;
-  std::vector<uint64_t> rr(nr);
-  std::vector<char> names(nr * 128);
-  if (nr) {
-    char* d_names = (char*)bg_alloc(c, nr * 128);
-    if (!d_names) return BG_E_NOMEM;
-    BG_LAUNCH(c, "k_gather_tokens", k_gather_tokens, dim3(bg_blocks(nr, 256)), dim3(256), txt,
-                       run_tok, run_len, nr, d_names);
-    BG_HIP(c, hipGetLastError());
-    BG_HIP(c, hipMemcpyAsync(rr.data(), run_row, 8 * nr, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipMemcpyAsync(names.data(), d_names, nr * 128, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipStreamSynchronize(c->stream));
-    bg_release(c, d_names);
-  }
-  std::vector<uint64_t> order(nr);
-  for (uint64_t k = 0; k < nr; ++k) order[k] = k;
-  std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return rr[a] < rr[b]; });
+  int rc = report_status(c, idx, *c->hstat);
+  if (rc) return rc;
+  if (in.kind == BG_BED5 && (c->hstat->flags & 1ULL)) T->score_int = false;
+  T->has_zero_len = (c->hstat->flags & 2ULL) != 0;
+  // a trailing run may own only the dropped unterminated last line: no rows
+  uint32_t nkeep = nr;
+  while (nkeep > 0 && rows[nkeep - 1] == ~0ULL) --nkeep;
+  T->run_name.resize(nkeep);
   T->run_row0.clear();
-  T->run_name.clear();
-  for (uint64_t k : order) {
-    T->run_row0.push_back(rr[k]);
-    T->run_name.emplace_back(&names[k * 128], strnlen(&names[k * 128], 128));
-  }
-  for (size_t k = 1; k < T->run_name.size(); ++k) {
-    if (strcmp(T->run_name[k - 1].c_str(), T->run_name[k].c_str()) >= 0) {
-      char msg[320];
-      snprintf(msg, sizeof(msg),
-               "input %d, data line %llu: chromosome '%s' follows '%s' (%s input is not sorted "
-               "per sort-bed)",
-               idx + 1, (unsigned long long)T->run_row0[k] + 1, T->run_name[k].c_str(),
-               T->run_name[k - 1].c_str(), kind_name(in.kind));
-      return bg_fail(c, BG_E_UNSORTED, msg);
-    }
-  }
-  T->run_row0.push_back(rows);
-  bg_release(c, run_row);
-  bg_release(c, run_tok);
-  bg_release(c, run_len);
-  bg_release(c, cnt);
-  bg_release(c, row0);
-  bg_release(c, lastnl);
-  bg_release(c, prevnl);
-  bg_release(c, d_rows);
+  for (uint32_t k = 0; k < nkeep; ++k) T->run_row0.push_back(rows[k]);
+  T->run_row0.push_back(T->n);
+  for (uint32_t k = 0; k < nkeep; ++k)
+    if (rows[k] == ~0ULL) return bg_fail(c, BG_E_PARSE, "internal: chromosome run without a row");
+  bg_release(c, d_pos);
+  bg_release(c, d_hash);
+  bg_release(c, d_gid);
+  bg_release(c, d_row);
+  bg_release(c, S.row0);
+  S.row0 = nullptr;
   return 0;
 }
 
-int bg_key_tables(bg_ctx* c, bg_set* s) {
-  // global dictionary: union of names, strcmp order
+static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>& gid) {
   std::vector<std::string> all;
   for (bg_table* T : s->t)
     for (auto& nm : T->run_name) all.push_back(nm);
@@ -493,9 +760,7 @@ int bg_key_tables(bg_ctx* c, bg_set* s) {
   all.erase(std::unique(all.begin(), all.end()), all.end());
   if (all.size() >= (1u << 22)) return bg_fail(c, BG_E_UNSUPPORTED, "too many chromosomes");
   s->names = all;
-  std::map<std::string, int32_t> gid;
   for (size_t k = 0; k < all.size(); ++k) gid[all[k]] = (int32_t)k;
-  // packed names on device
   std::vector<uint32_t> off(all.size() + 1, 0), len(all.size() + 1, 0);
   std::string packed;
   for (size_t k = 0; k < all.size(); ++k) {
@@ -512,34 +777,7 @@ int bg_key_tables(bg_ctx* c, bg_set* s) {
     BG_HIP(c, hipMemcpyAsync(s->d_names, packed.data(), packed.size(), hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemcpyAsync(s->d_name_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemcpyAsync(s->d_name_len, len.data(), 4 * len.size(), hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
-  BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
-  std::vector<uint64_t*> tmp_rows;
-  std::vector<int32_t*> tmp_gid;
-  for (size_t f = 0; f < s->t.size(); ++f) {
-    bg_table* T = s->t[f];
-    if (T->n == 0) continue;
-    const uint32_t nr = (uint32_t)T->run_name.size();
-    std::vector<int32_t> g(nr);
-    for (uint32_t k = 0; k < nr; ++k) g[k] = gid[T->run_name[k]];
-    uint64_t* d_r0 = (uint64_t*)bg_alloc(c, 8ull * (nr + 1));
-    int32_t* d_g = (int32_t*)bg_alloc(c, 4ull * nr);
-    if (!d_r0 || !d_g) return BG_E_NOMEM;
-    // copies are from pageable vectors: make them synchronous w.r.t. the host below
-    BG_HIP(c, hipMemcpyAsync(d_r0, T->run_row0.data(), 8ull * (nr + 1), hipMemcpyHostToDevice, c->stream));
-    BG_HIP(c, hipMemcpyAsync(d_g, g.data(), 4ull * nr, hipMemcpyHostToDevice, c->stream));
-    BG_LAUNCH(c, "k_key", k_key, dim3(bg_blocks(T->n, BG_NT)), dim3(BG_NT), T->ks, T->ke,
-                       T->n, d_r0, d_g, nr, c->dstat);
-    BG_HIP(c, hipGetLastError());
-    BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipStreamSynchronize(c->stream));
-    bg_release(c, d_r0);
-    bg_release(c, d_g);
-    int rc = report_status(c, (int)f, *c->hstat);
-    if (rc) return rc;
-    T->has_zero_len = (c->hstat->flags & 2ULL) != 0;
-    BG_HIP(c, hipMemsetAsync(&c->dstat->flags, 0, 8, c->stream));
-  }
+  BG_HIP(c, hipStreamSynchronize(c->stream));  // host vectors go out of scope
   return 0;
 }
 
@@ -548,16 +786,35 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   *out = nullptr;
   bg_set* s = new bg_set();
   s->ctx = c;
-  for (int i = 0; i < n; ++i) {
+  std::vector<LoadState> st(n);
+  int rc = 0;
+  for (int i = 0; i < n && !rc; ++i) {
     bg_table* T = new bg_table();
     s->t.push_back(T);
-    int rc = parse_one(c, i, inputs[i], T);
-    if (rc) { bg_set_free(s); return rc; }
+    rc = scout_one(c, i, inputs[i], T, st[i]);
   }
+  bg_mark(c, "scout");
+  std::map<std::string, int32_t> gid;
+  if (!rc) rc = build_dictionary(c, s, gid);
+  if (!rc) {
+    rc = bg_hip_ok(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
+  }
+  for (int i = 0; i < n && !rc; ++i) {
+    rc = parse_one(c, i, inputs[i], s->t[i], st[i], gid);
+    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->flags, 0, 8, c->stream));
+  }
+  for (auto& S : st) bg_release(c, S.row0);
+  if (rc) {
+    bg_set_free(s);
+    return rc;
+  }
+  for (bg_table* T : s->t)  // keep every column non-null for empty inputs
+    if (!T->ks) {
+      T->ks = (int64_t*)bg_alloc(c, 8);
+      T->ke = (int64_t*)bg_alloc(c, 8);
+    }
   bg_mark(c, "parse");
-  int rc = bg_key_tables(c, s);
-  if (rc) { bg_set_free(s); return rc; }
-  bg_mark(c, "key");
   *out = s;
   return 0;
 }

@@ -1,0 +1,125 @@
+// bg_parse.h — branch-free BED field extraction shared by the GPU loader and its CPU
+// unit test (tests/cpu/test_parse_helpers.cpp compiles this header with g++).
+//
+// A line's first 32 bytes are held as 8 little-endian dwords W[0..7]. Per dword, SWAR
+// byte classification yields 4-bit groups for "whitespace" ({' ', \t..\r}) and "digit";
+// the fields (chrom token, start digits, end digits) then fall out of count-trailing-
+// zeros on the two 32-bit masks, and each number is converted 8 digits at a time with
+// the 3-multiply SWAR decimal conversion. Anything the masks cannot decide (fields past
+// 32 bytes, '+' signs, > 16 digits, malformed text) returns 0 and the caller takes the
+// byte-by-byte path, which applies the full grammar and reports errors.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define BG_HD __host__ __device__ __forceinline__
+#else
+#define BG_HD static inline
+#endif
+
+BG_HD uint32_t bgp_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+
+// bit 7 of each byte of m80 -> 4-bit group (byte 0 -> bit 0)
+BG_HD uint32_t bgp_group4(uint32_t m80) {
+  return ((((m80 >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// per-byte classes of one dword: ws4 = {' ', 0x09..0x0D}, dg4 = {'0'..'9'}
+BG_HD void bgp_classify(uint32_t x, uint32_t& ws4, uint32_t& dg4) {
+  const uint32_t hi = x & 0x80808080u;  // bytes >= 0x80 are neither
+  const uint32_t lo7 = x & 0x7F7F7F7Fu;
+  const uint32_t y = lo7 ^ 0x20202020u;
+  const uint32_t nz20 = (y + 0x7F7F7F7Fu) & 0x80808080u;
+  const uint32_t eq20 = ~nz20 & 0x80808080u;
+  const uint32_t ge9 = (lo7 + 0x77777777u) & 0x80808080u;
+  const uint32_t ge14 = (lo7 + 0x72727272u) & 0x80808080u;
+  const uint32_t ws = (eq20 | (ge9 & ~ge14)) & ~hi & 0x80808080u;
+  const uint32_t ge48 = (lo7 + 0x50505050u) & 0x80808080u;
+  const uint32_t ge58 = (lo7 + 0x46464646u) & 0x80808080u;
+  const uint32_t dg = ge48 & ~ge58 & ~hi & 0x80808080u;
+  ws4 = bgp_group4(ws);
+  dg4 = bgp_group4(dg);
+}
+
+// bytes [o, o+4) of the 8-byte little-endian sequence (lo, hi), o in 0..3
+BG_HD uint32_t bgp_align(uint32_t lo, uint32_t hi, uint32_t o) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, o);
+#else
+  return o ? (lo >> (8 * o)) | (hi << (32 - 8 * o)) : lo;
+#endif
+}
+
+// value of the first L (1..8) ASCII digits of v (first digit in the low byte)
+BG_HD uint64_t bgp_swar8(uint64_t v, int L) {
+  v -= 0x3030303030303030ull;
+  v <<= 8 * (8 - L);
+  v = (v * 10) + (v >> 8);
+  v = (((v & 0x000000FF000000FFull) * (100 + (1000000ull << 32))) +
+       (((v >> 16) & 0x000000FF000000FFull) * (1 + (10000ull << 32)))) >> 32;
+  return v;
+}
+
+// value of L (1..16) ASCII digits held in lo8 (digits 0..7) and hi8 (8..15)
+BG_HD uint64_t bgp_digits(uint64_t lo8, uint64_t hi8, int L) {
+  if (L <= 8) return bgp_swar8(lo8, L);
+  const int h = L - 8;  // leading digits, then the last 8
+  const uint64_t head = bgp_swar8(lo8, h);
+  const uint64_t tail = (h == 8) ? hi8 : ((lo8 >> (8 * h)) | (hi8 << (64 - 8 * h)));
+  return head * 100000000ull + bgp_swar8(tail, 8);
+}
+
+struct BgpFields {
+  uint32_t a0, a1;  // chrom token [a0, a1)
+  uint32_t s0, s1;  // start digits
+  uint32_t e0, e1;  // end digits; rest starts at e1
+};
+
+// W: bytes [0, 32) of the line; len: line length (bytes before '\n').
+// returns 1: fields found; 0: undecided here (use the byte path); -1: blank line
+BG_HD int bgp_fields(const uint32_t W[8], uint32_t len, BgpFields& F) {
+  uint32_t WS = 0, DG = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t w4, d4;
+    bgp_classify(W[i], w4, d4);
+    WS |= w4 << (4 * i);
+    DG |= d4 << (4 * i);
+  }
+  if (len < 32) {  // bytes past the line end act as whitespace
+    const uint32_t endm = ~0u << len;
+    WS |= endm;
+    DG &= ~endm;
+  }
+  const uint32_t NW = ~WS;
+  if (NW == 0) return len <= 32 ? -1 : 0;
+  F.a0 = bgp_ctz(NW);
+  uint32_t m = WS & (~0u << F.a0);
+  if (!m) return 0;
+  F.a1 = bgp_ctz(m);
+  if (F.a1 >= 31) return 0;
+  m = NW & (~0u << F.a1);
+  if (!m) return 0;
+  F.s0 = bgp_ctz(m);
+  if (!((DG >> F.s0) & 1u)) return 0;
+  m = ~DG & (~0u << F.s0);
+  if (!m) return 0;
+  F.s1 = bgp_ctz(m);
+  if (!((WS >> F.s1) & 1u) || F.s1 >= 31) return 0;
+  m = NW & (~0u << F.s1);
+  if (!m) return 0;
+  F.e0 = bgp_ctz(m);
+  if (!((DG >> F.e0) & 1u)) return 0;
+  m = ~DG & (~0u << F.e0);
+  if (!m) return 0;  // end digits may continue past the window
+  F.e1 = bgp_ctz(m);
+  if (F.s1 - F.s0 > 16 || F.e1 - F.e0 > 16) return 0;
+  if (F.e1 > len) return 0;
+  return 1;
+}
+
+// FNV-1a 64 over a chromosome token (run identity; same function everywhere)
+#define BGP_FNV_OFF 1469598103934665603ull
+#define BGP_FNV_PRIME 1099511628211ull
+BG_HD uint64_t bgp_hash_step(uint64_t h, uint8_t b) { return (h ^ b) * BGP_FNV_PRIME; }
+BG_HD uint64_t bgp_hash_final(uint64_t h, uint32_t len) { return (h ^ len) * BGP_FNV_PRIME; }

@@ -21,29 +21,46 @@
 //  element_of(rows, O)  = exact covered bp by two binary searches + prefix sums of
 //                         component lengths, then the reference's double-precision
 //                         test (:1094-1096)
-// Count pass and write pass share one device function per kernel (reduce-then-scan
-// between them), so outputs are deterministic and exactly sized.
+// Memory access: every kernel reads its inputs coalesced. components() uses a
+// wave-striped layout (lane l of wave w handles rows w*W + k*64 + l) with 64-lane
+// max-scans and ballots; the merge-path kernels stage each 2048-element diagonal tile
+// of both inputs in LDS first. Count pass and write pass share one device function
+// (reduce-then-scan between them), so outputs are deterministic and exactly sized.
 #include <climits>
 
 #include "bg_internal.h"
 
-#define CT_ITEMS 16
-#define CT_TILE (BG_NT * CT_ITEMS)
+#define CT_ITEMS 8                    // rows per lane per wave in components()
+#define CT_WROWS (64 * CT_ITEMS)      // rows per wave
+#define CT_TILE (BG_NT * CT_ITEMS)    // rows per workgroup (4 waves)
 #define MP_ITEMS 8
-#define MP_TILE (BG_NT * MP_ITEMS)
+#define MP_TILE (BG_NT * MP_ITEMS)    // merged elements per workgroup
+
+__device__ __forceinline__ int64_t wave_max_all(int64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (int64_t)__shfl_xor(v, d, 64));
+  return v;
+}
 
 // ------------------------------- components ---------------------------------------
 __global__ void __launch_bounds__(BG_NT) k_tile_max(const int64_t* __restrict__ E, uint64_t n,
                                                     int64_t* __restrict__ tmax) {
-  __shared__ int64_t sh[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE + (uint64_t)threadIdx.x * CT_ITEMS;
+  __shared__ int64_t wm[BG_NT / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE;
   int64_t m = LLONG_MIN;
 #pragma unroll
-  for (int k = 0; k < CT_ITEMS; ++k)
-    if (base + k < n) m = max(m, E[base + k]);
-  int64_t tot;
-  (void)block_excl_scan(m, OpMax(), (int64_t)LLONG_MIN, sh, &tot);
-  if (threadIdx.x == 0) tmax[blockIdx.x] = tot;
+  for (int k = 0; k < CT_ITEMS; ++k) {
+    const uint64_t i = base + (uint64_t)k * BG_NT + threadIdx.x;
+    if (i < n) m = max(m, E[i]);
+  }
+  m = wave_max_all(m);
+  if (bg_lane() == 0) wm[bg_wave()] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = wm[0];
+    for (int w = 1; w < BG_NT / 64; ++w) t = max(t, wm[w]);
+    tmax[blockIdx.x] = t;
+  }
 }
 
 template <bool WRITE>
@@ -51,47 +68,67 @@ __global__ void __launch_bounds__(BG_NT) k_components(
     const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
     const int64_t* __restrict__ carry, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
     int64_t* __restrict__ CS, int64_t* __restrict__ CE) {
-  __shared__ int64_t shm[BG_NT / 64 + 1];
-  __shared__ uint32_t shc[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE + (uint64_t)threadIdx.x * CT_ITEMS;
+  __shared__ int64_t wmax[BG_NT / 64];
+  __shared__ uint32_t wcnt[BG_NT / 64];
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t wbase = (uint64_t)blockIdx.x * CT_TILE + (uint64_t)w * CT_WROWS;
   int64_t vs[CT_ITEMS], ve[CT_ITEMS];
   int64_t lm = LLONG_MIN;
 #pragma unroll
   for (int k = 0; k < CT_ITEMS; ++k) {
-    const bool in = base + k < n;
-    vs[k] = in ? S[base + k] : LLONG_MAX;
-    ve[k] = in ? E[base + k] : LLONG_MIN;
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    const bool in = i < n;
+    vs[k] = in ? S[i] : LLONG_MAX;
+    ve[k] = in ? E[i] : LLONG_MIN;
     lm = max(lm, ve[k]);
   }
-  int64_t tot;
-  int64_t run = block_excl_scan(lm, OpMax(), (int64_t)LLONG_MIN, shm, &tot);
-  run = max(run, carry[blockIdx.x]);
-  uint32_t flags = 0, c = 0;
+  lm = wave_max_all(lm);
+  if (lane == 0) wmax[w] = lm;
+  __syncthreads();
+  int64_t run = carry[blockIdx.x];
+  for (int q = 0; q < w; ++q) run = max(run, wmax[q]);
+  uint64_t bal[CT_ITEMS];
   int64_t incl[CT_ITEMS];
+  uint32_t c = 0;
 #pragma unroll
   for (int k = 0; k < CT_ITEMS; ++k) {
-    const bool in = base + k < n;
-    if (in && vs[k] > run) { flags |= 1u << k; ++c; }
-    run = max(run, ve[k]);
-    incl[k] = run;
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    const int64_t inc = wave_incl_scan(ve[k], OpMax());
+    int64_t ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = LLONG_MIN;
+    const bool f = (i < n) && vs[k] > max(run, ex);
+    incl[k] = max(run, inc);
+    bal[k] = __ballot(f);
+    c += __popcll(bal[k]);
+    run = max(run, (int64_t)__shfl(inc, 63, 64));
   }
-  uint32_t btot;
-  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  if (lane == 0) wcnt[w] = c;
+  __syncthreads();
   if (!WRITE) {
-    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    if (threadIdx.x == 0) {
+      uint64_t t = 0;
+      for (int q = 0; q < BG_NT / 64; ++q) t += wcnt[q];
+      cnt[blockIdx.x] = t;
+    }
     return;
   }
-  uint64_t q = off[blockIdx.x] + o;  // components opened before this thread's rows
+  uint64_t q0 = off[blockIdx.x];
+  for (int q = 0; q < w; ++q) q0 += wcnt[q];
+  const uint64_t lt = (1ULL << lane) - 1, le = lt | (1ULL << lane);
+  uint64_t before = 0;
 #pragma unroll
   for (int k = 0; k < CT_ITEMS; ++k) {
-    const uint64_t i = base + k;
-    if (i >= n) break;
-    if (flags & (1u << k)) CS[q++] = vs[k];
-    bool next_opens;
-    if (i + 1 >= n) next_opens = true;
-    else if (k + 1 < CT_ITEMS) next_opens = (flags >> (k + 1)) & 1u;
-    else next_opens = S[i + 1] > incl[k];
-    if (next_opens) CE[q - 1] = incl[k];
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    if (i < n) {
+      if ((bal[k] >> lane) & 1ULL) CS[q0 + before + __popcll(bal[k] & lt)] = vs[k];
+      bool next_opens;
+      if (i + 1 >= n) next_opens = true;
+      else if (lane < 63) next_opens = (bal[k] >> (lane + 1)) & 1ULL;
+      else if (k + 1 < CT_ITEMS) next_opens = bal[k + 1] & 1ULL;
+      else next_opens = S[i + 1] > incl[k];
+      if (next_opens) CE[q0 + before + __popcll(bal[k] & le) - 1] = incl[k];
+    }
+    before += __popcll(bal[k]);
   }
 }
 
@@ -113,86 +150,102 @@ __global__ void __launch_bounds__(BG_NT) k_merge_sorted(const int64_t* __restric
   }
 }
 
-// ------------------------------- intersect ----------------------------------------
-template <bool WRITE>
-__global__ void __launch_bounds__(BG_NT) k_intersect2(
+// ------------------------------- merge-path tiles ---------------------------------
+// part[b] = number of X elements among the first min(b*MP_TILE, nx+ny) elements of the
+// merge of X (key XK) and Y (key YK), ties Y first
+__global__ void k_mp_partition(const int64_t* __restrict__ XK, uint64_t nx,
+                               const int64_t* __restrict__ YK, uint64_t ny, uint32_t nparts,
+                               uint64_t* __restrict__ part) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nparts) return;
+  const uint64_t d = min((uint64_t)b * MP_TILE, nx + ny);
+  part[b] = merge_path_ystrict(XK, nx, YK, ny, d);
+}
+
+enum { MP_INTERSECT = 0, MP_DIFFERENCE = 1 };
+
+// One 2048-element diagonal tile of merge(X, Y). LDS holds X[i0-1 .. i1) then
+// Y[j0-1 .. j1] (+1 for difference's "next O start"); sentinels outside the arrays.
+//   MP_INTERSECT : X, Y = component lists, keys = starts
+//   MP_DIFFERENCE: X = reference components (key start), Y = other components (key end)
+template <int MODE, bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_mp_tile(
     const int64_t* __restrict__ XS, const int64_t* __restrict__ XE, uint64_t nx,
     const int64_t* __restrict__ YS, const int64_t* __restrict__ YE, uint64_t ny,
-    uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, int64_t* __restrict__ OS,
-    int64_t* __restrict__ OE) {
+    const uint64_t* __restrict__ part, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+    int64_t* __restrict__ OS, int64_t* __restrict__ OE) {
+  __shared__ int64_t ls_[MP_TILE + 4];
+  __shared__ int64_t le_[MP_TILE + 4];
   __shared__ uint32_t shc[BG_NT / 64 + 1];
-  const uint64_t d0 = ((uint64_t)blockIdx.x * BG_NT + threadIdx.x) * MP_ITEMS;
   const uint64_t nz = nx + ny;
+  const uint64_t d0 = (uint64_t)blockIdx.x * MP_TILE;
+  const uint64_t d1 = min(d0 + MP_TILE, nz);
+  const uint64_t i0 = part[blockIdx.x], i1 = part[blockIdx.x + 1];
+  const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+  const uint32_t nxl = (uint32_t)(i1 - i0), nyl = (uint32_t)(j1 - j0);
+  const uint32_t xb = 0, yb = nxl + 1;  // LDS slots: X[i0-1+q] at xb+q, Y[j0-1+q] at yb+q
+  for (uint32_t q = threadIdx.x; q < nxl + 1; q += BG_NT) {
+    const int64_t gi = (int64_t)i0 - 1 + q;
+    ls_[xb + q] = gi >= 0 ? XS[gi] : LLONG_MIN;
+    le_[xb + q] = gi >= 0 ? XE[gi] : LLONG_MIN;
+  }
+  for (uint32_t q = threadIdx.x; q < nyl + 2; q += BG_NT) {
+    const int64_t gj = (int64_t)j0 - 1 + q;
+    const bool in = gj >= 0 && (uint64_t)gj < ny;
+    ls_[yb + q] = in ? YS[gj] : (gj < 0 ? LLONG_MIN : LLONG_MAX);
+    le_[yb + q] = in ? YE[gj] : (gj < 0 ? LLONG_MIN : LLONG_MAX);
+  }
+  __syncthreads();
+  const int64_t* xk = ls_ + xb + 1;  // local X[0..nxl)
+  const int64_t* yk = (MODE == MP_INTERSECT ? ls_ : le_) + yb + 1;
   int64_t ps[MP_ITEMS], pe[MP_ITEMS];
   uint32_t c = 0;
-  if (d0 < nz) {
-    uint64_t i = merge_path_ystrict(XS, nx, YS, ny, d0), j = d0 - i;
-    int64_t lastx_e = i > 0 ? XE[i - 1] : LLONG_MIN;
-    int64_t lasty_e = j > 0 ? YE[j - 1] : LLONG_MIN;
-    for (int k = 0; k < MP_ITEMS && d0 + k < nz; ++k) {
-      const bool takex = i < nx && (j >= ny || XS[i] < YS[j]);
-      int64_t s, e, pend;
-      if (takex) {
-        s = XS[i]; e = XE[i]; pend = lasty_e; lastx_e = e; ++i;
+  const uint32_t dl = threadIdx.x * MP_ITEMS, dn = (uint32_t)(d1 - d0);
+  if (dl < dn) {
+    // local merge path on the LDS slices (ties: Y first)
+    uint32_t lo = dl > nyl ? dl - nyl : 0, hi = dl < nxl ? dl : nxl;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (xk[mid] < yk[dl - 1 - mid]) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t i = lo, j = dl - lo;  // local indices; global = i0 + i, j0 + j
+    for (int k = 0; k < MP_ITEMS && dl + k < dn; ++k) {
+      const bool takex = i < nxl && (j >= nyl || xk[i] < yk[j]);
+      if (MODE == MP_INTERSECT) {
+        int64_t s, e, pend;
+        if (takex) { s = ls_[xb + 1 + i]; e = le_[xb + 1 + i]; pend = le_[yb + j]; ++i; }
+        else { s = ls_[yb + 1 + j]; e = le_[yb + 1 + j]; pend = le_[xb + i]; ++j; }
+        const int64_t h = min(e, pend);
+        if (h > s) { ps[c] = s; pe[c] = h; ++c; }
       } else {
-        s = YS[j]; e = YE[j]; pend = lastx_e; lasty_e = e; ++j;
+        if (takex) {
+          const int64_t a = ls_[xb + 1 + i], b = le_[xb + 1 + i];
+          const int64_t qs = ls_[yb + 1 + j];  // first O ending after a (LLONG_MAX if none)
+          if (qs >= b) { ps[c] = a; pe[c] = b; ++c; }
+          else if (qs > a) { ps[c] = a; pe[c] = qs; ++c; }
+          ++i;
+        } else {
+          if (i0 + i > 0) {
+            const int64_t oe = le_[yb + 1 + j], rb = le_[xb + i];
+            if (rb > oe) {
+              const int64_t nxt = min(rb, ls_[yb + 2 + j]);
+              ps[c] = oe; pe[c] = nxt; ++c;
+            }
+          }
+          ++j;
+        }
       }
-      const int64_t hi = min(e, pend);
-      if (hi > s) { ps[c] = s; pe[c] = hi; ++c; }
     }
   }
   uint32_t btot;
-  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  const uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
   if (!WRITE) {
     if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
     return;
   }
   const uint64_t q = off[blockIdx.x] + o;
   for (uint32_t k = 0; k < c; ++k) { OS[q + k] = ps[k]; OE[q + k] = pe[k]; }
-}
-
-// ------------------------------- difference ---------------------------------------
-// R: reference components (by start); O: other components, merged against R by END.
-template <bool WRITE>
-__global__ void __launch_bounds__(BG_NT) k_difference(
-    const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
-    const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
-    uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, int64_t* __restrict__ DS,
-    int64_t* __restrict__ DE) {
-  __shared__ uint32_t shc[BG_NT / 64 + 1];
-  const uint64_t d0 = ((uint64_t)blockIdx.x * BG_NT + threadIdx.x) * MP_ITEMS;
-  const uint64_t nz = nr + no;
-  int64_t ps[MP_ITEMS], pe[MP_ITEMS];
-  uint32_t c = 0;
-  if (d0 < nz) {
-    uint64_t i = merge_path_ystrict(RS, nr, OE_, no, d0), j = d0 - i;
-    for (int k = 0; k < MP_ITEMS && d0 + k < nz; ++k) {
-      const bool taker = i < nr && (j >= no || RS[i] < OE_[j]);
-      if (taker) {
-        const int64_t a = RS[i], b = RE[i];
-        if (j >= no || OS_[j] >= b) { ps[c] = a; pe[c] = b; ++c; }
-        else if (OS_[j] > a) { ps[c] = a; pe[c] = OS_[j]; ++c; }
-        ++i;
-      } else {
-        if (i > 0) {
-          const int64_t oe = OE_[j], rb = RE[i - 1];
-          if (rb > oe) {
-            const int64_t nxt = (j + 1 < no) ? min(rb, OS_[j + 1]) : rb;
-            ps[c] = oe; pe[c] = nxt; ++c;
-          }
-        }
-        ++j;
-      }
-    }
-  }
-  uint32_t btot;
-  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
-  if (!WRITE) {
-    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
-    return;
-  }
-  const uint64_t q = off[blockIdx.x] + o;
-  for (uint32_t k = 0; k < c; ++k) { DS[q + k] = ps[k]; DE[q + k] = pe[k]; }
 }
 
 // ------------------------------- element-of ---------------------------------------
@@ -237,23 +290,30 @@ __global__ void __launch_bounds__(BG_NT) k_compact_flags(const uint8_t* __restri
                                                          uint64_t n, uint64_t* __restrict__ cnt,
                                                          const uint64_t* __restrict__ off,
                                                          uint64_t* __restrict__ rows) {
-  __shared__ uint32_t shc[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * CF_TILE + (uint64_t)threadIdx.x * CF_ITEMS;
-  uint32_t f = 0, c = 0;
+  __shared__ uint32_t wc[BG_NT / 64];
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t wbase = (uint64_t)blockIdx.x * CF_TILE + (uint64_t)w * 64 * CF_ITEMS;
+  uint64_t bal[CF_ITEMS];
+  uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < CF_ITEMS; ++k)
-    if (base + k < n && flag[base + k]) { f |= 1u << k; ++c; }
-  uint32_t btot;
-  uint32_t o = block_excl_scan(c, OpSum(), 0u, shc, &btot);
+  for (int k = 0; k < CF_ITEMS; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    bal[k] = __ballot(i < n && flag[i]);
+    c += __popcll(bal[k]);
+  }
+  if (lane == 0) wc[w] = c;
+  __syncthreads();
   if (!WRITE) {
-    if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
+    if (threadIdx.x == 0) cnt[blockIdx.x] = (uint64_t)wc[0] + wc[1] + wc[2] + wc[3];
     return;
   }
-  uint64_t q = off[blockIdx.x] + o;
-  while (f) {
-    int k = __ffs(f) - 1;
-    rows[q++] = base + k;
-    f &= f - 1;
+  uint64_t q = off[blockIdx.x];
+  for (int v = 0; v < w; ++v) q += wc[v];
+  const uint64_t lt = (1ULL << lane) - 1;
+#pragma unroll
+  for (int k = 0; k < CF_ITEMS; ++k) {
+    if ((bal[k] >> lane) & 1ULL) rows[q + __popcll(bal[k] & lt)] = wbase + (uint64_t)k * 64 + lane;
+    q += __popcll(bal[k]);
   }
 }
 
@@ -282,8 +342,7 @@ static int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
 
 // count pass -> scan -> allocate exact output -> write pass
 template <typename CountFn, typename WriteFn>
-static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint64_t* total,
-                            uint64_t** off_out) {
+static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint64_t* total) {
   uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
   uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
   if (!cnt || !d_tot) return BG_E_NOMEM;
@@ -297,8 +356,7 @@ static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint
   bg_release(c, d_tot);
   if ((rc = wf(cnt, *total))) return rc;
   BG_HIP(c, hipGetLastError());
-  if (off_out) *off_out = cnt;
-  else bg_release(c, cnt);
+  bg_release(c, cnt);
   return 0;
 }
 
@@ -316,18 +374,17 @@ static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
   rc = count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        BG_LAUNCH(c, "k_components_count", k_components<false>, dim3(nb), dim3(BG_NT), in.s, in.e, n,
-                           carry, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
-                           (int64_t*)nullptr);
+        BG_LAUNCH(c, "k_components_count", k_components<false>, dim3(nb), dim3(BG_NT), in.s, in.e,
+                  n, carry, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
       },
       [&](uint64_t* off, uint64_t tot) -> int {
         int r = ivl_alloc(c, out, tot);
         if (r) return r;
-        BG_LAUNCH(c, "k_components_write", k_components<true>, dim3(nb), dim3(BG_NT), in.s, in.e, n,
-                           carry, (uint64_t*)nullptr, off, out.s, out.e);
+        BG_LAUNCH(c, "k_components_write", k_components<true>, dim3(nb), dim3(BG_NT), in.s, in.e,
+                  n, carry, (uint64_t*)nullptr, off, out.s, out.e);
         return 0;
       },
-      &total, nullptr);
+      &total);
   bg_release(c, carry);
   return rc;
 }
@@ -336,53 +393,42 @@ static int merge_sorted(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& z) {
   int rc = ivl_alloc(c, z, x.n + y.n);
   if (rc) return rc;
   if (x.n + y.n == 0) return 0;
-  BG_LAUNCH(c, "k_merge_sorted", k_merge_sorted, dim3(bg_blocks(x.n + y.n, MP_TILE)), dim3(BG_NT), x.s, x.e, x.n, y.s, y.e, y.n, z.s, z.e);
+  BG_LAUNCH(c, "k_merge_sorted", k_merge_sorted, dim3(bg_blocks(x.n + y.n, MP_TILE)), dim3(BG_NT),
+            x.s, x.e, x.n, y.s, y.e, y.n, z.s, z.e);
   BG_HIP(c, hipGetLastError());
   return 0;
 }
 
-static int intersect2(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out) {
+// merge-path tile operation over X and Y (MODE: intersect / difference)
+template <int MODE>
+static int mp_op(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out, const char* cname,
+                 const char* wname) {
   const uint64_t nz = x.n + y.n;
   const unsigned nb = bg_blocks(nz, MP_TILE);
+  if (nb == 0) return ivl_alloc(c, out, 0);
+  uint64_t* part = (uint64_t*)bg_alloc(c, 8ull * (nb + 1));
+  if (!part) return BG_E_NOMEM;
+  const int64_t* yk = (MODE == MP_INTERSECT) ? y.s : y.e;
+  BG_LAUNCH(c, "k_mp_partition", k_mp_partition, dim3(bg_blocks(nb + 1, 256)), dim3(256), x.s, x.n,
+            yk, y.n, nb, part);
+  BG_HIP(c, hipGetLastError());
   uint64_t total = 0;
-  return count_scan_write(
+  int rc = count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        BG_LAUNCH(c, "k_intersect2_count", k_intersect2<false>, dim3(nb), dim3(BG_NT), x.s, x.e, x.n,
-                           y.s, y.e, y.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
-                           (int64_t*)nullptr);
+        BG_LAUNCH(c, cname, (k_mp_tile<MODE, false>), dim3(nb), dim3(BG_NT), x.s, x.e, x.n, y.s, y.e,
+                  y.n, part, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
       },
       [&](uint64_t* off, uint64_t tot) -> int {
         int r = ivl_alloc(c, out, tot);
         if (r) return r;
-        if (nb)
-          BG_LAUNCH(c, "k_intersect2_write", k_intersect2<true>, dim3(nb), dim3(BG_NT), x.s, x.e,
-                             x.n, y.s, y.e, y.n, (uint64_t*)nullptr, off, out.s, out.e);
+        BG_LAUNCH(c, wname, (k_mp_tile<MODE, true>), dim3(nb), dim3(BG_NT), x.s, x.e, x.n, y.s, y.e,
+                  y.n, part, (uint64_t*)nullptr, off, out.s, out.e);
         return 0;
       },
-      &total, nullptr);
-}
-
-static int difference2(bg_ctx* c, const Ivl& r, const Ivl& o, Ivl& out) {
-  const uint64_t nz = r.n + o.n;
-  const unsigned nb = bg_blocks(nz, MP_TILE);
-  uint64_t total = 0;
-  return count_scan_write(
-      c, nb,
-      [&](uint64_t* cnt) {
-        BG_LAUNCH(c, "k_difference_count", k_difference<false>, dim3(nb), dim3(BG_NT), r.s, r.e, r.n,
-                           o.s, o.e, o.n, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr,
-                           (int64_t*)nullptr);
-      },
-      [&](uint64_t* off, uint64_t tot) -> int {
-        int rr = ivl_alloc(c, out, tot);
-        if (rr) return rr;
-        if (nb)
-          BG_LAUNCH(c, "k_difference_write", k_difference<true>, dim3(nb), dim3(BG_NT), r.s, r.e,
-                             r.n, o.s, o.e, o.n, (uint64_t*)nullptr, off, out.s, out.e);
-        return 0;
-      },
-      &total, nullptr);
+      &total);
+  bg_release(c, part);
+  return rc;
 }
 
 static Ivl table_ivl(bg_table* T) {
@@ -460,7 +506,7 @@ extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg
   for (int k = 1; k < nf; ++k) {
     Ivl ck, p;
     if ((rc = components(c, table_ivl(set->t[files[k]]), ck))) return rc;
-    if ((rc = intersect2(c, acc, ck, p))) return rc;
+    if ((rc = mp_op<MP_INTERSECT>(c, acc, ck, p, "k_intersect_count", "k_intersect_write"))) return rc;
     ivl_free(c, acc);
     ivl_free(c, ck);
     acc = p;
@@ -478,7 +524,7 @@ extern "C" int bg_difference(bg_ctx* c, bg_set* set, int ref, const int* others,
   Ivl r, o, d;
   if ((rc = components(c, table_ivl(set->t[ref]), r))) return rc;
   if ((rc = union_components(c, set, others, no, o))) return rc;
-  if ((rc = difference2(c, r, o, d))) return rc;
+  if ((rc = mp_op<MP_DIFFERENCE>(c, r, o, d, "k_difference_count", "k_difference_write"))) return rc;
   ivl_free(c, r);
   ivl_free(c, o);
   *out = new_ivl_result(c, set, d);
@@ -498,14 +544,13 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   uint8_t* flag = (uint8_t*)bg_alloc(c, R->n ? R->n : 1);
   if (!P || !flag) return BG_E_NOMEM;
   if (o.n) {
-    BG_LAUNCH(c, "k_lengths", k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), o.s, o.e,
-                       o.n, P);
+    BG_LAUNCH(c, "k_lengths", k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), o.s, o.e, o.n, P);
     BG_HIP(c, hipGetLastError());
   }
   if ((rc = bg_scan_sum_u64(c, P, P, o.n, P + o.n))) return rc;
   if (R->n) {
     BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
-                       R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
+              R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
     BG_HIP(c, hipGetLastError());
   }
   const unsigned nb = bg_blocks(R->n, CF_TILE);
@@ -514,18 +559,18 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   rc = count_scan_write(
       c, nb,
       [&](uint64_t* cnt) {
-        BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag, R->n,
-                           cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
+        BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag,
+                  R->n, cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
       },
       [&](uint64_t* off, uint64_t tot) -> int {
         rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
         if (!rows) return BG_E_NOMEM;
         if (nb)
           BG_LAUNCH(c, "k_compact_flags_write", k_compact_flags<true>, dim3(nb), dim3(BG_NT), flag,
-                             R->n, (uint64_t*)nullptr, off, rows);
+                    R->n, (uint64_t*)nullptr, off, rows);
         return 0;
       },
-      &total, nullptr);
+      &total);
   if (rc) return rc;
   bg_release(c, P);
   bg_release(c, flag);

@@ -89,15 +89,15 @@ def kernel_bytes(name, w):
     (what each kernel must read and write at minimum)."""
     tb, rows, comps, out, obytes = w["text"], w["rows"], w["comps"], w["out"], w["out_bytes"]
     table = {
-        # text read + raw start/end written, per file (2 launches per step)
+        # per file (2 launches per step): text read + keyed start/end written
         "k_parse": (tb + 16 * rows) / 2,
-        "k_nl_count": tb / 2,
-        "k_key": 32 * rows / 2,
+        "k_scout": tb / 2,
         "k_tile_max": 8 * rows / 2,
         "k_components_count": 16 * rows / 2,
         "k_components_write": (16 * rows + 16 * comps) / 2,
-        "k_intersect2_count": 16 * comps,
-        "k_intersect2_write": 16 * comps + 16 * out,
+        # one launch per step: both component lists read (+ pieces written)
+        "k_intersect_count": 16 * comps,
+        "k_intersect_write": 16 * comps + 16 * out,
         "k_fmt_count": 16 * out,
         "k_fmt_write": 16 * out + obytes,
     }
