@@ -94,61 +94,76 @@ __device__ __forceinline__ uint64_t line_token(const TileText& T, int64_t p, int
     ++p;
   }
   tok = p;
-  uint64_t h = BGP_FNV_OFF;
-  uint32_t n = 0;
+  uint64_t h = BGP_FNV_OFF;  // bgp_hash_words over zero-padded 32-bit words
+  uint32_t n = 0, w = 0;
   while ((uint64_t)p < T.nb) {
     uint8_t ch = T.at(p);
     if (ch == '\n' || bg_isws(ch)) break;
-    h = bgp_hash_step(h, ch);
+    w |= (uint32_t)ch << (8 * (n & 3));
     ++n;
+    if ((n & 3) == 0) { h = (h ^ w) * BGP_FNV_PRIME; w = 0; }
     ++p;
   }
+  if (n & 3) h = (h ^ w) * BGP_FNV_PRIME;
   len = n;
-  return bgp_hash_final(h, n);
+  return (h ^ n) * BGP_FNV_PRIME;
 }
 
 // -------------------------------------------------------------------------------------
-// k_scout: newline count per tile + first owned line and its chromosome token
+// k_scout: newline count + first '\n' offset per tile (pure streaming read)
 // -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt, uint64_t nb,
                                                  uint64_t* __restrict__ cnt,
-                                                 int64_t* __restrict__ fls,
-                                                 uint64_t* __restrict__ fhash) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
-  __shared__ uint64_t shc[BG_NT / 64 + 1];
-  __shared__ uint32_t shm[BG_NT / 64 + 1];
-  const int64_t t0 = (int64_t)blockIdx.x * TT;
-  uint4 v0, v1;
-  stage_tile(txt, nb, t0, buf, v0, v1);
-  uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-  uint64_t c = 0;
-  uint32_t first = TT;
+                                                 uint32_t* __restrict__ fnl) {
+  __shared__ uint64_t shc[BG_NT / 64];
+  __shared__ uint32_t shm[BG_NT / 64];
+  const int64_t b = (int64_t)blockIdx.x * TT + (int64_t)threadIdx.x * 32;
+  const uint4 v0 = load16(txt, b, nb), v1 = load16(txt, b + 16, nb);
+  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t c = 0, first = TT;
 #pragma unroll
   for (int k = 7; k >= 0; --k) {
-    uint32_t m = nl_mask4(w[k]);
+    const uint32_t m = nl_mask4(w[k]);
     c += __popc(m);
     if (m) first = threadIdx.x * 32 + 4 * k + (__ffs(m) - 1) / 8;
   }
-  uint64_t tc;
-  (void)block_excl_scan(c, OpSum(), (uint64_t)0, shc, &tc);
-  uint32_t fmin;
-  (void)block_excl_scan(first, OpMin(), (uint32_t)TT, shm, &fmin);
-  if (threadIdx.x == 0) {
-    cnt[blockIdx.x] = tc;
-    int64_t ls = -1;
-    if (t0 == 0 || buf[HB - 1] == '\n') ls = t0;
-    else if (fmin + 1 < TT) ls = t0 + fmin + 1;
-    if (ls >= 0 && (uint64_t)ls >= nb) ls = -1;
-    uint64_t h = 0;
-    if (ls >= 0) {
-      TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
-      int64_t tok;
-      uint32_t len;
-      h = line_token(T, ls, tok, len);
-    }
-    fls[blockIdx.x] = ls;
-    fhash[blockIdx.x] = h;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    c += __shfl_xor(c, d, 64);
+    first = min(first, (uint32_t)__shfl_xor(first, d, 64));
   }
+  if (bg_lane() == 0) { shc[bg_wave()] = c; shm[bg_wave()] = first; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    uint32_t f = TT;
+    for (int q = 0; q < BG_NT / 64; ++q) { t += shc[q]; f = min(f, shm[q]); }
+    cnt[blockIdx.x] = t;
+    fnl[blockIdx.x] = f;
+  }
+}
+
+// first owned line of each tile and the hash of its chromosome token (one thread per
+// tile, reads a few bytes)
+__global__ void k_tokhash(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
+                          const uint32_t* __restrict__ fnl, int64_t* __restrict__ fls,
+                          uint64_t* __restrict__ fhash) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const int64_t t0 = (int64_t)t * TT;
+  int64_t ls = -1;
+  if (t0 == 0 || txt[t0 - 1] == '\n') ls = t0;
+  else if (fnl[t] + 1 < TT) ls = t0 + fnl[t] + 1;
+  if (ls >= 0 && (uint64_t)ls >= nb) ls = -1;
+  uint64_t h = 0;
+  if (ls >= 0) {
+    TileText T{txt, txt, 0, 0, nb};  // global reads only
+    int64_t tok;
+    uint32_t len;
+    h = line_token(T, ls, tok, len);
+  }
+  fls[t] = ls;
+  fhash[t] = h;
 }
 
 // tile t may hold a chromosome change iff its first token differs from the next
@@ -355,11 +370,14 @@ __device__ __forceinline__ void parse_line_slow(const TileText& T, int64_t ls, i
   int64_t p = ls;
   while (p < le && bg_isws(T.at(p))) ++p;
   if (p == le) { L.err = ERR_BLANK; return; }
-  L.tok = p;
-  uint64_t h = BGP_FNV_OFF;
-  while (p < le && !bg_isws(T.at(p))) { h = bgp_hash_step(h, T.at(p)); ++p; }
-  L.toklen = (uint32_t)(p - L.tok);
-  L.hash = bgp_hash_final(h, L.toklen);
+  {
+    int64_t tk;
+    uint32_t tl;
+    L.hash = line_token(T, p, tk, tl);
+    L.tok = tk;
+    L.toklen = tl;
+    p = tk + tl;
+  }
   if (L.toklen > BG_CHR_MAX) { L.err = ERR_CHROM; return; }
   while (p < le && bg_isws(T.at(p))) ++p;
   if (!parse_u64(T, p, le, L.start)) { L.err = ERR_PARSE; return; }
@@ -389,36 +407,45 @@ __device__ __forceinline__ void lds16(const uint8_t* buf, uint32_t q, uint64_t& 
   hi = (uint64_t)bgp_align(x2, x3, o) | ((uint64_t)bgp_align(x3, x4, o) << 32);
 }
 
-// fast path: fields from the line's first 32 bytes (LDS) -> true if decided
-__device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const TileText& T, int64_t ls,
+// 32-bit window of a per-tile class bitmap starting at local byte offset p (bit j of
+// the result = byte p + j); m holds one 32-bit word per 32 tile bytes
+__device__ __forceinline__ uint32_t mask_window(const uint32_t* m, uint32_t p) {
+  const uint32_t w = p >> 5, b = p & 31;
+  const uint64_t two = (uint64_t)m[w] | ((uint64_t)m[w + 1] << 32);
+  return (uint32_t)(two >> b);
+}
+
+// fast path: fields from the tile's class bitmaps + LDS bytes -> true if decided.
+// q: local offset of the line start inside the tile (0 <= q < TT).
+__device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32_t* wsm,
+                                                const uint32_t* dgm, uint32_t q, int64_t ls,
                                                 int64_t le, Line& L) {
-  if (ls < T.lo || ls + 52 > T.hi + 32) return false;
-  const uint32_t q = (uint32_t)(ls - T.lo);
-  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (q & ~3u));
-  const uint32_t o = q & 3u;
-  uint32_t x[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) x[i] = d[i];
-  uint32_t W[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) W[i] = bgp_align(x[i], x[i + 1], o);
   BgpFields F;
-  const int r = bgp_fields(W, (uint32_t)(le - ls), F);
+  const int r = bgp_fields_masks(mask_window(wsm, q), mask_window(dgm, q), (uint32_t)(le - ls), F);
   if (r != 1) return false;  // blank lines and errors take the byte path (messages)
   const uint32_t toklen = F.a1 - F.a0;
-  if (toklen > BG_CHR_MAX) return false;
+  const uint32_t b = q + HB;  // LDS byte offset of the line start
   uint64_t lo, hi;
-  lds16(buf, q + F.s0, lo, hi);
-  L.start = bgp_digits(lo, hi, (int)(F.s1 - F.s0));
-  lds16(buf, q + F.e0, lo, hi);
-  L.end = bgp_digits(lo, hi, (int)(F.e1 - F.e0));
-  if (F.s1 - F.s0 > 13) L.start = ~0ULL;
-  if (F.e1 - F.e0 > 13) L.end = ~0ULL;
+  lds16(buf, b + F.s0, lo, hi);
+  L.start = (F.s1 - F.s0 > 13) ? ~0ULL : bgp_digits(lo, hi, (int)(F.s1 - F.s0));
+  lds16(buf, b + F.e0, lo, hi);
+  L.end = (F.e1 - F.e0 > 13) ? ~0ULL : bgp_digits(lo, hi, (int)(F.e1 - F.e0));
+  if (toklen <= 16) {
+    lds16(buf, b + F.a0, lo, hi);
+    L.hash = bgp_hash16(lo, hi, toklen);
+  } else {
+    if (toklen > BG_CHR_MAX) return false;
+    uint64_t h = BGP_FNV_OFF;
+    uint32_t w = 0;
+    for (uint32_t i = 0; i < toklen; ++i) {
+      w |= (uint32_t)buf[b + F.a0 + i] << (8 * (i & 3));
+      if ((i & 3) == 3) { h = (h ^ w) * BGP_FNV_PRIME; w = 0; }
+    }
+    if (toklen & 3) h = (h ^ w) * BGP_FNV_PRIME;
+    L.hash = (h ^ toklen) * BGP_FNV_PRIME;
+  }
   L.tok = ls + F.a0;
   L.toklen = toklen;
-  uint64_t h = BGP_FNV_OFF;
-  for (uint32_t i = 0; i < toklen; ++i) h = bgp_hash_step(h, buf[q + F.a0 + i]);
-  L.hash = bgp_hash_final(h, toklen);
   L.rest = ls + F.e1;
   L.err = 0;
   L.score = 0;
@@ -435,10 +462,27 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
   __shared__ uint16_t lst[LCAP + 1];
   __shared__ int64_t lkey[LCAP];
   __shared__ uint32_t shs[BG_NT / 64 + 1];
+  __shared__ uint32_t wsm[TT / 32 + HA / 32 + 1];  // class bitmaps: bit = byte
+  __shared__ uint32_t dgm[TT / 32 + HA / 32 + 1];
   __shared__ uint32_t runlo, runhi;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   uint4 v0, v1;
   stage_tile(txt, nb, t0, buf, v0, v1);
+  {  // classify this thread's 32 bytes once (SWAR), publish the masks
+    const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t ws, dg;
+    bgp_classify8(W, ws, dg);
+    wsm[threadIdx.x] = ws;
+    dgm[threadIdx.x] = dg;
+    if (threadIdx.x < HA / 32 + 1) {  // the halo after the tile
+      const int64_t hb = t0 + TT + 32 * (int64_t)threadIdx.x;
+      const uint4 h0 = load16(txt, hb, nb), h1 = load16(txt, hb + 16, nb);
+      const uint32_t H[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      bgp_classify8(H, ws, dg);
+      wsm[TT / 32 + threadIdx.x] = ws;
+      dgm[TT / 32 + threadIdx.x] = dg;
+    }
+  }
   if (threadIdx.x == 0) {  // runs that can occur in this tile
     runlo = run_of(R, t0, 0, R.n - 1);
     runhi = run_of(R, t0 + TT - 1, 0, R.n - 1);
@@ -461,7 +505,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : find_nl(T, ls);
     if (le < 0) continue;
     Line Ln;
-    if (kind == BG_BED5 || !parse_line_fast(buf, T, ls, le, Ln)) {
+    if (kind == BG_BED5 || !parse_line_fast(buf, wsm, dgm, lst[k], ls, le, Ln)) {
       parse_line_slow(T, ls, le, kind, Ln);
       if (Ln.err) {
         if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
@@ -573,7 +617,10 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   uint32_t* blist = (uint32_t*)bg_alloc(c, 4ull * nt);
   // small counters block: [0] rows, [1] nboundary (u32), [2] nrec (u32)
   uint64_t* ctr = (uint64_t*)bg_alloc(c, 64);
-  const uint32_t RC = std::min<uint32_t>(REC_CAP, 4 * nt + 16);
+  uint32_t* fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
+  if (!fnl) return BG_E_NOMEM;
+  // a boundary tile records at most one entry per line (+1): TT/6 lines at most
+  const uint32_t RC = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
   int64_t* rpos = (int64_t*)bg_alloc(c, 8ull * RC);
   uint64_t* rhash = (uint64_t*)bg_alloc(c, 8ull * RC);
   int64_t* rtok = (int64_t*)bg_alloc(c, 8ull * RC);
@@ -581,7 +628,10 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   if (!cnt || !S.row0 || !fls || !fhash || !blist || !ctr || !rpos || !rhash || !rtok || !rlen)
     return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(ctr, 0, 64, c->stream));
-  BG_LAUNCH(c, "k_scout", k_scout, dim3(nt), dim3(BG_NT), txt, S.nb, cnt, fls, fhash);
+  BG_LAUNCH(c, "k_scout", k_scout, dim3(nt), dim3(BG_NT), txt, S.nb, cnt, fnl);
+  BG_HIP(c, hipGetLastError());
+  BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, fnl, fls,
+            fhash);
   BG_HIP(c, hipGetLastError());
   int rc = bg_scan_sum_u64(c, cnt, S.row0, nt, &ctr[0]);
   if (rc) return rc;
@@ -676,6 +726,7 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   bg_release(c, fls);
   bg_release(c, fhash);
   bg_release(c, blist);
+  bg_release(c, fnl);
   bg_release(c, ctr);
   bg_release(c, rpos);
   bg_release(c, rhash);

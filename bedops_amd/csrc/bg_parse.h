@@ -75,10 +75,10 @@ struct BgpFields {
   uint32_t e0, e1;  // end digits; rest starts at e1
 };
 
-// W: bytes [0, 32) of the line; len: line length (bytes before '\n').
-// returns 1: fields found; 0: undecided here (use the byte path); -1: blank line
-BG_HD int bgp_fields(const uint32_t W[8], uint32_t len, BgpFields& F) {
-  uint32_t WS = 0, DG = 0;
+// class masks of 32 bytes held as 8 dwords: bit j = byte j
+BG_HD void bgp_classify8(const uint32_t W[8], uint32_t& WS, uint32_t& DG) {
+  WS = 0;
+  DG = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     uint32_t w4, d4;
@@ -86,6 +86,12 @@ BG_HD int bgp_fields(const uint32_t W[8], uint32_t len, BgpFields& F) {
     WS |= w4 << (4 * i);
     DG |= d4 << (4 * i);
   }
+}
+
+// WS/DG: class masks of the line's first 32 bytes (bit j = byte j); len: line length
+// (bytes before '\n'). returns 1: fields found; 0: undecided here (use the byte
+// path); -1: blank line
+BG_HD int bgp_fields_masks(uint32_t WS, uint32_t DG, uint32_t len, BgpFields& F) {
   if (len < 32) {  // bytes past the line end act as whitespace
     const uint32_t endm = ~0u << len;
     WS |= endm;
@@ -116,6 +122,34 @@ BG_HD int bgp_fields(const uint32_t W[8], uint32_t len, BgpFields& F) {
   if (F.s1 - F.s0 > 16 || F.e1 - F.e0 > 16) return 0;
   if (F.e1 > len) return 0;
   return 1;
+}
+
+// W: bytes [0, 32) of the line
+BG_HD int bgp_fields(const uint32_t W[8], uint32_t len, BgpFields& F) {
+  uint32_t WS, DG;
+  bgp_classify8(W, WS, DG);
+  return bgp_fields_masks(WS, DG, len, F);
+}
+
+// Token hash over 32-bit little-endian words of the token (zero padded), then the
+// length: identical whether computed byte by byte or from 16-byte register windows.
+BG_HD uint64_t bgp_hash_words(const uint32_t* w, uint32_t nwords, uint32_t len) {
+  uint64_t h = 1469598103934665603ull;
+  for (uint32_t i = 0; i < nwords; ++i) h = (h ^ w[i]) * 1099511628211ull;
+  return (h ^ len) * 1099511628211ull;
+}
+// up to 16 token bytes given as lo (bytes 0..7) and hi (8..15) of the token start
+BG_HD uint64_t bgp_hash16(uint64_t lo, uint64_t hi, uint32_t len) {
+  if (len < 16) {
+    if (len <= 8) {
+      hi = 0;
+      lo = len == 8 ? lo : (lo & ((1ull << (8 * len)) - 1));
+    } else {
+      hi &= (1ull << (8 * (len - 8))) - 1;
+    }
+  }
+  uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  return bgp_hash_words(w, (len + 3) / 4, len);
 }
 
 // FNV-1a 64 over a chromosome token (run identity; same function everywhere)
