@@ -112,34 +112,47 @@ __device__ __forceinline__ uint64_t line_token(const TileText& T, int64_t p, int
 // -------------------------------------------------------------------------------------
 // k_scout: newline count + first '\n' offset per tile (pure streaming read)
 // -------------------------------------------------------------------------------------
+#define SCOUT_TILES 4  // tiles per workgroup: 8 x 16-B loads in flight per thread
 __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt, uint64_t nb,
-                                                 uint64_t* __restrict__ cnt,
+                                                 uint32_t ntiles, uint64_t* __restrict__ cnt,
                                                  uint32_t* __restrict__ fnl) {
-  __shared__ uint64_t shc[BG_NT / 64];
-  __shared__ uint32_t shm[BG_NT / 64];
-  const int64_t b = (int64_t)blockIdx.x * TT + (int64_t)threadIdx.x * 32;
-  const uint4 v0 = load16(txt, b, nb), v1 = load16(txt, b + 16, nb);
-  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-  uint32_t c = 0, first = TT;
+  __shared__ uint32_t shc[SCOUT_TILES][BG_NT / 64];
+  __shared__ uint32_t shm[SCOUT_TILES][BG_NT / 64];
+  uint4 v[SCOUT_TILES][2];
 #pragma unroll
-  for (int k = 7; k >= 0; --k) {
-    const uint32_t m = nl_mask4(w[k]);
-    c += __popc(m);
-    if (m) first = threadIdx.x * 32 + 4 * k + (__ffs(m) - 1) / 8;
+  for (int q = 0; q < SCOUT_TILES; ++q) {  // issue every load first
+    const int64_t b = ((int64_t)blockIdx.x * SCOUT_TILES + q) * TT + (int64_t)threadIdx.x * 32;
+    v[q][0] = load16(txt, b, nb);
+    v[q][1] = load16(txt, b + 16, nb);
   }
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    c += __shfl_xor(c, d, 64);
-    first = min(first, (uint32_t)__shfl_xor(first, d, 64));
+  for (int q = 0; q < SCOUT_TILES; ++q) {
+    const uint32_t w[8] = {v[q][0].x, v[q][0].y, v[q][0].z, v[q][0].w,
+                           v[q][1].x, v[q][1].y, v[q][1].z, v[q][1].w};
+    uint32_t c = 0, first = TT;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+      const uint32_t m = nl_mask4(w[k]);
+      c += __popc(m);
+      if (m) first = threadIdx.x * 32 + 4 * k + (__ffs(m) - 1) / 8;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      c += __shfl_xor(c, d, 64);
+      first = min(first, (uint32_t)__shfl_xor(first, d, 64));
+    }
+    if (bg_lane() == 0) { shc[q][bg_wave()] = c; shm[q][bg_wave()] = first; }
   }
-  if (bg_lane() == 0) { shc[bg_wave()] = c; shm[bg_wave()] = first; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    uint32_t f = TT;
-    for (int q = 0; q < BG_NT / 64; ++q) { t += shc[q]; f = min(f, shm[q]); }
-    cnt[blockIdx.x] = t;
-    fnl[blockIdx.x] = f;
+  if (threadIdx.x < SCOUT_TILES) {
+    const uint32_t t = blockIdx.x * SCOUT_TILES + threadIdx.x;
+    if (t < ntiles) {
+      uint64_t s = 0;
+      uint32_t f = TT;
+      for (int w = 0; w < BG_NT / 64; ++w) { s += shc[threadIdx.x][w]; f = min(f, shm[threadIdx.x][w]); }
+      cnt[t] = s;
+      fnl[t] = f;
+    }
   }
 }
 
@@ -453,8 +466,18 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   return true;
 }
 
+// runs that can occur in each tile: [runlo, runhi] by position
+__global__ void k_run_range(RunTable R, uint32_t ntiles, uint32_t* __restrict__ runlo,
+                            uint32_t* __restrict__ runhi) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  runlo[t] = run_of(R, (int64_t)t * TT, 0, R.n - 1);
+  runhi[t] = run_of(R, (int64_t)t * TT + TT - 1, 0, R.n - 1);
+}
+
 __global__ void __launch_bounds__(BG_NT) k_parse(
     const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
     bg_dstatus* st) {
@@ -464,10 +487,12 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
   __shared__ uint32_t shs[BG_NT / 64 + 1];
   __shared__ uint32_t wsm[TT / 32 + HA / 32 + 1];  // class bitmaps: bit = byte
   __shared__ uint32_t dgm[TT / 32 + HA / 32 + 1];
-  __shared__ uint32_t runlo, runhi;
+  __shared__ uint32_t hnl;  // first '\n' in the halo after the tile (local offset)
   const int64_t t0 = (int64_t)blockIdx.x * TT;
+  if (threadIdx.x == 0) hnl = ~0u;
   uint4 v0, v1;
   stage_tile(txt, nb, t0, buf, v0, v1);
+  __syncthreads();
   {  // classify this thread's 32 bytes once (SWAR), publish the masks
     const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     uint32_t ws, dg;
@@ -481,13 +506,13 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
       bgp_classify8(H, ws, dg);
       wsm[TT / 32 + threadIdx.x] = ws;
       dgm[TT / 32 + threadIdx.x] = dg;
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t m = nl_mask4(H[k]);
+        if (m) { atomicMin(&hnl, TT + 32 * threadIdx.x + 4 * k + (__ffs(m) - 1) / 8); break; }
+      }
     }
   }
-  if (threadIdx.x == 0) {  // runs that can occur in this tile
-    runlo = run_of(R, t0, 0, R.n - 1);
-    runhi = run_of(R, t0 + TT - 1, 0, R.n - 1);
-  }
-  __syncthreads();
+  const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];  // runs in this tile
   bool has0;
   const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, LCAP + 1, shs, has0);
   const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1);  // row of the first owned line
@@ -496,13 +521,16 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     return;
   }
   TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
-  const uint32_t rl = runlo, rh = runhi;
+  // end of the tile's last line: the tile's last byte, the halo, or further on
+  const int64_t last_end = L == 0 ? -1
+                           : (buf[HB + TT - 1] == '\n') ? t0 + TT - 1
+                           : (hnl != ~0u ? t0 + hnl : find_nl(T, t0 + TT + HA + 32));
   for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
     const int64_t ls = t0 + lst[k];
     const uint64_t r = r0 + k;
     lkey[k] = LLONG_MIN;
     if (r >= nrows) continue;  // unterminated last line (dropped like the reference)
-    const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : find_nl(T, ls);
+    const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
     if (le < 0) continue;
     Line Ln;
     if (kind == BG_BED5 || !parse_line_fast(buf, wsm, dgm, lst[k], ls, le, Ln)) {
@@ -628,7 +656,8 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   if (!cnt || !S.row0 || !fls || !fhash || !blist || !ctr || !rpos || !rhash || !rtok || !rlen)
     return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(ctr, 0, 64, c->stream));
-  BG_LAUNCH(c, "k_scout", k_scout, dim3(nt), dim3(BG_NT), txt, S.nb, cnt, fnl);
+  BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
+            cnt, fnl);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, fnl, fls,
             fhash);
@@ -770,9 +799,17 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   BG_HIP(c, hipMemcpyAsync(d_gid, g.data(), 4ull * nr, hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemsetAsync(d_row, 0xff, 8ull * nr, c->stream));
   RunTable R{d_pos, d_hash, d_gid, d_row, nr};
-  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0,
-            in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, c->dstat);
+  uint32_t* rlo = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
+  uint32_t* rhi = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
+  if (!rlo || !rhi) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_run_range", k_run_range, dim3(bg_blocks(S.ntiles, 256)), dim3(256), R, S.ntiles,
+            rlo, rhi);
   BG_HIP(c, hipGetLastError());
+  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, rlo,
+            rhi, in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, c->dstat);
+  BG_HIP(c, hipGetLastError());
+  bg_release(c, rlo);
+  bg_release(c, rhi);
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, c->dstat);
   BG_HIP(c, hipGetLastError());

@@ -43,23 +43,49 @@ __device__ __forceinline__ int64_t wave_max_all(int64_t v) {
 }
 
 // ------------------------------- components ---------------------------------------
+// max end of each components() tile; one workgroup covers TM_TILES tiles with 16-byte
+// loads (16 in flight per thread)
+#define TM_TILES 4
 __global__ void __launch_bounds__(BG_NT) k_tile_max(const int64_t* __restrict__ E, uint64_t n,
-                                                    int64_t* __restrict__ tmax) {
-  __shared__ int64_t wm[BG_NT / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * CT_TILE;
-  int64_t m = LLONG_MIN;
+                                                    uint32_t ntiles, int64_t* __restrict__ tmax) {
+  __shared__ int64_t wm[TM_TILES][BG_NT / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * TM_TILES * CT_TILE;  // elements
+  constexpr int NV = TM_TILES * CT_TILE / 2 / BG_NT;                 // vectors per thread
+  int64_t m[TM_TILES];
 #pragma unroll
-  for (int k = 0; k < CT_ITEMS; ++k) {
-    const uint64_t i = base + (uint64_t)k * BG_NT + threadIdx.x;
-    if (i < n) m = max(m, E[i]);
+  for (int q = 0; q < TM_TILES; ++q) m[q] = LLONG_MIN;
+  if (base + (uint64_t)TM_TILES * CT_TILE <= n) {
+    const longlong2* E2 = reinterpret_cast<const longlong2*>(E + base);
+    longlong2 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = E2[k * BG_NT + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int q = (k * BG_NT * 2) / CT_TILE;
+      m[q] = max(m[q], max((int64_t)v[k].x, (int64_t)v[k].y));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int q = (k * BG_NT * 2) / CT_TILE;
+      const uint64_t i = base + 2ull * (k * BG_NT + threadIdx.x);
+      if (i < n) m[q] = max(m[q], E[i]);
+      if (i + 1 < n) m[q] = max(m[q], E[i + 1]);
+    }
   }
-  m = wave_max_all(m);
-  if (bg_lane() == 0) wm[bg_wave()] = m;
+#pragma unroll
+  for (int q = 0; q < TM_TILES; ++q) {
+    const int64_t x = wave_max_all(m[q]);
+    if (bg_lane() == 0) wm[q][bg_wave()] = x;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t t = wm[0];
-    for (int w = 1; w < BG_NT / 64; ++w) t = max(t, wm[w]);
-    tmax[blockIdx.x] = t;
+  if (threadIdx.x < TM_TILES) {
+    const uint32_t t = blockIdx.x * TM_TILES + threadIdx.x;
+    if (t < ntiles) {
+      int64_t x = wm[threadIdx.x][0];
+      for (int w = 1; w < BG_NT / 64; ++w) x = max(x, wm[threadIdx.x][w]);
+      tmax[t] = x;
+    }
   }
 }
 
@@ -366,7 +392,8 @@ static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
   const unsigned nb = bg_blocks(n, CT_TILE);
   int64_t* carry = (int64_t*)bg_alloc(c, 8ull * nb);
   if (!carry) return BG_E_NOMEM;
-  BG_LAUNCH(c, "k_tile_max", k_tile_max, dim3(nb), dim3(BG_NT), in.e, n, carry);
+  BG_LAUNCH(c, "k_tile_max", k_tile_max, dim3(bg_blocks(nb, TM_TILES)), dim3(BG_NT), in.e, n, nb,
+            carry);
   BG_HIP(c, hipGetLastError());
   int rc = bg_scan_max_i64(c, carry, carry, nb, LLONG_MIN);
   if (rc) return rc;
