@@ -2,16 +2,16 @@
 """bench.py — headline benchmark of the bedops_amd sweep path on MI355X.
 
 Metric (BASELINE.json): intervals/sec of `bedops --intersect A.bed B.bed`, 100M x 100M
-sorted BED3 (SURVEY.md Appendix D generator, seeds 42/43), per GPU.
+sorted BED3 (SURVEY.md Appendix D generator, seeds 42/43).
 
-One step = one whole pass of the GPU path over the input text already resident in
-HBM: parse both files (k_nl_count, scans, k_parse, k_key) -> per-file merge
-(k_components) -> intersect (k_intersect2) -> render the sorted BED text back into
-HBM (k_fmt_*). With N GPUs (one process per GPU, torch.distributed over RCCL) the
-dataset is N x 100M rows per file (weak scaling), chromosomes are assigned to ranks by
-longest-processing-time on contig length, every rank runs the step on its shard and
-the per-rank texts are sent to rank 0 over xGMI (RCCL point-to-point) and reassembled
-there in strcmp chromosome order — the one exchange the path has.
+One step = one whole pass of the GPU path over the input text already resident in HBM:
+load both files (k_scout, k_tokhash, run/dictionary kernels, k_parse) -> per-file merge
+(k_tile_max, k_components_*) -> intersect (k_mp_partition, k_intersect_*) -> render the
+sorted BED text back into HBM (k_fmt_*). With N GPUs (one process per GPU,
+torch.distributed over RCCL) the dataset is N x 100M rows per file (weak scaling),
+chromosomes go to ranks by bedops_amd.shard.assign (LPT), every rank runs the step on its
+shard and bedops_amd.shard.gather_text sends the per-chromosome texts to rank 0 over xGMI,
+where they land in strcmp chromosome order — the one exchange the path has.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -34,6 +34,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 REF_INTERSECT = {"rows": 38507974, "bytes": 917848625, "sha16": "2495074965b49d74"}
 
 
+# bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
+PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
+            "k_intersect_count": "k_mp_tile<0, false>", "k_intersect_write": "k_mp_tile<0, true>"}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -53,17 +58,14 @@ def bedgen_lib():
     return L
 
 
-def lpt_shards(L, world):
-    """contig index -> rank, longest-processing-time on contig length"""
+def contig_shards(L, world):
+    """contig index -> rank: bedops_amd.shard.assign (LPT) on contig length, which is
+    proportional to the generator's rows per contig"""
+    from bedops_amd.shard import assign
     n = L.bedgen_ncontigs()
-    lens = [(L.bedgen_contig_len(c), c) for c in range(n)]
-    load = [0] * world
-    owner = {}
-    for ln, c in sorted(lens, reverse=True):
-        r = min(range(world), key=lambda k: (load[k], k))
-        owner[c] = r
-        load[r] += ln
-    return owner, load
+    owner, load = assign({L.bedgen_contig_name(c).decode(): L.bedgen_contig_len(c)
+                          for c in range(n)}, world)
+    return {c: owner[L.bedgen_contig_name(c).decode()] for c in range(n)}, load
 
 
 def gen(L, n, seed, mask, mode=3):
@@ -149,6 +151,8 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000, help="rows per file per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--load-only", action="store_true",
+                    help="time the loader stage alone (text in HBM -> keyed columns)")
     ap.add_argument("--profile-all", action="store_true",
                     help="time every kernel during the timed steps (default: only the dominant one)")
     args = ap.parse_args()
@@ -167,7 +171,7 @@ def main():
     from bedops_amd import BED3, Engine
 
     L = bedgen_lib()
-    owner, _ = lpt_shards(L, world)
+    owner, _ = contig_shards(L, world)
     mask = sum(1 << c for c, r in owner.items() if r == rank)
     N = args.rows * world
     t0 = time.perf_counter()
@@ -186,11 +190,14 @@ def main():
 
     eng = Engine(local)
     ncontigs = L.bedgen_ncontigs()
-    strcmp_order = sorted(range(ncontigs), key=lambda c: L.bedgen_contig_name(c))
     state = {}
 
     def step():
         s = eng.load([((ta.data_ptr(), na), BED3), ((tb_.data_ptr(), nb), BED3)])
+        if args.load_only:
+            state["out_rows"] = state["out_bytes"] = 0
+            s.free()
+            return
         r = eng.op("-i", s, [0, 1])
         nbytes = r.format()
         state["out_rows"] = r.rows()
@@ -203,42 +210,20 @@ def main():
         r.free()
         s.free()
 
+    contig_names = [L.bedgen_contig_name(c).decode() for c in range(ncontigs)]
+    chrom_owner = {contig_names[c]: owner[c] for c in range(ncontigs)}
+
     def gather_to_rank0(r, s, nbytes):
-        # per-rank text -> rank 0 over RCCL p2p; rank 0 reassembles in strcmp chrom order
+        # the path's one exchange: per-chromosome text -> rank 0 over RCCL, in strcmp order
+        from bedops_amd.shard import gather_text
         names = s.chroms()
-        spans = r.chrom_spans(len(names))
-        meta = torch.full((ncontigs, 2), -1, dtype=torch.int64)
-        for g, nm in enumerate(names):
-            c = [k for k in range(ncontigs) if L.bedgen_contig_name(k).decode() == nm][0]
-            meta[c, 0], meta[c, 1] = spans[g], spans[g + 1]
-        meta = meta.to(dev)
-        allmeta = [torch.empty_like(meta) for _ in range(world)]
-        dist.all_gather(allmeta, meta)
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([nbytes], dtype=torch.int64, device=dev))
-        sizes = [int(x.item()) for x in sizes]
+        sp = r.chrom_spans(len(names))
+        spans = {nm: (sp[g], sp[g + 1]) for g, nm in enumerate(names) if sp[g + 1] > sp[g]}
         buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
         r.copy_to_device(buf.data_ptr(), max(nbytes, 1))
+        out = gather_text(dist, buf, spans, contig_names, chrom_owner, rank, world)
         if rank == 0:
-            recv = [buf] + [torch.empty(max(sizes[k], 1), dtype=torch.uint8, device=dev)
-                            for k in range(1, world)]
-            reqs = [dist.irecv(recv[k], src=k) for k in range(1, world)]
-            for q in reqs:
-                q.wait()
-            total = sum(sizes)
-            out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
-            pos = 0
-            am = [m.cpu() for m in allmeta]
-            for c in strcmp_order:
-                own = owner[c]
-                a, b = int(am[own][c, 0]), int(am[own][c, 1])
-                if a < 0 or b <= a:
-                    continue
-                out[pos:pos + (b - a)].copy_(recv[own][a:b])
-                pos += b - a
-            state["gathered"] = pos
-        else:
-            dist.send(buf, dst=0)
+            state["gathered"] = int(out.numel())
 
     # warmup; the first warmup step profiles every kernel to find the dominant one
     eng.prof_enable("*")
@@ -300,7 +285,7 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(pick)
+                traffic = json.load(open(pmc)).get(PMC_NAME.get(pick, pick), {}).get("bytes")
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
