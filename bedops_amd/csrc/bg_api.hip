@@ -330,6 +330,8 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->rows);
   bg_release(c, r->cnt);
   bg_release(c, r->isum);
+  bg_release(c, r->left);
+  bg_release(c, r->right);
   bg_release(c, r->text);
   bg_release(c, r->toff);
   delete r;

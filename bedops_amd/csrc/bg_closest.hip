@@ -1,0 +1,367 @@
+// bg_closest.hip — K6: closest-features <input-file> <query-file>.
+//
+// Reference: FeatDist::findDistances (applications/bed/closestfeats/src/ClosestFeature.cpp:
+// 260-413) walks the sorted <input-file> rows ("ref" rows b) once; for each b it reads
+// <query-file> rows ("candidates" c) through a BedReader whose LIFO cache
+// (closestfeats/src/BedReader.hpp:55-80) gets back a list of rows the previous b kept.
+// Which rows that cache keeps is NOT "every row that could still matter": a new best
+// left empties it (ClosestFeature.cpp:300-304, :369-373), so a row that overlapped an
+// earlier b and ends later than the new left is gone for every later b. The chosen
+// left/right therefore depend on the history of the scan, not only on b (verified
+// against the restatement in oracle/closest_oracle.c: a cache-free search differs on
+// nested inputs). The GPU reproduces the sequential state machine exactly:
+//
+//   state between two ref rows = (file position fp, cached rows in pop order)
+//
+// - k_closest_chunks: one thread per chunk of CQ consecutive ref rows. Chunk 0 starts
+//   from the true initial state. Chunk k > 0 starts SPECULATIVELY CW rows earlier from
+//   (fp = CBACK rows before the first candidate at or after that row, empty cache),
+//   replays those CW rows without output (the state forgets its history quickly: it only
+//   holds the current left/right and overlapping rows), records the state it reached at
+//   its first own row, then emits left/right for its rows and records its final state.
+// - k_closest_check: chunk k is exact iff its recorded start state equals chunk k-1's
+//   final state (and chunk k-1 is exact): induction from chunk 0.
+// - k_closest_fix: chunks whose start differs from a stable predecessor's final state
+//   re-run from that state; check again; after a few rounds any remainder is resolved by
+//   one in-order pass (k_closest_serial), so the result is exact in every case.
+// The row-by-row rules below follow ClosestFeature.cpp:284-401 line for line in meaning;
+// getDistance :244-255 and the centroid proportion :226-239 use the same double
+// arithmetic. Output (PrintAll / PrintShortest, Printers.hpp:46-205) is rendered by
+// bg_format.hip from the per-row (left, right) candidate indices.
+#include <climits>
+
+#include "bg_internal.h"
+
+#define CQ 32      // ref rows per chunk
+#define CW 8       // speculative warm-up rows before a chunk
+#define CBACK 64   // candidates before the warm-up row where the speculative read starts
+#define CMAX 128   // capacity of the cache and of the per-row kept list
+#define FIX_ROUNDS 8
+
+struct ClArgs {
+  const int64_t* qs;  // ref rows (<input-file>), keyed
+  const int64_t* qe;
+  uint64_t nq;
+  const int64_t* cs;  // candidates (<query-file>), keyed
+  const int64_t* ce;
+  uint64_t nc;
+  int overlaps;
+  int64_t* left;
+  int64_t* right;
+  // recorded states: slot 2k = chunk k's start state, 2k+1 = its final state
+  uint64_t* st_fp;
+  uint32_t* st_n;
+  uint32_t* st_c;  // CMAX candidate indices per slot, in stack order (top last)
+  uint32_t nchunks;
+  uint32_t* flag;
+  uint32_t* nflag;
+  bg_dstatus* st;
+};
+
+struct ClState {
+  uint64_t fp;
+  uint32_t n;
+  uint32_t c[CMAX];
+};
+
+#define D_MINUS LLONG_MIN
+#define D_PLUS LLONG_MAX
+
+// getDistance(c, b): ClosestFeature.cpp:244-255 on keyed coordinates
+__device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, int64_t be) {
+  const int64_t gc = cs >> BG_KEY_SHIFT, gb = bs >> BG_KEY_SHIFT;
+  if (gc != gb) return gc < gb ? D_MINUS : D_PLUS;
+  if (ce <= bs) return -((bs - ce) + 1);
+  if (be <= cs) return (cs - be) + 1;
+  return 0;
+}
+
+// replay ref rows [b0, b1) from state S; emit: write left/right. false on overflow
+__device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, bool emit) {
+  uint32_t kept[CMAX];  // the std::list "read" of findDistances
+  for (uint64_t b = b0; b < b1; ++b) {
+    const int64_t bs = A.qs[b], be = A.qe[b];
+    int64_t ld = D_MINUS, rdist = D_PLUS;
+    int64_t left = -1, right = -1, c = -1;
+    bool lc = false;  // leftCached
+    uint32_t nk = 0;
+    bool ovf = false;
+#define KEEP(x)                      \
+  do {                               \
+    if (nk == CMAX) ovf = true;      \
+    else kept[nk++] = (uint32_t)(x); \
+  } while (0)
+    for (;;) {
+      if (S.n) c = S.c[--S.n];
+      else if (S.fp < A.nc) c = (int64_t)S.fp++;
+      else { c = -1; break; }
+      const int64_t cs = A.cs[c], ce = A.ce[c];
+      const int64_t d = cl_dist(cs, ce, bs, be);
+      if (d == D_MINUS) continue;  // earlier chromosome: dropped
+      if (d == D_PLUS) {           // later chromosome: keep for the next rows
+        if (left >= 0 && !lc) KEEP(left);
+        lc = left >= 0;
+        if (right >= 0) KEEP(right);
+        KEEP(c);
+        break;
+      }
+      if (d < 0 && d >= ld) {  // new best left: everything kept so far is dropped
+        nk = 0;
+        ovf = false;
+        ld = d;
+        left = c;
+        lc = false;
+      } else if (d < 0) {  // an earlier row that ends sooner: dropped
+        if (!lc) KEEP(left);
+        lc = true;
+      } else if (d > 0 && d < rdist) {  // first row to the right
+        if (left >= 0 && !lc) KEEP(left);
+        lc = left >= 0;
+        rdist = d;
+        right = c;
+        KEEP(c);
+        break;
+      } else if (d > 0) {  // one row too far (right already overlapping)
+        if (left >= 0 && !lc) KEEP(left);
+        lc = left >= 0;
+        if (right >= 0) KEEP(right);
+        KEEP(c);
+        break;
+      } else if (A.overlaps) {  // overlap
+        if (cs <= bs) {  // hangs over the left edge
+          if (left >= 0 && A.ce[left] <= ce && !lc) {
+            // the old left is never the closest left again: dropped
+          } else if (left >= 0 && !lc) {
+            KEEP(left);
+          }
+          left = c;
+          ld = 0;
+          lc = false;
+        } else if (be <= ce) {  // hangs over the right edge
+          if (left >= 0 && !lc) KEEP(left);
+          lc = left >= 0;
+          if (right >= 0) KEEP(right);
+          right = c;
+          rdist = 0;
+        } else {  // inside b: side by the centroid proportion
+          const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
+          const double cst = (double)(cs & BG_COORD_MASK);
+          const double prop =
+              cen < cst ? 0.0
+                        : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
+          if (ld == 0) {
+            if (prop < 0.5) {
+              if (!lc) KEEP(left);
+              lc = true;
+              if (right >= 0) KEEP(right);
+              right = c;
+              rdist = 0;
+            } else {
+              if (!lc) KEEP(left);
+              lc = true;
+              KEEP(c);
+            }
+          } else if (prop >= 0.5) {
+            nk = 0;
+            ovf = false;
+            lc = false;
+            left = c;
+            ld = 0;
+          } else {
+            if (left >= 0 && !lc) KEEP(left);
+            lc = left >= 0;
+            if (right >= 0) KEEP(right);
+            right = c;
+            rdist = 0;
+          }
+        }
+      } else {  // overlap with --no-overlaps: kept for later rows
+        if (left >= 0 && !lc) {
+          KEEP(left);
+          lc = true;
+        }
+        KEEP(c);
+      }
+    }
+    if (c < 0 && left >= 0 && !lc) KEEP(left);
+    if (c < 0 && right >= 0) KEEP(right);
+#undef KEEP
+    // BedReader::PushBack(list): the list comes back out in list order
+    if (ovf || S.n + nk > CMAX) return false;
+    for (uint32_t i = nk; i-- > 0;) S.c[S.n++] = kept[i];
+    if (emit) {
+      A.left[b] = left;
+      A.right[b] = right;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ void cl_save(const ClArgs& A, uint64_t slot, const ClState& S) {
+  A.st_fp[slot] = S.fp;
+  A.st_n[slot] = S.n;
+  for (uint32_t i = 0; i < S.n; ++i) A.st_c[slot * CMAX + i] = S.c[i];
+}
+__device__ __forceinline__ void cl_load(const ClArgs& A, uint64_t slot, ClState& S) {
+  S.fp = A.st_fp[slot];
+  S.n = A.st_n[slot];
+  for (uint32_t i = 0; i < S.n; ++i) S.c[i] = A.st_c[slot * CMAX + i];
+}
+__device__ __forceinline__ bool cl_same(const ClArgs& A, uint64_t x, uint64_t y) {
+  if (A.st_fp[x] != A.st_fp[y] || A.st_n[x] != A.st_n[y]) return false;
+  for (uint32_t i = 0; i < A.st_n[x]; ++i)
+    if (A.st_c[x * CMAX + i] != A.st_c[y * CMAX + i]) return false;
+  return true;
+}
+
+__device__ __forceinline__ void cl_overflow(const ClArgs& A, uint64_t b) {
+  bg_report(A.st, b, ERR_RANGE);
+}
+
+__global__ void __launch_bounds__(BG_NT) k_closest_chunks(ClArgs A) {
+  const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
+  if (k >= A.nchunks) return;
+  const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
+  ClState S;
+  S.n = 0;
+  S.fp = 0;
+  if (k > 0) {
+    const uint64_t qw = q0 - CW;
+    const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
+    S.fp = p > CBACK ? p - CBACK : 0;
+    if (!cl_run(A, qw, q0, S, false)) {  // speculation overflowed: leave it to the fix-up
+      S.n = 0;
+      S.fp = ~0ull;  // a start state no predecessor ends in
+      cl_save(A, 2ull * k, S);
+      S.fp = ~0ull - 1;  // a final state no successor starts from
+      cl_save(A, 2ull * k + 1, S);
+      return;
+    }
+  }
+  cl_save(A, 2ull * k, S);
+  if (!cl_run(A, q0, q1, S, true)) {
+    cl_overflow(A, q0);
+    return;
+  }
+  cl_save(A, 2ull * k + 1, S);
+}
+
+__global__ void k_closest_check(ClArgs A) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= A.nchunks) return;
+  const bool bad = k > 0 && !cl_same(A, 2ull * k, 2ull * (k - 1) + 1);
+  A.flag[k] = bad;
+  if (bad) atomicAdd(A.nflag, 1u);
+}
+
+// re-run chunks whose predecessor is consistent (its final state is stable this round)
+__global__ void __launch_bounds__(BG_NT) k_closest_fix(ClArgs A) {
+  const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
+  if (k == 0 || k >= A.nchunks || !A.flag[k] || A.flag[k - 1]) return;
+  const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
+  ClState S;
+  cl_load(A, 2ull * (k - 1) + 1, S);
+  cl_save(A, 2ull * k, S);
+  if (!cl_run(A, q0, q1, S, true)) {
+    cl_overflow(A, q0);
+    return;
+  }
+  cl_save(A, 2ull * k + 1, S);
+}
+
+// last resort: one in-order pass (exact for any input)
+__global__ void k_closest_serial(ClArgs A) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (uint32_t k = 1; k < A.nchunks; ++k) {
+    if (cl_same(A, 2ull * k, 2ull * (k - 1) + 1)) continue;
+    const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
+    ClState S;
+    cl_load(A, 2ull * (k - 1) + 1, S);
+    cl_save(A, 2ull * k, S);
+    if (!cl_run(A, q0, q1, S, true)) {
+      cl_overflow(A, q0);
+      return;
+    }
+    cl_save(A, 2ull * k + 1, S);
+  }
+}
+
+extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_closest_opts* o,
+                          bg_result** out) {
+  if (!c || !set || !o || !out || ref < 0 || query < 0 || ref >= (int)set->t.size() ||
+      query >= (int)set->t.size())
+    return BG_E_ARG;
+  *out = nullptr;
+  bg_table* Q = set->t[ref];
+  bg_table* C = set->t[query];
+  if (!Q->rest_off || !C->rest_off)
+    return bg_fail(c, BG_E_ARG, "closest-features needs both inputs loaded as BG_BED3_REST");
+  if (C->n >= (1ull << 32))
+    return bg_fail(c, BG_E_UNSUPPORTED, "more than 2^32 rows in <query-file>");
+  bg_result* r = new bg_result();
+  r->ctx = c;
+  r->set = set;
+  r->kind = RES_CLOSEST;
+  r->tab = ref;
+  r->tab2 = query;
+  r->copts = *o;
+  r->copts.delim[15] = 0;
+  r->n = Q->n;
+  const uint64_t n = Q->n ? Q->n : 1;
+  r->left = (int64_t*)bg_alloc(c, 8 * n);
+  r->right = (int64_t*)bg_alloc(c, 8 * n);
+  if (!r->left || !r->right) { bg_result_free(r); return BG_E_NOMEM; }
+  if (Q->n == 0) { *out = r; return 0; }
+
+  ClArgs A;
+  A.qs = Q->ks; A.qe = Q->ke; A.nq = Q->n;
+  A.cs = C->ks; A.ce = C->ke; A.nc = C->n;
+  A.overlaps = !o->no_overlaps;
+  A.left = r->left; A.right = r->right;
+  A.nchunks = (uint32_t)((Q->n + CQ - 1) / CQ);
+  const uint64_t slots = 2ull * A.nchunks;
+  A.st_fp = (uint64_t*)bg_alloc(c, 8 * slots);
+  A.st_n = (uint32_t*)bg_alloc(c, 4 * slots);
+  A.st_c = (uint32_t*)bg_alloc(c, 4 * CMAX * slots);
+  A.flag = (uint32_t*)bg_alloc(c, 4ull * A.nchunks);
+  A.nflag = (uint32_t*)bg_alloc(c, 4);
+  A.st = c->dstat;
+  int rc = 0;
+  if (!A.st_fp || !A.st_n || !A.st_c || !A.flag || !A.nflag) rc = BG_E_NOMEM;
+  if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
+  if (!rc) {
+    BG_LAUNCH(c, "k_closest_chunks", k_closest_chunks, dim3(bg_blocks(A.nchunks, BG_NT)),
+              dim3(BG_NT), A);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  uint32_t bad = 0;
+  for (int round = 0; !rc; ++round) {
+    rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 4, c->stream));
+    if (rc) break;
+    BG_LAUNCH(c, "k_closest_check", k_closest_check, dim3(bg_blocks(A.nchunks, 256)), dim3(256), A);
+    rc = bg_hip_ok(c, hipMemcpyAsync(&bad, A.nflag, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+    if (rc || bad == 0) break;
+    if (round == FIX_ROUNDS) {
+      BG_LAUNCH(c, "k_closest_serial", k_closest_serial, dim3(1), dim3(64), A);
+      rc = bg_hip_ok(c, hipGetLastError());
+      break;  // the in-order pass leaves every chunk consistent
+    }
+    BG_LAUNCH(c, "k_closest_fix", k_closest_fix, dim3(bg_blocks(A.nchunks, BG_NT)), dim3(BG_NT), A);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus),
+                                            hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  bg_release(c, A.st_fp);
+  bg_release(c, A.st_n);
+  bg_release(c, A.st_c);
+  bg_release(c, A.flag);
+  bg_release(c, A.nflag);
+  if (!rc && c->hstat->first_bad != ~0ULL)
+    rc = bg_fail(c, BG_E_UNSUPPORTED,
+                 "closest-features: more than 128 rows of <query-file> held at once (deeply nested input)");
+  if (rc) { bg_result_free(r); return rc; }
+  *out = r;
+  return 0;
+}

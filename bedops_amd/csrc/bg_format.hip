@@ -11,6 +11,7 @@
 // tile to HBM with 16-byte stores (byte stores only at the two unaligned edges).
 // %.{p}lf is rendered exactly: the double's binary value times 10^p is rounded half-to-
 // even in 128-bit integer arithmetic, which is what glibc printf does.
+#include <climits>
 #include <cstring>
 
 #include "bg_internal.h"
@@ -42,6 +43,15 @@ struct FmtArgs {
   int dlen;
   char delim[16];
   uint64_t n;
+  // closest-features: second table + chosen rows
+  const int64_t* s2;
+  const int64_t* e2;
+  const char* text2;
+  const uint64_t* rest_off2;
+  const uint32_t* rest_len2;
+  const int64_t* left;
+  const int64_t* right;
+  int shortest, print_dist, no_ref;
 };
 
 __device__ __forceinline__ int dec_len_u64(uint64_t v) {
@@ -129,9 +139,113 @@ struct LdsOut {
   __device__ __forceinline__ void put(char c) { *p++ = c; }
 };
 
+template <typename Out>
+__device__ __forceinline__ void put_i64(Out& o, int64_t v) {
+  if (v < 0) {
+    o.put('-');
+    const uint64_t u = (uint64_t)0 - (uint64_t)v;
+    put_u64(o, u, dec_len_u64(u));
+  } else {
+    put_u64(o, (uint64_t)v, dec_len_u64((uint64_t)v));
+  }
+}
+
+// "%s\t%lu\t%lu%s": chrom, start, end, verbatim rest (B3Rest print, Bed.hpp:321-325)
+template <typename Out>
+__device__ __forceinline__ void put_row(const FmtArgs& A, Out& o, int64_t s, int64_t e,
+                                        const char* rest, uint32_t rl) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  const uint32_t nl = A.name_len[g];
+  const char* nm = A.names + A.name_off[g];
+  for (uint32_t q = 0; q < nl; ++q) o.put(nm[q]);
+  o.put('\t');
+  const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
+  put_u64(o, cs, dec_len_u64(cs));
+  o.put('\t');
+  put_u64(o, ce, dec_len_u64(ce));
+  for (uint32_t q = 0; q < rl; ++q) o.put(rest[q]);
+}
+
+template <typename Out>
+__device__ __forceinline__ void put_delim(const FmtArgs& A, Out& o) {
+  for (int d = 0; d < A.dlen; ++d) o.put(A.delim[d]);
+}
+
+// getDistance(x, ref) of closest-features (ClosestFeature.cpp:244-255), same chromosome
+__device__ __forceinline__ int64_t cf_dist(int64_t xs, int64_t xe, int64_t bs, int64_t be) {
+  if (xe <= bs) return -((bs - xe) + 1);
+  if (be <= xs) return (xs - be) + 1;
+  return 0;
+}
+
+// one closest-features line: PrintAll (Printers.hpp:54-93) or PrintShortest (:112-200)
+template <typename Out>
+__device__ __forceinline__ void render_closest(const FmtArgs& A, uint64_t k, Out& o) {
+  const int64_t bs = A.s[k], be = A.e[k];
+  if (!A.no_ref) {
+    put_row(A, o, bs, be, A.text + A.rest_off[k], A.rest_len[k]);
+    put_delim(A, o);
+  }
+  const int64_t L = A.left[k], R = A.right[k];
+  auto cand = [&](int64_t x, int zero_dist) {
+    put_row(A, o, A.s2[x], A.e2[x], A.text2 + A.rest_off2[x], A.rest_len2[x]);
+    if (A.print_dist) {
+      put_delim(A, o);
+      if (zero_dist) o.put('0');
+      else put_i64(o, cf_dist(A.s2[x], A.e2[x], bs, be));
+    }
+  };
+  auto na = [&]() {
+    o.put('N');
+    o.put('A');
+    if (A.print_dist) {
+      put_delim(A, o);
+      o.put('N');
+      o.put('A');
+    }
+  };
+  if (!A.shortest) {
+    if (L >= 0) cand(L, 0);
+    else na();
+    put_delim(A, o);
+    if (R >= 0) cand(R, 0);
+    else na();
+    o.put('\n');
+    return;
+  }
+  if (L < 0 && R < 0) {
+    na();
+    o.put('\n');
+    return;
+  }
+  int64_t d1 = LLONG_MAX, d2 = LLONG_MAX;
+  if (L >= 0) {
+    if (A.e2[L] <= bs) {  // <= as getDistance
+      d1 = (bs - A.e2[L]) + 1;
+      if (R < 0) { cand(L, 0); o.put('\n'); return; }
+    } else {  // overlapping or adjacent left: printed with distance 0
+      cand(L, 1);
+      o.put('\n');
+      return;
+    }
+  }
+  if (R >= 0) {
+    if (L < 0) { cand(R, 0); o.put('\n'); return; }
+    if (be <= A.s2[R]) d2 = (A.s2[R] - be) + 1;
+    else { cand(R, 1); o.put('\n'); return; }
+  }
+  if (d1 <= d2) cand(L, 0);
+  else cand(R, 0);
+  o.put('\n');
+}
+
 // renders (or measures) line k; returns false on a value outside the GPU range
 template <typename Out>
 __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
+  if (A.kind == RES_CLOSEST) {
+    render_closest(A, k, o);
+    return true;
+  }
   if (A.kind == RES_MAP) {
     const int32_t c = A.cnt[k];
     if (A.skip_unmapped && c == 0) return true;
@@ -259,6 +373,26 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.text = T->text;
     A.rest_off = T->rest_off;
     A.rest_len = T->rest_len;
+  } else if (r->kind == RES_CLOSEST) {
+    bg_table* T = s->t[r->tab];
+    bg_table* U = s->t[r->tab2];
+    A.s = T->ks;
+    A.e = T->ke;
+    A.text = T->text;
+    A.rest_off = T->rest_off;
+    A.rest_len = T->rest_len;
+    A.s2 = U->ks;
+    A.e2 = U->ke;
+    A.text2 = U->text;
+    A.rest_off2 = U->rest_off;
+    A.rest_len2 = U->rest_len;
+    A.left = r->left;
+    A.right = r->right;
+    A.shortest = r->copts.shortest;
+    A.print_dist = r->copts.print_dist;
+    A.no_ref = r->copts.no_ref;
+    A.dlen = (int)strnlen(r->copts.delim, 15);
+    memcpy(A.delim, r->copts.delim, A.dlen);
   } else {
     A.s = s->t[r->tab]->ks;  // reference rows (chromosome spans)
     A.e = s->t[r->tab]->ke;

@@ -95,7 +95,7 @@ struct bg_set {
   uint32_t max_name_len = 0;
 };
 
-enum { RES_IVL = 0, RES_ROWS = 1, RES_MAP = 2 };
+enum { RES_IVL = 0, RES_ROWS = 1, RES_MAP = 2, RES_CLOSEST = 3 };
 
 struct bg_result {
   bg_ctx* ctx = nullptr;
@@ -112,6 +112,11 @@ struct bg_result {
   int32_t* cnt = nullptr;
   int64_t* isum = nullptr;
   bg_map_opts mopts;
+  // RES_CLOSEST: per row of table `tab`, the chosen rows of table `tab2` (-1: NA)
+  int64_t* left = nullptr;
+  int64_t* right = nullptr;
+  int tab2 = -1;
+  bg_closest_opts copts;
   // rendered text
   char* text = nullptr;
   uint64_t nbytes = 0;

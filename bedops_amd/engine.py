@@ -23,7 +23,7 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_result_text_device", "bg_result_copy_text", "bg_result_write", "bg_result_free",
            "bg_stats", "bg_host_alloc", "bg_host_free", "bg_prof_enable", "bg_prof_read",
            "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
-           "bg_set_chrom_name"]
+           "bg_set_chrom_name", "bg_closest"]
 
 
 def lib_path():
@@ -46,6 +46,12 @@ class _MapOpts(ctypes.Structure):
     _fields_ = [("overlap_bp", ctypes.c_uint64), ("n_ops", ctypes.c_int),
                 ("ops", ctypes.c_int * 16), ("precision", ctypes.c_int),
                 ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
+                ("delim", ctypes.c_char * 16)]
+
+
+class _ClosestOpts(ctypes.Structure):
+    _fields_ = [("shortest", ctypes.c_int), ("print_dist", ctypes.c_int),
+                ("no_ref", ctypes.c_int), ("no_overlaps", ctypes.c_int),
                 ("delim", ctypes.c_char * 16)]
 
 
@@ -81,6 +87,7 @@ def load_library():
     L.bg_element_of.argtypes = [vp, vp, i32, ctypes.POINTER(i32), i32, ctypes.c_double, i32,
                                 i32, ctypes.POINTER(vp)]
     L.bg_map.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_MapOpts), ctypes.POINTER(vp)]
+    L.bg_closest.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_ClosestOpts), ctypes.POINTER(vp)]
     L.bg_result_rows.argtypes = [vp, ctypes.POINTER(u64)]
     L.bg_result_format.argtypes = [vp, vp, ctypes.POINTER(u64)]
     L.bg_result_text_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
@@ -300,6 +307,28 @@ class Engine:
             o.delim = delim.encode()
             h = ctypes.c_void_p()
             self._check(self.L.bg_map(self.ctx, s.h, 0, 1, ctypes.byref(o), ctypes.byref(h)))
+            r = Result(self, h)
+            try:
+                return r.text()
+            finally:
+                r.free()
+        finally:
+            s.free()
+
+    # -------------------------------------------------------------- closest-features
+    def closest(self, input_text, query_text, shortest=False, dist=False, no_ref=False,
+                no_overlaps=False, delim="|", chrom=None):
+        """closest-features [flags] <input-file> <query-file> on in-memory texts -> bytes"""
+        s = self.load([(input_text, BED3_REST), (query_text, BED3_REST)])
+        try:
+            if chrom:
+                s.restrict_chrom(chrom)
+            o = _ClosestOpts()
+            o.shortest, o.print_dist = int(bool(shortest)), int(bool(dist))
+            o.no_ref, o.no_overlaps = int(bool(no_ref)), int(bool(no_overlaps))
+            o.delim = delim.encode()
+            h = ctypes.c_void_p()
+            self._check(self.L.bg_closest(self.ctx, s.h, 0, 1, ctypes.byref(o), ctypes.byref(h)))
             r = Result(self, h)
             try:
                 return r.text()

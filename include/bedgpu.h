@@ -17,8 +17,9 @@
  *   bg_map ............... WindowSweep::sweep overload 2 + MultiVisitor{Count,Average}
  *                          (interfaces/src/algorithm/sweep/WindowSweepImpl.cpp:168-256,
  *                           algorithm/visitors/other/MultiVisitor.hpp:45-129)
- *   bg_closest ........... FeatDist::findDistances + PrintShortest
- *                          (applications/bed/closestfeats/src/ClosestFeature.cpp:260-413, Printers.hpp:104-205)
+ *   bg_closest ........... FeatDist::findDistances + PrintAll / PrintShortest
+ *                          (applications/bed/closestfeats/src/ClosestFeature.cpp:260-413,
+ *                           Printers.hpp:46-205; options closestfeats/src/Input.hpp:46-103)
  *   bg_result_format /
  *   bg_result_write ...... record() -> printf("%s\t%lu\t%lu\n") (Bedops.cpp:148-152, Bed.hpp:228-232,321-325),
  *                          visitor printing ("%d", "%.6lf", "NAN": Formats.hpp:31-50, NaN.cpp:26)
@@ -77,6 +78,14 @@ typedef struct bg_map_opts {
 #define BG_MAP_COUNT 1
 #define BG_MAP_MEAN 2
 
+typedef struct bg_closest_opts {
+  int shortest;       /* --closest / --shortest: one element per row, ties to the left */
+  int print_dist;     /* --dist: signed distance columns                              */
+  int no_ref;         /* --no-ref: do not echo the <input-file> row                   */
+  int no_overlaps;    /* --no-overlaps                                                */
+  char delim[16];     /* --delim (default "|")                                        */
+} bg_closest_opts;
+
 /* context */
 int bg_open(bg_ctx** ctx, int device);
 void bg_close(bg_ctx* ctx);
@@ -99,6 +108,10 @@ int bg_element_of(bg_ctx* ctx, bg_set* set, int ref, const int* others, int noth
                   double threshold, int use_percent, int invert, bg_result** out);
 int bg_map(bg_ctx* ctx, bg_set* set, int ref, int map, const bg_map_opts* opts,
            bg_result** out);
+/* closest-features <input-file> <query-file>: `ref` = the <input-file> table, `query` =
+ * the <query-file> table, both loaded as BG_BED3_REST; one output line per ref row */
+int bg_closest(bg_ctx* ctx, bg_set* set, int ref, int query, const bg_closest_opts* opts,
+               bg_result** out);
 
 /* results */
 int bg_result_rows(const bg_result* res, uint64_t* rows);

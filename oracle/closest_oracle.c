@@ -1,0 +1,307 @@
+/*
+ * oracle/closest_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C) of the reference `closest-features` for the GPU hot path.
+ * Used only by tests/ (parity checker); never linked into libbedgpu or the CLIs.
+ *
+ * It restates the reference's control flow step by step, including the reader's
+ * push-back cache, because the left/right choice depends on what that cache holds:
+ *   option parsing ......................... applications/bed/closestfeats/src/Input.hpp:46-103
+ *   both inputs read as B3Rest ............. ClosestFeature.cpp:217-221
+ *   BedReader (LIFO cache, PushBack(list)) . closestfeats/src/BedReader.hpp:55-80
+ *   getDistance ............................ ClosestFeature.cpp:244-255
+ *   proportionOverlapLeft / getCentroid .... ClosestFeature.cpp:226-239
+ *   findDistances .......................... ClosestFeature.cpp:260-413
+ *   PrintAll / PrintShortest ............... closestfeats/src/Printers.hpp:46-205
+ *   "NA" ................................... ClosestFeature.cpp:56
+ * PARITY UNPINNED: the reference ships no closest-features known-answer tests and SURVEY.md
+ * records no output hash for it, so this restatement is checked only against the cited
+ * control flow and hand-worked cases (tests/test_oracle.py).
+ *
+ * usage: closest_oracle [--closest|--shortest] [--dist] [--no-ref] [--no-overlaps]
+ *                       [--delim D] [--chrom C] [--ec|--header] <input-file> <query-file>
+ */
+#include "bedio.h"
+
+static chrom_pool_t POOL;
+static bedfile_t Q;  /* <input-file>: every row gets one output line (reference "ref") */
+static bedfile_t C;  /* <query-file>: candidates (reference "nonRef") */
+
+static const int64_t PLUS_INF = INT64_MAX, MINUS_INF = INT64_MIN;
+
+/* --- candidate reader with the reference's LIFO cache (BedReader.hpp:55-80) --- */
+static int64_t* cache;
+static int64_t ncache, capcache, next_row;
+
+static int64_t read_line(void) {
+  if (ncache) return cache[--ncache];
+  if (next_row < C.n) return next_row++;
+  return -1;
+}
+
+static void push_back_list(const int64_t* l, int64_t n) { /* insert(end, rbegin, rend) */
+  for (int64_t i = n - 1; i >= 0; --i) {
+    if (ncache == capcache) {
+      capcache = capcache ? 2 * capcache : 64;
+      cache = (int64_t*)realloc(cache, (size_t)capcache * sizeof(int64_t));
+    }
+    cache[ncache++] = l[i];
+  }
+}
+
+/* the std::list<BedType2*> read of findDistances */
+static int64_t* rd;
+static int64_t nrd, caprd;
+static void rd_push(int64_t x) {
+  if (nrd == caprd) {
+    caprd = caprd ? 2 * caprd : 64;
+    rd = (int64_t*)realloc(rd, (size_t)caprd * sizeof(int64_t));
+  }
+  rd[nrd++] = x;
+}
+
+/* getDistance(b1 = candidate c, b2 = query b), ClosestFeature.cpp:244-255 */
+static int64_t get_distance(const bedfile_t* F1, int64_t i, const bedfile_t* F2, int64_t j) {
+  int v = strcmp(POOL.names[F1->chrom[i]], POOL.names[F2->chrom[j]]);
+  if (v != 0) return v < 0 ? MINUS_INF : PLUS_INF;
+  if (F1->end[i] <= F2->start[j]) return -(int64_t)(F2->start[j] - F1->end[i] + 1);
+  if (F2->end[j] <= F1->start[i]) return (int64_t)(F1->start[i] - F2->end[j] + 1);
+  return 0;
+}
+
+static double centroid(int64_t b) { return ((double)Q.end[b] - 1.0 + (double)Q.start[b]) / 2.0; }
+
+static double proportion_overlap_left(int64_t c, double marker) {
+  if (marker < (double)C.start[c]) return 0.;
+  return (marker + 1 - (double)C.start[c]) / (double)(C.end[c] - C.start[c]);
+}
+
+/* --- printers (Printers.hpp) --- */
+static const char* DELIM = "|";
+static int print_dist = 0, suppress_ref = 0, shortest = 0;
+
+static void print_row(const bedfile_t* F, int64_t i) {
+  printf("%s\t%" PRIu64 "\t%" PRIu64 "%s", POOL.names[F->chrom[i]], F->start[i], F->end[i],
+         F->rest[i]);
+}
+
+static void print_all(int64_t b, int64_t left, int64_t right) {
+  if (!suppress_ref) {
+    print_row(&Q, b);
+    fputs(DELIM, stdout);
+  }
+  if (left >= 0) {
+    print_row(&C, left);
+    if (print_dist) printf("%s%" PRId64, DELIM, get_distance(&C, left, &Q, b));
+  } else {
+    fputs("NA", stdout);
+    if (print_dist) printf("%sNA", DELIM);
+  }
+  fputs(DELIM, stdout);
+  if (right >= 0) {
+    print_row(&C, right);
+    if (print_dist) printf("%s%" PRId64, DELIM, get_distance(&C, right, &Q, b));
+  } else {
+    fputs("NA", stdout);
+    if (print_dist) printf("%sNA", DELIM);
+  }
+  fputs("\n", stdout);
+}
+
+static void print_pick(int64_t b, int64_t x, int zero) {
+  print_row(&C, x);
+  if (print_dist) {
+    if (zero) printf("%s0", DELIM);
+    else printf("%s%" PRId64, DELIM, get_distance(&C, x, &Q, b));
+  }
+  fputs("\n", stdout);
+}
+
+static void print_shortest(int64_t b, int64_t left, int64_t right) {
+  int64_t d1 = INT64_MAX, d2 = INT64_MAX;
+  if (!suppress_ref) {
+    print_row(&Q, b);
+    fputs(DELIM, stdout);
+  }
+  if (left < 0 && right < 0) {
+    fputs("NA", stdout);
+    if (print_dist) printf("%sNA", DELIM);
+    fputs("\n", stdout);
+    return;
+  }
+  if (left >= 0) {
+    if (C.end[left] <= Q.start[b]) {
+      d1 = (int64_t)(Q.start[b] - C.end[left] + 1);
+      if (right < 0) { print_pick(b, left, 0); return; }
+    } else {
+      print_pick(b, left, 1);
+      return;
+    }
+  }
+  if (right >= 0) {
+    if (left < 0) { print_pick(b, right, 0); return; }
+    if (Q.end[b] <= C.start[right]) d2 = (int64_t)(C.start[right] - Q.end[b] + 1);
+    else { print_pick(b, right, 1); return; }
+  }
+  if (d1 <= d2) print_pick(b, left, 0);
+  else print_pick(b, right, 0);
+}
+
+/* --- findDistances, ClosestFeature.cpp:260-413 --- */
+static void find_distances(int allow_overlaps) {
+  for (int64_t b = 0; b < Q.n; ++b) {
+    int64_t left_dist = MINUS_INF, right_dist = PLUS_INF;
+    int64_t left = -1, right = -1, c = -1;
+    int left_cached = 0;
+    nrd = 0;
+    while ((c = read_line()) >= 0) {
+      const int64_t dist = get_distance(&C, c, &Q, b);
+      if (dist == MINUS_INF) continue; /* catch the candidates up */
+      if (dist == PLUS_INF) {          /* catch the queries up */
+        if (left >= 0 && !left_cached) rd_push(left);
+        left_cached = left >= 0;
+        if (right >= 0) rd_push(right);
+        rd_push(c);
+        break;
+      }
+      if (dist < 0 && dist >= left_dist) {
+        nrd = 0; /* a new best left makes everything cached obsolete */
+        left_dist = dist;
+        left = c;
+        left_cached = 0;
+      } else if (dist < 0) {
+        if (!left_cached) rd_push(left);
+        left_cached = 1;
+      } else if (dist > 0 && dist < right_dist) {
+        if (left >= 0 && !left_cached) rd_push(left);
+        left_cached = left >= 0;
+        right_dist = dist;
+        right = c;
+        rd_push(c);
+        break;
+      } else if (dist > 0) {
+        if (left >= 0 && !left_cached) rd_push(left);
+        left_cached = left >= 0;
+        if (right >= 0) rd_push(right);
+        rd_push(c);
+        break;
+      } else if (allow_overlaps) { /* dist == 0 */
+        if (C.start[c] <= Q.start[b]) { /* hangs over the left edge */
+          if (left >= 0 && C.end[left] <= C.end[c] && !left_cached) {
+            /* dropped: never the closest left again */
+          } else if (left >= 0 && !left_cached) {
+            rd_push(left);
+          }
+          left = c;
+          left_dist = 0;
+          left_cached = 0;
+        } else if (Q.end[b] <= C.end[c]) { /* hangs over the right edge */
+          if (left >= 0 && !left_cached) rd_push(left);
+          left_cached = left >= 0;
+          if (right >= 0) rd_push(right);
+          right = c;
+          right_dist = 0;
+        } else { /* contained in the query row */
+          const double prop = proportion_overlap_left(c, centroid(b));
+          if (0 == left_dist) {
+            if (prop < 0.5) {
+              if (!left_cached) rd_push(left);
+              left_cached = 1;
+              if (right >= 0) rd_push(right);
+              right = c;
+              right_dist = 0;
+            } else {
+              if (!left_cached) rd_push(left);
+              left_cached = 1;
+              rd_push(c);
+            }
+          } else if (prop >= 0.5) {
+            nrd = 0;
+            left_cached = 0;
+            left = c;
+            left_dist = 0;
+          } else {
+            if (left >= 0 && !left_cached) rd_push(left);
+            left_cached = left >= 0;
+            if (right >= 0) rd_push(right);
+            right = c;
+            right_dist = 0;
+          }
+        }
+      } else { /* overlap, --no-overlaps: cache it for later queries */
+        if (left >= 0 && !left_cached) {
+          rd_push(left);
+          left_cached = 1;
+        }
+        rd_push(c);
+      }
+    }
+    if (c < 0 && left >= 0 && !left_cached) rd_push(left);
+    if (c < 0 && right >= 0) rd_push(right);
+    push_back_list(rd, nrd);
+    nrd = 0;
+    if (shortest) print_shortest(b, left, right);
+    else print_all(b, left, right);
+  }
+}
+
+static void filter_chrom(bedfile_t* f, const char* chrom) {
+  int64_t w = 0;
+  for (int64_t i = 0; i < f->n; ++i) {
+    if (strcmp(POOL.names[f->chrom[i]], chrom) != 0) continue;
+    f->chrom[w] = f->chrom[i];
+    f->start[w] = f->start[i];
+    f->end[w] = f->end[i];
+    f->rest[w] = f->rest[i];
+    ++w;
+  }
+  f->n = w;
+}
+
+static int die(const char* msg) {
+  fprintf(stderr, "May use closest-features --help for more help.\n\nError: %s\n", msg);
+  return EXIT_FAILURE;
+}
+
+int main(int argc, char** argv) {
+  int allow_overlaps = 1;
+  const char* chrom = NULL;
+  int i = 1, outopt = 0;
+  if (argc == 1) return die("no input");
+  for (; i < argc; ++i) {
+    const char* a = argv[i];
+    if (!strcmp(a, "--ec") || !strcmp(a, "--header")) continue;
+    if (!strcmp(a, "--no-overlaps")) { allow_overlaps = 0; continue; }
+    if (!strcmp(a, "--delim")) {
+      if (++i >= argc) return die("No value given for --delim.");
+      DELIM = argv[i];
+      continue;
+    }
+    if (!strcmp(a, "--chrom")) {
+      if (++i >= argc) return die("No value given for --chrome.");
+      chrom = argv[i];
+      continue;
+    }
+    if (!strcmp(a, "--closest") || !strcmp(a, "--shortest")) {
+      if (outopt) return die("Multiple output options not allowed.");
+      shortest = outopt = 1;
+      continue;
+    }
+    if (!strcmp(a, "--dist")) { print_dist = 1; continue; }
+    if (!strcmp(a, "--no-ref")) { suppress_ref = 1; continue; }
+    if (i + 2 != argc) return die("Unknown option");
+    break;
+  }
+  if (i + 2 != argc) return die("Not enough input files given.");
+  FILE* fq = open_input(argv[i]);
+  FILE* fc = open_input(argv[i + 1]);
+  if (!fq || !fc) return die("Unable to find file");
+  read_bed3(fq, &POOL, &Q, 1);
+  read_bed3(fc, &POOL, &C, 1);
+  if (chrom) {
+    filter_chrom(&Q, chrom);
+    filter_chrom(&C, chrom);
+  }
+  find_distances(allow_overlaps);
+  return 0;
+}

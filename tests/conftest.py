@@ -23,7 +23,8 @@ def _make(*targets):
 def oracle_bin():
     _make("oracle")
     return {"bedops": os.path.join(ROOT, "oracle", "build", "bedops_oracle"),
-            "bedmap": os.path.join(ROOT, "oracle", "build", "bedmap_oracle")}
+            "bedmap": os.path.join(ROOT, "oracle", "build", "bedmap_oracle"),
+            "closest": os.path.join(ROOT, "oracle", "build", "closest_oracle")}
 
 
 @pytest.fixture(scope="session")
@@ -31,7 +32,8 @@ def gpu_bin():
     """The drop-in front-ends (C, linked to libbedgpu.so)."""
     _make("lib", "cli")
     return {"bedops": os.path.join(ROOT, "bedops_amd", "bin", "bedops"),
-            "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap")}
+            "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap"),
+            "closest": os.path.join(ROOT, "bedops_amd", "bin", "closest-features")}
 
 
 @pytest.fixture(scope="session")

@@ -207,3 +207,78 @@ def test_intersect_and_element_of_100M_reference_hash(eng, bedgen):
     out = eng.bedops("-e", [a, b], spec="1")
     assert out.count(b"\n") == 90223158 and len(out) == 2150489515
     assert _h(out) == "98a8a1c8a72bf6f5"
+
+
+# ---------------------------------------------------------------------------------
+# closest-features: the GPU replay of the reference's reader cache vs the oracle
+# ---------------------------------------------------------------------------------
+CLOSEST_OPTS = [[], ["--closest"], ["--dist"], ["--closest", "--dist"], ["--no-overlaps"],
+                ["--no-overlaps", "--closest", "--dist"], ["--no-ref"], ["--delim", "\t"]]
+
+
+def _closest_kwargs(args):
+    kw = {"shortest": "--closest" in args, "dist": "--dist" in args,
+          "no_ref": "--no-ref" in args, "no_overlaps": "--no-overlaps" in args}
+    if "--delim" in args:
+        kw["delim"] = args[args.index("--delim") + 1]
+    return kw
+
+
+def test_closest_hand_cases_gpu(eng):
+    from test_oracle import CLOSEST_C, CLOSEST_KATS, CLOSEST_Q
+    for args, want in CLOSEST_KATS:
+        got = eng.closest(CLOSEST_Q.encode(), CLOSEST_C.encode(), **_closest_kwargs(args))
+        assert got.decode() == want, args
+
+
+@pytest.mark.parametrize("shape", ["sparse", "dense", "nested", "zero"])
+@pytest.mark.parametrize("args", CLOSEST_OPTS, ids=lambda a: "_".join(a) or "default")
+def test_random_closest_vs_oracle(eng, oracle_bin, shape, args):
+    rng = random.Random(hash((shape, tuple(args))) & 0xffffffff)
+    nq, nc, span, ml, zf = {"sparse": (3000, 400, 200000, 100, 0.0),
+                            "dense": (2000, 20000, 50000, 60, 0.0),
+                            "nested": (3000, 3000, 100000, 3000, 0.0),
+                            "zero": (2500, 2500, 10000, 80, 0.1)}[shape]
+    q = randbed.text(randbed.rows(rng, nq, span=span, maxlen=ml, zero_frac=zf), rest="cols", rng=rng)
+    c = randbed.text(randbed.rows(rng, nc, span=span, maxlen=ml, zero_frac=zf), rest="cols", rng=rng)
+    with tempfile.TemporaryDirectory() as td:
+        want = run_oracle(oracle_bin["closest"], args, [q, c], td)
+    got = eng.closest(q.encode(), c.encode(), **_closest_kwargs(args))
+    assert got == want
+
+
+def test_closest_edge_inputs(eng, oracle_bin):
+    cases = [("", "chr1\t1\t2\n"), ("chr1\t1\t2\n", ""), ("", ""),
+             ("chr1\t5\t5\nchr1\t5\t9\n", "chr1\t5\t5\nchr1\t9\t9\n"),
+             ("chrA\t10\t20\nchrB\t10\t20\n", "chrB\t1\t2\nchrC\t3\t4\n")]
+    for q, c in cases:
+        for args in (["--closest", "--dist"], []):
+            with tempfile.TemporaryDirectory() as td:
+                want = run_oracle(oracle_bin["closest"], args, [q, c], td)
+            assert eng.closest(q.encode(), c.encode(), **_closest_kwargs(args)) == want, (q, c, args)
+
+
+def test_closest_cli_and_chrom(gpu_bin, oracle_bin, tmp_path):
+    rng = random.Random(7)
+    q = randbed.text(randbed.rows(rng, 5000, span=30000), rest="cols", rng=rng)
+    c = randbed.text(randbed.rows(rng, 8000, span=30000), rest="cols", rng=rng)
+    pq, pc = tmp_path / "q.bed", tmp_path / "c.bed"
+    pq.write_text(q)
+    pc.write_text(c)
+    for args in (["--closest", "--dist"], ["--chrom", "chr10"], ["--no-overlaps", "--chrom", "chrX"]):
+        want = subprocess.run([oracle_bin["closest"], *args, str(pq), str(pc)],
+                              stdout=subprocess.PIPE, check=True).stdout
+        got = subprocess.run([gpu_bin["closest"], *args, str(pq), str(pc)],
+                             stdout=subprocess.PIPE, check=True).stdout
+        assert got == want, args
+
+
+@pytest.mark.slow
+def test_closest_large_vs_oracle(eng, oracle_bin, bedgen, tmp_path):
+    q = subprocess.run([bedgen, "1000000", "46"], stdout=subprocess.PIPE, check=True).stdout
+    c = subprocess.run([bedgen, "20000000", "47"], stdout=subprocess.PIPE, check=True).stdout
+    (tmp_path / "q.bed").write_bytes(q)
+    (tmp_path / "c.bed").write_bytes(c)
+    want = subprocess.run([oracle_bin["closest"], "--closest", str(tmp_path / "q.bed"),
+                           str(tmp_path / "c.bed")], stdout=subprocess.PIPE, check=True).stdout
+    assert eng.closest(q, c, shortest=True) == want

@@ -52,3 +52,56 @@ def test_oracle_bedmap_small_known_answer(oracle_bin, tmp_path):
     out = subprocess.run([oracle_bin["bedmap"], "--count", "--mean", str(ref), str(mp)],
                          stdout=subprocess.PIPE, check=True).stdout
     assert out == b"2|6.500000\n0|NAN\n"
+
+
+# hand-worked closest-features cases (ClosestFeature.cpp:260-413, Printers.hpp:46-205):
+# q1 [100,200): b [60,90) is the left (distance -(100-90+1) = -11); c [150,160) lies inside
+# q1 and starts after its centroid 149.5 (proportion 0 < 0.5, no overlapping left yet), so
+# it is the right; --closest prints the overlapping right. q2 [500,510): d [300,400) left
+# (-101), e [505,600) hangs over the right edge. q3: no candidate on chr2 -> NA.
+CLOSEST_Q = "chr1\t100\t200\tq1\nchr1\t500\t510\tq2\nchr2\t10\t20\tq3\n"
+CLOSEST_C = ("chr1\t10\t50\ta\nchr1\t60\t90\tb\nchr1\t150\t160\tc\nchr1\t300\t400\td\n"
+             "chr1\t505\t600\te\nchr3\t1\t2\tf\n")
+CLOSEST_KATS = [
+    ([], "chr1\t100\t200\tq1|chr1\t60\t90\tb|chr1\t150\t160\tc\n"
+         "chr1\t500\t510\tq2|chr1\t300\t400\td|chr1\t505\t600\te\n"
+         "chr2\t10\t20\tq3|NA|NA\n"),
+    (["--closest"], "chr1\t100\t200\tq1|chr1\t150\t160\tc\n"
+                    "chr1\t500\t510\tq2|chr1\t505\t600\te\nchr2\t10\t20\tq3|NA\n"),
+    (["--dist"], "chr1\t100\t200\tq1|chr1\t60\t90\tb|-11|chr1\t150\t160\tc|0\n"
+                 "chr1\t500\t510\tq2|chr1\t300\t400\td|-101|chr1\t505\t600\te|0\n"
+                 "chr2\t10\t20\tq3|NA|NA|NA|NA\n"),
+    (["--closest", "--dist"], "chr1\t100\t200\tq1|chr1\t150\t160\tc|0\n"
+                              "chr1\t500\t510\tq2|chr1\t505\t600\te|0\nchr2\t10\t20\tq3|NA|NA\n"),
+    (["--no-overlaps"], "chr1\t100\t200\tq1|chr1\t60\t90\tb|chr1\t300\t400\td\n"
+                        "chr1\t500\t510\tq2|chr1\t300\t400\td|NA\nchr2\t10\t20\tq3|NA|NA\n"),
+    (["--no-ref", "--closest", "--delim", ";"], "chr1\t150\t160\tc\nchr1\t505\t600\te\nNA\n"),
+]
+
+
+def test_oracle_closest_hand_cases(oracle_bin, tmp_path):
+    q, c = tmp_path / "q.bed", tmp_path / "c.bed"
+    q.write_text(CLOSEST_Q)
+    c.write_text(CLOSEST_C)
+    for args, want in CLOSEST_KATS:
+        out = subprocess.run([oracle_bin["closest"], *args, str(q), str(c)],
+                             stdout=subprocess.PIPE, check=True).stdout.decode()
+        assert out == want, args
+
+
+def test_closest_cache_free_model_is_not_the_reference(oracle_bin, tmp_path):
+    """Documents why the GPU replays the reference's cache: a candidate that overlapped an
+    earlier row and ends after a later-found left row is dropped by the reference
+    (ClosestFeature.cpp:300-304), so a cache-free nearest-left search would differ."""
+    import model_closest
+    q, c = tmp_path / "q.bed", tmp_path / "c.bed"
+    # row 1 [150,170): c0 [79,156) overlaps it; c1 [122,148) is a new best left and
+    # empties the kept list, dropping c0. Row 2 [178,202): the true nearest left is c0
+    # (ends 156) but the reference reports c1.
+    q.write_text("chr1\t150\t170\tr1\nchr1\t178\t202\tr2\n")
+    c.write_text("chr1\t79\t156\tc0\nchr1\t122\t148\tc1\n")
+    out = subprocess.run([oracle_bin["closest"], "--no-overlaps", str(q), str(c)],
+                         stdout=subprocess.PIPE, check=True).stdout.decode().splitlines()
+    assert out[1] == "chr1\t178\t202\tr2|chr1\t122\t148\tc1|NA"
+    left, _ = model_closest.pick([(79, 156), (122, 148)], (178, 202), allow_overlaps=False)
+    assert left == 0  # cache-free answer: c0
