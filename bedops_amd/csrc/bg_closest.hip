@@ -29,13 +29,14 @@
 // arithmetic. Output (PrintAll / PrintShortest, Printers.hpp:46-205) is rendered by
 // bg_format.hip from the per-row (left, right) candidate indices.
 #include <climits>
+#include <cstring>
 
 #include "bg_internal.h"
 
-#define CQ 32      // ref rows per chunk
+#define CQ 64      // ref rows per chunk
 #define CW 8       // speculative warm-up rows before a chunk
 #define CBACK 64   // candidates before the warm-up row where the speculative read starts
-#define CMAX 128   // capacity of the cache and of the per-row kept list
+#define CAP0 256   // initial capacity of the cache stack / kept list (x4 on overflow)
 #define FIX_ROUNDS 8
 
 struct ClArgs {
@@ -48,20 +49,23 @@ struct ClArgs {
   int overlaps;
   int64_t* left;
   int64_t* right;
-  // recorded states: slot 2k = chunk k's start state, 2k+1 = its final state
+  // per chunk k: slot 2k = start state (snapshot), slot 2k+1 = working / final state,
+  // kl[k] = the per-row kept list; each holds `cap` candidate indices
   uint64_t* st_fp;
   uint32_t* st_n;
-  uint32_t* st_c;  // CMAX candidate indices per slot, in stack order (top last)
+  uint32_t* st_c;  // cache stack per slot, bottom first (pop from the top = last)
+  uint32_t* kl;
+  uint32_t cap;
   uint32_t nchunks;
   uint32_t* flag;
   uint32_t* nflag;
-  bg_dstatus* st;
+  uint32_t* overflow;
 };
 
 struct ClState {
   uint64_t fp;
   uint32_t n;
-  uint32_t c[CMAX];
+  uint32_t* c;  // stack storage (global, `cap` entries)
 };
 
 #define D_MINUS LLONG_MIN
@@ -77,18 +81,19 @@ __device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, i
 }
 
 // replay ref rows [b0, b1) from state S; emit: write left/right. false on overflow
-__device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, bool emit) {
-  uint32_t kept[CMAX];  // the std::list "read" of findDistances
+__device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, uint32_t* kept,
+                       bool emit) {
+  const uint32_t cap = A.cap;
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
     int64_t ld = D_MINUS, rdist = D_PLUS;
     int64_t left = -1, right = -1, c = -1;
     bool lc = false;  // leftCached
-    uint32_t nk = 0;
+    uint32_t nk = 0;  // the std::list "read" of findDistances
     bool ovf = false;
 #define KEEP(x)                      \
   do {                               \
-    if (nk == CMAX) ovf = true;      \
+    if (nk == cap) ovf = true;       \
     else kept[nk++] = (uint32_t)(x); \
   } while (0)
     for (;;) {
@@ -187,7 +192,7 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, bo
     if (c < 0 && right >= 0) KEEP(right);
 #undef KEEP
     // BedReader::PushBack(list): the list comes back out in list order
-    if (ovf || S.n + nk > CMAX) return false;
+    if (ovf || S.n + nk > cap) return false;
     for (uint32_t i = nk; i-- > 0;) S.c[S.n++] = kept[i];
     if (emit) {
       A.left[b] = left;
@@ -197,53 +202,63 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, bo
   return true;
 }
 
-__device__ __forceinline__ void cl_save(const ClArgs& A, uint64_t slot, const ClState& S) {
-  A.st_fp[slot] = S.fp;
-  A.st_n[slot] = S.n;
-  for (uint32_t i = 0; i < S.n; ++i) A.st_c[slot * CMAX + i] = S.c[i];
+__device__ __forceinline__ uint32_t* cl_slot(const ClArgs& A, uint64_t slot) {
+  return A.st_c + slot * A.cap;
 }
-__device__ __forceinline__ void cl_load(const ClArgs& A, uint64_t slot, ClState& S) {
-  S.fp = A.st_fp[slot];
-  S.n = A.st_n[slot];
-  for (uint32_t i = 0; i < S.n; ++i) S.c[i] = A.st_c[slot * CMAX + i];
+__device__ __forceinline__ void cl_copy(const ClArgs& A, uint64_t from, uint64_t to) {
+  const uint32_t n = A.st_n[from];
+  A.st_fp[to] = A.st_fp[from];
+  A.st_n[to] = n;
+  const uint32_t* x = cl_slot(A, from);
+  uint32_t* y = cl_slot(A, to);
+  for (uint32_t i = 0; i < n; ++i) y[i] = x[i];
 }
 __device__ __forceinline__ bool cl_same(const ClArgs& A, uint64_t x, uint64_t y) {
   if (A.st_fp[x] != A.st_fp[y] || A.st_n[x] != A.st_n[y]) return false;
+  const uint32_t* a = cl_slot(A, x);
+  const uint32_t* b = cl_slot(A, y);
   for (uint32_t i = 0; i < A.st_n[x]; ++i)
-    if (A.st_c[x * CMAX + i] != A.st_c[y * CMAX + i]) return false;
+    if (a[i] != b[i]) return false;
   return true;
 }
 
-__device__ __forceinline__ void cl_overflow(const ClArgs& A, uint64_t b) {
-  bg_report(A.st, b, ERR_RANGE);
+// run chunk k's own rows from the state held in its working slot
+__device__ __forceinline__ void cl_own(const ClArgs& A, uint32_t k) {
+  const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
+  const uint64_t w = 2ull * k + 1;
+  ClState S{A.st_fp[w], A.st_n[w], cl_slot(A, w)};
+  if (!cl_run(A, q0, q1, S, A.kl + (uint64_t)k * A.cap, true)) {
+    atomicOr(A.overflow, 1u);
+    S.fp = ~0ull - 1;  // a final state no successor starts from
+    S.n = 0;
+  }
+  A.st_fp[w] = S.fp;
+  A.st_n[w] = S.n;
 }
 
 __global__ void __launch_bounds__(BG_NT) k_closest_chunks(ClArgs A) {
   const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
   if (k >= A.nchunks) return;
-  const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
-  ClState S;
-  S.n = 0;
-  S.fp = 0;
+  const uint64_t q0 = (uint64_t)k * CQ;
+  const uint64_t w = 2ull * k + 1;
+  ClState S{0, 0, cl_slot(A, w)};
   if (k > 0) {
     const uint64_t qw = q0 - CW;
     const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
     S.fp = p > CBACK ? p - CBACK : 0;
-    if (!cl_run(A, qw, q0, S, false)) {  // speculation overflowed: leave it to the fix-up
-      S.n = 0;
-      S.fp = ~0ull;  // a start state no predecessor ends in
-      cl_save(A, 2ull * k, S);
-      S.fp = ~0ull - 1;  // a final state no successor starts from
-      cl_save(A, 2ull * k + 1, S);
+    if (!cl_run(A, qw, q0, S, A.kl + (uint64_t)k * A.cap, false)) {
+      // speculation overflowed: leave this chunk to the fix-up
+      A.st_fp[2ull * k] = ~0ull;  // a start state no predecessor ends in
+      A.st_n[2ull * k] = 0;
+      A.st_fp[w] = ~0ull - 1;
+      A.st_n[w] = 0;
       return;
     }
   }
-  cl_save(A, 2ull * k, S);
-  if (!cl_run(A, q0, q1, S, true)) {
-    cl_overflow(A, q0);
-    return;
-  }
-  cl_save(A, 2ull * k + 1, S);
+  A.st_fp[w] = S.fp;
+  A.st_n[w] = S.n;
+  cl_copy(A, w, 2ull * k);  // snapshot of the start state
+  cl_own(A, k);
 }
 
 __global__ void k_closest_check(ClArgs A) {
@@ -258,15 +273,9 @@ __global__ void k_closest_check(ClArgs A) {
 __global__ void __launch_bounds__(BG_NT) k_closest_fix(ClArgs A) {
   const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
   if (k == 0 || k >= A.nchunks || !A.flag[k] || A.flag[k - 1]) return;
-  const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
-  ClState S;
-  cl_load(A, 2ull * (k - 1) + 1, S);
-  cl_save(A, 2ull * k, S);
-  if (!cl_run(A, q0, q1, S, true)) {
-    cl_overflow(A, q0);
-    return;
-  }
-  cl_save(A, 2ull * k + 1, S);
+  cl_copy(A, 2ull * (k - 1) + 1, 2ull * k);
+  cl_copy(A, 2ull * k, 2ull * k + 1);
+  cl_own(A, k);
 }
 
 // last resort: one in-order pass (exact for any input)
@@ -274,16 +283,57 @@ __global__ void k_closest_serial(ClArgs A) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (uint32_t k = 1; k < A.nchunks; ++k) {
     if (cl_same(A, 2ull * k, 2ull * (k - 1) + 1)) continue;
-    const uint64_t q0 = (uint64_t)k * CQ, q1 = min(q0 + CQ, A.nq);
-    ClState S;
-    cl_load(A, 2ull * (k - 1) + 1, S);
-    cl_save(A, 2ull * k, S);
-    if (!cl_run(A, q0, q1, S, true)) {
-      cl_overflow(A, q0);
-      return;
-    }
-    cl_save(A, 2ull * k + 1, S);
+    cl_copy(A, 2ull * (k - 1) + 1, 2ull * k);
+    cl_copy(A, 2ull * k, 2ull * k + 1);
+    cl_own(A, k);
   }
+}
+
+// one attempt at capacity A.cap; *ovf set if some state outgrew it
+static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf) {
+  *ovf = false;
+  const uint64_t slots = 2ull * A.nchunks;
+  A.st_fp = (uint64_t*)bg_alloc(c, 8 * slots);
+  A.st_n = (uint32_t*)bg_alloc(c, 4 * slots);
+  A.st_c = (uint32_t*)bg_alloc(c, 4ull * A.cap * slots);
+  A.kl = (uint32_t*)bg_alloc(c, 4ull * A.cap * A.nchunks);
+  A.flag = (uint32_t*)bg_alloc(c, 4ull * A.nchunks);
+  A.nflag = (uint32_t*)bg_alloc(c, 8);
+  A.overflow = A.nflag + 1;
+  int rc = 0;
+  if (!A.st_fp || !A.st_n || !A.st_c || !A.kl || !A.flag || !A.nflag) rc = BG_E_NOMEM;
+  if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 8, c->stream));
+  if (!rc) {
+    BG_LAUNCH(c, "k_closest_chunks", k_closest_chunks, dim3(bg_blocks(A.nchunks, BG_NT)),
+              dim3(BG_NT), A);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  uint32_t h[2] = {0, 0};
+  for (int round = 0; !rc; ++round) {
+    rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 4, c->stream));
+    if (rc) break;
+    BG_LAUNCH(c, "k_closest_check", k_closest_check, dim3(bg_blocks(A.nchunks, 256)), dim3(256), A);
+    rc = bg_hip_ok(c, hipMemcpyAsync(h, A.nflag, 8, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+    if (rc || h[0] == 0 || h[1]) break;
+    if (round == FIX_ROUNDS) {
+      BG_LAUNCH(c, "k_closest_serial", k_closest_serial, dim3(1), dim3(64), A);
+      rc = bg_hip_ok(c, hipGetLastError());
+      if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(h, A.nflag, 8, hipMemcpyDeviceToHost, c->stream));
+      if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+      break;  // the in-order pass leaves every chunk consistent
+    }
+    BG_LAUNCH(c, "k_closest_fix", k_closest_fix, dim3(bg_blocks(A.nchunks, BG_NT)), dim3(BG_NT), A);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  *ovf = h[1] != 0;
+  bg_release(c, A.st_fp);
+  bg_release(c, A.st_n);
+  bg_release(c, A.st_c);
+  bg_release(c, A.kl);
+  bg_release(c, A.flag);
+  bg_release(c, A.nflag);
+  return rc;
 }
 
 extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_closest_opts* o,
@@ -314,53 +364,24 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
   if (Q->n == 0) { *out = r; return 0; }
 
   ClArgs A;
+  memset(&A, 0, sizeof(A));
   A.qs = Q->ks; A.qe = Q->ke; A.nq = Q->n;
   A.cs = C->ks; A.ce = C->ke; A.nc = C->n;
   A.overlaps = !o->no_overlaps;
   A.left = r->left; A.right = r->right;
   A.nchunks = (uint32_t)((Q->n + CQ - 1) / CQ);
-  const uint64_t slots = 2ull * A.nchunks;
-  A.st_fp = (uint64_t*)bg_alloc(c, 8 * slots);
-  A.st_n = (uint32_t*)bg_alloc(c, 4 * slots);
-  A.st_c = (uint32_t*)bg_alloc(c, 4 * CMAX * slots);
-  A.flag = (uint32_t*)bg_alloc(c, 4ull * A.nchunks);
-  A.nflag = (uint32_t*)bg_alloc(c, 4);
-  A.st = c->dstat;
   int rc = 0;
-  if (!A.st_fp || !A.st_n || !A.st_c || !A.flag || !A.nflag) rc = BG_E_NOMEM;
-  if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
-  if (!rc) {
-    BG_LAUNCH(c, "k_closest_chunks", k_closest_chunks, dim3(bg_blocks(A.nchunks, BG_NT)),
-              dim3(BG_NT), A);
-    rc = bg_hip_ok(c, hipGetLastError());
-  }
-  uint32_t bad = 0;
-  for (int round = 0; !rc; ++round) {
-    rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 4, c->stream));
-    if (rc) break;
-    BG_LAUNCH(c, "k_closest_check", k_closest_check, dim3(bg_blocks(A.nchunks, 256)), dim3(256), A);
-    rc = bg_hip_ok(c, hipMemcpyAsync(&bad, A.nflag, 4, hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
-    if (rc || bad == 0) break;
-    if (round == FIX_ROUNDS) {
-      BG_LAUNCH(c, "k_closest_serial", k_closest_serial, dim3(1), dim3(64), A);
-      rc = bg_hip_ok(c, hipGetLastError());
-      break;  // the in-order pass leaves every chunk consistent
+  // the reader cache of the reference can hold many rows on nested inputs: grow the
+  // per-chunk state capacity until it fits (bounded by device memory)
+  for (A.cap = CAP0;; A.cap *= 4) {
+    bool ovf = false;
+    rc = closest_pass(c, A, &ovf);
+    if (rc || !ovf) break;
+    if (3ull * 4ull * A.cap * A.nchunks * 4 > (64ull << 30)) {
+      rc = bg_fail(c, BG_E_UNSUPPORTED, "closest-features: reader cache too deep for device memory");
+      break;
     }
-    BG_LAUNCH(c, "k_closest_fix", k_closest_fix, dim3(bg_blocks(A.nchunks, BG_NT)), dim3(BG_NT), A);
-    rc = bg_hip_ok(c, hipGetLastError());
   }
-  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus),
-                                            hipMemcpyDeviceToHost, c->stream));
-  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
-  bg_release(c, A.st_fp);
-  bg_release(c, A.st_n);
-  bg_release(c, A.st_c);
-  bg_release(c, A.flag);
-  bg_release(c, A.nflag);
-  if (!rc && c->hstat->first_bad != ~0ULL)
-    rc = bg_fail(c, BG_E_UNSUPPORTED,
-                 "closest-features: more than 128 rows of <query-file> held at once (deeply nested input)");
   if (rc) { bg_result_free(r); return rc; }
   *out = r;
   return 0;

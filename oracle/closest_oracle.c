@@ -39,6 +39,8 @@ static int64_t read_line(void) {
   return -1;
 }
 
+static int64_t max_depth; /* largest cache + kept-list size seen (CLOSEST_ORACLE_DEPTH=1) */
+
 static void push_back_list(const int64_t* l, int64_t n) { /* insert(end, rbegin, rend) */
   for (int64_t i = n - 1; i >= 0; --i) {
     if (ncache == capcache) {
@@ -238,6 +240,7 @@ static void find_distances(int allow_overlaps) {
     }
     if (c < 0 && left >= 0 && !left_cached) rd_push(left);
     if (c < 0 && right >= 0) rd_push(right);
+    if (ncache + nrd > max_depth) max_depth = ncache + nrd;
     push_back_list(rd, nrd);
     nrd = 0;
     if (shortest) print_shortest(b, left, right);
@@ -303,5 +306,6 @@ int main(int argc, char** argv) {
     filter_chrom(&C, chrom);
   }
   find_distances(allow_overlaps);
+  if (getenv("CLOSEST_ORACLE_DEPTH")) fprintf(stderr, "max_depth %" PRId64 "\n", max_depth);
   return 0;
 }
