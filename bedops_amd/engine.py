@@ -287,27 +287,32 @@ class Engine:
             s.free()
 
     # -------------------------------------------------------------- bedmap
+    def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",
+               skip_unmapped=False):
+        """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result"""
+        names = {"count": MAP_COUNT, "mean": MAP_MEAN}
+        o = _MapOpts()
+        o.overlap_bp = overlap_bp
+        o.n_ops = len(ops)
+        for k, op in enumerate(ops):
+            o.ops[k] = names[op]
+        o.precision = precision
+        o.scientific = 0
+        o.skip_unmapped = 1 if skip_unmapped else 0
+        o.delim = delim.encode()
+        h = ctypes.c_void_p()
+        self._check(self.L.bg_map(self.ctx, s.h, ref, map_, ctypes.byref(o), ctypes.byref(h)))
+        return Result(self, h)
+
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
                skip_unmapped=False, chrom=None):
-        names = {"count": MAP_COUNT, "mean": MAP_MEAN}
         need5 = "mean" in ops
         s = self.load([(ref_text, BED3), (map_text if map_text is not None else ref_text,
                                           BED5 if need5 else BED3)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)
-            o = _MapOpts()
-            o.overlap_bp = overlap_bp
-            o.n_ops = len(ops)
-            for k, op in enumerate(ops):
-                o.ops[k] = names[op]
-            o.precision = precision
-            o.scientific = 0
-            o.skip_unmapped = 1 if skip_unmapped else 0
-            o.delim = delim.encode()
-            h = ctypes.c_void_p()
-            self._check(self.L.bg_map(self.ctx, s.h, 0, 1, ctypes.byref(o), ctypes.byref(h)))
-            r = Result(self, h)
+            r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped)
             try:
                 return r.text()
             finally:
@@ -316,6 +321,17 @@ class Engine:
             s.free()
 
     # -------------------------------------------------------------- closest-features
+    def closest_op(self, s, ref=0, query=1, shortest=False, dist=False, no_ref=False,
+                   no_overlaps=False, delim="|"):
+        """closest-features on loaded set `s` (both tables BED3_REST) -> Result"""
+        o = _ClosestOpts()
+        o.shortest, o.print_dist = int(bool(shortest)), int(bool(dist))
+        o.no_ref, o.no_overlaps = int(bool(no_ref)), int(bool(no_overlaps))
+        o.delim = delim.encode()
+        h = ctypes.c_void_p()
+        self._check(self.L.bg_closest(self.ctx, s.h, ref, query, ctypes.byref(o), ctypes.byref(h)))
+        return Result(self, h)
+
     def closest(self, input_text, query_text, shortest=False, dist=False, no_ref=False,
                 no_overlaps=False, delim="|", chrom=None):
         """closest-features [flags] <input-file> <query-file> on in-memory texts -> bytes"""
@@ -323,13 +339,7 @@ class Engine:
         try:
             if chrom:
                 s.restrict_chrom(chrom)
-            o = _ClosestOpts()
-            o.shortest, o.print_dist = int(bool(shortest)), int(bool(dist))
-            o.no_ref, o.no_overlaps = int(bool(no_ref)), int(bool(no_overlaps))
-            o.delim = delim.encode()
-            h = ctypes.c_void_p()
-            self._check(self.L.bg_closest(self.ctx, s.h, 0, 1, ctypes.byref(o), ctypes.byref(h)))
-            r = Result(self, h)
+            r = self.closest_op(s, 0, 1, shortest, dist, no_ref, no_overlaps, delim)
             try:
                 return r.text()
             finally:

@@ -88,58 +88,107 @@ def to_device(torch, L, p, nb, dev):
 # ----------------------------------------------------------------------------- roofline
 def kernel_bytes(name, w):
     """algorithmic HBM bytes per launch of kernel `name` for workload sizes `w`
-    (DESIGN.md §Roofline: what each kernel must read and write at minimum)."""
-    tb, rows, comps, out, obytes = w["text"], w["rows"], w["comps"], w["out"], w["out_bytes"]
+    (DESIGN.md §4: what each kernel must read and write at minimum)."""
+    texts, rows, kinds = w["texts"], w["rows"], w["kinds"]
+    nf = len(texts)
+    col = {0: 16, 1: 28, 2: 24}  # keyed start/end (+ rest span 12 B | score 8 B) per row
+    out, obytes, comps = w["out"], w["out_bytes"], w["comps"]
     table = {
-        # per file (2 launches per step): text read + keyed start/end written
-        "k_parse": (tb + 16 * rows) / 2,
-        "k_scout": tb / 2,
-        "k_tile_max": 8 * rows / 2,
-        "k_components_count": 16 * rows / 2,
-        "k_components_write": (16 * rows + 16 * comps) / 2,
+        # one launch per input file: text read + columns written (mean over the files)
+        "k_parse": sum(t + col[k] * r for t, r, k in zip(texts, rows, kinds)) / nf,
+        "k_scout": sum(texts) / nf,
+        "k_tile_max": 8 * sum(rows) / nf,
+        "k_components_count": 16 * sum(rows) / nf,
+        "k_components_write": (16 * sum(rows) + 16 * comps) / nf,
         # one launch per step: both component lists read (+ pieces written)
         "k_intersect_count": 16 * comps,
         "k_intersect_write": 16 * comps + 16 * out,
         "k_fmt_count": 16 * out,
         "k_fmt_write": 16 * out + obytes,
+        # bedmap: ref keys, map keys + score read; count + sum written
+        "k_map_count_sum": 28 * rows[0] + 24 * rows[-1],
+        # closest: every ref row and every candidate read once; left/right written
+        "k_closest_chunks": 32 * rows[0] + 16 * rows[-1],
+        # element-of: ref keys read + one flag per row; union prefix searched (cached)
+        "k_element_flags": 17 * rows[0],
     }
     return table.get(name)
 
 
 # ----------------------------------------------------------------------------- cpu baseline
-def cpu_baseline(A_bytes, B_bytes, max_rows=35_000_000):
-    """Time the CPU oracle (plain-C restatement of the reference sweep; the reference
-    itself is not buildable in this image) on a bounded sample: the leading
-    whole chromosomes of A and B (same generator, same order) up to ~max_rows rows."""
-    exe = os.path.join(ROOT, "oracle", "build", "bedops_oracle")
+def cpu_baseline(L, W, target_s=15.0):
+    """Time the CPU oracle (plain-C restatement of the reference; the reference itself is
+    not buildable in this image) on a bounded sample of the same workload:
+    the leading whole contigs (strcmp order) of every input, about `target_s` seconds of
+    single-thread work at the oracle's expected rate."""
+    exe = os.path.join(ROOT, "oracle", "build", W["oracle"])
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "oracle"], cwd=ROOT, check=True)
-    cut_names = [b"chr12", b"chr11", b"chr10"]
-    best = None
-    for nm in cut_names:  # largest prefix of whole contigs under max_rows rows
-        ia, ib = A_bytes.find(b"\n" + nm + b"\t"), B_bytes.find(b"\n" + nm + b"\t")
-        if ia < 0 or ib < 0:
-            continue
-        ra, rb = A_bytes.count(b"\n", 0, ia + 1), B_bytes.count(b"\n", 0, ib + 1)
-        if ra + rb <= max_rows * 2:
-            best = (ia + 1, ib + 1, ra, rb, nm)
+    n = L.bedgen_ncontigs()
+    lens = [L.bedgen_contig_len(c) for c in range(n)]
+    total = float(sum(lens))
+    budget = W["cpu_rate"] * target_s
+    rows_all = sum(W["rows"])
+    mask, used = 0, 0.0
+    for c in range(n):  # contigs in strcmp order
+        share = rows_all * lens[c] / total
+        if mask and used + share > budget:
             break
-    if best is None:
-        return None
-    ia, ib, ra, rb, nm = best
+        mask |= 1 << c
+        used += share
+    last = L.bedgen_contig_name(max(c for c in range(n) if (mask >> c) & 1)).decode()
     with tempfile.TemporaryDirectory() as td:
-        pa, pb = os.path.join(td, "a.bed"), os.path.join(td, "b.bed")
-        with open(pa, "wb") as f:
-            f.write(A_bytes[:ia])
-        with open(pb, "wb") as f:
-            f.write(B_bytes[:ib])
+        paths, nrows = [], 0
+        for i, (seed, mode) in enumerate(W["gen"]):
+            p, nb, r = gen(L, W["rows"][i], seed, mask, mode)
+            path = os.path.join(td, f"in{i}.bed")
+            with open(path, "wb") as f:
+                f.write(memoryview((ctypes.c_char * nb).from_address(p.value)))
+            L.bedgen_free(p)
+            paths.append(path)
+            nrows += r
         with open(os.path.join(td, "out.bed"), "wb") as fo:
             t0 = time.perf_counter()
-            subprocess.run([exe, "-i", pa, pb], stdout=fo, check=True)
+            subprocess.run([exe, *W["cpu_args"], *paths], stdout=fo, check=True)
             dt = time.perf_counter() - t0
-    return {"value": (ra + rb) / dt, "unit": "intervals/s", "cores": 1, "kind": "port",
-            "sample": f"bedops_oracle -i on the contigs before {nm.decode()} of A100M/B100M "
-                      f"({ra}+{rb} rows, file->file, {dt:.2f} s, 1 thread)"}
+    return {"value": nrows / dt, "unit": "intervals/s", "cores": 1, "kind": "port",
+            "sample": f"{W['oracle']} {' '.join(W['cpu_args'])} on contigs chr1..{last} (strcmp "
+                      f"order) of the same inputs: {nrows} rows, file->file, {dt:.2f} s, 1 thread"}
+
+
+# ----------------------------------------------------------------------------- workloads
+# BASELINE.json configs on the GPU path. "intersect" (configs[1]) is the headline metric
+# and the default; the others are measured with --workload for DESIGN.md.
+# gen: (seed, 3 = BED3 | 5 = BED5) per input; rows: per input at N = 1.
+WORKLOADS = {
+    "intersect": {"gen": [(42, 3), (43, 3)], "rows": [100_000_000, 100_000_000],
+                  "kinds": [0, 0], "oracle": "bedops_oracle", "cpu_args": ["-i"],
+                  "cpu_rate": 8.5e6, "ref": REF_INTERSECT,
+                  "desc": "bedops --intersect A.bed B.bed: BED3 text in HBM -> parse -> merge -> "
+                          "intersect -> BED text in HBM"},
+    "element-of": {"gen": [(44, 3), (45, 3)], "rows": [200_000_000, 200_000_000],
+                   "kinds": [1, 0], "oracle": "bedops_oracle", "cpu_args": ["-e", "1"],
+                   "cpu_rate": 3e6, "ref": None,
+                   "desc": "bedops --element-of 1 A.bed B.bed (configs[3] shape, 200M x 200M)"},
+    "bedmap": {"gen": [(7, 3), (8, 5)], "rows": [50_000_000, 500_000_000], "kinds": [0, 2],
+               "oracle": "bedmap_oracle", "cpu_args": ["--count", "--mean"], "cpu_rate": 2e6,
+               "ref": None, "desc": "bedmap --count --mean ref.bed map.bed (configs[2], 50M x 500M "
+                                    "BED5 map)"},
+    "closest": {"gen": [(46, 3), (47, 3)], "rows": [10_000_000, 1_000_000_000], "kinds": [1, 1],
+                "oracle": "closest_oracle", "cpu_args": ["--closest"], "cpu_rate": 4e6,
+                "ref": None, "desc": "closest-features --closest query.bed ref.bed (configs[4], "
+                                     "10M x 1B)"},
+}
+
+
+def run_op(eng, name, s):
+    if name == "intersect":
+        return eng.op("-i", s, [0, 1])
+    if name == "element-of":
+        return eng.op("-e", s, [0, 1], "1")
+    if name == "bedmap":
+        return eng.map_op(s, ["count", "mean"], 0, 1)
+    return eng.closest_op(s, 0, 1, shortest=True)
 
 
 # ----------------------------------------------------------------------------- main
@@ -148,7 +197,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=100_000_000, help="rows per file per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="intersect")
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="rows per input per GPU = scale x the workload's size (tests/smoke)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--load-only", action="store_true",
@@ -156,6 +207,7 @@ def main():
     ap.add_argument("--profile-all", action="store_true",
                     help="time every kernel during the timed steps (default: only the dominant one)")
     args = ap.parse_args()
+    W = WORKLOADS[args.workload]
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,37 +220,36 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
 
-    from bedops_amd import BED3, Engine
+    from bedops_amd import Engine
 
     L = bedgen_lib()
     owner, _ = contig_shards(L, world)
     mask = sum(1 << c for c, r in owner.items() if r == rank)
-    N = args.rows * world
+    per_gpu = [int(r * args.scale) for r in W["rows"]]
     t0 = time.perf_counter()
-    pa, na, ra = gen(L, N, 42, mask)
-    pb, nb, rb = gen(L, N, 43, mask)
-    log(f"[rank {rank}] generated A {ra} rows/{na} B, B {rb} rows/{nb} B in {time.perf_counter()-t0:.1f}s")
-    ta = to_device(torch, L, pa, na, dev)
-    tb_ = to_device(torch, L, pb, nb, dev)
-    A_bytes = B_bytes = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        A_bytes = bytes((ctypes.c_char * na).from_address(pa.value))
-        B_bytes = bytes((ctypes.c_char * nb).from_address(pb.value))
-    L.bedgen_free(pa)
-    L.bedgen_free(pb)
+    bufs, texts, rows = [], [], []
+    for (seed, mode), n in zip(W["gen"], per_gpu):
+        p, nb, r = gen(L, n * world, seed, mask, mode)
+        bufs.append(to_device(torch, L, p, nb, dev))
+        L.bedgen_free(p)
+        texts.append(nb)
+        rows.append(r)
+    log(f"[rank {rank}] {args.workload}: generated {rows} rows / {texts} bytes in "
+        f"{time.perf_counter() - t0:.1f}s")
     torch.cuda.synchronize(dev)
 
     eng = Engine(local)
     ncontigs = L.bedgen_ncontigs()
     state = {}
+    inputs = [((t.data_ptr(), nb), k) for t, nb, k in zip(bufs, texts, W["kinds"])]
 
     def step():
-        s = eng.load([((ta.data_ptr(), na), BED3), ((tb_.data_ptr(), nb), BED3)])
+        s = eng.load(inputs)
         if args.load_only:
             state["out_rows"] = state["out_bytes"] = 0
             s.free()
             return
-        r = eng.op("-i", s, [0, 1])
+        r = run_op(eng, args.workload, s)
         nbytes = r.format()
         state["out_rows"] = r.rows()
         state["out_bytes"] = nbytes
@@ -233,14 +284,14 @@ def main():
             first = eng.prof_read()
             eng.prof_enable("")
     dominant = max(first.items(), key=lambda kv: kv[1][1])[0]
-    # component counts of A and B (sizes the merge/intersect kernels' algorithmic bytes)
-    s = eng.load([((ta.data_ptr(), na), BED3), ((tb_.data_ptr(), nb), BED3)])
     comps = 0
-    for f in (0, 1):
-        m = eng.op("-m", s, [f])
-        comps += m.rows()
-        m.free()
-    s.free()
+    if args.workload == "intersect":  # component counts size the merge/intersect kernels
+        s = eng.load(inputs)
+        for f in (0, 1):
+            m = eng.op("-m", s, [f])
+            comps += m.rows()
+            m.free()
+        s.free()
     eng.prof_enable("*" if args.profile_all else dominant)
     torch.cuda.synchronize(dev)
     if dist:
@@ -259,11 +310,11 @@ def main():
         et = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(et, op=dist.ReduceOp.MAX)
         elapsed = float(et.item())
-        rows_all = torch.tensor([ra + rb], dtype=torch.int64, device=dev)
+        rows_all = torch.tensor([sum(rows)], dtype=torch.int64, device=dev)
         dist.all_reduce(rows_all)
         total_rows = int(rows_all.item())
     else:
-        total_rows = ra + rb
+        total_rows = sum(rows)
     prof = eng.prof_read()
 
     if rank != 0:
@@ -272,7 +323,7 @@ def main():
         return
 
     # roofline of the dominant kernel, from its launches inside the timed region
-    sizes = {"text": na + nb, "rows": ra + rb, "out": state["out_rows"],
+    sizes = {"texts": texts, "rows": rows, "kinds": W["kinds"], "out": state["out_rows"],
              "out_bytes": state["out_bytes"], "comps": comps}
     roof = None
     pick = dominant
@@ -283,7 +334,7 @@ def main():
         gbs = per_launch / avg_s / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and args.workload == "intersect":
             try:
                 traffic = json.load(open(pmc)).get(PMC_NAME.get(pick, pick), {}).get("bytes")
             except Exception:
@@ -294,32 +345,33 @@ def main():
                 "bytes_per_launch": int(per_launch)}
 
     verify = None
-    if world == 1 and not args.no_verify and args.rows == 100_000_000:
+    if world == 1 and not args.no_verify and not args.load_only and args.scale == 1.0:
         state["keep"] = True
         step()
         txt = state.pop("text")
         verify = {"rows": txt.count(b"\n"), "bytes": len(txt),
                   "sha16": hashlib.sha256(txt).hexdigest()[:16]}
-        verify["matches_reference"] = (verify == {**REF_INTERSECT} or
-                                       (verify["rows"] == REF_INTERSECT["rows"] and
-                                        verify["bytes"] == REF_INTERSECT["bytes"] and
-                                        verify["sha16"] == REF_INTERSECT["sha16"]))
+        if W["ref"]:
+            verify["matches_reference"] = all(verify[k] == W["ref"][k] for k in W["ref"])
         del txt
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and A_bytes is not None:
-        cpu = cpu_baseline(A_bytes, B_bytes)
+    if world == 1 and not args.no_cpu_baseline and rank == 0:
+        cpu = cpu_baseline(L, W)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = total_rows * args.steps / elapsed
     line = {
-        "metric": METRIC, "value": round(value, 1), "unit": "intervals/s", "n_gpus": world,
+        "metric": METRIC if args.workload == "intersect" else
+        f"intervals/sec, {W['desc'].split(' (')[0]}",
+        "value": round(value, 1), "unit": "intervals/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic (SURVEY.md App. D generator, seeds 42/43; BED text resident in HBM)",
-        "config": {"workload": "bedops --intersect A.bed B.bed: BED3 text in HBM -> parse -> "
-                               "merge -> intersect -> BED text in HBM",
-                   "rows_per_file": args.rows * world, "rows_per_gpu_per_file": args.rows,
+        "data": "synthetic (SURVEY.md App. D generator, seeds "
+                f"{'/'.join(str(g[0]) for g in W['gen'])}; BED text resident in HBM)",
+        "config": {"workload": W["desc"] + (" (loader only)" if args.load_only else ""),
+                   "rows_per_input": [r * world for r in per_gpu],
+                   "rows_per_gpu_per_input": per_gpu,
                    "parallelism": "single GPU" if world == 1 else
                    f"{world} GPUs, chromosome shards (LPT) + RCCL gather to rank 0",
                    "output_rows": state["out_rows"] if world == 1 else None},
