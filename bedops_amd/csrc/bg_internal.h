@@ -80,6 +80,7 @@ struct bg_table {
   double* score = nullptr;  // BG_BED5
   bool score_int = true;     // every score is an integer (exact sums)
   bool has_zero_len = false; // some row has end == start
+  int64_t maxlen = 0;        // max (end - start) over the rows (window bound for sweeps)
   // chromosome runs (host, sorted by row): rows [row0[k], row0[k+1]) are chrom names[k]
   std::vector<uint64_t> run_row0;
   std::vector<std::string> run_name;

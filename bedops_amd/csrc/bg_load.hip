@@ -525,6 +525,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
   const int64_t last_end = L == 0 ? -1
                            : (buf[HB + TT - 1] == '\n') ? t0 + TT - 1
                            : (hnl != ~0u ? t0 + hnl : find_nl(T, t0 + TT + HA + 32));
+  int64_t mlen = 0;  // longest row of this thread (window bound of bedmap / closest)
   for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
     const int64_t ls = t0 + lst[k];
     const uint64_t r = r0 + k;
@@ -550,6 +551,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     if (R.pos[run] == ls) R.row[run] = r;
     if (Ln.end > BG_MAX_COORD || Ln.start > Ln.end) bg_report(st, r, ERR_RANGE);
     if (Ln.start == Ln.end) atomicOr(&st->flags, 2ULL);
+    mlen = max(mlen, (int64_t)(Ln.end - Ln.start));
     const int64_t g = (int64_t)R.gid[run] << BG_KEY_SHIFT;
     const int64_t ks = g | (int64_t)(Ln.start & BG_COORD_MASK);
     KS[r] = ks;
@@ -564,6 +566,10 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
       if (!Ln.scoreint) atomicOr(&st->flags, 1ULL);
     }
   }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mlen = max(mlen, (int64_t)__shfl_xor(mlen, d, 64));
+  // the running max settles within the first blocks: atomics only when it grows
+  if (bg_lane() == 0 && mlen > *(volatile long long*)&st->maxlen) atomicMax(&st->maxlen, (long long)mlen);
   __syncthreads();
   for (uint32_t k = threadIdx.x + 1; k < L; k += BG_NT)
     if (lkey[k] != LLONG_MIN && lkey[k - 1] != LLONG_MIN && lkey[k] < lkey[k - 1])
@@ -821,6 +827,7 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   if (rc) return rc;
   if (in.kind == BG_BED5 && (c->hstat->flags & 1ULL)) T->score_int = false;
   T->has_zero_len = (c->hstat->flags & 2ULL) != 0;
+  T->maxlen = c->hstat->maxlen;
   // a trailing run may own only the dropped unterminated last line: no rows
   uint32_t nkeep = nr;
   while (nkeep > 0 && rows[nkeep - 1] == ~0ULL) --nkeep;
@@ -890,7 +897,7 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   }
   for (int i = 0; i < n && !rc; ++i) {
     rc = parse_one(c, i, inputs[i], s->t[i], st[i], gid);
-    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->flags, 0, 8, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->flags, 0, 16, c->stream));  // flags, maxlen
   }
   for (auto& S : st) bg_release(c, S.row0);
   if (rc) {

@@ -8,7 +8,8 @@
 // For every reference row r that yields the multiset
 //   S(r) = { m : same chrom, min(r.e, m.e) - max(r.s, m.s) >= N }
 // (verified by randomized differential tests against the reference).
-// GPU form: map rows are start-sorted, so with L = max map length every m in S(r)
+// GPU form: map rows are start-sorted, so with L = max map length (computed by the
+// loader) every m in S(r)
 // has m.s in [r.s - L + 1, r.e): two binary searches bound the candidates, one
 // thread per reference row accumulates count and the exact integer score sum.
 // Exactness: the reference keeps ONE running double across the file
@@ -19,19 +20,6 @@
 #include <climits>
 
 #include "bg_internal.h"
-
-__global__ void __launch_bounds__(BG_NT) k_max_len(const int64_t* __restrict__ S,
-                                                   const int64_t* __restrict__ E, uint64_t n,
-                                                   bg_dstatus* st) {
-  __shared__ int64_t sh[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * BG_NT * 16 + threadIdx.x * 16;
-  int64_t m = 0;
-  for (int k = 0; k < 16; ++k)
-    if (base + k < n) m = max(m, E[base + k] - S[base + k]);
-  int64_t tot;
-  (void)block_excl_scan(m, OpMax(), (int64_t)0, sh, &tot);
-  if (threadIdx.x == 0) atomicMax(&st->maxlen, (long long)tot);
-}
 
 __global__ void __launch_bounds__(BG_NT) k_map_count_sum(
     const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
@@ -80,16 +68,10 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (need_score && !M->score_int)
     return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean yet");
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
-  if (M->n)
-    BG_LAUNCH(c, "k_max_len", k_max_len, dim3(bg_blocks(M->n, BG_NT * 16)), dim3(BG_NT),
-                       M->ks, M->ke, M->n, c->dstat);
-  BG_HIP(c, hipGetLastError());
   int32_t* cnt = (int32_t*)bg_alloc(c, 4 * (R->n ? R->n : 1));
   int64_t* isum = need_score ? (int64_t*)bg_alloc(c, 8 * (R->n ? R->n : 1)) : nullptr;
   if (!cnt || (need_score && !isum)) return BG_E_NOMEM;
-  BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  const int64_t L = c->hstat->maxlen > 0 ? c->hstat->maxlen : 1;
+  const int64_t L = M->maxlen > 0 ? M->maxlen : 1;  // longest map row (from the loader)
   if (R->n)
     BG_LAUNCH(c, "k_map_count_sum", k_map_count_sum, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
                        R->ks, R->ke, R->n, M->ks, M->ke, need_score ? M->score : nullptr, M->n, L,
