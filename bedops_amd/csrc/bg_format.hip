@@ -54,20 +54,35 @@ struct FmtArgs {
   int shortest, print_dist, no_ref;
 };
 
+// decimal digits of v: compares, no division (coordinates are < 10^12)
 __device__ __forceinline__ int dec_len_u64(uint64_t v) {
   int l = 1;
-  while (v >= 10) { v /= 10; ++l; }
+  if (v >= 10000000000ull) {
+    l += 10;
+    v /= 10000000000ull;
+  }
+  const uint32_t w = (uint32_t)v;  // < 10^10 here
+  l += (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
+       (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
   return l;
 }
 __device__ __forceinline__ int dec_len_i32(int32_t v) {
   return v < 0 ? 1 + dec_len_u64((uint64_t)(-(int64_t)v)) : dec_len_u64((uint64_t)v);
 }
 
+// v as exactly `len` digits; 32-bit division by 10 when v fits (the common case)
 template <typename Out>
 __device__ __forceinline__ void put_u64(Out& o, uint64_t v, int len) {
-  for (int k = len - 1; k >= 0; --k) {
+  int k = len - 1;
+  for (; k >= 0 && (v >> 32) != 0; --k) {
     o.put_at(k, (char)('0' + v % 10));
     v /= 10;
+  }
+  uint32_t w = (uint32_t)v;
+  for (; k >= 0; --k) {
+    const uint32_t q = w / 10u;
+    o.put_at(k, (char)('0' + (w - 10u * q)));
+    w = q;
   }
   o.adv(len);
 }

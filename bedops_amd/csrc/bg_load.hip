@@ -229,72 +229,84 @@ __device__ __forceinline__ int64_t find_nl(const TileText& T, int64_t from) {
   return -1;
 }
 
-// k_tile_runs: records (position, token hash, token span) of every line in a boundary
+// k_tile_runs: records (position, token hash, token bytes) of every line in a boundary
 // tile whose token differs from the previous line's, plus the tile's first line and the
-// next tile's first line
+// next tile's first line. Grid-strided over the boundary list, whose length it reads on
+// the device (no host round trip between k_boundary and this kernel).
+__device__ __forceinline__ void put_record(const TileText& T, int64_t p, uint64_t h, int64_t tok,
+                                           uint32_t len, uint32_t cap, int64_t* rpos,
+                                           uint64_t* rhash, char* rname, uint32_t* rlen,
+                                           uint32_t* nrec) {
+  const uint32_t q = atomicAdd(nrec, 1u);
+  if (q >= cap) return;  // the host reports the overflow
+  rpos[q] = p;
+  rhash[q] = h;
+  rlen[q] = len;
+  char* o = rname + 128ull * q;
+  const uint32_t n = len < 127 ? len : 127;
+  for (uint32_t i = 0; i < n; ++i) o[i] = (char)T.at(tok + i);
+  o[n] = 0;
+}
+
 __global__ void __launch_bounds__(BG_NT) k_tile_runs(
     const uint8_t* __restrict__ txt, uint64_t nb, const uint32_t* __restrict__ tiles,
-    const int64_t* __restrict__ fls, const uint64_t* __restrict__ fhash, uint32_t ntiles,
-    int64_t* __restrict__ rpos, uint64_t* __restrict__ rhash, int64_t* __restrict__ rtok,
+    const uint32_t* __restrict__ ntiles_b, const int64_t* __restrict__ fls, uint32_t ntiles,
+    uint32_t cap, int64_t* __restrict__ rpos, uint64_t* __restrict__ rhash, char* __restrict__ rname,
     uint32_t* __restrict__ rlen, uint32_t* __restrict__ nrec) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
   __shared__ uint16_t lst[TT + 1];
   __shared__ uint32_t shs[BG_NT / 64 + 1];
-  const uint32_t t = tiles[blockIdx.x];
-  const int64_t t0 = (int64_t)t * TT;
-  uint4 v0, v1;
-  stage_tile(txt, nb, t0, buf, v0, v1);
-  __syncthreads();
-  bool has0;
-  const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, TT + 1, shs, has0);
-  TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
-  for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
-    const int64_t p = t0 + lst[k];
-    if ((uint64_t)p >= nb) continue;
-    int64_t tok;
-    uint32_t len;
-    const uint64_t h = line_token(T, p, tok, len);
-    bool rec = (k == 0);
-    if (!rec) {
-      int64_t ptok;
-      uint32_t plen;
-      rec = line_token(T, t0 + lst[k - 1], ptok, plen) != h;
-    }
-    if (rec) {
-      const uint32_t q = atomicAdd(nrec, 1u);
-      if (q < REC_CAP) { rpos[q] = p; rhash[q] = h; rtok[q] = tok; rlen[q] = len; }
-    }
-  }
-  if (threadIdx.x == 0) {  // first line of the next tile that has one
-    uint32_t u = t + 1;
-    while (u < ntiles && fls[u] < 0) ++u;
-    if (u < ntiles) {
+  const uint32_t nbd = *ntiles_b;
+  for (uint32_t bi = blockIdx.x; bi < nbd; bi += gridDim.x) {
+    const uint32_t t = tiles[bi];
+    const int64_t t0 = (int64_t)t * TT;
+    uint4 v0, v1;
+    __syncthreads();  // the previous tile's readers are done with the LDS
+    stage_tile(txt, nb, t0, buf, v0, v1);
+    __syncthreads();
+    bool has0;
+    const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, TT + 1, shs, has0);
+    TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
+    for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
+      const int64_t p = t0 + lst[k];
+      if ((uint64_t)p >= nb) continue;
       int64_t tok;
       uint32_t len;
-      const uint64_t h = line_token(T, fls[u], tok, len);
-      const uint32_t q = atomicAdd(nrec, 1u);
-      if (q < REC_CAP) { rpos[q] = fls[u]; rhash[q] = h; rtok[q] = tok; rlen[q] = len; }
+      const uint64_t h = line_token(T, p, tok, len);
+      bool rec = (k == 0);
+      if (!rec) {
+        int64_t ptok;
+        uint32_t plen;
+        rec = line_token(T, t0 + lst[k - 1], ptok, plen) != h;
+      }
+      if (rec) put_record(T, p, h, tok, len, cap, rpos, rhash, rname, rlen, nrec);
+    }
+    if (threadIdx.x == 0) {  // first line of the next tile that has one
+      uint32_t u = t + 1;
+      while (u < ntiles && fls[u] < 0) ++u;
+      if (u < ntiles) {
+        int64_t tok;
+        uint32_t len;
+        const uint64_t h = line_token(T, fls[u], tok, len);
+        put_record(T, fls[u], h, tok, len, cap, rpos, rhash, rname, rlen, nrec);
+      }
     }
   }
-}
-
-// gather the chromosome tokens of run records into fixed 128-byte slots
-__global__ void k_gather_tokens(const uint8_t* __restrict__ txt, const int64_t* rtok,
-                                const uint32_t* rlen, uint32_t n, char* out) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const uint32_t len = rlen[k];
-  for (uint32_t i = 0; i < 128; ++i) out[k * 128ull + i] = (i < len) ? (char)txt[rtok[k] + i] : 0;
 }
 
 // -------------------------------------------------------------------------------------
 // k_parse
 // -------------------------------------------------------------------------------------
+struct RunInfo {
+  int64_t pos;    // byte position of the run's first line (ascending over runs)
+  uint64_t hash;  // token hash (bgp_hash_words form)
+  uint64_t tlo, thi;  // first 16 token bytes, zero padded (fast-path identity check)
+  uint32_t tlen;  // token length
+  int32_t gid;    // global chromosome id
+};
 struct RunTable {
-  const int64_t* pos;    // byte position of each run's first line, ascending
-  const uint64_t* hash;  // token hash of the run
-  const int32_t* gid;    // global chromosome id
-  uint64_t* row;         // out: row index of each run's first line
+  const RunInfo* info;
+  uint64_t* row;  // out: row index of each run's first line
   uint32_t n;
 };
 
@@ -302,7 +314,7 @@ __device__ __forceinline__ uint32_t run_of(const RunTable& R, int64_t p, uint32_
   // last k in [lo, hi] with pos[k] <= p
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
-    if (R.pos[mid] <= p) lo = mid;
+    if (R.info[mid].pos <= p) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -429,40 +441,42 @@ __device__ __forceinline__ uint32_t mask_window(const uint32_t* m, uint32_t p) {
 }
 
 // fast path: fields from the tile's class bitmaps + LDS bytes -> true if decided.
-// q: local offset of the line start inside the tile (0 <= q < TT).
+// q: local offset of the line start inside the tile (0 <= q < TT). The chromosome token
+// is returned as its first 16 bytes (zero padded) + length; tokens longer than 16 bytes
+// take the byte path.
+struct Fast {
+  uint64_t start, end;
+  uint64_t tlo, thi;
+  uint32_t toklen;
+  uint32_t rest;  // local offset (from the line start) of the rest
+};
 __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32_t* wsm,
-                                                const uint32_t* dgm, uint32_t q, int64_t ls,
-                                                int64_t le, Line& L) {
+                                                const uint32_t* dgm, uint32_t q, uint32_t len,
+                                                Fast& L) {
   BgpFields F;
-  const int r = bgp_fields_masks(mask_window(wsm, q), mask_window(dgm, q), (uint32_t)(le - ls), F);
+  const int r = bgp_fields_masks(mask_window(wsm, q), mask_window(dgm, q), len, F);
   if (r != 1) return false;  // blank lines and errors take the byte path (messages)
   const uint32_t toklen = F.a1 - F.a0;
+  if (toklen > 16 || F.s1 - F.s0 > 13 || F.e1 - F.e0 > 13) return false;
   const uint32_t b = q + HB;  // LDS byte offset of the line start
   uint64_t lo, hi;
   lds16(buf, b + F.s0, lo, hi);
-  L.start = (F.s1 - F.s0 > 13) ? ~0ULL : bgp_digits(lo, hi, (int)(F.s1 - F.s0));
+  L.start = bgp_digits(lo, hi, (int)(F.s1 - F.s0));
   lds16(buf, b + F.e0, lo, hi);
-  L.end = (F.e1 - F.e0 > 13) ? ~0ULL : bgp_digits(lo, hi, (int)(F.e1 - F.e0));
-  if (toklen <= 16) {
-    lds16(buf, b + F.a0, lo, hi);
-    L.hash = bgp_hash16(lo, hi, toklen);
-  } else {
-    if (toklen > BG_CHR_MAX) return false;
-    uint64_t h = BGP_FNV_OFF;
-    uint32_t w = 0;
-    for (uint32_t i = 0; i < toklen; ++i) {
-      w |= (uint32_t)buf[b + F.a0 + i] << (8 * (i & 3));
-      if ((i & 3) == 3) { h = (h ^ w) * BGP_FNV_PRIME; w = 0; }
+  L.end = bgp_digits(lo, hi, (int)(F.e1 - F.e0));
+  lds16(buf, b + F.a0, lo, hi);
+  if (toklen < 16) {
+    if (toklen <= 8) {
+      hi = 0;
+      lo = toklen == 8 ? lo : (lo & ((1ull << (8 * toklen)) - 1));
+    } else {
+      hi &= (1ull << (8 * (toklen - 8))) - 1;
     }
-    if (toklen & 3) h = (h ^ w) * BGP_FNV_PRIME;
-    L.hash = (h ^ toklen) * BGP_FNV_PRIME;
   }
-  L.tok = ls + F.a0;
+  L.tlo = lo;
+  L.thi = hi;
   L.toklen = toklen;
-  L.rest = ls + F.e1;
-  L.err = 0;
-  L.score = 0;
-  L.scoreint = 1;
+  L.rest = F.e1;
   return true;
 }
 
@@ -473,6 +487,21 @@ __global__ void k_run_range(RunTable R, uint32_t ntiles, uint32_t* __restrict__ 
   if (t >= ntiles) return;
   runlo[t] = run_of(R, (int64_t)t * TT, 0, R.n - 1);
   runhi[t] = run_of(R, (int64_t)t * TT + TT - 1, 0, R.n - 1);
+}
+
+// keys (+ rest span / score) of one parsed row; false if the chromosome does not match
+// the run the row's position falls in (unsorted input)
+__device__ __forceinline__ void emit_row(const RunTable& R, uint32_t run, int64_t ls, uint64_t r,
+                                         uint64_t start, uint64_t end, int64_t* KS, int64_t* KE,
+                                         bg_dstatus* st, int64_t& key, int64_t& mlen) {
+  if (R.info[run].pos == ls) R.row[run] = r;
+  if (end > BG_MAX_COORD || start > end) bg_report(st, r, ERR_RANGE);
+  if (start == end) atomicOr(&st->flags, 2ULL);
+  mlen = max(mlen, (int64_t)(end - start));
+  const int64_t g = (int64_t)R.info[run].gid << BG_KEY_SHIFT;
+  key = g | (int64_t)(start & BG_COORD_MASK);
+  KS[r] = key;
+  KE[r] = g | (int64_t)(end & BG_COORD_MASK);
 }
 
 __global__ void __launch_bounds__(BG_NT) k_parse(
@@ -489,6 +518,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
   __shared__ uint32_t dgm[TT / 32 + HA / 32 + 1];
   __shared__ uint32_t hnl;  // first '\n' in the halo after the tile (local offset)
   const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int64_t PENDING = LLONG_MIN + 1;  // lkey of a line left to the byte path
   if (threadIdx.x == 0) hnl = ~0u;
   uint4 v0, v1;
   stage_tile(txt, nb, t0, buf, v0, v1);
@@ -499,10 +529,9 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     bgp_classify8(W, ws, dg);
     wsm[threadIdx.x] = ws;
     dgm[threadIdx.x] = dg;
-    if (threadIdx.x < HA / 32 + 1) {  // the halo after the tile
-      const int64_t hb = t0 + TT + 32 * (int64_t)threadIdx.x;
-      const uint4 h0 = load16(txt, hb, nb), h1 = load16(txt, hb + 16, nb);
-      const uint32_t H[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    if (threadIdx.x < HA / 32 + 1) {  // the halo after the tile, from its LDS copy
+      const uint32_t* hw = reinterpret_cast<const uint32_t*>(&buf[HB + TT + 32 * threadIdx.x]);
+      const uint32_t H[8] = {hw[0], hw[1], hw[2], hw[3], hw[4], hw[5], hw[6], hw[7]};
       bgp_classify8(H, ws, dg);
       wsm[TT / 32 + threadIdx.x] = ws;
       dgm[TT / 32 + threadIdx.x] = dg;
@@ -520,43 +549,60 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     if (threadIdx.x == 0) bg_report(st, r0, ERR_PARSE);
     return;
   }
-  TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
   // end of the tile's last line: the tile's last byte, the halo, or further on
+  TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
   const int64_t last_end = L == 0 ? -1
                            : (buf[HB + TT - 1] == '\n') ? t0 + TT - 1
                            : (hnl != ~0u ? t0 + hnl : find_nl(T, t0 + TT + HA + 32));
   int64_t mlen = 0;  // longest row of this thread (window bound of bedmap / closest)
+  // hot loop: BED3 / BED3+rest lines decided by the masks; the rest is queued
   for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
     const int64_t ls = t0 + lst[k];
     const uint64_t r = r0 + k;
-    lkey[k] = LLONG_MIN;
-    if (r >= nrows) continue;  // unterminated last line (dropped like the reference)
+    int64_t key = LLONG_MIN;
     const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
-    if (le < 0) continue;
-    Line Ln;
-    if (kind == BG_BED5 || !parse_line_fast(buf, wsm, dgm, lst[k], ls, le, Ln)) {
-      parse_line_slow(T, ls, le, kind, Ln);
-      if (Ln.err) {
-        if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
-        bg_report(st, r, Ln.err);
-        KS[r] = KE[r] = 0;
-        continue;
+    // r >= nrows: the unterminated last line (dropped like the reference)
+    if (r < nrows && le >= 0) {
+      Fast F;
+      const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+      const RunInfo& I = R.info[run];
+      if (kind != BG_BED5 && parse_line_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F) &&
+          F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
+        emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
+        if (rest_off) {
+          rest_off[r] = (uint64_t)(ls + F.rest);
+          rest_len[r] = (uint32_t)(le - ls - F.rest);
+        }
+      } else {
+        key = PENDING;
       }
     }
+    lkey[k] = key;
+  }
+  // cold loop: the full grammar, byte by byte (BED5, long tokens, odd spacing, errors);
+  // same line-to-thread mapping, so no barrier is needed before it
+  for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
+    if (lkey[k] != PENDING) continue;
+    lkey[k] = LLONG_MIN;
+    const int64_t ls = t0 + lst[k];
+    const uint64_t r = r0 + k;
+    const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
+    Line Ln;
+    parse_line_slow(T, ls, le, kind, Ln);
+    if (Ln.err) {
+      if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
+      bg_report(st, r, Ln.err);
+      KS[r] = KE[r] = 0;
+      continue;
+    }
     const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
-    if (Ln.hash != R.hash[run]) {  // a chromosome outside the run order: unsorted input
+    if (Ln.hash != R.info[run].hash) {  // a chromosome outside the run order: unsorted input
       bg_report(st, r, ERR_UNSORTED);
       continue;
     }
-    if (R.pos[run] == ls) R.row[run] = r;
-    if (Ln.end > BG_MAX_COORD || Ln.start > Ln.end) bg_report(st, r, ERR_RANGE);
-    if (Ln.start == Ln.end) atomicOr(&st->flags, 2ULL);
-    mlen = max(mlen, (int64_t)(Ln.end - Ln.start));
-    const int64_t g = (int64_t)R.gid[run] << BG_KEY_SHIFT;
-    const int64_t ks = g | (int64_t)(Ln.start & BG_COORD_MASK);
-    KS[r] = ks;
-    KE[r] = g | (int64_t)(Ln.end & BG_COORD_MASK);
-    lkey[k] = ks;
+    int64_t key;
+    emit_row(R, run, ls, r, Ln.start, Ln.end, KS, KE, st, key, mlen);
+    lkey[k] = key;
     if (rest_off) {
       rest_off[r] = (uint64_t)Ln.rest;
       rest_len[r] = (uint32_t)(le - Ln.rest);
@@ -613,18 +659,49 @@ static int report_status(bg_ctx* c, int file, const bg_dstatus& h) {
   return bg_fail(c, rc, msg);
 }
 
-// per-input loader state between the passes
+// per-input loader state between the phases
 struct LoadState {
   const uint8_t* txt = nullptr;
   uint64_t nb = 0;
   uint32_t ntiles = 0;
-  uint64_t* row0 = nullptr;  // tile row offsets (device)
+  uint32_t rc = 0;             // record capacity
+  uint64_t* row0 = nullptr;    // tile row offsets (device)
+  uint64_t* cnt = nullptr;
+  int64_t* fls = nullptr;
+  uint64_t* fhash = nullptr;
+  uint32_t* fnl = nullptr;
+  uint32_t* blist = nullptr;
+  int64_t* rpos = nullptr;     // run records
+  uint64_t* rhash = nullptr;
+  char* rname = nullptr;
+  uint32_t* rlen = nullptr;
   std::vector<int64_t> run_pos;
   std::vector<uint64_t> run_hash;
+  // host copies of the records
+  std::vector<int64_t> h_pos;
+  std::vector<uint64_t> h_hash;
+  std::vector<char> h_name;
+  std::vector<uint32_t> h_len;
+  // phase 3
+  std::vector<RunInfo> info;
+  RunInfo* d_info = nullptr;
+  uint64_t* d_row = nullptr;
+  uint32_t* rlo = nullptr;
+  uint32_t* rhi = nullptr;
+  std::vector<uint64_t> rows;
 };
 
-// pass 1: text to HBM, scout, row offsets, chromosome runs
-static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S) {
+static void release_state(bg_ctx* c, LoadState& S) {
+  for (void* p : {(void*)S.row0, (void*)S.cnt, (void*)S.fls, (void*)S.fhash, (void*)S.fnl,
+                  (void*)S.blist, (void*)S.rpos, (void*)S.rhash, (void*)S.rname, (void*)S.rlen,
+                  (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi})
+    bg_release(c, p);
+  S = LoadState();
+}
+
+// phase 1 (no host round trip): text to HBM, scout, row offsets, chromosome-run records.
+// ctr[0] = rows, ctr[1] = boundary tiles (u32), ctr[2] = run records (u32)
+static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, uint64_t* ctr) {
   T->kind = in.kind;
   const uint8_t* txt;
   if (in.on_device) {
@@ -644,109 +721,59 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
   S.ntiles = in.nbytes ? bg_blocks(in.nbytes, TT) : 0;
   if (S.ntiles == 0) return 0;
   const uint32_t nt = S.ntiles;
-  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
+  // a boundary tile records at most one entry per line (+1)
+  S.rc = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
+  S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
-  int64_t* fls = (int64_t*)bg_alloc(c, 8ull * nt);
-  uint64_t* fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
-  uint32_t* blist = (uint32_t*)bg_alloc(c, 4ull * nt);
-  // small counters block: [0] rows, [1] nboundary (u32), [2] nrec (u32)
-  uint64_t* ctr = (uint64_t*)bg_alloc(c, 64);
-  uint32_t* fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
-  if (!fnl) return BG_E_NOMEM;
-  // a boundary tile records at most one entry per line (+1): TT/6 lines at most
-  const uint32_t RC = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
-  int64_t* rpos = (int64_t*)bg_alloc(c, 8ull * RC);
-  uint64_t* rhash = (uint64_t*)bg_alloc(c, 8ull * RC);
-  int64_t* rtok = (int64_t*)bg_alloc(c, 8ull * RC);
-  uint32_t* rlen = (uint32_t*)bg_alloc(c, 4ull * RC);
-  if (!cnt || !S.row0 || !fls || !fhash || !blist || !ctr || !rpos || !rhash || !rtok || !rlen)
+  S.fls = (int64_t*)bg_alloc(c, 8ull * nt);
+  S.fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
+  S.blist = (uint32_t*)bg_alloc(c, 4ull * nt);
+  S.fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
+  S.rpos = (int64_t*)bg_alloc(c, 8ull * S.rc);
+  S.rhash = (uint64_t*)bg_alloc(c, 8ull * S.rc);
+  S.rname = (char*)bg_alloc(c, 128ull * S.rc);
+  S.rlen = (uint32_t*)bg_alloc(c, 4ull * S.rc);
+  if (!S.cnt || !S.row0 || !S.fls || !S.fhash || !S.blist || !S.fnl || !S.rpos || !S.rhash ||
+      !S.rname || !S.rlen)
     return BG_E_NOMEM;
-  BG_HIP(c, hipMemsetAsync(ctr, 0, 64, c->stream));
   BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
-            cnt, fnl);
+            S.cnt, S.fnl);
   BG_HIP(c, hipGetLastError());
-  BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, fnl, fls,
-            fhash);
+  BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, S.fnl,
+            S.fls, S.fhash);
   BG_HIP(c, hipGetLastError());
-  int rc = bg_scan_sum_u64(c, cnt, S.row0, nt, &ctr[0]);
+  int rc = bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
   if (rc) return rc;
   uint32_t* nbound = reinterpret_cast<uint32_t*>(&ctr[1]);
   uint32_t* nrec = reinterpret_cast<uint32_t*>(&ctr[2]);
-  BG_LAUNCH(c, "k_boundary", k_boundary, dim3(bg_blocks(nt, 256)), dim3(256), fls, fhash, nt, blist,
-            nbound);
+  BG_LAUNCH(c, "k_boundary", k_boundary, dim3(bg_blocks(nt, 256)), dim3(256), S.fls, S.fhash, nt,
+            S.blist, nbound);
   BG_HIP(c, hipGetLastError());
-  uint64_t hc[3];
-  BG_HIP(c, hipMemcpyAsync(hc, ctr, 24, hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  T->n = hc[0];
-  const uint32_t nbd = (uint32_t)hc[1];
-  if (nbd) {
-    BG_LAUNCH(c, "k_tile_runs", k_tile_runs, dim3(nbd), dim3(BG_NT), txt, S.nb, blist, fls, fhash,
-              nt, rpos, rhash, rtok, rlen, nrec);
-    BG_HIP(c, hipGetLastError());
-  }
-  uint32_t nr = 0;
-  BG_HIP(c, hipMemcpyAsync(&nr, nrec, 4, hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  if (nr > RC) return bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input");
-  std::vector<int64_t> pos(nr), tok(nr);
-  std::vector<uint64_t> hs(nr);
-  std::vector<uint32_t> len(nr);
-  if (nr) {
-    BG_HIP(c, hipMemcpyAsync(pos.data(), rpos, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipMemcpyAsync(hs.data(), rhash, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipStreamSynchronize(c->stream));
-  }
-  // runs: records by position, consecutive duplicates removed
+  BG_LAUNCH(c, "k_tile_runs", k_tile_runs, dim3(std::min<uint32_t>(nt, 1024)), dim3(BG_NT), txt,
+            S.nb, S.blist, nbound, S.fls, nt, S.rc, S.rpos, S.rhash, S.rname, S.rlen, nrec);
+  BG_HIP(c, hipGetLastError());
+  return 0;
+}
+
+// phase 2 (host): the records of one input -> its chromosome runs, strcmp order checked
+static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S) {
+  const uint32_t nr = (uint32_t)S.h_pos.size();
   std::vector<uint32_t> ord(nr);
   for (uint32_t k = 0; k < nr; ++k) ord[k] = k;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return pos[a] < pos[b]; });
-  std::vector<uint32_t> keep;
-  for (uint32_t k : ord) {
-    if (!keep.empty() && pos[keep.back()] == pos[k]) continue;
-    if (!keep.empty() && hs[keep.back()] == hs[k]) continue;
-    keep.push_back(k);
-  }
-  // names of the runs
-  const uint32_t nk = (uint32_t)keep.size();
-  std::vector<char> names(128ull * (nk ? nk : 1));
-  if (nk) {
-    std::vector<int64_t> ktok(nk);
-    std::vector<uint32_t> klen(nk);
-    // record spans are on the device; gather them by index
-    std::vector<int64_t> all_tok(nr);
-    std::vector<uint32_t> all_len(nr);
-    BG_HIP(c, hipMemcpyAsync(all_tok.data(), rtok, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipMemcpyAsync(all_len.data(), rlen, 4ull * nr, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipStreamSynchronize(c->stream));
-    for (uint32_t i = 0; i < nk; ++i) {
-      ktok[i] = all_tok[keep[i]];
-      klen[i] = all_len[keep[i]];
-      if (klen[i] > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
-    }
-    int64_t* d_tok = (int64_t*)bg_alloc(c, 8ull * nk);
-    uint32_t* d_len = (uint32_t*)bg_alloc(c, 4ull * nk);
-    char* d_names = (char*)bg_alloc(c, 128ull * nk);
-    if (!d_tok || !d_len || !d_names) return BG_E_NOMEM;
-    BG_HIP(c, hipMemcpyAsync(d_tok, ktok.data(), 8ull * nk, hipMemcpyHostToDevice, c->stream));
-    BG_HIP(c, hipMemcpyAsync(d_len, klen.data(), 4ull * nk, hipMemcpyHostToDevice, c->stream));
-    BG_LAUNCH(c, "k_gather_tokens", k_gather_tokens, dim3(bg_blocks(nk, 256)), dim3(256), txt,
-              d_tok, d_len, nk, d_names);
-    BG_HIP(c, hipGetLastError());
-    BG_HIP(c, hipMemcpyAsync(names.data(), d_names, 128ull * nk, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipStreamSynchronize(c->stream));
-    bg_release(c, d_tok);
-    bg_release(c, d_len);
-    bg_release(c, d_names);
-  }
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return S.h_pos[a] < S.h_pos[b]; });
   T->run_name.clear();
   S.run_pos.clear();
   S.run_hash.clear();
-  for (uint32_t i = 0; i < nk; ++i) {
-    const uint32_t k = keep[i];
-    S.run_pos.push_back(pos[k]);
-    S.run_hash.push_back(hs[k]);
-    T->run_name.emplace_back(&names[128ull * i], strnlen(&names[128ull * i], 128));
+  int64_t last_pos = -1;
+  uint64_t last_hash = 0;
+  for (uint32_t k : ord) {  // runs: records by position, consecutive duplicates removed
+    if (!S.run_pos.empty() && (last_pos == S.h_pos[k] || last_hash == S.h_hash[k])) continue;
+    if (S.h_len[k] > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
+    last_pos = S.h_pos[k];
+    last_hash = S.h_hash[k];
+    S.run_pos.push_back(S.h_pos[k]);
+    S.run_hash.push_back(S.h_hash[k]);
+    T->run_name.emplace_back(&S.h_name[128ull * k], strnlen(&S.h_name[128ull * k], 128));
   }
   for (size_t k = 1; k < T->run_name.size(); ++k) {
     if (strcmp(T->run_name[k - 1].c_str(), T->run_name[k].c_str()) >= 0) {
@@ -757,22 +784,12 @@ static int scout_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
       return bg_fail(c, BG_E_UNSORTED, msg);
     }
   }
-  bg_release(c, cnt);
-  bg_release(c, fls);
-  bg_release(c, fhash);
-  bg_release(c, blist);
-  bg_release(c, fnl);
-  bg_release(c, ctr);
-  bg_release(c, rpos);
-  bg_release(c, rhash);
-  bg_release(c, rtok);
-  bg_release(c, rlen);
   return 0;
 }
 
-// pass 2: keyed parse with the global dictionary
-static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S,
-                     const std::map<std::string, int32_t>& gid) {
+// phase 3 (no host round trip): keyed parse with the global dictionary
+static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
+                     const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
   const uint64_t na = T->n ? T->n : 1;
   T->ks = (int64_t*)bg_alloc(c, 8 * na);
   T->ke = (int64_t*)bg_alloc(c, 8 * na);
@@ -787,66 +804,67 @@ static int parse_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSt
     if (!T->score) return BG_E_NOMEM;
   }
   const uint32_t nr = (uint32_t)S.run_pos.size();
-  T->run_row0.assign(1, 0);
-  if (S.ntiles == 0 || T->n == 0 || nr == 0) {
-    T->run_row0.assign(1, 0);
-    T->run_name.clear();
-    return 0;
+  if (S.ntiles == 0 || T->n == 0 || nr == 0) return 0;
+  S.info.resize(nr);
+  for (uint32_t k = 0; k < nr; ++k) {
+    RunInfo& I = S.info[k];
+    const std::string& nm = T->run_name[k];
+    I.pos = S.run_pos[k];
+    I.hash = S.run_hash[k];
+    I.tlen = (uint32_t)nm.size();
+    uint8_t tb[16] = {0};
+    memcpy(tb, nm.data(), std::min<size_t>(16, nm.size()));
+    memcpy(&I.tlo, tb, 8);
+    memcpy(&I.thi, tb + 8, 8);
+    I.gid = gid.at(nm);
   }
-  std::vector<int32_t> g(nr);
-  for (uint32_t k = 0; k < nr; ++k) g[k] = gid.at(T->run_name[k]);
-  int64_t* d_pos = (int64_t*)bg_alloc(c, 8ull * nr);
-  uint64_t* d_hash = (uint64_t*)bg_alloc(c, 8ull * nr);
-  int32_t* d_gid = (int32_t*)bg_alloc(c, 4ull * nr);
-  uint64_t* d_row = (uint64_t*)bg_alloc(c, 8ull * nr);
-  if (!d_pos || !d_hash || !d_gid || !d_row) return BG_E_NOMEM;
-  BG_HIP(c, hipMemcpyAsync(d_pos, S.run_pos.data(), 8ull * nr, hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemcpyAsync(d_hash, S.run_hash.data(), 8ull * nr, hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemcpyAsync(d_gid, g.data(), 4ull * nr, hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemsetAsync(d_row, 0xff, 8ull * nr, c->stream));
-  RunTable R{d_pos, d_hash, d_gid, d_row, nr};
-  uint32_t* rlo = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
-  uint32_t* rhi = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
-  if (!rlo || !rhi) return BG_E_NOMEM;
+  S.d_info = (RunInfo*)bg_alloc(c, sizeof(RunInfo) * nr);
+  S.d_row = (uint64_t*)bg_alloc(c, 8ull * nr);
+  S.rlo = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
+  S.rhi = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
+  if (!S.d_info || !S.d_row || !S.rlo || !S.rhi) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(S.d_info, S.info.data(), sizeof(RunInfo) * nr, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemsetAsync(S.d_row, 0xff, 8ull * nr, c->stream));
+  RunTable R{S.d_info, S.d_row, nr};
   BG_LAUNCH(c, "k_run_range", k_run_range, dim3(bg_blocks(S.ntiles, 256)), dim3(256), R, S.ntiles,
-            rlo, rhi);
+            S.rlo, S.rhi);
   BG_HIP(c, hipGetLastError());
-  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, rlo,
-            rhi, in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, c->dstat);
+  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
+            S.rhi, in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
   BG_HIP(c, hipGetLastError());
-  bg_release(c, rlo);
-  bg_release(c, rhi);
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
-            S.row0, S.ntiles, T->n, c->dstat);
+            S.row0, S.ntiles, T->n, st);
   BG_HIP(c, hipGetLastError());
-  std::vector<uint64_t> rows(nr);
-  BG_HIP(c, hipMemcpyAsync(rows.data(), d_row, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  int rc = report_status(c, idx, *c->hstat);
-  if (rc) return rc;
-  if (in.kind == BG_BED5 && (c->hstat->flags & 1ULL)) T->score_int = false;
-  T->has_zero_len = (c->hstat->flags & 2ULL) != 0;
-  T->maxlen = c->hstat->maxlen;
-  // a trailing run may own only the dropped unterminated last line: no rows
-  uint32_t nkeep = nr;
-  while (nkeep > 0 && rows[nkeep - 1] == ~0ULL) --nkeep;
-  T->run_name.resize(nkeep);
-  T->run_row0.clear();
-  for (uint32_t k = 0; k < nkeep; ++k) T->run_row0.push_back(rows[k]);
-  T->run_row0.push_back(T->n);
-  for (uint32_t k = 0; k < nkeep; ++k)
-    if (rows[k] == ~0ULL) return bg_fail(c, BG_E_PARSE, "internal: chromosome run without a row");
-  bg_release(c, d_pos);
-  bg_release(c, d_hash);
-  bg_release(c, d_gid);
-  bg_release(c, d_row);
-  bg_release(c, S.row0);
-  S.row0 = nullptr;
+  S.rows.resize(nr);  // copied back after every input's parse is queued
   return 0;
 }
 
-static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>& gid) {
+// after phase 3: per-input status, flags and the run -> row table
+static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S,
+                      const bg_dstatus& h) {
+  T->run_row0.assign(1, 0);
+  if (S.ntiles == 0 || T->n == 0 || S.run_pos.empty()) {
+    T->run_name.clear();
+    return 0;
+  }
+  int rc = report_status(c, idx, h);
+  if (rc) return rc;
+  if (in.kind == BG_BED5 && (h.flags & 1ULL)) T->score_int = false;
+  T->has_zero_len = (h.flags & 2ULL) != 0;
+  T->maxlen = h.maxlen;
+  // a trailing run may own only the dropped unterminated last line: no rows
+  uint32_t nkeep = (uint32_t)S.rows.size();
+  while (nkeep > 0 && S.rows[nkeep - 1] == ~0ULL) --nkeep;
+  T->run_name.resize(nkeep);
+  T->run_row0.clear();
+  for (uint32_t k = 0; k < nkeep; ++k) T->run_row0.push_back(S.rows[k]);
+  T->run_row0.push_back(T->n);
+  return 0;
+}
+
+static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>& gid,
+                            std::string& packed, std::vector<uint32_t>& off,
+                            std::vector<uint32_t>& len) {
   std::vector<std::string> all;
   for (bg_table* T : s->t)
     for (auto& nm : T->run_name) all.push_back(nm);
@@ -856,8 +874,8 @@ static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>
   if (all.size() >= (1u << 22)) return bg_fail(c, BG_E_UNSUPPORTED, "too many chromosomes");
   s->names = all;
   for (size_t k = 0; k < all.size(); ++k) gid[all[k]] = (int32_t)k;
-  std::vector<uint32_t> off(all.size() + 1, 0), len(all.size() + 1, 0);
-  std::string packed;
+  off.assign(all.size() + 1, 0);
+  len.assign(all.size() + 1, 0);
   for (size_t k = 0; k < all.size(); ++k) {
     off[k] = (uint32_t)packed.size();
     len[k] = (uint32_t)all[k].size();
@@ -872,34 +890,75 @@ static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>
     BG_HIP(c, hipMemcpyAsync(s->d_names, packed.data(), packed.size(), hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemcpyAsync(s->d_name_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemcpyAsync(s->d_name_len, len.data(), 4 * len.size(), hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));  // host vectors go out of scope
   return 0;
 }
 
+// Three host round trips per call, whatever the number of inputs: run-record counts, run
+// records, final statuses.
 extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   if (!c || n <= 0 || !inputs || !out) return BG_E_ARG;
   *out = nullptr;
   bg_set* s = new bg_set();
   s->ctx = c;
   std::vector<LoadState> st(n);
-  int rc = 0;
-  for (int i = 0; i < n && !rc; ++i) {
-    bg_table* T = new bg_table();
-    s->t.push_back(T);
-    rc = scout_one(c, i, inputs[i], T, st[i]);
-  }
-  bg_mark(c, "scout");
+  // per input: 8 counters (phase 1) + one status block (phase 3)
+  uint64_t* ctr = (uint64_t*)bg_alloc(c, 64ull * n);
+  bg_dstatus* dst = (bg_dstatus*)bg_alloc(c, sizeof(bg_dstatus) * n);
+  std::vector<uint64_t> hctr(8ull * n);
+  std::vector<bg_dstatus> hst(n);
+  std::string packed;
+  std::vector<uint32_t> off, len;
   std::map<std::string, int32_t> gid;
-  if (!rc) rc = build_dictionary(c, s, gid);
-  if (!rc) {
-    rc = bg_hip_ok(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
-  }
+  int rc = (!ctr || !dst) ? BG_E_NOMEM : 0;
+  if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(ctr, 0, 64ull * n, c->stream));
   for (int i = 0; i < n && !rc; ++i) {
-    rc = parse_one(c, i, inputs[i], s->t[i], st[i], gid);
-    if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(&c->dstat->flags, 0, 16, c->stream));  // flags, maxlen
+    s->t.push_back(new bg_table());
+    rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
   }
-  for (auto& S : st) bg_release(c, S.row0);
+  // round trip 1: rows and record counts of every input
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hctr.data(), ctr, 64ull * n, hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < n && !rc; ++i) {
+    LoadState& S = st[i];
+    s->t[i]->n = S.ntiles ? hctr[8ull * i] : 0;
+    const uint32_t nr = (uint32_t)hctr[8ull * i + 2];
+    if (nr > S.rc) { rc = bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input"); break; }
+    S.h_pos.resize(nr);
+    S.h_hash.resize(nr);
+    S.h_name.resize(128ull * nr);
+    S.h_len.resize(nr);
+    if (!nr) continue;
+    rc = bg_hip_ok(c, hipMemcpyAsync(S.h_pos.data(), S.rpos, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_hash.data(), S.rhash, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_name.data(), S.rname, 128ull * nr, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_len.data(), S.rlen, 4ull * nr, hipMemcpyDeviceToHost, c->stream));
+  }
+  // round trip 2: the run records
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < n && !rc; ++i) rc = runs_one(c, i, inputs[i], s->t[i], st[i]);
+  bg_mark(c, "scout");
+  if (!rc) rc = build_dictionary(c, s, gid, packed, off, len);
+  if (!rc) {
+    for (auto& h : hst) {
+      memset(&h, 0, sizeof(h));
+      h.first_bad = ~0ULL;
+    }
+    rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst.data(), sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
+  }
+  for (int i = 0; i < n && !rc; ++i) rc = parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
+  // round trip 3: statuses and run rows of every input (pageable copies block the host,
+  // so they are issued only once all parses are queued)
+  for (int i = 0; i < n && !rc; ++i)
+    if (!st[i].rows.empty())
+      rc = bg_hip_ok(c, hipMemcpyAsync(st[i].rows.data(), st[i].d_row, 8ull * st[i].rows.size(),
+                                       hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hst.data(), dst, sizeof(bg_dstatus) * n, hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < n && !rc; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
+  if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies read the host vectors
+  for (auto& S : st) release_state(c, S);
+  bg_release(c, ctr);
+  bg_release(c, dst);
   if (rc) {
     bg_set_free(s);
     return rc;
