@@ -432,6 +432,18 @@ __device__ __forceinline__ void lds16(const uint8_t* buf, uint32_t q, uint64_t& 
   hi = (uint64_t)bgp_align(x2, x3, o) | ((uint64_t)bgp_align(x3, x4, o) << 32);
 }
 
+// the 12 bytes of LDS ending at byte offset e (e >= 12, e + 4 <= LBUF)
+__device__ __forceinline__ void lds12_end(const uint8_t* buf, uint32_t e, uint32_t& d1,
+                                          uint32_t& d2, uint32_t& d3) {
+  const uint32_t q = e - 12;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (q & ~3u));
+  const uint32_t o = q & 3u;
+  const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3];
+  d1 = bgp_align(x0, x1, o);
+  d2 = bgp_align(x1, x2, o);
+  d3 = bgp_align(x2, x3, o);
+}
+
 // 32-bit window of a per-tile class bitmap starting at local byte offset p (bit j of
 // the result = byte p + j); m holds one 32-bit word per 32 tile bytes
 __device__ __forceinline__ uint32_t mask_window(const uint32_t* m, uint32_t p) {
@@ -457,13 +469,14 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   const int r = bgp_fields_masks(mask_window(wsm, q), mask_window(dgm, q), len, F);
   if (r != 1) return false;  // blank lines and errors take the byte path (messages)
   const uint32_t toklen = F.a1 - F.a0;
-  if (toklen > 16 || F.s1 - F.s0 > 13 || F.e1 - F.e0 > 13) return false;
-  const uint32_t b = q + HB;  // LDS byte offset of the line start
+  if (toklen > 16 || F.s1 - F.s0 > 12 || F.e1 - F.e0 > 12) return false;
+  const uint32_t b = q + HB;  // LDS byte offset of the line start (>= HB = 16)
+  uint32_t d1, d2, d3;
+  lds12_end(buf, b + F.s1, d1, d2, d3);
+  L.start = bgp_digits_r(d1, d2, d3, (int)(F.s1 - F.s0));
+  lds12_end(buf, b + F.e1, d1, d2, d3);
+  L.end = bgp_digits_r(d1, d2, d3, (int)(F.e1 - F.e0));
   uint64_t lo, hi;
-  lds16(buf, b + F.s0, lo, hi);
-  L.start = bgp_digits(lo, hi, (int)(F.s1 - F.s0));
-  lds16(buf, b + F.e0, lo, hi);
-  L.end = bgp_digits(lo, hi, (int)(F.e1 - F.e0));
   lds16(buf, b + F.a0, lo, hi);
   if (toklen < 16) {
     if (toklen <= 8) {

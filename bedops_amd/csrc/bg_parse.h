@@ -24,21 +24,23 @@ BG_HD uint32_t bgp_group4(uint32_t m80) {
   return ((((m80 >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// per-byte classes of one dword: ws4 = {' ', 0x09..0x0D}, dg4 = {'0'..'9'}
+// per-byte classes of one dword: ws4 = {' ', 0x09..0x0D}, dg4 = {'0'..'9'} (bit i = byte i).
+// Both 4-bit groups come out of ONE multiply: byte i carries its ws flag in bit 0 and its
+// digit flag in bit 4, and x * 0x00204081 gathers bit 0 of byte i at bit 21+i and bit 4 of
+// byte i at bit 25+i (the 32 partial products land on distinct bits: no carries).
 BG_HD void bgp_classify(uint32_t x, uint32_t& ws4, uint32_t& dg4) {
   const uint32_t hi = x & 0x80808080u;  // bytes >= 0x80 are neither
   const uint32_t lo7 = x & 0x7F7F7F7Fu;
-  const uint32_t y = lo7 ^ 0x20202020u;
-  const uint32_t nz20 = (y + 0x7F7F7F7Fu) & 0x80808080u;
-  const uint32_t eq20 = ~nz20 & 0x80808080u;
-  const uint32_t ge9 = (lo7 + 0x77777777u) & 0x80808080u;
-  const uint32_t ge14 = (lo7 + 0x72727272u) & 0x80808080u;
-  const uint32_t ws = (eq20 | (ge9 & ~ge14)) & ~hi & 0x80808080u;
-  const uint32_t ge48 = (lo7 + 0x50505050u) & 0x80808080u;
-  const uint32_t ge58 = (lo7 + 0x46464646u) & 0x80808080u;
+  const uint32_t nz20 = ((lo7 ^ 0x20202020u) + 0x7F7F7F7Fu);  // bit 7: byte != ' '
+  const uint32_t ge9 = lo7 + 0x77777777u;
+  const uint32_t ge14 = lo7 + 0x72727272u;
+  const uint32_t ws = (~nz20 | (ge9 & ~ge14)) & ~hi & 0x80808080u;
+  const uint32_t ge48 = lo7 + 0x50505050u;
+  const uint32_t ge58 = lo7 + 0x46464646u;
   const uint32_t dg = ge48 & ~ge58 & ~hi & 0x80808080u;
-  ws4 = bgp_group4(ws);
-  dg4 = bgp_group4(dg);
+  const uint32_t p = ((ws >> 7) | (dg >> 3)) * 0x00204081u;
+  ws4 = (p >> 21) & 0xFu;
+  dg4 = (p >> 25) & 0xFu;
 }
 
 // bytes [o, o+4) of the 8-byte little-endian sequence (lo, hi), o in 0..3
@@ -67,6 +69,40 @@ BG_HD uint64_t bgp_digits(uint64_t lo8, uint64_t hi8, int L) {
   const uint64_t head = bgp_swar8(lo8, h);
   const uint64_t tail = (h == 8) ? hi8 : ((lo8 >> (8 * h)) | (hi8 << (64 - 8 * h)));
   return head * 100000000ull + bgp_swar8(tail, 8);
+}
+
+// sum of byte products a.b[i] * w.b[i] + c (v_dot4_u32_u8 on the GPU), mod 2^32
+BG_HD uint32_t bgp_udot4(uint32_t a, uint32_t w, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_udot4(a, w, c, false);
+#else
+  for (int i = 0; i < 4; ++i) c += ((a >> (8 * i)) & 0xFFu) * ((w >> (8 * i)) & 0xFFu);
+  return c;
+#endif
+}
+
+// four ASCII digits (first digit in the low byte) -> value, via two byte dot products
+BG_HD uint32_t bgp_dig4(uint32_t d) {
+  const uint32_t hi2 = bgp_udot4(d, 0x0000010Au, 0u);           // 10*x0 + x1 (+ 528)
+  const uint32_t lo2 = bgp_udot4(d, 0x010A0000u, 0u - 53328u);  // 10*x2 + x3 (+ 528 - 53328)
+  return hi2 * 100u + lo2;                                      // 100*(.. - 528) + ..
+}
+
+// value of the last L (1..12) ASCII digits of the 12 bytes d1|d2|d3 (the number's last
+// digit is the high byte of d3); bytes before the number are ignored. Only 32-bit VALU
+// work plus one 32x32->64 multiply-add.
+BG_HD uint64_t bgp_digits_r(uint32_t d1, uint32_t d2, uint32_t d3, int L) {
+  const int k1 = L >= 12 ? 0 : (L <= 8 ? 4 : 12 - L);  // leading bytes of d1 to ignore
+  const int k2 = L >= 8 ? 0 : (L <= 4 ? 4 : 8 - L);
+  const int k3 = L >= 4 ? 0 : 4 - L;
+  const uint32_t m1 = (uint32_t)(~0ull << (8 * k1));  // bytes that belong to the number
+  const uint32_t m2 = (uint32_t)(~0ull << (8 * k2));
+  const uint32_t m3 = (uint32_t)(~0ull << (8 * k3));
+  d1 = (d1 & m1) | (0x30303030u & ~m1);  // others read as '0'
+  d2 = (d2 & m2) | (0x30303030u & ~m2);
+  d3 = (d3 & m3) | (0x30303030u & ~m3);
+  const uint32_t g23 = bgp_dig4(d2) * 10000u + bgp_dig4(d3);
+  return (uint64_t)bgp_dig4(d1) * 100000000ull + g23;
 }
 
 struct BgpFields {

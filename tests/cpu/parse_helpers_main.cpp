@@ -1,11 +1,28 @@
 // CPU driver for bedops_amd/csrc/bg_parse.h (the loader's SWAR field extraction).
 // Reads lines on stdin; for each prints "fast a0 a1 start end rest", "slow" or "blank".
+#include <initializer_list>
 #include <stdio.h>
 #include <string.h>
 
 #include "../../bedops_amd/csrc/bg_parse.h"
 
+static int naive_ws(unsigned b) { return b == ' ' || (b >= 9 && b <= 13); }
+static int naive_dg(unsigned b) { return b >= '0' && b <= '9'; }
+
 int main() {
+  // bgp_classify against a per-byte restatement: every byte value in every position
+  for (uint32_t pos = 0; pos < 4; ++pos)
+    for (uint32_t v = 0; v < 256; ++v)
+      for (uint32_t fill : {0x00000000u, 0x20202020u, 0x39393939u, 0xFFFFFFFFu, 0x0A09300Bu}) {
+        const uint32_t x = (fill & ~(0xFFu << (8 * pos))) | (v << (8 * pos));
+        uint32_t ws, dg, w2 = 0, d2 = 0;
+        bgp_classify(x, ws, dg);
+        for (int i = 0; i < 4; ++i) {
+          w2 |= (uint32_t)naive_ws((x >> (8 * i)) & 0xFF) << i;
+          d2 |= (uint32_t)naive_dg((x >> (8 * i)) & 0xFF) << i;
+        }
+        if (ws != w2 || dg != d2) { printf("CLASSIFY %08x\n", x); return 1; }
+      }
   static char line[1 << 16];
   while (fgets(line, sizeof(line), stdin)) {
     size_t len = strlen(line);
@@ -30,6 +47,20 @@ int main() {
     memcpy(&lo, d, 8);
     memcpy(&hi, d + 8, 8);
     uint64_t e = bgp_digits(lo, hi, (int)(F.e1 - F.e0));
+    // right-aligned form (the one the kernel uses): the 12 bytes ending at the last digit
+    for (int which = 0; which < 2; ++which) {
+      const uint32_t b0 = which ? F.e0 : F.s0, b1 = which ? F.e1 : F.s1;
+      if (b1 - b0 > 12) continue;
+      unsigned char w[12];
+      for (int i = 0; i < 12; ++i) {
+        const int at = (int)b1 - 12 + i;
+        w[i] = at >= 0 ? (unsigned char)line[at] : 0x55;
+      }
+      uint32_t d[3];
+      memcpy(d, w, 12);
+      const uint64_t v = bgp_digits_r(d[0], d[1], d[2], (int)(b1 - b0));
+      if (v != (which ? e : s)) { printf("MISMATCH %llu\n", (unsigned long long)v); return 1; }
+    }
     printf("fast %u %u %llu %llu %u\n", F.a0, F.a1, (unsigned long long)s, (unsigned long long)e, F.e1);
   }
   return 0;
