@@ -268,6 +268,26 @@ __device__ __forceinline__ uint64_t lower_bound_i64(const int64_t* A, uint64_t n
   }
   return lo;
 }
+// first index k in [lo, hi) with A[k] >= v (hi if none)
+__device__ __forceinline__ uint64_t lower_bound_in(const int64_t* A, uint64_t lo, uint64_t hi,
+                                                   int64_t v) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (A[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// first index k in [lo, hi) with A[k] > v (hi if none)
+__device__ __forceinline__ uint64_t upper_bound_in(const int64_t* A, uint64_t lo, uint64_t hi,
+                                                   int64_t v) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (A[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
 // first index k with A[k] > v
 __device__ __forceinline__ uint64_t upper_bound_i64(const int64_t* A, uint64_t n, int64_t v) {
   uint64_t lo = 0, hi = n;

@@ -493,6 +493,42 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   return true;
 }
 
+// BED5 fast path: "<ws> id <ws> score" after the end field, score a plain unsigned
+// integer of <= 12 digits followed by whitespace or the line end (the common bedmap map
+// file); anything else (signs, decimals, exponents, long fields) takes the byte path.
+// q: local line start, len: line length, e1: end of the `end` digits (line-relative).
+__device__ __forceinline__ bool parse_score_fast(const uint8_t* buf, const uint32_t* wsm,
+                                                 const uint32_t* dgm, uint32_t q, uint32_t len,
+                                                 uint32_t e1, double& score) {
+  uint32_t WS = mask_window(wsm, q + e1), DG = mask_window(dgm, q + e1);
+  const uint32_t l2 = len - e1;  // bytes from e1 to the line end
+  if (l2 < 32) {                 // bytes past the line end act as whitespace
+    const uint32_t endm = ~0u << l2;
+    WS |= endm;
+    DG &= ~endm;
+  }
+  if (!(WS & 1u)) return false;  // the end digits must be followed by whitespace
+  const uint32_t NW = ~WS;
+  if (!NW) return false;
+  const uint32_t i0 = bgp_ctz(NW);  // id
+  const uint32_t m1 = WS & (~0u << i0);
+  if (!m1) return false;
+  const uint32_t i1 = bgp_ctz(m1);
+  if (i1 >= 31) return false;
+  const uint32_t m2 = NW & (~0u << i1);
+  if (!m2) return false;
+  const uint32_t c0 = bgp_ctz(m2);  // score
+  if (c0 >= l2 || !((DG >> c0) & 1u)) return false;
+  const uint32_t m3 = ~DG & (~0u << c0);
+  if (!m3) return false;
+  const uint32_t c1 = bgp_ctz(m3);
+  if (!((WS >> c1) & 1u) || c1 - c0 > 12) return false;  // digits end at whitespace / line end
+  uint32_t d1, d2, d3;
+  lds12_end(buf, q + HB + e1 + c1, d1, d2, d3);
+  score = (double)bgp_digits_r(d1, d2, d3, (int)(c1 - c0));
+  return true;
+}
+
 // runs that can occur in each tile: [runlo, runhi] by position
 __global__ void k_run_range(RunTable R, uint32_t ntiles, uint32_t* __restrict__ runlo,
                             uint32_t* __restrict__ runhi) {
@@ -579,13 +615,17 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
       Fast F;
       const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
       const RunInfo& I = R.info[run];
-      if (kind != BG_BED5 && parse_line_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F) &&
-          F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
+      double sc = 0;
+      if (parse_line_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F) &&
+          F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi &&
+          (kind != BG_BED5 ||
+           parse_score_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F.rest, sc))) {
         emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
         if (rest_off) {
           rest_off[r] = (uint64_t)(ls + F.rest);
           rest_len[r] = (uint32_t)(le - ls - F.rest);
         }
+        if (score) score[r] = sc;
       } else {
         key = PENDING;
       }

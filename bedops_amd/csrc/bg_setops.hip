@@ -282,20 +282,41 @@ __global__ void __launch_bounds__(BG_NT) k_lengths(const int64_t* __restrict__ S
   if (i < n) L[i] = (uint64_t)(E[i] - S[i]);
 }
 
+// One thread per reference row; the workgroup first bounds the component range its rows
+// can touch (two searches over the whole list), so each row's own searches run over a
+// few hundred cache-resident components instead of the whole list.
 __global__ void __launch_bounds__(BG_NT) k_element_flags(
     const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
     const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
     const uint64_t* __restrict__ P, double thres, int use_pct, int invert,
     uint8_t* __restrict__ flag) {
-  const uint64_t r = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (r >= nr) return;
-  const int64_t s = RS[r], e = RE[r];
-  const uint64_t lo = upper_bound_i64(OE_, no, s);  // first component ending after s
+  __shared__ int64_t wmax[BG_NT / 64];
+  __shared__ uint64_t bnd[2];
+  const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
+  const uint64_t r = r0 + threadIdx.x;
+  const bool live = r < nr;
+  const int64_t s = live ? RS[r] : LLONG_MAX, e = live ? RE[r] : LLONG_MIN;
+  const int64_t em = wave_max_all(e);
+  if (bg_lane() == 0) wmax[bg_wave()] = em;
+  __syncthreads();
+  if (threadIdx.x == 0) bnd[0] = upper_bound_i64(OE_, no, RS[r0]);  // rows start at >= RS[r0]
+  if (threadIdx.x == 64) {
+    int64_t m = wmax[0];
+    for (int w = 1; w < BG_NT / 64; ++w) m = max(m, wmax[w]);
+    bnd[1] = lower_bound_i64(OS_, no, m);  // no row ends after m
+  }
+  __syncthreads();
+  if (!live) return;
+  const uint64_t blo = bnd[0], bhi = max(bnd[0], bnd[1]);
+  // exact within [blo, bhi]: a row's first component ending after s is >= blo, and its
+  // first component starting at/after e is <= bhi; a clamped lo == bhi means no overlap,
+  // which decides like "nothing left" below (keep = invert)
+  const uint64_t lo = upper_bound_in(OE_, blo, bhi, s);  // first component ending after s
   bool keep;
   if (lo >= no) {
     keep = invert;  // nothing left to be an element of (Bedops.cpp:1044-1048)
   } else {
-    const uint64_t hi = lower_bound_i64(OS_, no, e);  // first component starting at/after e
+    const uint64_t hi = lower_bound_in(OS_, blo, bhi, e);  // first component starting at/after e
     uint64_t ov = 0;
     if (lo < hi) {
       ov = P[hi] - P[lo];
