@@ -10,7 +10,8 @@ on a weight such as its row count); each rank runs the engine on its chromosomes
 input exchange); `gather_text()` is the one exchange of the path: rank 0 receives every
 rank's formatted bytes, chromosome by chromosome, straight into its place in the final
 strcmp-ordered buffer (sizes via all_gather, then point-to-point send/recv: RCCL over xGMI
-with the "nccl" backend, gloo on CPU for the tests).
+with the "nccl" backend, gloo on CPU for the tests). gather_text_async posts the transfers
+and returns, so a pipeline can compute the next batch while this one moves.
 """
 
 
@@ -35,14 +36,29 @@ def strcmp_order(names):
     return sorted(names, key=_key)
 
 
-def gather_text(dist, text, spans, names, owner, rank, world):
-    """Reassemble sorted output on rank 0.
+class PendingGather:
+    """Transfers of one reassembly in flight; wait() returns the output on rank 0."""
+
+    def __init__(self, works, out, keep):
+        self.works, self.out, self._keep = works, out, keep
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works, self._keep = [], None
+        return self.out
+
+
+def gather_text_async(dist, text, spans, names, owner, rank, world, size_group=None):
+    """Post the reassembly of sorted output on rank 0 and return without waiting.
 
     text:   this rank's formatted bytes (uint8 torch tensor, on the collective's device).
     spans:  {chrom: (begin, end)} byte range of each of this rank's chromosomes in `text`
             (chromosomes absent from the output may be omitted).
     names:  every chromosome of the job (any order); owner: chrom -> rank.
-    Returns the whole output (uint8 tensor) on rank 0, None elsewhere.
+    size_group: optional process group (e.g. gloo, CPU tensors) for the per-chromosome
+            byte counts, so that exchanging them never queues behind earlier transfers.
+    The bytes land chromosome by chromosome straight into their place in rank 0's output.
     """
     import torch
 
@@ -55,12 +71,12 @@ def gather_text(dist, text, spans, names, owner, rank, world):
         if owner[c] != rank:
             raise ValueError(f"rank {rank} has output for {c!r}, owned by rank {owner[c]}")
         mine[idx[c]] = b - a
-    mine = mine.to(dev)
+    if size_group is None:
+        mine = mine.to(dev)
     parts = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine)
-    lens = [0] * len(order)
-    for i, c in enumerate(order):
-        lens[i] = int(parts[owner[c]][i].item())
+    dist.all_gather(parts, mine, group=size_group)
+    parts = [p.cpu() for p in parts]
+    lens = [int(parts[owner[c]][i]) for i, c in enumerate(order)]
 
     if rank != 0:
         ops = []
@@ -68,8 +84,7 @@ def gather_text(dist, text, spans, names, owner, rank, world):
             if owner[c] == rank and lens[idx[c]] > 0:
                 a, b = spans[c]
                 ops.append(dist.P2POp(dist.isend, text[a:b], 0))
-        _run(dist, ops)
-        return None
+        return PendingGather(_post(dist, ops), None, text)
 
     total = sum(lens)
     out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
@@ -84,15 +99,18 @@ def gather_text(dist, text, spans, names, owner, rank, world):
             else:
                 ops.append(dist.P2POp(dist.irecv, out[pos:pos + n], owner[c]))
         pos += n
-    _run(dist, ops)
-    return out[:total]
+    return PendingGather(_post(dist, ops), out[:total], text)
 
 
-def _run(dist, ops):
+def gather_text(dist, text, spans, names, owner, rank, world, size_group=None):
+    """Reassemble sorted output on rank 0 (blocking form of gather_text_async).
+    Returns the whole output (uint8 tensor) on rank 0, None elsewhere."""
+    return gather_text_async(dist, text, spans, names, owner, rank, world, size_group).wait()
+
+
+def _post(dist, ops):
     # one grouped launch of all point-to-point transfers (ncclGroupStart/End under RCCL)
-    if ops:
-        for q in dist.batch_isend_irecv(ops):
-            q.wait()
+    return dist.batch_isend_irecv(ops) if ops else []
 
 
 def spans_from_text(data):

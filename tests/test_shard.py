@@ -25,10 +25,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, files, mode, exe, outdir):
+def _worker(rank, world, port, files, mode, exe, outdir, pipelined=False):
     import torch
     import torch.distributed as dist
-    from bedops_amd.shard import assign, gather_text, spans_from_text
+    from bedops_amd.shard import assign, gather_text, gather_text_async, spans_from_text
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
@@ -50,16 +50,24 @@ def _worker(rank, world, port, files, mode, exe, outdir):
         spans = spans_from_text(out)
         buf = torch.frombuffer(bytearray(out), dtype=torch.uint8) if out else \
             torch.empty(0, dtype=torch.uint8)
-        got = gather_text(dist, buf, spans, CHROMS, owner, rank, world)
+        if pipelined:  # two batches in flight before either is waited for (bench.py's loop)
+            sg = dist.new_group(backend="gloo")
+            p1 = gather_text_async(dist, buf, spans, CHROMS, owner, rank, world, sg)
+            p2 = gather_text_async(dist, buf.clone(), spans, CHROMS, owner, rank, world, sg)
+            got, got2 = p1.wait(), p2.wait()
+            if rank == 0:
+                assert bytes(got.numpy()) == bytes(got2.numpy())
+        else:
+            got = gather_text(dist, buf, spans, CHROMS, owner, rank, world)
         if rank == 0:
             open(os.path.join(outdir, "gathered.bed"), "wb").write(bytes(got.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, files, mode, exe, outdir):
+def _run(world, files, mode, exe, outdir, pipelined=False):
     import torch.multiprocessing as mp
-    mp.start_processes(_worker, args=(world, _free_port(), files, mode, exe, outdir),
+    mp.start_processes(_worker, args=(world, _free_port(), files, mode, exe, outdir, pipelined),
                        nprocs=world, start_method="spawn", join=True)
     return open(os.path.join(outdir, "gathered.bed"), "rb").read()
 
@@ -83,9 +91,11 @@ def test_spans_from_text():
     assert spans_from_text(b"") == {}
 
 
-@pytest.mark.parametrize("world,mode", [(2, ["-i"]), (2, ["-m"]), (3, ["-d"]),
-                                        (2, ["-e", "1"]), (3, ["-n", "50%"])])
-def test_sharded_equals_single_run(oracle_bin, world, mode):
+@pytest.mark.parametrize("world,mode,pipelined", [(2, ["-i"], False), (2, ["-m"], False),
+                                                  (3, ["-d"], False), (2, ["-e", "1"], False),
+                                                  (3, ["-n", "50%"], False), (2, ["-i"], True),
+                                                  (3, ["-m"], True)])
+def test_sharded_equals_single_run(oracle_bin, world, mode, pipelined):
     rng = random.Random(1000 + world)
     with tempfile.TemporaryDirectory() as td:
         files = []
@@ -96,5 +106,5 @@ def test_sharded_equals_single_run(oracle_bin, world, mode):
             files.append(p)
         exe = oracle_bin["bedops"]
         want = subprocess.run([exe, *mode, *files], capture_output=True, check=True).stdout
-        got = _run(world, files, mode, exe, td)
+        got = _run(world, files, mode, exe, td, pipelined)
         assert got == want
