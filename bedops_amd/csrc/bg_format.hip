@@ -16,9 +16,9 @@
 
 #include "bg_internal.h"
 
-#define FT_ROWS 4
+#define FT_ROWS 2
 #define FT_TILE (BG_NT * FT_ROWS)
-#define FT_LDS 32768
+#define FT_LDS 16384
 
 struct FmtArgs {
   int kind;
@@ -255,13 +255,13 @@ __device__ __forceinline__ void render_closest(const FmtArgs& A, uint64_t k, Out
 }
 
 // renders (or measures) line k; returns false on a value outside the GPU range
-template <typename Out>
+template <int KIND, typename Out>
 __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
-  if (A.kind == RES_CLOSEST) {
+  if (KIND == RES_CLOSEST) {
     render_closest(A, k, o);
     return true;
   }
-  if (A.kind == RES_MAP) {
+  if (KIND == RES_MAP) {
     const int32_t c = A.cnt[k];
     if (A.skip_unmapped && c == 0) return true;
     for (int q = 0; q < A.nops; ++q) {
@@ -283,7 +283,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
     o.put('\n');
     return true;
   }
-  const uint64_t r = (A.kind == RES_ROWS) ? A.rows[k] : k;
+  const uint64_t r = (KIND == RES_ROWS) ? A.rows[k] : k;
   const int64_t s = A.s[r], e = A.e[r];
   const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
   const uint32_t nl = A.name_len[g];
@@ -294,7 +294,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
   put_u64(o, cs, dec_len_u64(cs));
   o.put('\t');
   put_u64(o, ce, dec_len_u64(ce));
-  if (A.kind == RES_ROWS) {
+  if (KIND == RES_ROWS) {
     const uint32_t rl = A.rest_len[r];
     const char* rp = A.text + A.rest_off[r];
     for (uint32_t q = 0; q < rl; ++q) o.put(rp[q]);
@@ -303,6 +303,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
   return true;
 }
 
+template <int KIND>
 __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __restrict__ tb,
                                                      bg_dstatus* st) {
   __shared__ uint64_t sh[BG_NT / 64 + 1];
@@ -310,13 +311,14 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __rest
   CountOut co;
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
-    if (row < A.n && !render(A, row, co)) bg_report(st, row, ERR_RANGE);
+    if (row < A.n && !render<KIND>(A, row, co)) bg_report(st, row, ERR_RANGE);
   }
   uint64_t tot;
   (void)block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &tot);
   if (threadIdx.x == 0) tb[blockIdx.x] = tot;
 }
 
+template <int KIND>
 __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* __restrict__ toff,
                                                      char* __restrict__ out) {
   __shared__ uint64_t sh[BG_NT / 64 + 1];
@@ -329,7 +331,7 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     CountOut co;
-    if (row < A.n) render(A, row, co);
+    if (row < A.n) render<KIND>(A, row, co);
     uint64_t st;
     my[k] = tot + block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &st);
     tot += st;
@@ -339,14 +341,14 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
     for (int k = 0; k < FT_ROWS; ++k) {
       const uint64_t row = base + (uint64_t)k * BG_NT;
       LdsOut o{out + dst0 + my[k]};
-      if (row < A.n) render(A, row, o);
+      if (row < A.n) render<KIND>(A, row, o);
     }
     return;
   }
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     LdsOut o{buf + my[k]};
-    if (row < A.n) render(A, row, o);
+    if (row < A.n) render<KIND>(A, row, o);
   }
   __syncthreads();
   // stream buf[0, tot) -> out[dst0, dst0 + tot)
@@ -438,7 +440,12 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!tb || !d_tot) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   if (nb) {
-    BG_LAUNCH(c, "k_fmt_count", k_fmt_count, dim3(nb), dim3(BG_NT), A, tb, c->dstat);
+    switch (A.kind) {
+      case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
+      case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
+      case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
+      default: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, c->dstat);
+    }
     BG_HIP(c, hipGetLastError());
   }
   int rc = bg_scan_sum_u64(c, tb, tb, nb, d_tot);
@@ -451,7 +458,12 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   r->text = (char*)bg_alloc(c, total + 16);
   if (!r->text) return BG_E_NOMEM;
   if (nb) {
-    BG_LAUNCH(c, "k_fmt_write", k_fmt_write, dim3(nb), dim3(BG_NT), A, tb, r->text);
+    switch (A.kind) {
+      case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_ROWS: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_MAP: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      default: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, r->text);
+    }
     BG_HIP(c, hipGetLastError());
   }
   r->toff = tb;
@@ -466,6 +478,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
 // Byte offset of the first output line of every chromosome g of the set's dictionary;
 // out[nchroms] = total bytes, so chromosome g's lines are text[out[g], out[g+1]).
 // Used to reassemble per-GPU shards in strcmp chromosome order (multi-GPU path).
+template <int KIND>
 __global__ void k_chrom_spans(FmtArgs A, const uint64_t* __restrict__ toff, uint32_t nchroms,
                               uint64_t nbytes, uint64_t* __restrict__ out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -482,7 +495,7 @@ __global__ void k_chrom_spans(FmtArgs A, const uint64_t* __restrict__ toff, uint
   if (lo >= A.n) { out[g] = nbytes; return; }
   const uint64_t t = lo / FT_TILE;
   CountOut co;
-  for (uint64_t j = t * FT_TILE; j < lo; ++j) render(A, j, co);
+  for (uint64_t j = t * FT_TILE; j < lo; ++j) render<KIND>(A, j, co);
   out[g] = toff[t] + co.n;
 }
 
@@ -496,8 +509,14 @@ extern "C" int bg_result_chrom_spans(bg_ctx* c, bg_result* r, uint64_t* offsets,
   fill_args(r, A);
   uint64_t* d = (uint64_t*)bg_alloc(c, 8ull * (nc + 1));
   if (!d) return BG_E_NOMEM;
-  BG_LAUNCH(c, "k_chrom_spans", k_chrom_spans, dim3(bg_blocks(nc + 1, 64)), dim3(64), A, r->toff,
-            nc, r->nbytes, d);
+#define BG_SPANS(K) BG_LAUNCH(c, "k_chrom_spans", k_chrom_spans<K>, dim3(bg_blocks(nc + 1, 64)), dim3(64), A, r->toff, nc, r->nbytes, d)
+  switch (A.kind) {
+    case RES_IVL: BG_SPANS(RES_IVL); break;
+    case RES_ROWS: BG_SPANS(RES_ROWS); break;
+    case RES_MAP: BG_SPANS(RES_MAP); break;
+    default: BG_SPANS(RES_CLOSEST);
+  }
+#undef BG_SPANS
   BG_HIP(c, hipGetLastError());
   BG_HIP(c, hipMemcpyAsync(offsets, d, 8ull * (nc + 1), hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
