@@ -33,7 +33,7 @@
 #define CT_ITEMS 8                    // rows per lane per wave in components()
 #define CT_WROWS (64 * CT_ITEMS)      // rows per wave
 #define CT_TILE (BG_NT * CT_ITEMS)    // rows per workgroup (4 waves)
-#define MP_ITEMS 8
+#define MP_ITEMS 4
 #define MP_TILE (BG_NT * MP_ITEMS)    // merged elements per workgroup
 
 __device__ __forceinline__ int64_t wave_max_all(int64_t v) {
@@ -270,8 +270,13 @@ __global__ void __launch_bounds__(BG_NT) k_mp_tile(
     if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
     return;
   }
-  const uint64_t q = off[blockIdx.x] + o;
-  for (uint32_t k = 0; k < c; ++k) { OS[q + k] = ps[k]; OE[q + k] = pe[k]; }
+  // stage the tile's pieces in LDS (the input slices are no longer read), then store them
+  // with consecutive lanes on consecutive elements
+  __syncthreads();
+  for (uint32_t k = 0; k < c; ++k) { ls_[o + k] = ps[k]; le_[o + k] = pe[k]; }
+  __syncthreads();
+  const uint64_t q = off[blockIdx.x];
+  for (uint32_t k = threadIdx.x; k < btot; k += BG_NT) { OS[q + k] = ls_[k]; OE[q + k] = le_[k]; }
 }
 
 // ------------------------------- element-of ---------------------------------------
