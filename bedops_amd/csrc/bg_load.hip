@@ -196,27 +196,18 @@ __device__ __forceinline__ uint32_t tile_line_starts(const uint4& v0, const uint
                                                      uint16_t* ls, uint32_t cap,
                                                      uint32_t* shs, bool& has0) {
   has0 = (t0 == 0) || buf[HB - 1] == '\n';
-  uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-  uint32_t m[8], c = 0;
+  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t nlg = 0;  // bit j: byte j of this thread's 32 is '\n'
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    m[k] = nl_mask4(w[k]);
-    // a '\n' on the tile's last byte starts a line in the next tile
-    if (threadIdx.x == BG_NT - 1 && k == 7) m[k] &= 0x00808080u;
-    c += __popc(m[k]);
-  }
+  for (int k = 0; k < 8; ++k) nlg |= bgp_group4(nl_mask4(w[k])) << (4 * k);
+  // a '\n' on the tile's last byte starts a line in the next tile
+  if (threadIdx.x == BG_NT - 1) nlg &= 0x7FFFFFFFu;
   uint32_t tot;
-  uint32_t o = block_excl_scan(c, OpSum(), 0u, shs, &tot) + (has0 ? 1u : 0u);
+  uint32_t o = block_excl_scan((uint32_t)__popc(nlg), OpSum(), 0u, shs, &tot) + (has0 ? 1u : 0u);
   if (threadIdx.x == 0 && has0) ls[0] = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    uint32_t mm = m[k];
-    while (mm) {
-      const int bit = __ffs(mm) - 1;
-      if (o < cap) ls[o] = (uint16_t)(threadIdx.x * 32 + 4 * k + bit / 8 + 1);
-      ++o;
-      mm &= mm - 1;
-    }
+  for (uint32_t m = nlg; m; m &= m - 1) {  // one iteration per line start
+    if (o < cap) ls[o] = (uint16_t)(threadIdx.x * 32 + bgp_ctz(m) + 1);
+    ++o;
   }
   __syncthreads();
   return tot + (has0 ? 1u : 0u);
@@ -570,6 +561,10 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
   const int64_t PENDING = LLONG_MIN + 1;  // lkey of a line left to the byte path
   if (threadIdx.x == 0) hnl = ~0u;
   uint4 v0, v1;
+  if (threadIdx.x < 2 * ((HA + 32) / 32)) {  // halo mask words start empty (LDS atomics below)
+    if (threadIdx.x < (HA + 32) / 32) wsm[TT / 32 + threadIdx.x] = 0;
+    else dgm[TT / 32 + threadIdx.x - (HA + 32) / 32] = 0;
+  }
   stage_tile(txt, nb, t0, buf, v0, v1);
   __syncthreads();
   {  // classify this thread's 32 bytes once (SWAR), publish the masks
@@ -578,16 +573,19 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     bgp_classify8(W, ws, dg);
     wsm[threadIdx.x] = ws;
     dgm[threadIdx.x] = dg;
-    if (threadIdx.x < HA / 32 + 1) {  // the halo after the tile, from its LDS copy
-      const uint32_t* hw = reinterpret_cast<const uint32_t*>(&buf[HB + TT + 32 * threadIdx.x]);
-      const uint32_t H[8] = {hw[0], hw[1], hw[2], hw[3], hw[4], hw[5], hw[6], hw[7]};
-      bgp_classify8(H, ws, dg);
-      wsm[TT / 32 + threadIdx.x] = ws;
-      dgm[TT / 32 + threadIdx.x] = dg;
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t m = nl_mask4(H[k]);
-        if (m) { atomicMin(&hnl, TT + 32 * threadIdx.x + 4 * k + (__ffs(m) - 1) / 8); break; }
-      }
+  }
+  {  // the halo after the tile, from its LDS copy: one dword per thread (72 threads), the
+     // 4-bit groups merged into the mask words with LDS atomics
+    constexpr uint32_t HD = (HA + 32) / 4;
+    if (threadIdx.x < HD) {
+      const uint32_t x = reinterpret_cast<const uint32_t*>(&buf[HB + TT])[threadIdx.x];
+      uint32_t w4, d4;
+      bgp_classify(x, w4, d4);
+      const uint32_t sh = 4 * (threadIdx.x & 7);
+      if (w4) atomicOr(&wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
+      if (d4) atomicOr(&dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
+      const uint32_t m = nl_mask4(x);
+      if (m) atomicMin(&hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
     }
   }
   const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];  // runs in this tile

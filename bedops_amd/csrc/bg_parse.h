@@ -124,40 +124,50 @@ BG_HD void bgp_classify8(const uint32_t W[8], uint32_t& WS, uint32_t& DG) {
   }
 }
 
+// index of the lowest set bit; 0xFFFFFFFF for 0 (v_ffbl_b32 semantics)
+BG_HD uint32_t bgp_ffbl(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)(__ffs(x) - 1);
+#else
+  return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
+#endif
+}
+
 // WS/DG: class masks of the line's first 32 bytes (bit j = byte j); len: line length
 // (bytes before '\n'). returns 1: fields found; 0: undecided here (use the byte
-// path); -1: blank line
+// path); -1: blank line. Branch-free apart from the blank-line exit: every step runs and
+// one flag collects the checks (keeps the exec mask and the SGPRs out of the hot loop).
 BG_HD int bgp_fields_masks(uint32_t WS, uint32_t DG, uint32_t len, BgpFields& F) {
-  if (len < 32) {  // bytes past the line end act as whitespace
-    const uint32_t endm = ~0u << len;
-    WS |= endm;
-    DG &= ~endm;
-  }
+  const uint32_t endm = len < 32 ? (~0u << (len & 31)) : 0u;  // bytes past the line end
+  WS |= endm;                                                  // act as whitespace
+  DG &= ~endm;
   const uint32_t NW = ~WS;
   if (NW == 0) return len <= 32 ? -1 : 0;
-  F.a0 = bgp_ctz(NW);
-  uint32_t m = WS & (~0u << F.a0);
-  if (!m) return 0;
-  F.a1 = bgp_ctz(m);
-  if (F.a1 >= 31) return 0;
-  m = NW & (~0u << F.a1);
-  if (!m) return 0;
-  F.s0 = bgp_ctz(m);
-  if (!((DG >> F.s0) & 1u)) return 0;
-  m = ~DG & (~0u << F.s0);
-  if (!m) return 0;
-  F.s1 = bgp_ctz(m);
-  if (!((WS >> F.s1) & 1u) || F.s1 >= 31) return 0;
-  m = NW & (~0u << F.s1);
-  if (!m) return 0;
-  F.e0 = bgp_ctz(m);
-  if (!((DG >> F.e0) & 1u)) return 0;
-  m = ~DG & (~0u << F.e0);
-  if (!m) return 0;  // end digits may continue past the window
-  F.e1 = bgp_ctz(m);
-  if (F.s1 - F.s0 > 16 || F.e1 - F.e0 > 16) return 0;
-  if (F.e1 > len) return 0;
-  return 1;
+  const uint32_t a0 = bgp_ffbl(NW);
+  const uint32_t m1 = WS & (~0u << a0);
+  const uint32_t a1 = bgp_ffbl(m1);
+  const uint32_t m2 = NW & (~0u << (a1 & 31));
+  const uint32_t s0 = bgp_ffbl(m2);
+  const uint32_t m3 = ~DG & (~0u << (s0 & 31));
+  const uint32_t s1 = bgp_ffbl(m3);
+  const uint32_t m4 = NW & (~0u << (s1 & 31));
+  const uint32_t e0 = bgp_ffbl(m4);
+  const uint32_t m5 = ~DG & (~0u << (e0 & 31));
+  const uint32_t e1 = bgp_ffbl(m5);
+  // m1..m5 != 0 makes every index < 32
+  bool ok = (m1 != 0) & (a1 < 31) & (m2 != 0) & (m3 != 0) & (m4 != 0) & (m5 != 0);
+  ok &= ((DG >> (s0 & 31)) & 1u) != 0;   // start begins with a digit
+  ok &= ((WS >> (s1 & 31)) & 1u) != 0;   // and ends at whitespace
+  ok &= s1 < 31;
+  ok &= ((DG >> (e0 & 31)) & 1u) != 0;   // end begins with a digit (may run to the line end)
+  ok &= (s1 - s0 <= 16) & (e1 - e0 <= 16) & (e1 <= len);
+  F.a0 = a0;
+  F.a1 = a1;
+  F.s0 = s0;
+  F.s1 = s1;
+  F.e0 = e0;
+  F.e1 = e1;
+  return ok ? 1 : 0;
 }
 
 // W: bytes [0, 32) of the line
