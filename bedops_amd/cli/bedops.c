@@ -5,10 +5,10 @@
  * argv grammar follows applications/bed/bedops/src/Input.hpp:57-298 (process flags,
  * one operation, long->short option map :422-433, minimum file counts :389-420, the
  * -e/-n overlap spec :171-206 and :344-382, '-' for stdin :271-287); output and exit
- * behaviour follow Bedops.cpp:81-127. Operations on the GPU path: --merge,
- * --intersect, --difference, --element-of, --not-element-of. The
- * other operations (complement, symmdiff, everything, partition, chop) and --range
- * are reported as not available in this build instead of being approximated.
+ * behaviour follow Bedops.cpp:81-127. Every operation runs on the GPU: the hot path
+ * (--merge, --intersect, --difference, --element-of, --not-element-of; SURVEY.md
+ * §8(a)) and --complement [-L], --chop [bp] [--stagger nt] [-x], --symmdiff,
+ * --partition, --everything, with --range L:R|S padding (Input.hpp:86-127, 207-258).
  */
 #include <ctype.h>
 
@@ -28,12 +28,23 @@ static void usage(FILE* f) {
           "          --header             Accept headers (browser/track/#/@) in input files.\n"
           "          --help               Print this message and exit successfully.\n"
           "          --version            Print program information.\n\n"
-          "      Operations (GPU path): choose one of\n"
+          "          --range L:R          Add 'L' bp to all start coordinates and 'R' bp to end\n"
+          "                                 coordinates. Either value may be + or - to grow or\n"
+          "                                 shrink regions.  With the -e/-n operations, the first\n"
+          "                                 (reference) file is not padded, unlike all other files.\n"
+          "          --range S            Pad or shrink input file(s) coordinates symmetrically by S.\n"
+          "                                 This is shorthand for: --range -S:S.\n\n"
+          "      Operations: (choose one of)\n"
+          "          -c, --complement [-L] File1 [File]*\n"
           "          -d, --difference ReferenceFile File2 [File]*\n"
           "          -e, --element-of [bp | percentage] ReferenceFile File2 [File]*\n"
           "          -i, --intersect File1 File2 [File]*\n"
           "          -m, --merge File1 [File]*\n"
-          "          -n, --not-element-of [bp | percentage] ReferenceFile File2 [File]*\n",
+          "          -n, --not-element-of [bp | percentage] ReferenceFile File2 [File]*\n"
+          "          -p, --partition File1 [File]*\n"
+          "          -s, --symmdiff File1 File2 [File]*\n"
+          "          -u, --everything File1 [File]*\n"
+          "          -w, --chop [bp] [--stagger <nt>] [-x] File1 [File]*\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -96,12 +107,53 @@ static void set_subset(const char* str, double* thres, int* use_pct) {
   }
 }
 
+/* one side of --range (Input.hpp:89-111): digits and at most one '-', read like
+ * std::stringstream >> int */
+static int range_value(const char* v, const char* what) {
+  char b[256];
+  if (!*v) {
+    snprintf(b, sizeof(b), "integer expected for the '%s' value of --range L:R.", what);
+    bad_input(b);
+  }
+  if (!all_chars_in(v, "-0123456789")) {
+    snprintf(b, sizeof(b), "integer expected for the '%s' value of --range L:R.", what);
+    bad_input(b);
+  }
+  if (strchr(v, '-') != strrchr(v, '-')) {
+    snprintf(b, sizeof(b), "multiple '-' signs detected for '%s' value of --range option", what);
+    bad_input(b);
+  }
+  return atoi(v);
+}
+
+static void parse_range(const char* v, int* lpad, int* rpad) {
+  const char* colon = strchr(v, ':');
+  if (colon) {
+    char left[128];
+    size_t n = (size_t)(colon - v);
+    if (n >= sizeof(left)) n = sizeof(left) - 1;
+    memcpy(left, v, n);
+    left[n] = 0;
+    *lpad = range_value(left, "L");
+    *rpad = range_value(colon + 1, "R");
+  } else {
+    if (!all_chars_in(v, "-0123456789")) bad_input("integer value expected for --range");
+    if (strchr(v, '-') != strrchr(v, '-'))
+      bad_input("multiple '-' signs detected in <val> for --range option");
+    const int r = atoi(v);
+    *lpad = -r;
+    *rpad = r;
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc <= 1) {
     usage(stderr);
     return EXIT_FAILURE;
   }
-  int ec = 0, has_op = 0, has_chrom = 0;
+  int ec = 0, has_op = 0, has_chrom = 0, has_range = 0, lpad = 0, rpad = 0;
+  int full_left = 0, chop_x = 0;
+  long chop_bp = 1, chop_stagger = 0;
   char mode = 0;
   const char* chrom = NULL;
   double thres = 1.0;
@@ -118,7 +170,10 @@ int main(int argc, char** argv) {
       has_chrom = strcmp(chrom, "all") != 0;
       if (!has_chrom) chrom = NULL;
     } else if (!strcmp(nx, "--range")) {
-      die_msg(PROG, "--range is not available in this build (GPU path: -m -i -d -e -n)");
+      if (has_range) bad_input("--range specified multiple times.");
+      if (++a >= argc) bad_input("No value for --range given.");
+      parse_range(argv[a], &lpad, &rpad);
+      has_range = 1;
     } else if (!strcmp(nx, "--help") || !strncmp(nx, "--help-", 7)) {
       usage(stdout);
       return EXIT_SUCCESS;
@@ -155,13 +210,8 @@ int main(int argc, char** argv) {
       }
       mode = (char)tolower((unsigned char)op[1]);
       switch (mode) {
-        case 'm': minfiles = 1; break;
-        case 'i': case 'd': case 'e': case 'n': minfiles = 2; break;
-        case 'c': case 's': case 'u': case 'p': case 'w': {
-          char b[256];
-          snprintf(b, sizeof(b), "operation %s is not available in this build (GPU path: -m -i -d -e -n)", nx);
-          die_msg(PROG, b);
-        }
+        case 'm': case 'c': case 'p': case 'u': case 'w': minfiles = 1; break;
+        case 'i': case 'd': case 'e': case 'n': case 's': minfiles = 2; break;
         default: {
           char b[512];
           snprintf(b, sizeof(b), "Unknown operation: -%c", op[1]);
@@ -187,6 +237,45 @@ int main(int argc, char** argv) {
             }
           }
         }
+      } else if (mode == 'c') { /* -L (Input.hpp:207-220) */
+        int cnt = 0;
+        while (a + 1 < argc && !strcmp(argv[a + 1], "-L")) {
+          full_left = 1;
+          ++a;
+          ++cnt;
+        }
+        if (cnt > 1) bad_input("-L specified multiple times with --complement");
+      } else if (mode == 'w') { /* [bp] [--stagger nt] [-x] (Input.hpp:221-258) */
+        int cnt = 0, value_set = 0, aux_set = 0, stagger_set = 0;
+        while (a + 1 < argc) {
+          const char* q = argv[a + 1];
+          if (!strcmp(q, "--stagger")) {
+            if (stagger_set) bad_input("chop's --stagger suboption specified multiple times.");
+            if (a + 2 >= argc) bad_input("No #nt value found for --stagger suboption in --chop");
+            const char* v = argv[a + 2];
+            if (!all_chars_in(v, "1234567890"))
+              bad_input("Invalid --stagger suboption #nt value in --chop.  Expect a +integer.");
+            chop_stagger = atol(v);
+            if (chop_stagger <= 0) bad_input("nt setting for chop's --stagger suboption must be > 0");
+            stagger_set = aux_set = 1;
+            a += 2;
+          } else if (!strcmp(q, "-x")) {
+            if (chop_x) bad_input("chop's -x suboption specified multiple times.");
+            chop_x = aux_set = 1;
+            ++a;
+          } else if (all_chars_in(q, "1234567890")) {
+            if (value_set) bad_input("Stray integer found (invalid argument for --chop?)");
+            if (aux_set) bad_input("Stray integer value found: not valid for --chop");
+            chop_bp = atol(q);
+            if (chop_bp <= 0) bad_input("bp setting for chop must be > 0");
+            value_set = 1;
+            ++a;
+          } else {
+            break;
+          }
+          ++cnt;
+        }
+        if (cnt > 4) bad_input("Too many arguments for a --chop operation");
       }
     } else {
       break; /* "-" = stdin */
@@ -229,13 +318,18 @@ int main(int argc, char** argv) {
     in[i].data = tx[i].data;
     in[i].nbytes = tx[i].n;
     in[i].on_device = 0;
-    /* element-of keeps all columns of the reference file (Bedops.cpp:412-421) */
-    in[i].kind = ((mode == 'e' || mode == 'n') && i == 0) ? BG_BED3_REST : BG_BED3;
+    /* --everything keeps all columns of every file, element-of those of the reference
+     * file (Bedops.cpp:402-421) */
+    in[i].kind = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0)) ? BG_BED3_REST : BG_BED3;
   }
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);
   for (int i = 0; i < nf; ++i) free_text(&tx[i]);
   if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
+  /* --range pads every file but the element-of reference (Bedops.cpp:230-236) */
+  for (int i = 0; has_range && i < nf; ++i)
+    if (!((mode == 'e' || mode == 'n') && i == 0) && (rc = bg_set_pad(ctx, set, i, lpad, rpad)))
+      die_ctx(PROG, ctx, rc);
   int* idx = (int*)calloc((size_t)nf, sizeof(int));
   for (int i = 0; i < nf; ++i) idx[i] = i;
   bg_result* res = NULL;
@@ -245,6 +339,11 @@ int main(int argc, char** argv) {
     case 'd': rc = bg_difference(ctx, set, 0, idx + 1, nf - 1, &res); break;
     case 'e': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 0, &res); break;
     case 'n': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 1, &res); break;
+    case 'c': rc = bg_complement(ctx, set, idx, nf, full_left, &res); break;
+    case 'w': rc = bg_chop(ctx, set, idx, nf, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x, &res); break;
+    case 's': rc = bg_symmdiff(ctx, set, idx, nf, &res); break;
+    case 'p': rc = bg_partition(ctx, set, idx, nf, &res); break;
+    case 'u': rc = bg_everything(ctx, set, idx, nf, &res); break;
   }
   if (rc) die_ctx(PROG, ctx, rc);
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);

@@ -328,6 +328,7 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->s);
   bg_release(c, r->e);
   bg_release(c, r->rows);
+  bg_release(c, r->rlen);
   bg_release(c, r->cnt);
   bg_release(c, r->isum);
   bg_release(c, r->left);

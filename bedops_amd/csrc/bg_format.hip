@@ -2,7 +2,8 @@
 //
 // Replaces the reference's per-row printf calls:
 //   intervals  "%s\t%lu\t%lu\n"        record() Bedops.cpp:148-152 -> Bed.hpp:228-232
-//   rows+rest  "%s\t%lu\t%lu%s\n"      element-of, Bed.hpp:321-325 (rest = verbatim remainder)
+//   rows+rest  "%s\t%lu\t%lu%s\n"      element-of / everything, Bed.hpp:321-325 (rest = verbatim
+//                                     remainder)
 //   bedmap     "%d" / "%.{p}lf" / "NAN" joined by --delim, '\n' per ref row
 //              (MultiVisitor.hpp:83-98, CountVisitor.hpp:55-57, AverageVisitor.hpp:56-62,
 //               Formats.hpp:42-50, NaN.cpp:26)
@@ -26,6 +27,7 @@ struct FmtArgs {
   const int64_t* s;
   const int64_t* e;
   const uint64_t* rows;
+  const uint32_t* rlen;  // RES_MULTI: rows[k] = remainder address, rlen[k] its length
   const char* text;
   const uint64_t* rest_off;
   const uint32_t* rest_len;
@@ -298,6 +300,10 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
     const uint32_t rl = A.rest_len[r];
     const char* rp = A.text + A.rest_off[r];
     for (uint32_t q = 0; q < rl; ++q) o.put(rp[q]);
+  } else if (KIND == RES_MULTI) {
+    const uint32_t rl = A.rlen[k];
+    const char* rp = (const char*)A.rows[k];
+    for (uint32_t q = 0; q < rl; ++q) o.put(rp[q]);
   }
   o.put('\n');
   return true;
@@ -382,6 +388,11 @@ static void fill_args(bg_result* r, FmtArgs& A) {
   if (r->kind == RES_IVL) {
     A.s = r->s;
     A.e = r->e;
+  } else if (r->kind == RES_MULTI) {
+    A.s = r->s;
+    A.e = r->e;
+    A.rows = r->rows;
+    A.rlen = r->rlen;
   } else if (r->kind == RES_ROWS) {
     bg_table* T = s->t[r->tab];
     A.s = T->ks;
@@ -444,6 +455,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
       case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
+      case RES_MULTI: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MULTI>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
       default: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, c->dstat);
     }
     BG_HIP(c, hipGetLastError());
@@ -462,6 +474,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_MAP: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_MULTI: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MULTI>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       default: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, r->text);
     }
     BG_HIP(c, hipGetLastError());
@@ -488,7 +501,7 @@ __global__ void k_chrom_spans(FmtArgs A, const uint64_t* __restrict__ toff, uint
   uint64_t lo = 0, hi = A.n;  // first output row whose chromosome is >= g
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    const uint64_t r = A.rows ? A.rows[mid] : mid;
+    const uint64_t r = (KIND == RES_ROWS) ? A.rows[mid] : mid;
     if (A.s[r] < key) lo = mid + 1;
     else hi = mid;
   }
@@ -514,6 +527,7 @@ extern "C" int bg_result_chrom_spans(bg_ctx* c, bg_result* r, uint64_t* offsets,
     case RES_IVL: BG_SPANS(RES_IVL); break;
     case RES_ROWS: BG_SPANS(RES_ROWS); break;
     case RES_MAP: BG_SPANS(RES_MAP); break;
+    case RES_MULTI: BG_SPANS(RES_MULTI); break;
     default: BG_SPANS(RES_CLOSEST);
   }
 #undef BG_SPANS

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -96,7 +97,7 @@ struct bg_set {
   uint32_t max_name_len = 0;
 };
 
-enum { RES_IVL = 0, RES_ROWS = 1, RES_MAP = 2, RES_CLOSEST = 3 };
+enum { RES_IVL = 0, RES_ROWS = 1, RES_MAP = 2, RES_CLOSEST = 3, RES_MULTI = 4 };
 
 struct bg_result {
   bg_ctx* ctx = nullptr;
@@ -107,7 +108,10 @@ struct bg_result {
   int64_t* s = nullptr;
   int64_t* e = nullptr;
   // RES_ROWS: selected row indices of table `tab`
+  // RES_MULTI (--everything): s/e per output row, rows = device address of its verbatim
+  // remainder, rlen = remainder length
   uint64_t* rows = nullptr;
+  uint32_t* rlen = nullptr;
   int tab = -1;
   // RES_MAP: per reference row columns
   int32_t* cnt = nullptr;
@@ -162,6 +166,47 @@ int bg_scan_sum_u64(bg_ctx* c, const uint64_t* in, uint64_t* out, uint64_t n, ui
 int bg_scan_max_i64(bg_ctx* c, const int64_t* in, int64_t* out, uint64_t n, int64_t init);
 // copy one device uint64 to host (synchronises the stream)
 int bg_fetch_u64(bg_ctx* c, const uint64_t* d, uint64_t* h);
+
+// ---------------------------------------------------------------------------------
+// keyed interval lists and the shared sweep building blocks (bg_setops.hip)
+// ---------------------------------------------------------------------------------
+struct Ivl {
+  int64_t* s = nullptr;
+  int64_t* e = nullptr;
+  uint64_t n = 0;
+  bool owned = false;
+};
+void ivl_free(bg_ctx* c, Ivl& v);
+int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n);
+Ivl bg_table_ivl(bg_table* T);
+// components (maximal touching-merged pieces) of one start-sorted list / of a union
+int bg_components(bg_ctx* c, const Ivl& in, Ivl& out);
+int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out);
+bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v);
+int bg_check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf);
+int bg_compact_flags(bg_ctx* c, const uint8_t* flag, uint64_t n, uint64_t** rows, uint64_t* total);
+// stable ascending radix sort of uint64 keys with an optional uint32 payload (bg_sort.hip)
+int bg_sort_u64(bg_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n);
+
+// count pass -> scan -> allocate exact output -> write pass
+template <typename CountFn, typename WriteFn>
+static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint64_t* total) {
+  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
+  uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
+  if (!cnt || !d_tot) return BG_E_NOMEM;
+  if (nb) {
+    cf(cnt);
+    BG_HIP(c, hipGetLastError());
+  }
+  int rc = bg_scan_sum_u64(c, cnt, cnt, nb, d_tot);
+  if (rc) return rc;
+  if ((rc = bg_fetch_u64(c, d_tot, total))) return rc;
+  bg_release(c, d_tot);
+  if ((rc = wf(cnt, *total))) return rc;
+  BG_HIP(c, hipGetLastError());
+  bg_release(c, cnt);
+  return 0;
+}
 
 // ---------------------------------------------------------------------------------
 // device helpers

@@ -372,19 +372,12 @@ __global__ void __launch_bounds__(BG_NT) k_compact_flags(const uint8_t* __restri
 // =====================================================================================
 // host drivers
 // =====================================================================================
-struct Ivl {
-  int64_t* s = nullptr;
-  int64_t* e = nullptr;
-  uint64_t n = 0;
-  bool owned = false;
-};
-
-static void ivl_free(bg_ctx* c, Ivl& v) {
+void ivl_free(bg_ctx* c, Ivl& v) {
   if (v.owned) { bg_release(c, v.s); bg_release(c, v.e); }
   v = Ivl();
 }
 
-static int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
+int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
   v.n = n;
   v.s = (int64_t*)bg_alloc(c, 8 * (n ? n : 1));
   v.e = (int64_t*)bg_alloc(c, 8 * (n ? n : 1));
@@ -392,27 +385,28 @@ static int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
   return (v.s && v.e) ? 0 : BG_E_NOMEM;
 }
 
-// count pass -> scan -> allocate exact output -> write pass
-template <typename CountFn, typename WriteFn>
-static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint64_t* total) {
-  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
-  uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
-  if (!cnt || !d_tot) return BG_E_NOMEM;
-  if (nb) {
-    cf(cnt);
-    BG_HIP(c, hipGetLastError());
-  }
-  int rc = bg_scan_sum_u64(c, cnt, cnt, nb, d_tot);
-  if (rc) return rc;
-  if ((rc = bg_fetch_u64(c, d_tot, total))) return rc;
-  bg_release(c, d_tot);
-  if ((rc = wf(cnt, *total))) return rc;
-  BG_HIP(c, hipGetLastError());
-  bg_release(c, cnt);
-  return 0;
+// indices i with flag[i] != 0, in order (count -> scan -> write)
+int bg_compact_flags(bg_ctx* c, const uint8_t* flag, uint64_t n, uint64_t** rows, uint64_t* total) {
+  const unsigned nb = bg_blocks(n, CF_TILE);
+  *rows = nullptr;
+  return count_scan_write(
+      c, nb,
+      [&](uint64_t* cnt) {
+        BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag,
+                  n, cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
+      },
+      [&](uint64_t* off, uint64_t tot) -> int {
+        *rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
+        if (!*rows) return BG_E_NOMEM;
+        if (nb)
+          BG_LAUNCH(c, "k_compact_flags_write", k_compact_flags<true>, dim3(nb), dim3(BG_NT), flag,
+                    n, (uint64_t*)nullptr, off, *rows);
+        return 0;
+      },
+      total);
 }
 
-static int components(bg_ctx* c, const Ivl& in, Ivl& out) {
+int bg_components(bg_ctx* c, const Ivl& in, Ivl& out) {
   const uint64_t n = in.n;
   if (n == 0) return ivl_alloc(c, out, 0);
   const unsigned nb = bg_blocks(n, CT_TILE);
@@ -484,7 +478,7 @@ static int mp_op(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out, const char* cn
   return rc;
 }
 
-static Ivl table_ivl(bg_table* T) {
+Ivl bg_table_ivl(bg_table* T) {
   Ivl v;
   v.s = T->ks;
   v.e = T->ke;
@@ -494,17 +488,17 @@ static Ivl table_ivl(bg_table* T) {
 }
 
 // components of the union of the given tables
-static int union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out) {
+int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out) {
   Ivl acc;
-  int rc = components(c, table_ivl(set->t[files[0]]), acc);
+  int rc = bg_components(c, bg_table_ivl(set->t[files[0]]), acc);
   if (rc) return rc;
   for (int k = 1; k < nf; ++k) {
     Ivl ck, z, m;
-    if ((rc = components(c, table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = bg_components(c, bg_table_ivl(set->t[files[k]]), ck))) return rc;
     if ((rc = merge_sorted(c, acc, ck, z))) return rc;
     ivl_free(c, acc);
     ivl_free(c, ck);
-    if ((rc = components(c, z, m))) return rc;
+    if ((rc = bg_components(c, z, m))) return rc;
     ivl_free(c, z);
     acc = m;
   }
@@ -512,7 +506,7 @@ static int union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Iv
   return 0;
 }
 
-static bg_result* new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
+bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
   bg_result* r = new bg_result();
   r->ctx = c;
   r->set = set;
@@ -524,7 +518,7 @@ static bg_result* new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
   return r;
 }
 
-static int check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf) {
+int bg_check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf) {
   if (!c || !set || !files || nf < minf) return BG_E_ARG;
   for (int k = 0; k < nf; ++k)
     if (files[k] < 0 || files[k] >= (int)set->t.size()) return BG_E_ARG;
@@ -532,17 +526,17 @@ static int check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int min
 }
 
 extern "C" int bg_merge(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
-  int rc = check_files(c, set, files, nf, 1);
+  int rc = bg_check_files(c, set, files, nf, 1);
   if (rc) return rc;
   Ivl m;
-  if ((rc = union_components(c, set, files, nf, m))) return rc;
-  *out = new_ivl_result(c, set, m);
+  if ((rc = bg_union_components(c, set, files, nf, m))) return rc;
+  *out = bg_new_ivl_result(c, set, m);
   bg_mark(c, "merge");
   return 0;
 }
 
 extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
-  int rc = check_files(c, set, files, nf, 2);
+  int rc = bg_check_files(c, set, files, nf, 2);
   if (rc) return rc;
   // Zero-length rows (end == start; rejected by the reference's own --ec checker,
   // BedCheckIterator.hpp:619-620) make nextIntersectLine's output depend on its
@@ -555,44 +549,44 @@ extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg
                      "the GPU path (BEDOPS --ec rejects them: End coordinates must be greater "
                      "than start coordinates)");
   Ivl acc;
-  if ((rc = components(c, table_ivl(set->t[files[0]]), acc))) return rc;
+  if ((rc = bg_components(c, bg_table_ivl(set->t[files[0]]), acc))) return rc;
   for (int k = 1; k < nf; ++k) {
     Ivl ck, p;
-    if ((rc = components(c, table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = bg_components(c, bg_table_ivl(set->t[files[k]]), ck))) return rc;
     if ((rc = mp_op<MP_INTERSECT>(c, acc, ck, p, "k_intersect_count", "k_intersect_write"))) return rc;
     ivl_free(c, acc);
     ivl_free(c, ck);
     acc = p;
   }
-  *out = new_ivl_result(c, set, acc);
+  *out = bg_new_ivl_result(c, set, acc);
   bg_mark(c, "intersect");
   return 0;
 }
 
 extern "C" int bg_difference(bg_ctx* c, bg_set* set, int ref, const int* others, int no,
                              bg_result** out) {
-  int rc = check_files(c, set, others, no, 1);
+  int rc = bg_check_files(c, set, others, no, 1);
   if (rc) return rc;
   if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
   Ivl r, o, d;
-  if ((rc = components(c, table_ivl(set->t[ref]), r))) return rc;
-  if ((rc = union_components(c, set, others, no, o))) return rc;
+  if ((rc = bg_components(c, bg_table_ivl(set->t[ref]), r))) return rc;
+  if ((rc = bg_union_components(c, set, others, no, o))) return rc;
   if ((rc = mp_op<MP_DIFFERENCE>(c, r, o, d, "k_difference_count", "k_difference_write"))) return rc;
   ivl_free(c, r);
   ivl_free(c, o);
-  *out = new_ivl_result(c, set, d);
+  *out = bg_new_ivl_result(c, set, d);
   bg_mark(c, "difference");
   return 0;
 }
 
 extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others, int no,
                              double thres, int use_pct, int invert, bg_result** out) {
-  int rc = check_files(c, set, others, no, 1);
+  int rc = bg_check_files(c, set, others, no, 1);
   if (rc) return rc;
   if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
   bg_table* R = set->t[ref];
   Ivl o;
-  if ((rc = union_components(c, set, others, no, o))) return rc;
+  if ((rc = bg_union_components(c, set, others, no, o))) return rc;
   uint64_t* P = (uint64_t*)bg_alloc(c, 8 * (o.n + 1));
   uint8_t* flag = (uint8_t*)bg_alloc(c, R->n ? R->n : 1);
   if (!P || !flag) return BG_E_NOMEM;
@@ -606,24 +600,9 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
               R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
     BG_HIP(c, hipGetLastError());
   }
-  const unsigned nb = bg_blocks(R->n, CF_TILE);
   uint64_t total = 0;
   uint64_t* rows = nullptr;
-  rc = count_scan_write(
-      c, nb,
-      [&](uint64_t* cnt) {
-        BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag,
-                  R->n, cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr);
-      },
-      [&](uint64_t* off, uint64_t tot) -> int {
-        rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
-        if (!rows) return BG_E_NOMEM;
-        if (nb)
-          BG_LAUNCH(c, "k_compact_flags_write", k_compact_flags<true>, dim3(nb), dim3(BG_NT), flag,
-                    R->n, (uint64_t*)nullptr, off, rows);
-        return 0;
-      },
-      &total);
+  rc = bg_compact_flags(c, flag, R->n, &rows, &total);
   if (rc) return rc;
   bg_release(c, P);
   bg_release(c, flag);

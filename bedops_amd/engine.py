@@ -23,7 +23,8 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_result_text_device", "bg_result_copy_text", "bg_result_write", "bg_result_free",
            "bg_stats", "bg_host_alloc", "bg_host_free", "bg_prof_enable", "bg_prof_read",
            "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
-           "bg_set_chrom_name", "bg_closest"]
+           "bg_set_chrom_name", "bg_closest", "bg_complement", "bg_chop", "bg_partition",
+           "bg_symmdiff", "bg_everything", "bg_set_pad"]
 
 
 def lib_path():
@@ -86,6 +87,11 @@ def load_library():
     L.bg_difference.argtypes = [vp, vp, i32, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
     L.bg_element_of.argtypes = [vp, vp, i32, ctypes.POINTER(i32), i32, ctypes.c_double, i32,
                                 i32, ctypes.POINTER(vp)]
+    L.bg_complement.argtypes = [vp, vp, ctypes.POINTER(i32), i32, i32, ctypes.POINTER(vp)]
+    L.bg_chop.argtypes = [vp, vp, ctypes.POINTER(i32), i32, u64, u64, i32, ctypes.POINTER(vp)]
+    for fn in (L.bg_partition, L.bg_symmdiff, L.bg_everything):
+        fn.argtypes = [vp, vp, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.bg_set_pad.argtypes = [vp, vp, i32, i32, i32]
     L.bg_map.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_MapOpts), ctypes.POINTER(vp)]
     L.bg_closest.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_ClosestOpts), ctypes.POINTER(vp)]
     L.bg_result_rows.argtypes = [vp, ctypes.POINTER(u64)]
@@ -190,6 +196,10 @@ class InputSet:
     def restrict_chrom(self, chrom):
         self.eng._check(self.eng.L.bg_set_restrict_chrom(self.eng.ctx, self.h, chrom.encode()))
 
+    def pad(self, i, lpad, rpad):
+        """--range lpad:rpad applied to file i (BedPadReader.hpp:71-284)"""
+        self.eng._check(self.eng.L.bg_set_pad(self.eng.ctx, self.h, i, int(lpad), int(rpad)))
+
     def free(self):
         if self.h:
             self.eng.L.bg_set_free(self.h)
@@ -247,8 +257,9 @@ class Engine:
         return InputSet(self, h, keep)
 
     # -------------------------------------------------------------- bedops
-    def op(self, mode, s, files, spec=None):
-        """Run one bedops operation on loaded set `s` over file indices `files`."""
+    def op(self, mode, s, files, spec=None, full_left=False, chop=(1, 0, False)):
+        """Run one bedops operation on loaded set `s` over file indices `files`.
+        spec: -e/-n overlap; full_left: --complement -L; chop: (bp, stagger, -x)."""
         h = ctypes.c_void_p()
         idx = (ctypes.c_int * len(files))(*files)
         L = self.L
@@ -266,19 +277,39 @@ class Engine:
             rest = (ctypes.c_int * (len(files) - 1))(*files[1:])
             self._check(L.bg_element_of(self.ctx, s.h, files[0], rest, len(files) - 1, thr, pct,
                                         inv, ctypes.byref(h)))
+        elif mode in ("-c", "--complement"):
+            self._check(L.bg_complement(self.ctx, s.h, idx, len(files), int(bool(full_left)),
+                                        ctypes.byref(h)))
+        elif mode in ("-w", "--chop"):
+            bp, stagger, x = chop
+            self._check(L.bg_chop(self.ctx, s.h, idx, len(files), int(bp), int(stagger),
+                                  int(bool(x)), ctypes.byref(h)))
+        elif mode in ("-p", "--partition"):
+            self._check(L.bg_partition(self.ctx, s.h, idx, len(files), ctypes.byref(h)))
+        elif mode in ("-s", "--symmdiff"):
+            self._check(L.bg_symmdiff(self.ctx, s.h, idx, len(files), ctypes.byref(h)))
+        elif mode in ("-u", "--everything"):
+            self._check(L.bg_everything(self.ctx, s.h, idx, len(files), ctypes.byref(h)))
         else:
-            raise BedgpuError(-8, f"operation {mode} is not on the GPU path")
+            raise BedgpuError(-6, f"unknown operation {mode}")
         return Result(self, h)
 
-    def bedops(self, mode, texts, spec=None, chrom=None):
-        """bedops <mode> [spec] file1 file2 ... on in-memory BED texts -> output bytes."""
-        keep_rest = mode in ("-e", "--element-of", "-n", "--not-element-of")
-        s = self.load([(t, BED3_REST if (keep_rest and i == 0) else BED3)
+    def bedops(self, mode, texts, spec=None, chrom=None, pad=None, full_left=False,
+               chop=(1, 0, False)):
+        """bedops [--chrom C] [--range L:R] <mode> [spec] file1 file2 ... on in-memory BED
+        texts -> output bytes. pad = (lpad, rpad)."""
+        eo = mode in ("-e", "--element-of", "-n", "--not-element-of")
+        every = mode in ("-u", "--everything")
+        s = self.load([(t, BED3_REST if (every or (eo and i == 0)) else BED3)
                        for i, t in enumerate(texts)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)
-            r = self.op(mode, s, list(range(len(texts))), spec)
+            if pad is not None:
+                for i in range(len(texts)):
+                    if not (eo and i == 0):
+                        s.pad(i, pad[0], pad[1])
+            r = self.op(mode, s, list(range(len(texts))), spec, full_left, chop)
             try:
                 return r.text()
             finally:

@@ -14,6 +14,12 @@
  *   bg_intersect ......... doIntersection / nextIntersectLine (Bedops.cpp:575-587, :1105-1181)
  *   bg_difference ........ doDifference / nextDifferenceLine (Bedops.cpp:500-524, :950-1018)
  *   bg_element_of ........ doElementOf / nextElementOfLine (Bedops.cpp:538-566, :1023-1100)
+ *   bg_complement ........ doComplement / nextComplementLine (Bedops.cpp:475-489, :891-945)
+ *   bg_chop .............. doChop (Bedops.cpp:437-467)
+ *   bg_partition ......... doPartitions / nextPartitionGroup (Bedops.cpp:614-686, :1249-1337)
+ *   bg_symmdiff .......... doSymmetricDifference / nextSymmetricDiffLine (Bedops.cpp:697-747, :1343-1467)
+ *   bg_everything ........ doUnionAll / nextUnionAllLine (Bedops.cpp:752-786, :1472-1518)
+ *   bg_set_pad ........... BedPadReader --range padding (applications/bed/bedops/src/BedPadReader.hpp:71-284)
  *   bg_map ............... WindowSweep::sweep overload 2 + MultiVisitor{Count,Average}
  *                          (interfaces/src/algorithm/sweep/WindowSweepImpl.cpp:168-256,
  *                           algorithm/visitors/other/MultiVisitor.hpp:45-129)
@@ -106,6 +112,18 @@ int bg_difference(bg_ctx* ctx, bg_set* set, int ref, const int* others, int noth
                   bg_result** out);
 int bg_element_of(bg_ctx* ctx, bg_set* set, int ref, const int* others, int nothers,
                   double threshold, int use_percent, int invert, bg_result** out);
+/* --complement [-L]: gaps between the union's components (full_left: also from base 0) */
+int bg_complement(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, int full_left,
+                  bg_result** out);
+/* --chop chunk [--stagger n] [-x]: pieces of the union's components (stagger 0 = chunk) */
+int bg_chop(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, uint64_t chunk,
+            uint64_t stagger, int exclude_short, bg_result** out);
+int bg_partition(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
+int bg_symmdiff(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
+/* --everything: every row of every file (all loaded as BG_BED3_REST), merged in order */
+int bg_everything(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
+/* --range L:R applied to one loaded file (in place; before the operation) */
+int bg_set_pad(bg_ctx* ctx, bg_set* set, int file, int lpad, int rpad);
 int bg_map(bg_ctx* ctx, bg_set* set, int ref, int map, const bg_map_opts* opts,
            bg_result** out);
 /* closest-features <input-file> <query-file>: `ref` = the <input-file> table, `query` =

@@ -12,9 +12,10 @@ def _h(b):
 
 
 def test_testplan_kats_oracle(oracle_bin, tmp_path):
-    res = testplan_runner.run_testplan([oracle_bin["bedops"]], str(tmp_path),
-                                       modes={"m", "i", "d", "e", "n"})
-    assert len(res) == 28
+    """All 63 KATs: the hot-path modes and complement/chop/symmdiff/partition/everything
+    with --range, --chrom and -L."""
+    res = testplan_runner.run_testplan([oracle_bin["bedops"]], str(tmp_path))
+    assert len(res) == 63
     bad = [r for r in res if not r[2]]
     assert not bad, bad
 
