@@ -309,26 +309,35 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
   return true;
 }
 
+// bytes of every FT_TILE-row tile: one wave per tile (rows striped over the lanes, 64-lane
+// shuffle reduction), FC_TILES tiles per workgroup, no workgroup barrier
+#define FC_TILES 8
 template <int KIND>
 __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __restrict__ tb,
-                                                     bg_dstatus* st) {
-  __shared__ uint64_t sh[BG_NT / 64 + 1];
-  const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + threadIdx.x;  // rows striped
-  CountOut co;
-  for (int k = 0; k < FT_ROWS; ++k) {
-    const uint64_t row = base + (uint64_t)k * BG_NT;
-    if (row < A.n && !render<KIND>(A, row, co)) bg_report(st, row, ERR_RANGE);
+                                                     uint64_t ntiles, bg_dstatus* st) {
+  const int lane = bg_lane();
+  for (uint64_t t = (uint64_t)blockIdx.x * FC_TILES + bg_wave(); t < (uint64_t)(blockIdx.x + 1) * FC_TILES;
+       t += BG_NT / 64) {
+    if (t >= ntiles) return;
+    CountOut co;
+    const uint64_t base = t * FT_TILE + lane;
+#pragma unroll 2
+    for (int k = 0; k < FT_TILE / 64; ++k) {
+      const uint64_t row = base + (uint64_t)k * 64;
+      if (row < A.n && !render<KIND>(A, row, co)) bg_report(st, row, ERR_RANGE);
+    }
+    uint64_t v = co.n;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane == 0) tb[t] = v;
   }
-  uint64_t tot;
-  (void)block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &tot);
-  if (threadIdx.x == 0) tb[blockIdx.x] = tot;
 }
 
 template <int KIND>
 __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* __restrict__ toff,
                                                      char* __restrict__ out) {
   __shared__ uint64_t sh[BG_NT / 64 + 1];
-  __shared__ __attribute__((aligned(16))) char buf[FT_LDS];
+  __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
   // rows are striped over the threads (coalesced column reads); a row's byte offset
   // in the tile = all bytes of the previous stripes + its prefix inside its stripe
   const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + threadIdx.x;
@@ -351,30 +360,27 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
     }
     return;
   }
+  // stage with the same alignment mod 16 as the destination, so every aligned 16-byte
+  // chunk of the output is one aligned 16-byte LDS read
+  const uint32_t skew = (uint32_t)(dst0 & 15);
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
-    LdsOut o{buf + my[k]};
+    LdsOut o{buf + skew + my[k]};
     if (row < A.n) render<KIND>(A, row, o);
   }
   __syncthreads();
-  // stream buf[0, tot) -> out[dst0, dst0 + tot)
+  // stream buf[skew, skew + tot) -> out[dst0, dst0 + tot)
   const uint64_t a0 = dst0, a1 = dst0 + tot;
   const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;
+  const char* bb = buf + skew;
   if (al0 >= al1) {
-    for (uint64_t p = a0 + threadIdx.x; p < a1; p += BG_NT) out[p] = buf[p - a0];
+    for (uint64_t p = a0 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
     return;
   }
-  for (uint64_t p = a0 + threadIdx.x; p < al0; p += BG_NT) out[p] = buf[p - a0];
-  for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = buf[p - a0];
-  for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT) {
-    const char* src = buf + (p - a0);
-    uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      w[q] = (uint32_t)(uint8_t)src[4 * q] | ((uint32_t)(uint8_t)src[4 * q + 1] << 8) |
-             ((uint32_t)(uint8_t)src[4 * q + 2] << 16) | ((uint32_t)(uint8_t)src[4 * q + 3] << 24);
-    *reinterpret_cast<uint4*>(out + p) = make_uint4(w[0], w[1], w[2], w[3]);
-  }
+  for (uint64_t p = a0 + threadIdx.x; p < al0; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT)
+    *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
 }
 
 static void fill_args(bg_result* r, FmtArgs& A) {
@@ -446,17 +452,18 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   FmtArgs A;
   fill_args(r, A);
   const unsigned nb = bg_blocks(r->n, FT_TILE);
+  const unsigned nbc = bg_blocks(nb, FC_TILES);
   uint64_t* tb = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
   uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
   if (!tb || !d_tot) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   if (nb) {
     switch (A.kind) {
-      case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
-      case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
-      case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
-      case RES_MULTI: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MULTI>, dim3(nb), dim3(BG_NT), A, tb, c->dstat); break;
-      default: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, c->dstat);
+      case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_IVL>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      case RES_MULTI: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MULTI>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      default: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_CLOSEST>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat);
     }
     BG_HIP(c, hipGetLastError());
   }
