@@ -217,7 +217,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # a first collective over every rank initialises the RCCL communicator, so the
+        # later batched point-to-point transfers may involve only a subset of the ranks
+        dist.barrier(device_ids=[local])
     dev = torch.device("cuda", local)
 
     from bedops_amd import Engine
