@@ -319,8 +319,12 @@ int main(int argc, char** argv) {
     in[i].nbytes = tx[i].n;
     in[i].on_device = 0;
     /* --everything keeps all columns of every file, element-of those of the reference
-     * file (Bedops.cpp:402-421) */
-    in[i].kind = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0)) ? BG_BED3_REST : BG_BED3;
+     * file (Bedops.cpp:402-421); the other inputs of the set operations are read only as
+     * merged sets (getNextFileMergedCoords, Bedops.cpp:792-814), so they are parsed
+     * straight to their components unless --chrom/--range need the rows */
+    in[i].kind = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0)) ? BG_BED3_REST
+                 : (strchr("midencws", mode) && !chrom && !has_range && !env_no_set()) ? BG_BED3_SET
+                                                                                       : BG_BED3;
   }
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);

@@ -113,6 +113,13 @@ static int env_device(void) {
   return d ? atoi(d) : 0;
 }
 
+/* BEDGPU_SET=0: load every plain input with its row columns (BG_BED3) instead of
+ * straight to its merged set (BG_BED3_SET); same output, for A/B checks */
+static inline int env_no_set(void) {
+  const char* s = getenv("BEDGPU_SET");
+  return s && strcmp(s, "0") == 0;
+}
+
 static void maybe_stats(bg_ctx* ctx) {
   const char* s = getenv("BEDGPU_STATS");
   if (!s || !*s || strcmp(s, "0") == 0) return;

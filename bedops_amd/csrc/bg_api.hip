@@ -162,6 +162,8 @@ extern "C" int bg_open(bg_ctx** out, int device) {
     delete c;
     return BG_E_HIP;
   }
+  if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    c->ncu = 256;
   const char* st = getenv("BEDGPU_STATS");
   c->stats = st && *st && strcmp(st, "0") != 0;
   bg_mark(c, "open");
@@ -182,6 +184,17 @@ extern "C" void bg_close(bg_ctx* c) {
   hipHostFree(c->hstat);
   hipStreamDestroy(c->stream);
   delete c;
+}
+
+uint32_t bg_resident_blocks(bg_ctx* c, const void* kern) {
+  for (auto& kv : c->resident)
+    if (kv.first == kern) return kv.second;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BG_NT, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const uint32_t n = (uint32_t)per_cu * (uint32_t)c->ncu;
+  c->resident.push_back({kern, n});
+  return n;
 }
 
 extern "C" const char* bg_last_error(const bg_ctx* c) { return c ? c->err.c_str() : "no context"; }
@@ -211,6 +224,8 @@ extern "C" int bg_stats(const bg_ctx* cc, char* buf, uint64_t cap) {
 
 extern "C" int bg_set_restrict_chrom(bg_ctx* c, bg_set* s, const char* chrom) {
   if (!c || !s || !chrom) return BG_E_ARG;
+  for (bg_table* T : s->t)
+    if (T->is_set) return bg_fail(c, BG_E_ARG, "--chrom: an input was loaded as BG_BED3_SET (no rows kept)");
   for (bg_table* T : s->t) {
     uint64_t a = 0, b = 0;
     for (size_t k = 0; k + 1 < T->run_row0.size(); ++k)

@@ -350,6 +350,11 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
       query >= (int)set->t.size())
     return BG_E_ARG;
   *out = nullptr;
+  {
+    const int f[2] = {ref, query};
+    int rc0 = bg_need_rows(c, set, f, 2, "closest-features");
+    if (rc0) return rc0;
+  }
   bg_table* Q = set->t[ref];
   bg_table* C = set->t[query];
   if (!Q->rest_off || !C->rest_off)

@@ -47,6 +47,8 @@ struct bg_buf {
 
 struct bg_ctx {
   int device = 0;
+  int ncu = 256;  // compute units
+  std::vector<std::pair<const void*, uint32_t>> resident;  // kernel -> resident BG_NT blocks
   hipStream_t stream = nullptr;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
@@ -82,6 +84,11 @@ struct bg_table {
   bool score_int = true;     // every score is an integer (exact sums)
   bool has_zero_len = false; // some row has end == start
   int64_t maxlen = 0;        // max (end - start) over the rows (window bound for sweeps)
+  // BG_BED3_SET: the file's merged set only (ks/ke stay null)
+  bool is_set = false;
+  int64_t* cs = nullptr;
+  int64_t* ce = nullptr;
+  uint64_t nc = 0;
   // chromosome runs (host, sorted by row): rows [row0[k], row0[k+1]) are chrom names[k]
   std::vector<uint64_t> run_row0;
   std::vector<std::string> run_name;
@@ -128,6 +135,10 @@ struct bg_result {
   bool formatted = false;
   uint64_t* toff = nullptr;  // byte offset of each 1024-row format tile (kept for spans)
 };
+
+// workgroups of BG_NT threads of `kern` resident on the whole device at once (persistent
+// grid size; occupancy query x compute units, cached per kernel)
+uint32_t bg_resident_blocks(bg_ctx* c, const void* kern);
 
 // allocator / error helpers (bg_api.cpp)
 void* bg_alloc(bg_ctx* c, size_t bytes);
@@ -179,6 +190,10 @@ struct Ivl {
 void ivl_free(bg_ctx* c, Ivl& v);
 int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n);
 Ivl bg_table_ivl(bg_table* T);
+// the components of one table: a view of a BG_BED3_SET table's set, computed otherwise
+int bg_table_components(bg_ctx* c, bg_table* T, Ivl& out);
+// BG_E_ARG unless every listed table keeps its rows (not BG_BED3_SET)
+int bg_need_rows(bg_ctx* c, bg_set* set, const int* files, int nf, const char* what);
 // components (maximal touching-merged pieces) of one start-sorted list / of a union
 int bg_components(bg_ctx* c, const Ivl& in, Ivl& out);
 int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out);
@@ -240,6 +255,22 @@ struct OpMin {
   template <typename T>
   __device__ __forceinline__ T operator()(T a, T b) const { return a < b ? a : b; }
 };
+
+// DPP form of the most common scan (u32 sums: line starts, counts): row_shr 1/2/4/8 within
+// 16-lane rows, row_bcast 15/31 across them; lanes with no source read 0
+template <int CTRL, int RMASK, bool BC>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RMASK, 0xF, BC);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, OpSum) {
+  v += dpp32<0x111, 0xF, true>(v);
+  v += dpp32<0x112, 0xF, true>(v);
+  v += dpp32<0x114, 0xF, true>(v);
+  v += dpp32<0x118, 0xF, true>(v);
+  v += dpp32<0x142, 0xA, false>(v);
+  v += dpp32<0x143, 0xC, false>(v);
+  return v;
+}
 
 static inline int bg_hip_ok(bg_ctx* c, hipError_t e) {
   return e == hipSuccess ? 0 : bg_hip_fail(c, e, "HIP runtime call");

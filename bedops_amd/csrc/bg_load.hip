@@ -69,19 +69,35 @@ struct TileText {
   }
 };
 
+// A tile's bytes as registers: v0/v1 = this thread's 32 tile bytes, vh = one 16-byte
+// piece of the halos (threads < (HA+32)/16: after the tile; the last thread: before it)
+struct TileRegs {
+  uint4 v0, v1, vh;
+};
+__device__ __forceinline__ void load_tile(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
+                                          TileRegs& R) {
+  const int64_t b = t0 + (int64_t)threadIdx.x * 32;
+  R.v0 = load16(txt, b, nb);
+  R.v1 = load16(txt, b + 16, nb);
+  if (threadIdx.x < (HA + 32) / 16) R.vh = load16(txt, t0 + TT + (int64_t)threadIdx.x * 16, nb);
+  else if (threadIdx.x == BG_NT - 1) R.vh = load16(txt, t0 - HB, nb);
+}
+// [t0-HB, t0+TT+HA) into LDS (zeros outside the text)
+__device__ __forceinline__ void store_tile(uint8_t* buf, const TileRegs& R) {
+  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32]) = R.v0;
+  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32 + 16]) = R.v1;
+  if (threadIdx.x < (HA + 32) / 16) *reinterpret_cast<uint4*>(&buf[HB + TT + threadIdx.x * 16]) = R.vh;
+  else if (threadIdx.x == BG_NT - 1) *reinterpret_cast<uint4*>(&buf[0]) = R.vh;
+}
 // Stage [t0-HB, t0+TT+HA) into LDS (zeros outside the text). Each thread also returns
 // its 32 tile bytes in registers.
 __device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ txt, uint64_t nb,
                                            int64_t t0, uint8_t* buf, uint4& v0, uint4& v1) {
-  const int64_t b = t0 + (int64_t)threadIdx.x * 32;
-  v0 = load16(txt, b, nb);
-  v1 = load16(txt, b + 16, nb);
-  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32]) = v0;
-  *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * 32 + 16]) = v1;
-  if (threadIdx.x < (HA + 32) / 16)
-    *reinterpret_cast<uint4*>(&buf[HB + TT + threadIdx.x * 16]) =
-        load16(txt, t0 + TT + (int64_t)threadIdx.x * 16, nb);
-  if (threadIdx.x == BG_NT - 1) *reinterpret_cast<uint4*>(&buf[0]) = load16(txt, t0 - HB, nb);
+  TileRegs R;
+  load_tile(txt, nb, t0, R);
+  store_tile(buf, R);
+  v0 = R.v0;
+  v1 = R.v1;
 }
 
 // token [tok, tok+len) of the line starting at p (leading ws skipped, stops at ws or
@@ -157,16 +173,35 @@ __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt
 }
 
 // first owned line of each tile and the hash of its chromosome token (one thread per
-// tile, reads a few bytes)
+// tile, reads a few bytes). fnl: first '\n' per tile from k_scout, or nullptr: found here
+// by a forward scan (BG_BED3_SET loads have no scout pass)
 __global__ void k_tokhash(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
                           const uint32_t* __restrict__ fnl, int64_t* __restrict__ fls,
                           uint64_t* __restrict__ fhash) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
   const int64_t t0 = (int64_t)t * TT;
+  uint32_t f = TT;
+  if (fnl) {
+    f = fnl[t];
+  } else {
+    const int64_t te = min((int64_t)nb, t0 + TT);
+    for (int64_t q = t0; q < te; q += 16) {
+      const uint4 v = load16(txt, q, nb);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint32_t hit = TT;
+#pragma unroll
+      for (int k = 3; k >= 0; --k) {
+        const uint32_t m = nl_mask4(w[k]);
+        if (m) hit = (uint32_t)(q - t0) + 4 * k + (__ffs(m) - 1) / 8;
+      }
+      if (hit < TT) { f = hit; break; }
+    }
+    if (f >= (uint32_t)(te - t0)) f = TT;
+  }
   int64_t ls = -1;
   if (t0 == 0 || txt[t0 - 1] == '\n') ls = t0;
-  else if (fnl[t] + 1 < TT) ls = t0 + fnl[t] + 1;
+  else if (f + 1 < TT) ls = t0 + f + 1;
   if (ls >= 0 && (uint64_t)ls >= nb) ls = -1;
   uint64_t h = 0;
   if (ls >= 0) {
@@ -544,63 +579,110 @@ __device__ __forceinline__ void emit_row(const RunTable& R, uint32_t run, int64_
   KE[r] = g | (int64_t)(end & BG_COORD_MASK);
 }
 
+// one tile staged in LDS with its class bitmaps
+struct ParseBuf {
+  __attribute__((aligned(16))) uint8_t buf[LBUF];
+  uint32_t wsm[TT / 32 + HA / 32 + 1];  // class bitmaps: bit = byte
+  uint32_t dgm[TT / 32 + HA / 32 + 1];
+  uint32_t hnl;  // first '\n' in the halo after the tile (local offset)
+};
+// shared LDS of the parse kernels (NB staged tiles)
+template <int NB>
+struct ParseLdsT {
+  ParseBuf b[NB];
+  uint16_t lst[LCAP + 1];
+  uint32_t shs[BG_NT / 64 + 1];
+};
+
+// the halo words of B's bitmaps start empty (LDS atomics in prologue_core), hnl unset
+__device__ __forceinline__ void clear_halo(ParseBuf& B) {
+  if (threadIdx.x == 0) B.hnl = ~0u;
+  if (threadIdx.x < 2 * ((HA + 32) / 32)) {
+    if (threadIdx.x < (HA + 32) / 32) B.wsm[TT / 32 + threadIdx.x] = 0;
+    else B.dgm[TT / 32 + threadIdx.x - (HA + 32) / 32] = 0;
+  }
+}
+
+// One tile's prologue once its bytes are in B.buf (and visible to every wave) and its
+// halo words cleared: class bitmaps, line starts. v0/v1 = this thread's 32 tile bytes.
+// Returns the number of owned lines L (> LCAP: error reported, caller returns); r0 = row
+// of the first owned line; last_end = '\n' position ending the tile's last line.
+__device__ __forceinline__ uint32_t prologue_core(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                  const uint64_t* __restrict__ row0, int64_t t0,
+                                                  uint32_t tile, ParseBuf& B, uint16_t* lst,
+                                                  uint32_t* shs, uint4 v0, uint4 v1, uint64_t& r0,
+                                                  int64_t& last_end, bg_dstatus* st) {
+  {  // classify this thread's 32 bytes once (SWAR), publish the masks
+    const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t ws, dg;
+    bgp_classify8(W, ws, dg);
+    B.wsm[threadIdx.x] = ws;
+    B.dgm[threadIdx.x] = dg;
+  }
+  {  // the halo after the tile, from its LDS copy: one dword per thread (72 threads), the
+     // 4-bit groups merged into the mask words with LDS atomics
+    constexpr uint32_t HD = (HA + 32) / 4;
+    if (threadIdx.x < HD) {
+      const uint32_t x = reinterpret_cast<const uint32_t*>(&B.buf[HB + TT])[threadIdx.x];
+      uint32_t w4, d4;
+      bgp_classify(x, w4, d4);
+      const uint32_t sh = 4 * (threadIdx.x & 7);
+      if (w4) atomicOr(&B.wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
+      if (d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
+      const uint32_t m = nl_mask4(x);
+      if (m) atomicMin(&B.hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
+    }
+  }
+  bool has0;
+  const uint32_t L = tile_line_starts(v0, v1, B.buf, t0, lst, LCAP + 1, shs, has0);
+  r0 = (row0 ? row0[tile] : 0) + (has0 ? 0 : 1);  // row of the first owned line (if known)
+  if (L > LCAP) {  // > LCAP lines in 8 KiB: some line is shorter than any valid record
+    if (threadIdx.x == 0) bg_report(st, r0, ERR_PARSE);
+    return L;
+  }
+  // end of the tile's last line: the tile's last byte, the halo, or further on
+  TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
+  last_end = L == 0 ? -1
+             : (B.buf[HB + TT - 1] == '\n') ? t0 + TT - 1
+             : (B.hnl != ~0u ? t0 + B.hnl : find_nl(T, t0 + TT + HA + 32));
+  return L;
+}
+
+// prologue of a tile loaded into registers (load_tile); the LDS must be free
+template <int NB>
+__device__ __forceinline__ uint32_t tile_prologue(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                  const uint64_t* __restrict__ row0, int64_t t0,
+                                                  uint32_t tile, ParseLdsT<NB>& S, ParseBuf& B,
+                                                  const TileRegs& TR, uint64_t& r0,
+                                                  int64_t& last_end, bg_dstatus* st) {
+  clear_halo(B);
+  store_tile(B.buf, TR);
+  __syncthreads();
+  return prologue_core(txt, nb, row0, t0, tile, B, S.lst, S.shs, TR.v0, TR.v1, r0, last_end, st);
+}
+
 __global__ void __launch_bounds__(BG_NT) k_parse(
     const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
     bg_dstatus* st) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
-  __shared__ uint16_t lst[LCAP + 1];
+  __shared__ ParseLdsT<1> S;
   __shared__ int64_t lkey[LCAP];
-  __shared__ uint32_t shs[BG_NT / 64 + 1];
-  __shared__ uint32_t wsm[TT / 32 + HA / 32 + 1];  // class bitmaps: bit = byte
-  __shared__ uint32_t dgm[TT / 32 + HA / 32 + 1];
-  __shared__ uint32_t hnl;  // first '\n' in the halo after the tile (local offset)
+  uint8_t* buf = S.b[0].buf;
+  const uint16_t* lst = S.lst;
+  const uint32_t* wsm = S.b[0].wsm;
+  const uint32_t* dgm = S.b[0].dgm;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t PENDING = LLONG_MIN + 1;  // lkey of a line left to the byte path
-  if (threadIdx.x == 0) hnl = ~0u;
-  uint4 v0, v1;
-  if (threadIdx.x < 2 * ((HA + 32) / 32)) {  // halo mask words start empty (LDS atomics below)
-    if (threadIdx.x < (HA + 32) / 32) wsm[TT / 32 + threadIdx.x] = 0;
-    else dgm[TT / 32 + threadIdx.x - (HA + 32) / 32] = 0;
-  }
-  stage_tile(txt, nb, t0, buf, v0, v1);
-  __syncthreads();
-  {  // classify this thread's 32 bytes once (SWAR), publish the masks
-    const uint32_t W[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    uint32_t ws, dg;
-    bgp_classify8(W, ws, dg);
-    wsm[threadIdx.x] = ws;
-    dgm[threadIdx.x] = dg;
-  }
-  {  // the halo after the tile, from its LDS copy: one dword per thread (72 threads), the
-     // 4-bit groups merged into the mask words with LDS atomics
-    constexpr uint32_t HD = (HA + 32) / 4;
-    if (threadIdx.x < HD) {
-      const uint32_t x = reinterpret_cast<const uint32_t*>(&buf[HB + TT])[threadIdx.x];
-      uint32_t w4, d4;
-      bgp_classify(x, w4, d4);
-      const uint32_t sh = 4 * (threadIdx.x & 7);
-      if (w4) atomicOr(&wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
-      if (d4) atomicOr(&dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
-      const uint32_t m = nl_mask4(x);
-      if (m) atomicMin(&hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
-    }
-  }
+  uint64_t r0;
+  int64_t last_end;
+  TileRegs TR;
+  load_tile(txt, nb, t0, TR);
+  const uint32_t L = tile_prologue(txt, nb, row0, t0, blockIdx.x, S, S.b[0], TR, r0, last_end, st);
+  if (L > LCAP) return;
   const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];  // runs in this tile
-  bool has0;
-  const uint32_t L = tile_line_starts(v0, v1, buf, t0, lst, LCAP + 1, shs, has0);
-  const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1);  // row of the first owned line
-  if (L > LCAP) {  // > LCAP lines in 8 KiB: some line is shorter than any valid record
-    if (threadIdx.x == 0) bg_report(st, r0, ERR_PARSE);
-    return;
-  }
-  // end of the tile's last line: the tile's last byte, the halo, or further on
   TileText T{txt, buf, t0 - HB, t0 + TT + HA, nb};
-  const int64_t last_end = L == 0 ? -1
-                           : (buf[HB + TT - 1] == '\n') ? t0 + TT - 1
-                           : (hnl != ~0u ? t0 + hnl : find_nl(T, t0 + TT + HA + 32));
   int64_t mlen = 0;  // longest row of this thread (window bound of bedmap / closest)
   // hot loop: BED3 / BED3+rest lines decided by the masks; the rest is queued
   for (uint32_t k = threadIdx.x; k < L; k += BG_NT) {
@@ -684,6 +766,246 @@ __global__ void k_check_bounds(const int64_t* __restrict__ KS, const uint64_t* _
 }
 
 // -------------------------------------------------------------------------------------
+// BG_BED3_SET: parse straight to the file's merged set (components), no row columns.
+//
+// The file's components are what every set operation reads (mergeOverlap /
+// getNextFileMergedCoords, Bedops.cpp:792-814,865-886): row i opens a component iff
+// ks[i] > max(ke[0..i-1]). k_parse_set parses a tile (one line per thread per round of
+// BG_NT lines, in line order), and with block max-scans finds the tile's LOCAL
+// components (running max started at -inf), written to a staging area at the tile's
+// first row index (a tile has at least as many rows as local components). k_set_count /
+// k_set_write then apply the running max M of all earlier tiles: local components that
+// start at or below M merge into the component open on entry (a prefix of them, the
+// starts being increasing), the rest are global components. Row keys never reach HBM:
+// per 100M-row file this writes ~0.5 GB of staged components instead of 1.6 GB of keys
+// and drops the separate tile-max / components passes over those keys.
+// -------------------------------------------------------------------------------------
+struct SetTiles {
+  int64_t* tmax;   // max ke of the tile's rows (LLONG_MIN: none)
+  int64_t* tlast;  // max ks of the tile's rows (LLONG_MIN: none)
+  uint64_t* base;  // staging index of the tile's first local component (= its first row)
+  uint64_t* nloc;  // local components of the tile
+  uint32_t* absorbed;  // local components merged into the component open on entry
+  uint64_t* nrow;  // rows of the tile
+};
+
+// one line -> keys; false if the line is not a row (dropped tail, blank, error: reported).
+// Row numbers are not known here (no scout pass): errors are reported as row 0 and
+// bg_load re-reads the input with its row columns to report the exact line.
+__device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, const TileText& T,
+                                        const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
+                                        uint32_t k, uint32_t L, int64_t last_end, int64_t& ks,
+                                        int64_t& ke, bg_dstatus* st) {
+  const int64_t ls = t0 + lst[k];
+  const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
+  if (le < 0) return false;  // the unterminated last line (dropped, Bed.hpp:244-255 + feof)
+  const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+  const RunInfo& I = R.info[run];
+  uint64_t start, end;
+  Fast F;
+#if defined(BG_EXP) && BG_EXP == 1
+  if (true) { start = (uint64_t)ls; end = start + 10; } else
+#endif
+#if defined(BG_EXP) && BG_EXP == 2
+  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F)) {
+#else
+  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F) &&
+      F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
+#endif
+    start = F.start;
+    end = F.end;
+  } else {
+    Line Ln;
+    parse_line_slow(T, ls, le, BG_BED3, Ln);
+    if (Ln.err) {
+      bg_report(st, 0, Ln.err);
+      return false;
+    }
+    if (Ln.hash != I.hash) {  // a chromosome outside the run order: unsorted input
+      bg_report(st, 0, ERR_UNSORTED);
+      return false;
+    }
+    start = Ln.start;
+    end = Ln.end;
+  }
+  if (end > BG_MAX_COORD || start > end) bg_report(st, 0, ERR_RANGE);
+  if (start == end) atomicOr(&st->flags, 2ULL);
+  const int64_t g = (int64_t)I.gid << BG_KEY_SHIFT;
+  ks = g | (int64_t)(start & BG_COORD_MASK);
+  ke = g | (int64_t)(end & BG_COORD_MASK);
+  return true;
+}
+
+// 64-bit DPP lane moves and the wave-wide (64-lane) inclusive max scan built from them:
+// row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15/31 across rows (gfx9 DPP;
+// lanes with no source read 0, the identity of these unsigned scans)
+template <int CTRL, int RMASK, bool BC>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, RMASK, 0xF, BC);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, RMASK, 0xF, BC);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t wave_incl_max_u64(uint64_t v) {
+  v = max(v, dpp64<0x111, 0xF, true>(v));
+  v = max(v, dpp64<0x112, 0xF, true>(v));
+  v = max(v, dpp64<0x114, 0xF, true>(v));
+  v = max(v, dpp64<0x118, 0xF, true>(v));
+  v = max(v, dpp64<0x142, 0xA, false>(v));
+  v = max(v, dpp64<0x143, 0xC, false>(v));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x138, 0xF, true>(v); }
+
+// Keys inside the round loop are shifted by one, K = ks + 1 and E = ke + 1 (valid keys are
+// >= 0), so 0 means "no row" and is the identity of every max below.
+// BG_BED3_SET staging: local components of tile t go to slots [t * SCAP, t * SCAP + SCAP).
+// A tile with more (8 KiB of rows shorter than 16 bytes, almost all disjoint) sets
+// BG_SET_OVERFLOW and bg_load re-reads that input with its row columns (BG_BED3).
+#define SCAP 512
+#define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
+
+// one tile per workgroup. (Measured on MI355X and dropped: a persistent grid streaming the
+// next tile into a second LDS buffer by LDS-DMA while parsing this one — 2.3-2.4 vs 1.83 ms
+// per 100M-row file: this kernel is VALU-issue bound, not load-latency bound.)
+__global__ void __launch_bounds__(BG_NT) k_parse_set(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+  __shared__ ParseLdsT<1> S;
+  __shared__ uint64_t xe[2][BG_NT / 64], xk[2][BG_NT / 64];  // wave max E / last K, by parity
+  __shared__ uint32_t xc[2][BG_NT / 64];
+  __shared__ unsigned long long kmax;  // max K over the tile
+  __shared__ uint32_t nrow;            // rows of the tile
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t lt = (1ULL << lane) - 1;
+  const uint32_t tile = blockIdx.x;
+  const int64_t t0 = (int64_t)tile * TT;
+  const uint64_t base = (uint64_t)tile * SCAP;
+  if (threadIdx.x == 0) { kmax = 0; nrow = 0; }
+  int64_t last_end;
+  uint32_t L;
+  {
+    TileRegs TR;
+    load_tile(txt, nb, t0, TR);
+    uint64_t r0_unused;
+    L = tile_prologue(txt, nb, nullptr, t0, tile, S, S.b[0], TR, r0_unused, last_end, st);
+  }
+  if (L > LCAP) {  // error reported; leave an empty tile for the fix-up kernels
+    if (threadIdx.x == 0) {
+      TS.tmax[tile] = TS.tlast[tile] = LLONG_MIN;
+      TS.base[tile] = base;
+      TS.nloc[tile] = 0;
+      TS.nrow[tile] = 0;
+    }
+    return;
+  }
+  const ParseBuf& B = S.b[0];
+  const uint32_t rl = runlo[tile], rh = runhi[tile];
+  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
+  uint64_t carry_e = 0, carry_k = 0;  // max E of earlier rounds; K of the previous round's last line
+  uint64_t nc = 0;                    // local components so far
+  const uint32_t rounds = (L + BG_NT - 1) / BG_NT;
+  for (uint32_t j = 0; j < rounds; ++j) {  // block-uniform trip count (barriers inside)
+    const uint32_t k = j * BG_NT + threadIdx.x;
+    int64_t ks = 0, ke = 0;
+    const bool valid = k < L && set_row(B, S.lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
+    const uint64_t K = valid ? (uint64_t)ks + 1 : 0, E = valid ? (uint64_t)ke + 1 : 0;
+#if defined(BG_EXP) && BG_EXP == 3
+    if (valid) LCS[base + k % SCAP] = ks + ke;
+    continue;
+#endif
+    const uint64_t ie = wave_incl_max_u64(E);
+    const uint64_t pk = wave_shr1_u64(K);  // previous line's K (lane 0: from LDS below)
+    const int p = j & 1;
+    if (lane == 63) { xe[p][w] = ie; xk[p][w] = K; }
+    __syncthreads();
+    uint64_t pe = carry_e, te = carry_e;
+#pragma unroll
+    for (int q = 0; q < BG_NT / 64; ++q) {
+      if (q < w) pe = max(pe, xe[p][q]);
+      te = max(te, xe[p][q]);
+    }
+    const uint64_t prevK = lane ? pk : (w ? xk[p][w - 1] : carry_k);
+    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
+    const uint64_t ex_e = max(pe, wave_shr1_u64(ie));
+    const bool open = valid && K > ex_e;
+    const uint64_t bal = __ballot(open);
+    const uint64_t bv = __ballot(valid);
+    if (lane == 0) {
+      xc[p][w] = (uint32_t)__popcll(bal);
+      atomicAdd(&nrow, (uint32_t)__popcll(bv));
+    }
+    // the tile's largest K is on the last valid line of some wave
+    if (valid && (lane == 63 || !((bv >> (lane + 1)) & 1ULL))) atomicMax(&kmax, (unsigned long long)K);
+    __syncthreads();
+    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
+#pragma unroll
+    for (int q = 0; q < BG_NT / 64; ++q) {
+      if (q < w) pos += xc[p][q];
+      tot += xc[p][q];
+    }
+    if (open && pos < SCAP) {
+      LCS[base + pos] = ks;
+      if (pos > 0) LCE[base + pos - 1] = (int64_t)ex_e - 1;  // the previous local component ends here
+    }
+    carry_e = te;
+    carry_k = xk[p][BG_NT / 64 - 1];
+    nc += tot;
+  }
+  __syncthreads();  // kmax / nrow complete (also when the tile has no lines)
+  if (threadIdx.x == 0) {
+    if (nc > SCAP) {
+      atomicOr(&st->flags, BG_SET_OVERFLOW);
+      nc = 0;
+    }
+    if (nc > 0) LCE[base + nc - 1] = (int64_t)carry_e - 1;
+    TS.tmax[tile] = carry_e ? (int64_t)carry_e - 1 : LLONG_MIN;
+    TS.tlast[tile] = kmax ? (int64_t)kmax - 1 : LLONG_MIN;
+    TS.base[tile] = base;
+    TS.nloc[tile] = nc;
+    TS.nrow[tile] = nrow;
+  }
+}
+
+// per tile: sort check against every earlier tile, and how many local components the
+// running max of the earlier tiles absorbs (M: exclusive prefix max of tmax)
+__global__ void k_set_count(const int64_t* __restrict__ LCS, SetTiles TS,
+                            const int64_t* __restrict__ mex, const int64_t* __restrict__ sex,
+                            uint32_t ntiles, uint64_t* __restrict__ cnt, bg_dstatus* st) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t b = TS.base[t], n = TS.nloc[t];
+  if (n > 0 && LCS[b] < sex[t]) bg_report(st, 0, ERR_UNSORTED);  // first row < an earlier row
+  const uint64_t a = n ? upper_bound_in(LCS, b, b + n, mex[t]) - b : 0;
+  TS.absorbed[t] = (uint32_t)a;
+  cnt[t] = n - a;
+}
+
+// one wave per tile: global components of the tile -> CS/CE at its offset. CE[g] is the
+// running max just before component g+1 opens, written by the tile holding that opening
+// (the last one by the last tile).
+__global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__ LCS,
+                                                     const int64_t* __restrict__ LCE, SetTiles TS,
+                                                     const int64_t* __restrict__ mex,
+                                                     const uint64_t* __restrict__ off,
+                                                     uint32_t ntiles, int64_t* __restrict__ CS,
+                                                     int64_t* __restrict__ CE) {
+  const uint32_t t = blockIdx.x * (BG_NT / 64) + bg_wave();
+  if (t >= ntiles) return;
+  const uint64_t b = TS.base[t], n = TS.nloc[t], a = TS.absorbed[t], g0 = off[t];
+  const int64_t M = mex[t];
+  for (uint64_t j = a + bg_lane(); j < n; j += 64) {
+    const uint64_t g = g0 + (j - a);
+    CS[g] = LCS[b + j];
+    if (g > 0) CE[g - 1] = (j == a) ? max(M, a > 0 ? LCE[b + a - 1] : LLONG_MIN) : LCE[b + j - 1];
+  }
+  if (t + 1 == ntiles && bg_lane() == 0) {
+    const uint64_t total = g0 + (n - a);
+    if (total > 0) CE[total - 1] = max(M, TS.tmax[t]);
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // host side
 // -------------------------------------------------------------------------------------
 static const char* kind_name(int k) {
@@ -740,12 +1062,25 @@ struct LoadState {
   uint32_t* rlo = nullptr;
   uint32_t* rhi = nullptr;
   std::vector<uint64_t> rows;
+  // BG_BED3_SET staging
+  int64_t* lcs = nullptr;
+  int64_t* lce = nullptr;
+  int64_t* tmax = nullptr;
+  int64_t* tlast = nullptr;
+  int64_t* mex = nullptr;
+  int64_t* sex = nullptr;
+  uint64_t* tbase = nullptr;
+  uint64_t* nloc = nullptr;
+  uint64_t* tcnt = nullptr;
+  uint32_t* absorbed = nullptr;
 };
 
 static void release_state(bg_ctx* c, LoadState& S) {
   for (void* p : {(void*)S.row0, (void*)S.cnt, (void*)S.fls, (void*)S.fhash, (void*)S.fnl,
                   (void*)S.blist, (void*)S.rpos, (void*)S.rhash, (void*)S.rname, (void*)S.rlen,
-                  (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi})
+                  (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
+                  (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
+                  (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed})
     bg_release(c, p);
   S = LoadState();
 }
@@ -774,27 +1109,34 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   const uint32_t nt = S.ntiles;
   // a boundary tile records at most one entry per line (+1)
   S.rc = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
-  S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
-  S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
+  const bool set = in.kind == BG_BED3_SET;  // no row numbers: no scout pass
+  if (!set) {
+    S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
+    S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
+    S.fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
+    if (!S.cnt || !S.row0 || !S.fnl) return BG_E_NOMEM;
+  }
   S.fls = (int64_t*)bg_alloc(c, 8ull * nt);
   S.fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.blist = (uint32_t*)bg_alloc(c, 4ull * nt);
-  S.fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
   S.rpos = (int64_t*)bg_alloc(c, 8ull * S.rc);
   S.rhash = (uint64_t*)bg_alloc(c, 8ull * S.rc);
   S.rname = (char*)bg_alloc(c, 128ull * S.rc);
   S.rlen = (uint32_t*)bg_alloc(c, 4ull * S.rc);
-  if (!S.cnt || !S.row0 || !S.fls || !S.fhash || !S.blist || !S.fnl || !S.rpos || !S.rhash ||
-      !S.rname || !S.rlen)
+  if (!S.fls || !S.fhash || !S.blist || !S.rpos || !S.rhash || !S.rname || !S.rlen)
     return BG_E_NOMEM;
-  BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
-            S.cnt, S.fnl);
-  BG_HIP(c, hipGetLastError());
+  if (!set) {
+    BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
+              S.cnt, S.fnl);
+    BG_HIP(c, hipGetLastError());
+  }
   BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, S.fnl,
             S.fls, S.fhash);
   BG_HIP(c, hipGetLastError());
-  int rc = bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
-  if (rc) return rc;
+  if (!set) {
+    int rc = bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
+    if (rc) return rc;
+  }
   uint32_t* nbound = reinterpret_cast<uint32_t*>(&ctr[1]);
   uint32_t* nrec = reinterpret_cast<uint32_t*>(&ctr[2]);
   BG_LAUNCH(c, "k_boundary", k_boundary, dim3(bg_blocks(nt, 256)), dim3(256), S.fls, S.fhash, nt,
@@ -838,24 +1180,10 @@ static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSta
   return 0;
 }
 
-// phase 3 (no host round trip): keyed parse with the global dictionary
-static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
-                     const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
-  const uint64_t na = T->n ? T->n : 1;
-  T->ks = (int64_t*)bg_alloc(c, 8 * na);
-  T->ke = (int64_t*)bg_alloc(c, 8 * na);
-  if (!T->ks || !T->ke) return BG_E_NOMEM;
-  if (in.kind == BG_BED3_REST) {
-    T->rest_off = (uint64_t*)bg_alloc(c, 8 * na);
-    T->rest_len = (uint32_t*)bg_alloc(c, 4 * na);
-    if (!T->rest_off || !T->rest_len) return BG_E_NOMEM;
-  }
-  if (in.kind == BG_BED5) {
-    T->score = (double*)bg_alloc(c, 8 * na);
-    if (!T->score) return BG_E_NOMEM;
-  }
+// run table of one input on the device (+ the runs each tile can hold)
+static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
+                       const std::map<std::string, int32_t>& gid, RunTable& R) {
   const uint32_t nr = (uint32_t)S.run_pos.size();
-  if (S.ntiles == 0 || T->n == 0 || nr == 0) return 0;
   S.info.resize(nr);
   for (uint32_t k = 0; k < nr; ++k) {
     RunInfo& I = S.info[k];
@@ -876,10 +1204,34 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   if (!S.d_info || !S.d_row || !S.rlo || !S.rhi) return BG_E_NOMEM;
   BG_HIP(c, hipMemcpyAsync(S.d_info, S.info.data(), sizeof(RunInfo) * nr, hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemsetAsync(S.d_row, 0xff, 8ull * nr, c->stream));
-  RunTable R{S.d_info, S.d_row, nr};
+  R = RunTable{S.d_info, S.d_row, nr};
   BG_LAUNCH(c, "k_run_range", k_run_range, dim3(bg_blocks(S.ntiles, 256)), dim3(256), R, S.ntiles,
             S.rlo, S.rhi);
   BG_HIP(c, hipGetLastError());
+  return 0;
+}
+
+// phase 3 (no host round trip): keyed parse with the global dictionary
+static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
+                     const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
+  const uint64_t na = T->n ? T->n : 1;
+  T->ks = (int64_t*)bg_alloc(c, 8 * na);
+  T->ke = (int64_t*)bg_alloc(c, 8 * na);
+  if (!T->ks || !T->ke) return BG_E_NOMEM;
+  if (in.kind == BG_BED3_REST) {
+    T->rest_off = (uint64_t*)bg_alloc(c, 8 * na);
+    T->rest_len = (uint32_t*)bg_alloc(c, 4 * na);
+    if (!T->rest_off || !T->rest_len) return BG_E_NOMEM;
+  }
+  if (in.kind == BG_BED5) {
+    T->score = (double*)bg_alloc(c, 8 * na);
+    if (!T->score) return BG_E_NOMEM;
+  }
+  const uint32_t nr = (uint32_t)S.run_pos.size();
+  if (S.ntiles == 0 || T->n == 0 || nr == 0) return 0;
+  RunTable R;
+  int rc = upload_runs(c, T, S, gid, R);
+  if (rc) return rc;
   BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
             S.rhi, in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
   BG_HIP(c, hipGetLastError());
@@ -890,10 +1242,65 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   return 0;
 }
 
+// phase 3 for BG_BED3_SET: parse -> staged local components -> global components
+// (T->cs/T->ce, capacity = rows; the count lands in st->pad[0] and comes back with the
+// statuses)
+static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
+                         const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
+  T->is_set = true;
+  const uint32_t nr = (uint32_t)S.run_pos.size();
+  const uint32_t nt = S.ntiles;
+  const uint64_t cap = nt ? (uint64_t)nt * SCAP : 1;  // components <= staged slots
+  T->cs = (int64_t*)bg_alloc(c, 8 * cap);
+  T->ce = (int64_t*)bg_alloc(c, 8 * cap);
+  if (!T->cs || !T->ce) return BG_E_NOMEM;
+  if (nt == 0 || nr == 0) return 0;
+  RunTable R;
+  int rc = upload_runs(c, T, S, gid, R);
+  if (rc) return rc;
+  S.lcs = (int64_t*)bg_alloc(c, 8 * cap);
+  S.lce = (int64_t*)bg_alloc(c, 8 * cap);
+  S.tmax = (int64_t*)bg_alloc(c, 8ull * nt);
+  S.tlast = (int64_t*)bg_alloc(c, 8ull * nt);
+  S.mex = (int64_t*)bg_alloc(c, 8ull * nt);
+  S.sex = (int64_t*)bg_alloc(c, 8ull * nt);
+  S.tbase = (uint64_t*)bg_alloc(c, 8ull * nt);
+  S.nloc = (uint64_t*)bg_alloc(c, 8ull * nt);
+  S.tcnt = (uint64_t*)bg_alloc(c, 8ull * nt);
+  S.absorbed = (uint32_t*)bg_alloc(c, 4ull * nt);
+  S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);  // rows per tile
+  if (!S.lcs || !S.lce || !S.tmax || !S.tlast || !S.mex || !S.sex || !S.tbase || !S.nloc ||
+      !S.tcnt || !S.absorbed || !S.cnt)
+    return BG_E_NOMEM;
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt};
+  BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+            S.lcs, S.lce, TS, st);
+  BG_HIP(c, hipGetLastError());
+  if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
+  if ((rc = bg_scan_max_i64(c, S.tlast, S.sex, nt, LLONG_MIN))) return rc;
+  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, 256)), dim3(256), S.lcs, TS, S.mex,
+            S.sex, nt, S.tcnt, st);
+  BG_HIP(c, hipGetLastError());
+  if ((rc = bg_scan_sum_u64(c, S.tcnt, S.tcnt, nt, (uint64_t*)&st->pad[0]))) return rc;
+  if ((rc = bg_scan_sum_u64(c, S.cnt, S.cnt, nt, (uint64_t*)&st->pad[1]))) return rc;  // rows
+  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, BG_NT / 64)), dim3(BG_NT), S.lcs,
+            S.lce, TS, S.mex, S.tcnt, nt, T->cs, T->ce);
+  BG_HIP(c, hipGetLastError());
+  return 0;
+}
+
 // after phase 3: per-input status, flags and the run -> row table
 static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S,
                       const bg_dstatus& h) {
   T->run_row0.assign(1, 0);
+  if (T->is_set) {  // errors / overflow were handled by bg_load (re-read with row columns)
+    T->n = h.pad[1];
+    T->nc = h.pad[0];
+    T->has_zero_len = (h.flags & 2ULL) != 0;
+    T->run_row0.push_back(T->n);
+    if (S.ntiles == 0 || T->n == 0) T->run_name.clear();
+    return 0;
+  }
   if (S.ntiles == 0 || T->n == 0 || S.run_pos.empty()) {
     T->run_name.clear();
     return 0;
@@ -996,7 +1403,9 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     }
     rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst.data(), sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
   }
-  for (int i = 0; i < n && !rc; ++i) rc = parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
+  for (int i = 0; i < n && !rc; ++i)
+    rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i)
+                                       : parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
   // round trip 3: statuses and run rows of every input (pageable copies block the host,
   // so they are issued only once all parses are queued)
   for (int i = 0; i < n && !rc; ++i)
@@ -1005,17 +1414,33 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
                                        hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hst.data(), dst, sizeof(bg_dstatus) * n, hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
-  for (int i = 0; i < n && !rc; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
+  // a BG_BED3_SET input with an error (its exact line is not known) or a staging overflow:
+  // the whole load is redone with that input's row columns (BG_BED3)
+  bool redo = false;
+  for (int i = 0; i < n && !rc; ++i)
+    if (inputs[i].kind == BG_BED3_SET && st[i].ntiles &&
+        (hst[i].first_bad != ~0ULL || (hst[i].flags & BG_SET_OVERFLOW)))
+      redo = true;
+  for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
   if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies read the host vectors
   for (auto& S : st) release_state(c, S);
   bg_release(c, ctr);
   bg_release(c, dst);
-  if (rc) {
+  if (rc || redo) {
     bg_set_free(s);
-    return rc;
+    if (rc) return rc;
+    std::vector<bg_input> rows(inputs, inputs + n);
+    for (auto& in : rows)
+      if (in.kind == BG_BED3_SET) in.kind = BG_BED3;
+    return bg_load(c, n, rows.data(), out);
   }
   for (bg_table* T : s->t)  // keep every column non-null for empty inputs
-    if (!T->ks) {
+    if (T->is_set) {
+      if (!T->cs) {
+        T->cs = (int64_t*)bg_alloc(c, 8);
+        T->ce = (int64_t*)bg_alloc(c, 8);
+      }
+    } else if (!T->ks) {
       T->ks = (int64_t*)bg_alloc(c, 8);
       T->ke = (int64_t*)bg_alloc(c, 8);
     }
@@ -1036,6 +1461,8 @@ extern "C" void bg_set_free(bg_set* s) {
   for (bg_table* T : s->t) {
     bg_release(c, T->ks);
     bg_release(c, T->ke);
+    bg_release(c, T->cs);
+    bg_release(c, T->ce);
     bg_release(c, T->own_text);
     bg_release(c, T->rest_off);
     bg_release(c, T->rest_len);

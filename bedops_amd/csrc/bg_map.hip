@@ -52,6 +52,11 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (!c || !set || !opts || !out || ref < 0 || map < 0 || ref >= (int)set->t.size() ||
       map >= (int)set->t.size() || opts->n_ops <= 0 || opts->n_ops > 16)
     return BG_E_ARG;
+  {
+    const int f[2] = {ref, map};
+    int rc0 = bg_need_rows(c, set, f, 2, "bedmap");
+    if (rc0) return rc0;
+  }
   bool need_score = false;
   for (int k = 0; k < opts->n_ops; ++k) {
     if (opts->ops[k] == BG_MAP_MEAN) need_score = true;

@@ -492,6 +492,7 @@ extern "C" int bg_chop(bg_ctx* c, bg_set* set, const int* files, int nf, uint64_
 extern "C" int bg_partition(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
   int rc = bg_check_files(c, set, files, nf, 1);
   if (rc || !out) return rc ? rc : BG_E_ARG;
+  if ((rc = bg_need_rows(c, set, files, nf, "partition"))) return rc;
   std::vector<Ivl> lists;
   for (int k = 0; k < nf; ++k) lists.push_back(bg_table_ivl(set->t[files[k]]));
   Events E;
@@ -519,7 +520,7 @@ extern "C" int bg_symmdiff(bg_ctx* c, bg_set* set, const int* files, int nf, bg_
                      "than start coordinates)");
   std::vector<Ivl> comps(nf);
   for (int k = 0; k < nf; ++k)
-    if ((rc = bg_components(c, bg_table_ivl(set->t[files[k]]), comps[k]))) return rc;
+    if ((rc = bg_table_components(c, set->t[files[k]], comps[k]))) return rc;
   Events E;
   if ((rc = build_events(c, comps, E))) return rc;
   for (Ivl& v : comps) ivl_free(c, v);
@@ -609,6 +610,8 @@ extern "C" int bg_everything(bg_ctx* c, bg_set* set, const int* files, int nf, b
 extern "C" int bg_set_pad(bg_ctx* c, bg_set* set, int file, int lpad, int rpad) {
   if (!c || !set || file < 0 || file >= (int)set->t.size()) return BG_E_ARG;
   if (lpad == 0 && rpad == 0) return 0;
+  int rc0 = bg_need_rows(c, set, &file, 1, "--range");
+  if (rc0) return rc0;
   bg_table* T = set->t[file];
   const uint64_t n = T->n;
   PadArgs P;

@@ -487,14 +487,34 @@ Ivl bg_table_ivl(bg_table* T) {
   return v;
 }
 
+int bg_table_components(bg_ctx* c, bg_table* T, Ivl& out) {
+  if (T->is_set) {
+    out = Ivl();
+    out.s = T->cs;
+    out.e = T->ce;
+    out.n = T->nc;
+    out.owned = false;
+    return 0;
+  }
+  return bg_components(c, bg_table_ivl(T), out);
+}
+
+int bg_need_rows(bg_ctx* c, bg_set* set, const int* files, int nf, const char* what) {
+  for (int k = 0; k < nf; ++k)
+    if (set->t[files[k]]->is_set)
+      return bg_fail(c, BG_E_ARG, std::string(what) + ": input " + std::to_string(files[k] + 1) +
+                                      " was loaded as BG_BED3_SET (no rows kept)");
+  return 0;
+}
+
 // components of the union of the given tables
 int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& out) {
   Ivl acc;
-  int rc = bg_components(c, bg_table_ivl(set->t[files[0]]), acc);
+  int rc = bg_table_components(c, set->t[files[0]], acc);
   if (rc) return rc;
   for (int k = 1; k < nf; ++k) {
     Ivl ck, z, m;
-    if ((rc = bg_components(c, bg_table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = bg_table_components(c, set->t[files[k]], ck))) return rc;
     if ((rc = merge_sorted(c, acc, ck, z))) return rc;
     ivl_free(c, acc);
     ivl_free(c, ck);
@@ -507,6 +527,18 @@ int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& o
 }
 
 bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
+  if (!v.owned && v.s) {  // a view of a table's set: the result gets its own copy
+    Ivl w;
+    if (ivl_alloc(c, w, v.n)) return nullptr;
+    if (v.n) {
+      if (hipMemcpyAsync(w.s, v.s, 8 * v.n, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+          hipMemcpyAsync(w.e, v.e, 8 * v.n, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
+        ivl_free(c, w);
+        return nullptr;
+      }
+    }
+    v = w;
+  }
   bg_result* r = new bg_result();
   r->ctx = c;
   r->set = set;
@@ -531,6 +563,7 @@ extern "C" int bg_merge(bg_ctx* c, bg_set* set, const int* files, int nf, bg_res
   Ivl m;
   if ((rc = bg_union_components(c, set, files, nf, m))) return rc;
   *out = bg_new_ivl_result(c, set, m);
+  if (!*out) return BG_E_NOMEM;
   bg_mark(c, "merge");
   return 0;
 }
@@ -549,10 +582,10 @@ extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg
                      "the GPU path (BEDOPS --ec rejects them: End coordinates must be greater "
                      "than start coordinates)");
   Ivl acc;
-  if ((rc = bg_components(c, bg_table_ivl(set->t[files[0]]), acc))) return rc;
+  if ((rc = bg_table_components(c, set->t[files[0]], acc))) return rc;
   for (int k = 1; k < nf; ++k) {
     Ivl ck, p;
-    if ((rc = bg_components(c, bg_table_ivl(set->t[files[k]]), ck))) return rc;
+    if ((rc = bg_table_components(c, set->t[files[k]], ck))) return rc;
     if ((rc = mp_op<MP_INTERSECT>(c, acc, ck, p, "k_intersect_count", "k_intersect_write"))) return rc;
     ivl_free(c, acc);
     ivl_free(c, ck);
@@ -569,7 +602,7 @@ extern "C" int bg_difference(bg_ctx* c, bg_set* set, int ref, const int* others,
   if (rc) return rc;
   if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
   Ivl r, o, d;
-  if ((rc = bg_components(c, bg_table_ivl(set->t[ref]), r))) return rc;
+  if ((rc = bg_table_components(c, set->t[ref], r))) return rc;
   if ((rc = bg_union_components(c, set, others, no, o))) return rc;
   if ((rc = mp_op<MP_DIFFERENCE>(c, r, o, d, "k_difference_count", "k_difference_write"))) return rc;
   ivl_free(c, r);
@@ -585,6 +618,7 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   if (rc) return rc;
   if (ref < 0 || ref >= (int)set->t.size()) return BG_E_ARG;
   bg_table* R = set->t[ref];
+  if ((rc = bg_need_rows(c, set, &ref, 1, "element-of reference"))) return rc;
   Ivl o;
   if ((rc = bg_union_components(c, set, others, no, o))) return rc;
   uint64_t* P = (uint64_t*)bg_alloc(c, 8 * (o.n + 1));

@@ -10,7 +10,11 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
-BED3, BED3_REST, BED5 = 0, 1, 2
+BED3, BED3_REST, BED5, BED3_SET = 0, 1, 2, 3
+# operations that read only each input's merged set (or, for element-of, only the
+# non-reference inputs' sets): their inputs may be loaded as BED3_SET
+SET_MODES = {"-m", "--merge", "-i", "--intersect", "-d", "--difference", "-e", "--element-of",
+             "-n", "--not-element-of", "-c", "--complement", "-w", "--chop", "-s", "--symmdiff"}
 MAP_COUNT, MAP_MEAN = 1, 2
 
 ERRORS = {-1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
@@ -28,7 +32,8 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
 
 
 def lib_path():
-    return os.path.join(HERE, "lib", "libbedgpu.so")
+    # BEDGPU_LIB: an alternative build of the same library (A/B experiments)
+    return os.environ.get("BEDGPU_LIB") or os.path.join(HERE, "lib", "libbedgpu.so")
 
 
 class BedgpuError(RuntimeError):
@@ -295,12 +300,15 @@ class Engine:
         return Result(self, h)
 
     def bedops(self, mode, texts, spec=None, chrom=None, pad=None, full_left=False,
-               chop=(1, 0, False)):
+               chop=(1, 0, False), set_load=True):
         """bedops [--chrom C] [--range L:R] <mode> [spec] file1 file2 ... on in-memory BED
-        texts -> output bytes. pad = (lpad, rpad)."""
+        texts -> output bytes. pad = (lpad, rpad). set_load: inputs whose rows the
+        operation never reads are parsed straight to their merged set (BED3_SET), as the
+        bedops front-end does; False keeps the row columns (BED3)."""
         eo = mode in ("-e", "--element-of", "-n", "--not-element-of")
         every = mode in ("-u", "--everything")
-        s = self.load([(t, BED3_REST if (every or (eo and i == 0)) else BED3)
+        plain = BED3_SET if (set_load and mode in SET_MODES and not chrom and pad is None) else BED3
+        s = self.load([(t, BED3_REST if (every or (eo and i == 0)) else plain)
                        for i, t in enumerate(texts)])
         try:
             if chrom:

@@ -91,12 +91,15 @@ def kernel_bytes(name, w):
     (what each kernel must read and write at minimum)."""
     texts, rows, kinds = w["texts"], w["rows"], w["kinds"]
     nf = len(texts)
-    col = {0: 16, 1: 28, 2: 24}  # keyed start/end (+ rest span 12 B | score 8 B) per row
+    col = {0: 16, 1: 28, 2: 24, 3: 0}  # keyed start/end (+ rest span 12 B | score 8 B) per row
     out, obytes, comps = w["out"], w["out_bytes"], w["comps"]
     table = {
         # one launch per input file: text read + columns written (mean over the files)
         "k_parse": sum(t + col[k] * r for t, r, k in zip(texts, rows, kinds)) / nf,
         "k_scout": sum(texts) / nf,
+        # BG_BED3_SET: text read + the file's components written (staged once)
+        "k_parse_set": (sum(t for t, k in zip(texts, kinds) if k == 3) + 16 * comps)
+        / max(1, sum(1 for k in kinds if k == 3)),
         "k_tile_max": 8 * sum(rows) / nf,
         "k_components_count": 16 * sum(rows) / nf,
         "k_components_write": (16 * sum(rows) + 16 * comps) / nf,
@@ -162,12 +165,12 @@ def cpu_baseline(L, W, target_s=15.0):
 # gen: (seed, 3 = BED3 | 5 = BED5) per input; rows: per input at N = 1.
 WORKLOADS = {
     "intersect": {"gen": [(42, 3), (43, 3)], "rows": [100_000_000, 100_000_000],
-                  "kinds": [0, 0], "oracle": "bedops_oracle", "cpu_args": ["-i"],
+                  "kinds": [3, 3], "oracle": "bedops_oracle", "cpu_args": ["-i"],
                   "cpu_rate": 8.5e6, "ref": REF_INTERSECT,
                   "desc": "bedops --intersect A.bed B.bed: BED3 text in HBM -> parse -> merge -> "
                           "intersect -> BED text in HBM"},
     "element-of": {"gen": [(44, 3), (45, 3)], "rows": [200_000_000, 200_000_000],
-                   "kinds": [1, 0], "oracle": "bedops_oracle", "cpu_args": ["-e", "1"],
+                   "kinds": [1, 3], "oracle": "bedops_oracle", "cpu_args": ["-e", "1"],
                    "cpu_rate": 3e6, "ref": None,
                    "desc": "bedops --element-of 1 A.bed B.bed (configs[3] shape, 200M x 200M)"},
     "bedmap": {"gen": [(7, 3), (8, 5)], "rows": [50_000_000, 500_000_000], "kinds": [0, 2],
@@ -397,6 +400,9 @@ def main():
         "kernels_first_step_ms": {k: round(v[1], 4) for k, v in
                                   sorted(first.items(), key=lambda kv: -kv[1][1])},
     }
+    if args.profile_all:  # HIP-event time per timed step of every kernel
+        line["kernels_ms_per_step"] = {k: round(v[1] / args.steps, 4) for k, v in
+                                       sorted(prof.items(), key=lambda kv: -kv[1][1])}
     print(json.dumps(line), flush=True)
     eng.close()
     if dist:

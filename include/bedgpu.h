@@ -60,6 +60,12 @@ extern "C" {
 #define BG_BED3 0      /* chrom start end; remainder ignored            (Bed::B3NoRest) */
 #define BG_BED3_REST 1 /* remainder after `end` kept verbatim for output (Bed::B3Rest)  */
 #define BG_BED5 2      /* chrom start end id score; score parsed         (Bed::B5Rest)  */
+/* BED3 parsed straight to the file's merged set (getNextFileMergedCoords,
+ * Bedops.cpp:792-814): no per-row columns are kept. Valid for the inputs of
+ * merge/intersect/difference/complement/chop/symmdiff and element-of's non-reference
+ * files; operations that need rows (element-of's reference, partition, everything,
+ * bedmap, closest-features, --chrom, --range) refuse such a table with BG_E_ARG. */
+#define BG_BED3_SET 3
 
 typedef struct bg_ctx bg_ctx;
 typedef struct bg_set bg_set;       /* N parsed inputs sharing one chromosome dictionary */
@@ -69,7 +75,7 @@ typedef struct bg_input {
   const void* data;   /* BED text */
   uint64_t nbytes;
   int on_device;      /* 0: host memory (copied to HBM); 1: device pointer (16-B aligned) */
-  int kind;           /* BG_BED3 / BG_BED3_REST / BG_BED5 */
+  int kind;           /* BG_BED3 / BG_BED3_REST / BG_BED5 / BG_BED3_SET */
 } bg_input;
 
 typedef struct bg_map_opts {
