@@ -56,16 +56,17 @@ struct FmtArgs {
   int shortest, print_dist, no_ref;
 };
 
-// decimal digits of v: compares, no division (coordinates are < 10^12)
+// decimal digits of v: compares only, 32-bit ones when v fits (the common case)
 __device__ __forceinline__ int dec_len_u64(uint64_t v) {
-  int l = 1;
-  if (v >= 10000000000ull) {
-    l += 10;
-    v /= 10000000000ull;
+  if ((v >> 32) == 0) {
+    const uint32_t w = (uint32_t)v;
+    return 1 + (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
+           (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
   }
-  const uint32_t w = (uint32_t)v;  // < 10^10 here
-  l += (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
-       (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
+  int l = 10;  // v >= 2^32 > 10^9
+  uint64_t p = 10000000000ull;
+#pragma unroll
+  for (int k = 0; k < 10; ++k, p *= 10) l += v >= p;
   return l;
 }
 __device__ __forceinline__ int dec_len_i32(int32_t v) {

@@ -803,7 +803,7 @@ __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, 
   const RunInfo& I = R.info[run];
   uint64_t start, end;
   Fast F;
-#if defined(BG_EXP) && BG_EXP == 1
+#if defined(BG_EXP) && (BG_EXP == 1 || BG_EXP == 4)
   if (true) { start = (uint64_t)ls; end = start + 10; } else
 #endif
 #if defined(BG_EXP) && BG_EXP == 2
@@ -864,6 +864,107 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 #define SCAP 512
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
 
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
+  v = max(v, dpp32<0x111, 0xF, true>(v));
+  v = max(v, dpp32<0x112, 0xF, true>(v));
+  v = max(v, dpp32<0x114, 0xF, true>(v));
+  v = max(v, dpp32<0x118, 0xF, true>(v));
+  v = max(v, dpp32<0x142, 0xA, false>(v));
+  v = max(v, dpp32<0x143, 0xC, false>(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max_v(uint32_t v) { return wave_incl_max_u32(v); }
+__device__ __forceinline__ uint64_t wave_incl_max_v(uint64_t v) { return wave_incl_max_u64(v); }
+__device__ __forceinline__ uint32_t wave_shr1_v(uint32_t v) { return dpp32<0x138, 0xF, true>(v); }
+__device__ __forceinline__ uint64_t wave_shr1_v(uint64_t v) { return wave_shr1_u64(v); }
+
+// LDS of the set kernel's rounds
+struct SetLds {
+  uint64_t xe[2][BG_NT / 64], xk[2][BG_NT / 64];  // wave max E / last K, by round parity
+  uint32_t xc[2][BG_NT / 64];                     // wave component counts
+  unsigned long long kmax;                        // max K over the tile
+  uint32_t nrow;                                  // rows of the tile
+};
+
+// The rounds of one tile: BG_NT lines per round, one per thread, in line order. V is the
+// scan type: uint32_t for a tile inside one chromosome run (K = start + 1, E = end + 1 on
+// the coordinates; the key prefix gbase is uniform), uint64_t otherwise (K, E on the
+// keys, gbase = 0). 0 means "no row" and is the identity of every max. A coordinate
+// >= 2^32 - 2 in a one-run tile sets BG_SET_OVERFLOW (the input is re-read with rows).
+template <typename V>
+__device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* lst, const TileText& T,
+                                           const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
+                                           uint32_t L, int64_t last_end, int64_t gbase,
+                                           uint64_t base, int64_t* __restrict__ LCS,
+                                           int64_t* __restrict__ LCE, SetLds& X, uint64_t& nc,
+                                           V& carry_e, bg_dstatus* st) {
+  constexpr bool NARROW = sizeof(V) == 4;
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t lt = (1ULL << lane) - 1;
+  V carry_k = 0;  // K of the previous round's last line
+  const uint32_t rounds = (L + BG_NT - 1) / BG_NT;
+  for (uint32_t j = 0; j < rounds; ++j) {  // block-uniform trip count (barriers inside)
+    const uint32_t k = j * BG_NT + threadIdx.x;
+    int64_t ks = 0, ke = 0;
+    const bool valid = k < L && set_row(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
+    V K = 0, E = 0;
+    if (valid) {
+      if (NARROW) {
+        const uint64_t ce = (uint64_t)(ke & BG_COORD_MASK) + 1;
+        if (ce >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
+        K = (V)((uint64_t)(ks & BG_COORD_MASK) + 1);
+        E = (V)ce;
+      } else {
+        K = (V)ks + 1;
+        E = (V)ke + 1;
+      }
+    }
+#if defined(BG_EXP) && (BG_EXP == 3 || BG_EXP == 4)
+    if (valid) carry_e ^= (V)(ks + ke);
+    continue;
+#endif
+    const V ie = wave_incl_max_v(E);
+    const V pk = wave_shr1_v(K);  // previous line's K (lane 0: from LDS below)
+    const int p = j & 1;
+    if (lane == 63) { X.xe[p][w] = ie; X.xk[p][w] = K; }
+    __syncthreads();
+    V pe = carry_e, te = carry_e;
+#pragma unroll
+    for (int q = 0; q < BG_NT / 64; ++q) {
+      const V x = (V)X.xe[p][q];
+      if (q < w) pe = max(pe, x);
+      te = max(te, x);
+    }
+    const V prevK = lane ? pk : (w ? (V)X.xk[p][w - 1] : carry_k);
+    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
+    const V ex_e = max(pe, wave_shr1_v(ie));
+    const bool open = valid && K > ex_e;
+    const uint64_t bal = __ballot(open);
+    const uint64_t bv = __ballot(valid);
+    if (lane == 0) {
+      X.xc[p][w] = (uint32_t)__popcll(bal);
+      atomicAdd(&X.nrow, (uint32_t)__popcll(bv));
+    }
+    // the tile's largest K is on the last valid line of some wave
+    if (valid && (lane == 63 || !((bv >> (lane + 1)) & 1ULL)))
+      atomicMax(&X.kmax, (unsigned long long)K);
+    __syncthreads();
+    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
+#pragma unroll
+    for (int q = 0; q < BG_NT / 64; ++q) {
+      if (q < w) pos += X.xc[p][q];
+      tot += X.xc[p][q];
+    }
+    if (open && pos < SCAP) {
+      LCS[base + pos] = ks;
+      if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);  // previous local component ends here
+    }
+    carry_e = te;
+    carry_k = (V)X.xk[p][BG_NT / 64 - 1];
+    nc += tot;
+  }
+}
+
 // one tile per workgroup. (Measured on MI355X and dropped: a persistent grid streaming the
 // next tile into a second LDS buffer by LDS-DMA while parsing this one — 2.3-2.4 vs 1.83 ms
 // per 100M-row file: this kernel is VALU-issue bound, not load-latency bound.)
@@ -872,16 +973,11 @@ __global__ void __launch_bounds__(BG_NT) k_parse_set(
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
   __shared__ ParseLdsT<1> S;
-  __shared__ uint64_t xe[2][BG_NT / 64], xk[2][BG_NT / 64];  // wave max E / last K, by parity
-  __shared__ uint32_t xc[2][BG_NT / 64];
-  __shared__ unsigned long long kmax;  // max K over the tile
-  __shared__ uint32_t nrow;            // rows of the tile
-  const int lane = bg_lane(), w = bg_wave();
-  const uint64_t lt = (1ULL << lane) - 1;
+  __shared__ SetLds X;
   const uint32_t tile = blockIdx.x;
   const int64_t t0 = (int64_t)tile * TT;
   const uint64_t base = (uint64_t)tile * SCAP;
-  if (threadIdx.x == 0) { kmax = 0; nrow = 0; }
+  if (threadIdx.x == 0) { X.kmax = 0; X.nrow = 0; }
   int64_t last_end;
   uint32_t L;
   {
@@ -902,68 +998,32 @@ __global__ void __launch_bounds__(BG_NT) k_parse_set(
   const ParseBuf& B = S.b[0];
   const uint32_t rl = runlo[tile], rh = runhi[tile];
   const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
-  uint64_t carry_e = 0, carry_k = 0;  // max E of earlier rounds; K of the previous round's last line
-  uint64_t nc = 0;                    // local components so far
-  const uint32_t rounds = (L + BG_NT - 1) / BG_NT;
-  for (uint32_t j = 0; j < rounds; ++j) {  // block-uniform trip count (barriers inside)
-    const uint32_t k = j * BG_NT + threadIdx.x;
-    int64_t ks = 0, ke = 0;
-    const bool valid = k < L && set_row(B, S.lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
-    const uint64_t K = valid ? (uint64_t)ks + 1 : 0, E = valid ? (uint64_t)ke + 1 : 0;
-#if defined(BG_EXP) && BG_EXP == 3
-    if (valid) LCS[base + k % SCAP] = ks + ke;
-    continue;
-#endif
-    const uint64_t ie = wave_incl_max_u64(E);
-    const uint64_t pk = wave_shr1_u64(K);  // previous line's K (lane 0: from LDS below)
-    const int p = j & 1;
-    if (lane == 63) { xe[p][w] = ie; xk[p][w] = K; }
-    __syncthreads();
-    uint64_t pe = carry_e, te = carry_e;
-#pragma unroll
-    for (int q = 0; q < BG_NT / 64; ++q) {
-      if (q < w) pe = max(pe, xe[p][q]);
-      te = max(te, xe[p][q]);
-    }
-    const uint64_t prevK = lane ? pk : (w ? xk[p][w - 1] : carry_k);
-    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
-    const uint64_t ex_e = max(pe, wave_shr1_u64(ie));
-    const bool open = valid && K > ex_e;
-    const uint64_t bal = __ballot(open);
-    const uint64_t bv = __ballot(valid);
-    if (lane == 0) {
-      xc[p][w] = (uint32_t)__popcll(bal);
-      atomicAdd(&nrow, (uint32_t)__popcll(bv));
-    }
-    // the tile's largest K is on the last valid line of some wave
-    if (valid && (lane == 63 || !((bv >> (lane + 1)) & 1ULL))) atomicMax(&kmax, (unsigned long long)K);
-    __syncthreads();
-    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
-#pragma unroll
-    for (int q = 0; q < BG_NT / 64; ++q) {
-      if (q < w) pos += xc[p][q];
-      tot += xc[p][q];
-    }
-    if (open && pos < SCAP) {
-      LCS[base + pos] = ks;
-      if (pos > 0) LCE[base + pos - 1] = (int64_t)ex_e - 1;  // the previous local component ends here
-    }
-    carry_e = te;
-    carry_k = xk[p][BG_NT / 64 - 1];
-    nc += tot;
+  uint64_t nc = 0;  // local components
+  uint64_t cmax = 0;  // max E (+1; 0 = no row): coordinates for one-run tiles, keys otherwise
+  int64_t gbase = 0;
+  if (rl == rh) {  // one chromosome run: 32-bit scans on the coordinates
+    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
+    uint32_t ce = 0;
+    set_rounds<uint32_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
+    cmax = ce;
+  } else {
+    set_rounds<uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
   }
   __syncthreads();  // kmax / nrow complete (also when the tile has no lines)
+#if defined(BG_EXP) && (BG_EXP == 3 || BG_EXP == 4)
+  if (cmax == 12345) LCS[base] = 1;
+#endif
   if (threadIdx.x == 0) {
     if (nc > SCAP) {
       atomicOr(&st->flags, BG_SET_OVERFLOW);
       nc = 0;
     }
-    if (nc > 0) LCE[base + nc - 1] = (int64_t)carry_e - 1;
-    TS.tmax[tile] = carry_e ? (int64_t)carry_e - 1 : LLONG_MIN;
-    TS.tlast[tile] = kmax ? (int64_t)kmax - 1 : LLONG_MIN;
+    if (nc > 0) LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
+    TS.tlast[tile] = X.kmax ? (gbase | (int64_t)(X.kmax - 1)) : LLONG_MIN;
     TS.base[tile] = base;
     TS.nloc[tile] = nc;
-    TS.nrow[tile] = nrow;
+    TS.nrow[tile] = X.nrow;
   }
 }
 

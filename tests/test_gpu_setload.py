@@ -148,3 +148,20 @@ def test_set_load_staging_overflow_falls_back(eng, oracle_bin):
         with tempfile.TemporaryDirectory() as td:
             want = run_oracle(oracle_bin["bedops"], [mode], [a, b], td)
         assert eng.bedops(mode, [a, b]) == want, mode
+
+
+def test_set_load_coordinates_past_32_bits(eng, oracle_bin):
+    """one-chromosome tiles scan 32-bit coordinates; an end >= 2^32 - 2 makes the loader
+    redo the input with row columns, multi-chromosome tiles use 64-bit keys throughout"""
+    rng = random.Random(21)
+    big = 2**32 - 40
+    rs = sorted((c, big + rng.randrange(200), 0) for c in ["chr1", "chr2"] for _ in range(3000))
+    rs = [(c, s, s + rng.randint(1, 60)) for c, s, _ in rs]
+    rs.sort(key=lambda r: (r[0], r[1], r[2]))
+    a = randbed.text(rs).encode()
+    b = randbed.text(randbed.rows(rng, 4000, chroms=["chr1", "chr2"], span=2**33, maxlen=10**6)).encode()
+    for mode in ("-m", "-i", "-d"):
+        with tempfile.TemporaryDirectory() as td:
+            want = run_oracle(oracle_bin["bedops"], [mode], [a, b], td)
+        assert eng.bedops(mode, [a, b], set_load=False) == want, mode  # (printing >= 2^32)
+        assert eng.bedops(mode, [a, b]) == want, mode
