@@ -182,8 +182,38 @@ extern "C" void bg_close(bg_ctx* c) {
   for (auto e : c->prof_events) hipEventDestroy(e);
   hipFree(c->dstat);
   hipHostFree(c->hstat);
+  for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
   hipStreamDestroy(c->stream);
   delete c;
+}
+
+void bg_pin_reset(bg_ctx* c) {
+  c->pin_chunk = 0;
+  c->pin_used = 0;
+}
+
+void* bg_pin_take(bg_ctx* c, size_t bytes) {
+  bytes = (bytes + 63) & ~(size_t)63;
+  while (c->pin_chunk < c->pin_chunks.size()) {
+    auto& ch = c->pin_chunks[c->pin_chunk];
+    if (c->pin_used + bytes <= ch.second) {
+      void* p = ch.first + c->pin_used;
+      c->pin_used += bytes;
+      return p;
+    }
+    ++c->pin_chunk;
+    c->pin_used = 0;
+  }
+  const size_t sz = std::max<size_t>(bytes, 4u << 20);
+  char* p = nullptr;
+  if (hipHostMalloc((void**)&p, sz, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  c->pin_chunks.push_back({p, sz});
+  c->pin_chunk = c->pin_chunks.size() - 1;
+  c->pin_used = bytes;
+  return p;
 }
 
 uint32_t bg_resident_blocks(bg_ctx* c, const void* kern) {

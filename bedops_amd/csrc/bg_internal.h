@@ -49,6 +49,10 @@ struct bg_ctx {
   int device = 0;
   int ncu = 256;  // compute units
   std::vector<std::pair<const void*, uint32_t>> resident;  // kernel -> resident BG_NT blocks
+  // pinned host staging for the loader's small copies (async DMA, no bounce buffer):
+  // chunks are kept for the context's lifetime, handed out by a bump pointer reset per call
+  std::vector<std::pair<char*, size_t>> pin_chunks;
+  size_t pin_chunk = 0, pin_used = 0;
   hipStream_t stream = nullptr;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
@@ -139,6 +143,11 @@ struct bg_result {
 // workgroups of BG_NT threads of `kern` resident on the whole device at once (persistent
 // grid size; occupancy query x compute units, cached per kernel)
 uint32_t bg_resident_blocks(bg_ctx* c, const void* kern);
+
+// pinned host scratch valid until the next bg_pin_reset (the caller syncs before reading
+// device-to-host results); nullptr if pinned memory cannot be had
+void bg_pin_reset(bg_ctx* c);
+void* bg_pin_take(bg_ctx* c, size_t bytes);
 
 // allocator / error helpers (bg_api.cpp)
 void* bg_alloc(bg_ctx* c, size_t bytes);

@@ -259,16 +259,23 @@ __device__ __forceinline__ int64_t find_nl(const TileText& T, int64_t from) {
 // tile whose token differs from the previous line's, plus the tile's first line and the
 // next tile's first line. Grid-strided over the boundary list, whose length it reads on
 // the device (no host round trip between k_boundary and this kernel).
+// one chromosome-run record (copied to the host in one piece)
+struct RunRec {
+  int64_t pos;
+  uint64_t hash;
+  uint32_t len;
+  uint32_t pad;
+  char name[128];
+};
 __device__ __forceinline__ void put_record(const TileText& T, int64_t p, uint64_t h, int64_t tok,
-                                           uint32_t len, uint32_t cap, int64_t* rpos,
-                                           uint64_t* rhash, char* rname, uint32_t* rlen,
+                                           uint32_t len, uint32_t cap, RunRec* recs,
                                            uint32_t* nrec) {
   const uint32_t q = atomicAdd(nrec, 1u);
   if (q >= cap) return;  // the host reports the overflow
-  rpos[q] = p;
-  rhash[q] = h;
-  rlen[q] = len;
-  char* o = rname + 128ull * q;
+  recs[q].pos = p;
+  recs[q].hash = h;
+  recs[q].len = len;
+  char* o = recs[q].name;
   const uint32_t n = len < 127 ? len : 127;
   for (uint32_t i = 0; i < n; ++i) o[i] = (char)T.at(tok + i);
   o[n] = 0;
@@ -277,8 +284,7 @@ __device__ __forceinline__ void put_record(const TileText& T, int64_t p, uint64_
 __global__ void __launch_bounds__(BG_NT) k_tile_runs(
     const uint8_t* __restrict__ txt, uint64_t nb, const uint32_t* __restrict__ tiles,
     const uint32_t* __restrict__ ntiles_b, const int64_t* __restrict__ fls, uint32_t ntiles,
-    uint32_t cap, int64_t* __restrict__ rpos, uint64_t* __restrict__ rhash, char* __restrict__ rname,
-    uint32_t* __restrict__ rlen, uint32_t* __restrict__ nrec) {
+    uint32_t cap, RunRec* __restrict__ recs, uint32_t* __restrict__ nrec) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
   __shared__ uint16_t lst[TT + 1];
   __shared__ uint32_t shs[BG_NT / 64 + 1];
@@ -305,7 +311,7 @@ __global__ void __launch_bounds__(BG_NT) k_tile_runs(
         uint32_t plen;
         rec = line_token(T, t0 + lst[k - 1], ptok, plen) != h;
       }
-      if (rec) put_record(T, p, h, tok, len, cap, rpos, rhash, rname, rlen, nrec);
+      if (rec) put_record(T, p, h, tok, len, cap, recs, nrec);
     }
     if (threadIdx.x == 0) {  // first line of the next tile that has one
       uint32_t u = t + 1;
@@ -314,7 +320,7 @@ __global__ void __launch_bounds__(BG_NT) k_tile_runs(
         int64_t tok;
         uint32_t len;
         const uint64_t h = line_token(T, fls[u], tok, len);
-        put_record(T, fls[u], h, tok, len, cap, rpos, rhash, rname, rlen, nrec);
+        put_record(T, fls[u], h, tok, len, cap, recs, nrec);
       }
     }
   }
@@ -861,6 +867,12 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 // BG_BED3_SET staging: local components of tile t go to slots [t * SCAP, t * SCAP + SCAP).
 // A tile with more (8 KiB of rows shorter than 16 bytes, almost all disjoint) sets
 // BG_SET_OVERFLOW and bg_load re-reads that input with its row columns (BG_BED3).
+// 256-thread workgroups are admitted 8 per CU only with <= 80 SGPRs (MI355X_MICROARCH.md,
+// residency): capping the set kernel's SGPRs (a few spill to VGPR lanes) takes it from 6 to
+// 8 workgroups per CU, 1.73 -> 1.54 ms per 100M-row file
+#ifndef BG_SGPR_CAP
+#define BG_SGPR_CAP __attribute__((amdgpu_num_sgpr(80)))
+#endif
 #define SCAP 512
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
 
@@ -968,7 +980,7 @@ __device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* ls
 // one tile per workgroup. (Measured on MI355X and dropped: a persistent grid streaming the
 // next tile into a second LDS buffer by LDS-DMA while parsing this one — 2.3-2.4 vs 1.83 ms
 // per 100M-row file: this kernel is VALU-issue bound, not load-latency bound.)
-__global__ void __launch_bounds__(BG_NT) k_parse_set(
+__global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP k_parse_set(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
@@ -1027,18 +1039,48 @@ __global__ void __launch_bounds__(BG_NT) k_parse_set(
   }
 }
 
-// per tile: sort check against every earlier tile, and how many local components the
-// running max of the earlier tiles absorbs (M: exclusive prefix max of tmax)
-__global__ void k_set_count(const int64_t* __restrict__ LCS, SetTiles TS,
-                            const int64_t* __restrict__ mex, const int64_t* __restrict__ sex,
-                            uint32_t ntiles, uint64_t* __restrict__ cnt, bg_dstatus* st) {
+// per tile: sort check against the nearest earlier tile with rows (every tile is sorted
+// inside, or has reported it), how many local components the running max M of the
+// earlier tiles absorbs (mex = exclusive prefix max of tmax; the local starts increase,
+// so they are a prefix: a gallop from the front, usually 0 or 1 steps), and the tile's
+// rows summed into st->pad[1] (one atomic per workgroup)
+__global__ void __launch_bounds__(BG_NT) k_set_count(const int64_t* __restrict__ LCS, SetTiles TS,
+                                                     const int64_t* __restrict__ mex,
+                                                     uint32_t ntiles, uint64_t* __restrict__ cnt,
+                                                     bg_dstatus* st) {
+  __shared__ unsigned long long srows[BG_NT / 64];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const uint64_t b = TS.base[t], n = TS.nloc[t];
-  if (n > 0 && LCS[b] < sex[t]) bg_report(st, 0, ERR_UNSORTED);  // first row < an earlier row
-  const uint64_t a = n ? upper_bound_in(LCS, b, b + n, mex[t]) - b : 0;
-  TS.absorbed[t] = (uint32_t)a;
-  cnt[t] = n - a;
+  uint64_t rows = 0;
+  if (t < ntiles) {
+    const uint64_t b = TS.base[t], n = TS.nloc[t];
+    rows = TS.nrow[t];
+    if (n > 0 && t > 0) {
+      uint32_t u = t - 1;
+      while (u > 0 && TS.tlast[u] == LLONG_MIN) --u;  // tiles without rows (lines > 8 KiB)
+      if (LCS[b] < TS.tlast[u]) bg_report(st, 0, ERR_UNSORTED);  // first row < an earlier row
+    }
+    const int64_t M = mex[t];
+    uint64_t a = 0;
+    if (n && LCS[b] <= M) {
+      uint64_t step = 1;  // gallop, then bisect
+      while (a + step < n && LCS[b + a + step] <= M) {
+        a += step;
+        step <<= 1;
+      }
+      a = upper_bound_in(LCS, b + a + 1, b + min(n, a + step), M) - b;
+    }
+    TS.absorbed[t] = (uint32_t)a;
+    cnt[t] = n - a;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) rows += __shfl_xor(rows, d, 64);
+  if (bg_lane() == 0) srows[bg_wave()] = rows;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long r = 0;
+    for (int q = 0; q < BG_NT / 64; ++q) r += srows[q];
+    if (r) atomicAdd((unsigned long long*)&st->pad[1], r);
+  }
 }
 
 // one wave per tile: global components of the tile -> CS/CE at its offset. CE[g] is the
@@ -1104,24 +1146,20 @@ struct LoadState {
   uint64_t* fhash = nullptr;
   uint32_t* fnl = nullptr;
   uint32_t* blist = nullptr;
-  int64_t* rpos = nullptr;     // run records
-  uint64_t* rhash = nullptr;
-  char* rname = nullptr;
-  uint32_t* rlen = nullptr;
+  RunRec* recs = nullptr;      // run records (device)
   std::vector<int64_t> run_pos;
   std::vector<uint64_t> run_hash;
-  // host copies of the records
-  std::vector<int64_t> h_pos;
-  std::vector<uint64_t> h_hash;
-  std::vector<char> h_name;
-  std::vector<uint32_t> h_len;
+  // host copy of the records (pinned staging)
+  const RunRec* hrec = nullptr;
+  uint32_t nrec = 0;
+  uint64_t* hrow = nullptr;  // pinned: run -> first row (row loads)
   // phase 3
   std::vector<RunInfo> info;
   RunInfo* d_info = nullptr;
   uint64_t* d_row = nullptr;
   uint32_t* rlo = nullptr;
   uint32_t* rhi = nullptr;
-  std::vector<uint64_t> rows;
+  uint32_t nrows_run = 0;  // runs whose first row comes back (row loads)
   // BG_BED3_SET staging
   int64_t* lcs = nullptr;
   int64_t* lce = nullptr;
@@ -1137,7 +1175,7 @@ struct LoadState {
 
 static void release_state(bg_ctx* c, LoadState& S) {
   for (void* p : {(void*)S.row0, (void*)S.cnt, (void*)S.fls, (void*)S.fhash, (void*)S.fnl,
-                  (void*)S.blist, (void*)S.rpos, (void*)S.rhash, (void*)S.rname, (void*)S.rlen,
+                  (void*)S.blist, (void*)S.recs,
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
                   (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed})
@@ -1179,11 +1217,8 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   S.fls = (int64_t*)bg_alloc(c, 8ull * nt);
   S.fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.blist = (uint32_t*)bg_alloc(c, 4ull * nt);
-  S.rpos = (int64_t*)bg_alloc(c, 8ull * S.rc);
-  S.rhash = (uint64_t*)bg_alloc(c, 8ull * S.rc);
-  S.rname = (char*)bg_alloc(c, 128ull * S.rc);
-  S.rlen = (uint32_t*)bg_alloc(c, 4ull * S.rc);
-  if (!S.fls || !S.fhash || !S.blist || !S.rpos || !S.rhash || !S.rname || !S.rlen)
+  S.recs = (RunRec*)bg_alloc(c, sizeof(RunRec) * (size_t)S.rc);
+  if (!S.fls || !S.fhash || !S.blist || !S.recs)
     return BG_E_NOMEM;
   if (!set) {
     BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
@@ -1203,30 +1238,31 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
             S.blist, nbound);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_tile_runs", k_tile_runs, dim3(std::min<uint32_t>(nt, 1024)), dim3(BG_NT), txt,
-            S.nb, S.blist, nbound, S.fls, nt, S.rc, S.rpos, S.rhash, S.rname, S.rlen, nrec);
+            S.nb, S.blist, nbound, S.fls, nt, S.rc, S.recs, nrec);
   BG_HIP(c, hipGetLastError());
   return 0;
 }
 
 // phase 2 (host): the records of one input -> its chromosome runs, strcmp order checked
 static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadState& S) {
-  const uint32_t nr = (uint32_t)S.h_pos.size();
+  const uint32_t nr = S.nrec;
+  const RunRec* H = S.hrec;
   std::vector<uint32_t> ord(nr);
   for (uint32_t k = 0; k < nr; ++k) ord[k] = k;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return S.h_pos[a] < S.h_pos[b]; });
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return H[a].pos < H[b].pos; });
   T->run_name.clear();
   S.run_pos.clear();
   S.run_hash.clear();
   int64_t last_pos = -1;
   uint64_t last_hash = 0;
   for (uint32_t k : ord) {  // runs: records by position, consecutive duplicates removed
-    if (!S.run_pos.empty() && (last_pos == S.h_pos[k] || last_hash == S.h_hash[k])) continue;
-    if (S.h_len[k] > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
-    last_pos = S.h_pos[k];
-    last_hash = S.h_hash[k];
-    S.run_pos.push_back(S.h_pos[k]);
-    S.run_hash.push_back(S.h_hash[k]);
-    T->run_name.emplace_back(&S.h_name[128ull * k], strnlen(&S.h_name[128ull * k], 128));
+    if (!S.run_pos.empty() && (last_pos == H[k].pos || last_hash == H[k].hash)) continue;
+    if (H[k].len > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
+    last_pos = H[k].pos;
+    last_hash = H[k].hash;
+    S.run_pos.push_back(H[k].pos);
+    S.run_hash.push_back(H[k].hash);
+    T->run_name.emplace_back(H[k].name, strnlen(H[k].name, 128));
   }
   for (size_t k = 1; k < T->run_name.size(); ++k) {
     if (strcmp(T->run_name[k - 1].c_str(), T->run_name[k].c_str()) >= 0) {
@@ -1244,9 +1280,13 @@ static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSta
 static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
                        const std::map<std::string, int32_t>& gid, RunTable& R) {
   const uint32_t nr = (uint32_t)S.run_pos.size();
-  S.info.resize(nr);
+  RunInfo* info = (RunInfo*)bg_pin_take(c, sizeof(RunInfo) * nr);
+  if (!info) {
+    S.info.resize(nr);
+    info = S.info.data();
+  }
   for (uint32_t k = 0; k < nr; ++k) {
-    RunInfo& I = S.info[k];
+    RunInfo& I = info[k];
     const std::string& nm = T->run_name[k];
     I.pos = S.run_pos[k];
     I.hash = S.run_hash[k];
@@ -1262,7 +1302,7 @@ static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
   S.rlo = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
   S.rhi = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
   if (!S.d_info || !S.d_row || !S.rlo || !S.rhi) return BG_E_NOMEM;
-  BG_HIP(c, hipMemcpyAsync(S.d_info, S.info.data(), sizeof(RunInfo) * nr, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemcpyAsync(S.d_info, info, sizeof(RunInfo) * nr, hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemsetAsync(S.d_row, 0xff, 8ull * nr, c->stream));
   R = RunTable{S.d_info, S.d_row, nr};
   BG_LAUNCH(c, "k_run_range", k_run_range, dim3(bg_blocks(S.ntiles, 256)), dim3(256), R, S.ntiles,
@@ -1298,7 +1338,7 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, st);
   BG_HIP(c, hipGetLastError());
-  S.rows.resize(nr);  // copied back after every input's parse is queued
+  S.nrows_run = nr;  // copied back after every input's parse is queued
   return 0;
 }
 
@@ -1323,13 +1363,12 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
   S.tmax = (int64_t*)bg_alloc(c, 8ull * nt);
   S.tlast = (int64_t*)bg_alloc(c, 8ull * nt);
   S.mex = (int64_t*)bg_alloc(c, 8ull * nt);
-  S.sex = (int64_t*)bg_alloc(c, 8ull * nt);
   S.tbase = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.nloc = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.tcnt = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.absorbed = (uint32_t*)bg_alloc(c, 4ull * nt);
   S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);  // rows per tile
-  if (!S.lcs || !S.lce || !S.tmax || !S.tlast || !S.mex || !S.sex || !S.tbase || !S.nloc ||
+  if (!S.lcs || !S.lce || !S.tmax || !S.tlast || !S.mex || !S.tbase || !S.nloc ||
       !S.tcnt || !S.absorbed || !S.cnt)
     return BG_E_NOMEM;
   SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt};
@@ -1337,12 +1376,10 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
             S.lcs, S.lce, TS, st);
   BG_HIP(c, hipGetLastError());
   if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
-  if ((rc = bg_scan_max_i64(c, S.tlast, S.sex, nt, LLONG_MIN))) return rc;
-  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, 256)), dim3(256), S.lcs, TS, S.mex,
-            S.sex, nt, S.tcnt, st);
+  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, BG_NT)), dim3(BG_NT), S.lcs, TS,
+            S.mex, nt, S.tcnt, st);
   BG_HIP(c, hipGetLastError());
   if ((rc = bg_scan_sum_u64(c, S.tcnt, S.tcnt, nt, (uint64_t*)&st->pad[0]))) return rc;
-  if ((rc = bg_scan_sum_u64(c, S.cnt, S.cnt, nt, (uint64_t*)&st->pad[1]))) return rc;  // rows
   BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, BG_NT / 64)), dim3(BG_NT), S.lcs,
             S.lce, TS, S.mex, S.tcnt, nt, T->cs, T->ce);
   BG_HIP(c, hipGetLastError());
@@ -1371,11 +1408,11 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
   T->has_zero_len = (h.flags & 2ULL) != 0;
   T->maxlen = h.maxlen;
   // a trailing run may own only the dropped unterminated last line: no rows
-  uint32_t nkeep = (uint32_t)S.rows.size();
-  while (nkeep > 0 && S.rows[nkeep - 1] == ~0ULL) --nkeep;
+  uint32_t nkeep = S.hrow ? S.nrows_run : 0;
+  while (nkeep > 0 && S.hrow[nkeep - 1] == ~0ULL) --nkeep;
   T->run_name.resize(nkeep);
   T->run_row0.clear();
-  for (uint32_t k = 0; k < nkeep; ++k) T->run_row0.push_back(S.rows[k]);
+  for (uint32_t k = 0; k < nkeep; ++k) T->run_row0.push_back(S.hrow[k]);
   T->run_row0.push_back(T->n);
   return 0;
 }
@@ -1400,20 +1437,36 @@ static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>
     s->max_name_len = std::max<uint32_t>(s->max_name_len, len[k]);
     packed += all[k];
   }
-  s->d_names = (char*)bg_alloc(c, packed.size() + 16);
-  s->d_name_off = (uint32_t*)bg_alloc(c, 4 * off.size());
-  s->d_name_len = (uint32_t*)bg_alloc(c, 4 * len.size());
-  if (!s->d_names || !s->d_name_off || !s->d_name_len) return BG_E_NOMEM;
-  if (!packed.empty())
-    BG_HIP(c, hipMemcpyAsync(s->d_names, packed.data(), packed.size(), hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemcpyAsync(s->d_name_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice, c->stream));
-  BG_HIP(c, hipMemcpyAsync(s->d_name_len, len.data(), 4 * len.size(), hipMemcpyHostToDevice, c->stream));
+  // one device block: names (16-B padded) | offsets | lengths, one copy from pinned staging
+  const size_t nbn = (packed.size() + 16) & ~(size_t)15, nbo = 4 * off.size(), blk = nbn + 2 * nbo;
+  s->d_names = (char*)bg_alloc(c, blk);
+  if (!s->d_names) return BG_E_NOMEM;
+  s->d_name_off = (uint32_t*)(s->d_names + nbn);
+  s->d_name_len = (uint32_t*)(s->d_names + nbn + nbo);
+  char* h = (char*)bg_pin_take(c, blk);
+  std::vector<char> hv;
+  if (!h) {
+    hv.resize(blk);
+    h = hv.data();
+  }
+  memcpy(h, packed.data(), packed.size());
+  memcpy(h + nbn, off.data(), nbo);
+  memcpy(h + nbn + nbo, len.data(), nbo);
+  BG_HIP(c, hipMemcpyAsync(s->d_names, h, blk, hipMemcpyHostToDevice, c->stream));
+  if (!hv.empty()) BG_HIP(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 
 // Three host round trips per call, whatever the number of inputs: run-record counts, run
 // records, final statuses.
+#include <chrono>
+static double hp_now() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define HP(tag) do { if (hp) fprintf(stderr, "hp %-10s %9.1f\n", tag, hp_now() - hp0); } while (0)
 extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
+  static const bool hp = getenv("BEDGPU_HOSTPROF") != nullptr;
+  const double hp0 = hp ? hp_now() : 0;
   if (!c || n <= 0 || !inputs || !out) return BG_E_ARG;
   *out = nullptr;
   bg_set* s = new bg_set();
@@ -1422,58 +1475,69 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   // per input: 8 counters (phase 1) + one status block (phase 3)
   uint64_t* ctr = (uint64_t*)bg_alloc(c, 64ull * n);
   bg_dstatus* dst = (bg_dstatus*)bg_alloc(c, sizeof(bg_dstatus) * n);
-  std::vector<uint64_t> hctr(8ull * n);
-  std::vector<bg_dstatus> hst(n);
+  bg_pin_reset(c);
+  uint64_t* hctr = (uint64_t*)bg_pin_take(c, 64ull * n);
+  bg_dstatus* hst = (bg_dstatus*)bg_pin_take(c, sizeof(bg_dstatus) * n);
   std::string packed;
   std::vector<uint32_t> off, len;
   std::map<std::string, int32_t> gid;
-  int rc = (!ctr || !dst) ? BG_E_NOMEM : 0;
+  int rc = (!ctr || !dst || !hctr || !hst) ? BG_E_NOMEM : 0;
+  HP("alloc");
   if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(ctr, 0, 64ull * n, c->stream));
+  HP("memset");
   for (int i = 0; i < n && !rc; ++i) {
     s->t.push_back(new bg_table());
     rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
   }
+  HP("scout");
   // round trip 1: rows and record counts of every input
-  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hctr.data(), ctr, 64ull * n, hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hctr, ctr, 64ull * n, hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  HP("rt1");
   for (int i = 0; i < n && !rc; ++i) {
     LoadState& S = st[i];
     s->t[i]->n = S.ntiles ? hctr[8ull * i] : 0;
     const uint32_t nr = (uint32_t)hctr[8ull * i + 2];
     if (nr > S.rc) { rc = bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input"); break; }
-    S.h_pos.resize(nr);
-    S.h_hash.resize(nr);
-    S.h_name.resize(128ull * nr);
-    S.h_len.resize(nr);
+    S.nrec = nr;
     if (!nr) continue;
-    rc = bg_hip_ok(c, hipMemcpyAsync(S.h_pos.data(), S.rpos, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_hash.data(), S.rhash, 8ull * nr, hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_name.data(), S.rname, 128ull * nr, hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(S.h_len.data(), S.rlen, 4ull * nr, hipMemcpyDeviceToHost, c->stream));
+    RunRec* h = (RunRec*)bg_pin_take(c, sizeof(RunRec) * nr);
+    if (!h) { rc = BG_E_NOMEM; break; }
+    S.hrec = h;
+    rc = bg_hip_ok(c, hipMemcpyAsync(h, S.recs, sizeof(RunRec) * nr, hipMemcpyDeviceToHost, c->stream));
   }
   // round trip 2: the run records
+  HP("rec_copy");
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  HP("rt2");
   for (int i = 0; i < n && !rc; ++i) rc = runs_one(c, i, inputs[i], s->t[i], st[i]);
   bg_mark(c, "scout");
   if (!rc) rc = build_dictionary(c, s, gid, packed, off, len);
   if (!rc) {
-    for (auto& h : hst) {
-      memset(&h, 0, sizeof(h));
-      h.first_bad = ~0ULL;
+    for (int i = 0; i < n; ++i) {
+      memset(&hst[i], 0, sizeof(bg_dstatus));
+      hst[i].first_bad = ~0ULL;
     }
-    rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst.data(), sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
+    rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst, sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
   }
+  HP("dict");
   for (int i = 0; i < n && !rc; ++i)
     rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i)
                                        : parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
+  HP("parse_q");
   // round trip 3: statuses and run rows of every input (pageable copies block the host,
   // so they are issued only once all parses are queued)
   for (int i = 0; i < n && !rc; ++i)
-    if (!st[i].rows.empty())
-      rc = bg_hip_ok(c, hipMemcpyAsync(st[i].rows.data(), st[i].d_row, 8ull * st[i].rows.size(),
+    if (st[i].nrows_run) {
+      st[i].hrow = (uint64_t*)bg_pin_take(c, 8ull * st[i].nrows_run);
+      if (!st[i].hrow) { rc = BG_E_NOMEM; break; }
+      rc = bg_hip_ok(c, hipMemcpyAsync(st[i].hrow, st[i].d_row, 8ull * st[i].nrows_run,
                                        hipMemcpyDeviceToHost, c->stream));
-  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hst.data(), dst, sizeof(bg_dstatus) * n, hipMemcpyDeviceToHost, c->stream));
+    }
+  // (the status init above was read by the device before this copy overwrites it: stream order)
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hst, dst, sizeof(bg_dstatus) * n, hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  HP("rt3");
   // a BG_BED3_SET input with an error (its exact line is not known) or a staging overflow:
   // the whole load is redone with that input's row columns (BG_BED3)
   bool redo = false;
@@ -1482,7 +1546,7 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
         (hst[i].first_bad != ~0ULL || (hst[i].flags & BG_SET_OVERFLOW)))
       redo = true;
   for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
-  if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies read the host vectors
+  if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies use the pinned staging
   for (auto& S : st) release_state(c, S);
   bg_release(c, ctr);
   bg_release(c, dst);
@@ -1529,8 +1593,6 @@ extern "C" void bg_set_free(bg_set* s) {
     bg_release(c, T->score);
     delete T;
   }
-  bg_release(c, s->d_names);
-  bg_release(c, s->d_name_off);
-  bg_release(c, s->d_name_len);
+  bg_release(c, s->d_names);  // (offsets and lengths live in the same block)
   delete s;
 }
