@@ -894,8 +894,7 @@ __device__ __forceinline__ uint64_t wave_shr1_v(uint64_t v) { return wave_shr1_u
 struct SetLds {
   uint64_t xe[2][BG_NT / 64], xk[2][BG_NT / 64];  // wave max E / last K, by round parity
   uint32_t xc[2][BG_NT / 64];                     // wave component counts
-  unsigned long long kmax;                        // max K over the tile
-  uint32_t nrow;                                  // rows of the tile
+  uint64_t klast[2];  // K of the tile's last and second-to-last lines (0: not a row)
 };
 
 // The rounds of one tile: BG_NT lines per round, one per thread, in line order. V is the
@@ -952,14 +951,10 @@ __device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* ls
     const V ex_e = max(pe, wave_shr1_v(ie));
     const bool open = valid && K > ex_e;
     const uint64_t bal = __ballot(open);
-    const uint64_t bv = __ballot(valid);
-    if (lane == 0) {
-      X.xc[p][w] = (uint32_t)__popcll(bal);
-      atomicAdd(&X.nrow, (uint32_t)__popcll(bv));
-    }
-    // the tile's largest K is on the last valid line of some wave
-    if (valid && (lane == 63 || !((bv >> (lane + 1)) & 1ULL)))
-      atomicMax(&X.kmax, (unsigned long long)K);
+    if (lane == 0) X.xc[p][w] = (uint32_t)__popcll(bal);
+    // the tile's largest K (sorted rows): its last line's, or the one before when the last
+    // line is the file's dropped unterminated tail (any other non-row is an error)
+    if (k + 2 >= L && k < L) X.klast[L - 1 - k] = K;
     __syncthreads();
     uint64_t pos = nc + __popcll(bal & lt), tot = 0;
 #pragma unroll
@@ -989,7 +984,7 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP k_parse_set(
   const uint32_t tile = blockIdx.x;
   const int64_t t0 = (int64_t)tile * TT;
   const uint64_t base = (uint64_t)tile * SCAP;
-  if (threadIdx.x == 0) { X.kmax = 0; X.nrow = 0; }
+  if (threadIdx.x == 0) X.klast[0] = X.klast[1] = 0;
   int64_t last_end;
   uint32_t L;
   {
@@ -1021,7 +1016,7 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP k_parse_set(
   } else {
     set_rounds<uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
   }
-  __syncthreads();  // kmax / nrow complete (also when the tile has no lines)
+  __syncthreads();  // klast complete (also when the tile has no lines)
 #if defined(BG_EXP) && (BG_EXP == 3 || BG_EXP == 4)
   if (cmax == 12345) LCS[base] = 1;
 #endif
@@ -1032,10 +1027,11 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP k_parse_set(
     }
     if (nc > 0) LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
     TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
-    TS.tlast[tile] = X.kmax ? (gbase | (int64_t)(X.kmax - 1)) : LLONG_MIN;
+    const uint64_t kmax = X.klast[0] ? X.klast[0] : X.klast[1];
+    TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
     TS.base[tile] = base;
     TS.nloc[tile] = nc;
-    TS.nrow[tile] = X.nrow;
+    TS.nrow[tile] = L - ((L > 0 && last_end < 0) ? 1 : 0);  // (errors fail the load anyway)
   }
 }
 
