@@ -1082,24 +1082,54 @@ __global__ void __launch_bounds__(BG_NT) k_set_count(const int64_t* __restrict__
 // one wave per tile: global components of the tile -> CS/CE at its offset. CE[g] is the
 // running max just before component g+1 opens, written by the tile holding that opening
 // (the last one by the last tile).
+#define SW_TILES 64  // tiles per k_set_write workgroup
 __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__ LCS,
                                                      const int64_t* __restrict__ LCE, SetTiles TS,
                                                      const int64_t* __restrict__ mex,
                                                      const uint64_t* __restrict__ off,
                                                      uint32_t ntiles, int64_t* __restrict__ CS,
                                                      int64_t* __restrict__ CE) {
-  const uint32_t t = blockIdx.x * (BG_NT / 64) + bg_wave();
-  if (t >= ntiles) return;
-  const uint64_t b = TS.base[t], n = TS.nloc[t], a = TS.absorbed[t], g0 = off[t];
-  const int64_t M = mex[t];
-  for (uint64_t j = a + bg_lane(); j < n; j += 64) {
-    const uint64_t g = g0 + (j - a);
-    CS[g] = LCS[b + j];
-    if (g > 0) CE[g - 1] = (j == a) ? max(M, a > 0 ? LCE[b + a - 1] : LLONG_MIN) : LCE[b + j - 1];
+  // SW_TILES tiles per workgroup, their surviving components flattened over all threads
+  // (element e -> its tile by a search of the LDS prefix of counts): every load of a
+  // workgroup is independent, instead of a wave waiting on one tile's descriptor first
+  __shared__ uint32_t cpre[SW_TILES + 1];
+  __shared__ uint64_t src[SW_TILES], dst[SW_TILES];
+  __shared__ int64_t first_end[SW_TILES];  // CE value before the tile's first global component
+  const uint32_t t0 = blockIdx.x * SW_TILES;
+  const uint32_t nt = min((uint32_t)SW_TILES, ntiles - t0);
+  uint32_t c = 0;
+  if (threadIdx.x < nt) {
+    const uint32_t t = t0 + threadIdx.x;
+    const uint64_t b = TS.base[t], n = TS.nloc[t], a = TS.absorbed[t];
+    const int64_t M = mex[t];
+    c = (uint32_t)(n - a);
+    src[threadIdx.x] = b + a;
+    dst[threadIdx.x] = off[t];
+    first_end[threadIdx.x] = (c > 0) ? max(M, a > 0 ? LCE[b + a - 1] : LLONG_MIN) : 0;
+    if (t + 1 == ntiles) {  // the last component ends at the running max of everything
+      const uint64_t total = off[t] + c;
+      if (total > 0) CE[total - 1] = max(M, TS.tmax[t]);
+    }
   }
-  if (t + 1 == ntiles && bg_lane() == 0) {
-    const uint64_t total = g0 + (n - a);
-    if (total > 0) CE[total - 1] = max(M, TS.tmax[t]);
+  // exclusive scan of c over the first wave (SW_TILES == 64)
+  if (threadIdx.x < 64) {
+    const uint32_t inc = wave_incl_scan(c, OpSum());
+    cpre[threadIdx.x + 1] = inc;
+    if (threadIdx.x == 0) cpre[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t tot = cpre[nt];
+  for (uint32_t e = threadIdx.x; e < tot; e += BG_NT) {
+    uint32_t lo = 0, hi = nt - 1;  // last q with cpre[q] <= e
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (cpre[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t j = e - cpre[lo];
+    const uint64_t g = dst[lo] + j, sidx = src[lo] + j;
+    CS[g] = LCS[sidx];
+    if (g > 0) CE[g - 1] = j == 0 ? first_end[lo] : LCE[sidx - 1];
   }
 }
 
@@ -1376,7 +1406,7 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
             S.mex, nt, S.tcnt, st);
   BG_HIP(c, hipGetLastError());
   if ((rc = bg_scan_sum_u64(c, S.tcnt, S.tcnt, nt, (uint64_t*)&st->pad[0]))) return rc;
-  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, BG_NT / 64)), dim3(BG_NT), S.lcs,
+  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, SW_TILES)), dim3(BG_NT), S.lcs,
             S.lce, TS, S.mex, S.tcnt, nt, T->cs, T->ce);
   BG_HIP(c, hipGetLastError());
   return 0;

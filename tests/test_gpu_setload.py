@@ -165,3 +165,27 @@ def test_set_load_coordinates_past_32_bits(eng, oracle_bin):
             want = run_oracle(oracle_bin["bedops"], [mode], [a, b], td)
         assert eng.bedops(mode, [a, b], set_load=False) == want, mode  # (printing >= 2^32)
         assert eng.bedops(mode, [a, b]) == want, mode
+
+
+def test_chrom_spans_of_set_results(eng):
+    """the per-chromosome byte spans the multi-GPU gather uses, on set-loaded results"""
+    rng = random.Random(31)
+    chroms = ["chr1", "chr10", "chr2", "chr3", "chrX"]
+    a = randbed.text(randbed.rows(rng, 20000, chroms=chroms[:4], span=10**6, maxlen=300)).encode()
+    b = randbed.text(randbed.rows(rng, 20000, chroms=chroms[1:], span=10**6, maxlen=300)).encode()
+    from bedops_amd.engine import BED3_SET
+    s = eng.load([(a, BED3_SET), (b, BED3_SET)])
+    try:
+        names = s.chroms()
+        for mode in ("-i", "-m", "-d"):
+            r = eng.op(mode, s, [0, 1])
+            txt = r.text()
+            sp = r.chrom_spans(len(names))
+            assert sp[-1] == len(txt)
+            for g, nm in enumerate(names):
+                part = txt[sp[g]:sp[g + 1]]
+                want = b"".join(ln + b"\n" for ln in txt.split(b"\n") if ln.split(b"\t")[0] == nm.encode())
+                assert part == want, (mode, nm)
+            r.free()
+    finally:
+        s.free()
