@@ -84,116 +84,105 @@ __device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, i
   return 0;
 }
 
-// replay ref rows [b0, b1) from state S; emit: write left/right. false on overflow
+// replay ref rows [b0, b1) from state S; emit: write left/right. false on overflow.
+//
+// One candidate per iteration, in the order the reference reads them (the cache stack
+// first, then the file). The reference's branch chain (ClosestFeature.cpp:284-401) is
+// evaluated as flags: every case below sets some of
+//   reset   : the kept list is emptied (a new best left)
+//   keepL/R/C: the current left / right / this candidate is appended to the kept list,
+//             always in that order
+//   left, right, ld, rdist, lc (leftCached) updates, brk (the scan of b ends)
+// and the updates are applied with selects: the lanes of a wave take different cases on
+// almost every candidate, and a nested if-chain made each wave issue every case's
+// exec-mask bookkeeping in turn (SALU-bound: ~700 scalar instructions per candidate).
+//   case                                   reference lines
+//   d = -inf (earlier chromosome)          skip                           :289-291
+//   d < 0, d >= ld  (newleft)              reset; left = c                :300-305
+//   d < 0, d <  ld  (dropL)                keepL(!lc); lc = 1             :306-309
+//   d = +inf                               keepL; keepR; keepC; brk       :292-298
+//   d > 0, d < rdist (firstR)              keepL; right = c; keepC; brk   :315-323
+//   d > 0, else (farR)                     keepL; keepR; keepC; brk       :324-330
+//   d = 0, overlaps, cs <= bs (hangL)      keepL unless ce[left] <= ce; left = c, ld = 0
+//   d = 0, overlaps, be <= ce (hangR)      keepL; keepR; right = c, rdist = 0
+//   d = 0, overlaps, inside: by the centroid proportion (:227-239, :355-388)
+//   d = 0, no-overlaps (noov)              keepL (lc = 1); keepC          :389-397
 __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, uint32_t* kept,
                        bool emit) {
   const uint32_t cap = A.cap;
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
+    const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
     int64_t ld = D_MINUS, rdist = D_PLUS;
-    int64_t left = -1, right = -1, c = -1;
+    int64_t left = -1, right = -1, lce = 0;  // lce = ce[left]
     bool lc = false;  // leftCached
     uint32_t nk = 0;  // the std::list "read" of findDistances
-    bool ovf = false;
+    bool ovf = false, eof = false;
 #define KEEP(x)                      \
   do {                               \
     if (nk == cap) ovf = true;       \
     else kept[nk++] = (uint32_t)(x); \
   } while (0)
     for (;;) {
+      int64_t c;
       if (S.n) c = S.c[--S.n];
       else if (S.fp < A.nc) c = (int64_t)S.fp++;
-      else { c = -1; break; }
+      else { eof = true; break; }
       const int64_t cs = A.cs[c], ce = A.ce[c];
       const int64_t d = cl_dist(cs, ce, bs, be);
       if (d == D_MINUS) continue;  // earlier chromosome: dropped
-      if (d == D_PLUS) {           // later chromosome: keep for the next rows
-        if (left >= 0 && !lc) KEEP(left);
-        lc = left >= 0;
-        if (right >= 0) KEEP(right);
-        KEEP(c);
-        break;
-      }
-      if (d < 0 && d >= ld) {  // new best left: everything kept so far is dropped
+      const bool hasL = left >= 0, hasR = right >= 0;
+      const bool plus = d == D_PLUS;
+      const bool neg = d < 0;
+      const bool pos = d > 0 && !plus;
+      const bool newleft = neg && d >= ld;
+      const bool dropL = neg && !newleft;
+      const bool firstR = pos && d < rdist;
+      const bool farR = pos && !firstR;
+      const bool ovl = d == 0 && A.overlaps;
+      const bool noov = d == 0 && !A.overlaps;
+      const bool hangL = ovl && cs <= bs;
+      const bool hangR = ovl && !hangL && be <= ce;
+      const bool inside = ovl && !hangL && !hangR;
+      const double cst = (double)(cs & BG_COORD_MASK);
+      const double prop =
+          cen < cst ? 0.0
+                    : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
+      const bool half = prop < 0.5;
+      const bool in_a = inside && ld == 0 && half;    // keepL(!lc), lc = 1, keepR, right = c
+      const bool in_b = inside && ld == 0 && !half;   // keepL(!lc), lc = 1, keepC
+      const bool in_c = inside && ld != 0 && !half;   // reset, left = c, ld = 0, lc = 0
+      const bool in_d = inside && ld != 0 && half;    // keepL, keepR, right = c
+      const bool reset = newleft || in_c;
+      const bool keepL = hasL && !lc &&
+                         (plus || firstR || farR || hangR || in_d || noov || dropL || in_a || in_b ||
+                          (hangL && !(lce <= ce)));
+      const bool keepR = hasR && (plus || farR || hangR || in_a || in_d);
+      const bool keepC = plus || firstR || farR || in_b || noov;
+      if (reset) {
         nk = 0;
         ovf = false;
-        ld = d;
-        left = c;
-        lc = false;
-      } else if (d < 0) {  // an earlier row that ends sooner: dropped
-        if (!lc) KEEP(left);
-        lc = true;
-      } else if (d > 0 && d < rdist) {  // first row to the right
-        if (left >= 0 && !lc) KEEP(left);
-        lc = left >= 0;
-        rdist = d;
-        right = c;
-        KEEP(c);
-        break;
-      } else if (d > 0) {  // one row too far (right already overlapping)
-        if (left >= 0 && !lc) KEEP(left);
-        lc = left >= 0;
-        if (right >= 0) KEEP(right);
-        KEEP(c);
-        break;
-      } else if (A.overlaps) {  // overlap
-        if (cs <= bs) {  // hangs over the left edge
-          if (left >= 0 && A.ce[left] <= ce && !lc) {
-            // the old left is never the closest left again: dropped
-          } else if (left >= 0 && !lc) {
-            KEEP(left);
-          }
-          left = c;
-          ld = 0;
-          lc = false;
-        } else if (be <= ce) {  // hangs over the right edge
-          if (left >= 0 && !lc) KEEP(left);
-          lc = left >= 0;
-          if (right >= 0) KEEP(right);
-          right = c;
-          rdist = 0;
-        } else {  // inside b: side by the centroid proportion
-          const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
-          const double cst = (double)(cs & BG_COORD_MASK);
-          const double prop =
-              cen < cst ? 0.0
-                        : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
-          if (ld == 0) {
-            if (prop < 0.5) {
-              if (!lc) KEEP(left);
-              lc = true;
-              if (right >= 0) KEEP(right);
-              right = c;
-              rdist = 0;
-            } else {
-              if (!lc) KEEP(left);
-              lc = true;
-              KEEP(c);
-            }
-          } else if (prop >= 0.5) {
-            nk = 0;
-            ovf = false;
-            lc = false;
-            left = c;
-            ld = 0;
-          } else {
-            if (left >= 0 && !lc) KEEP(left);
-            lc = left >= 0;
-            if (right >= 0) KEEP(right);
-            right = c;
-            rdist = 0;
-          }
-        }
-      } else {  // overlap with --no-overlaps: kept for later rows
-        if (left >= 0 && !lc) {
-          KEEP(left);
-          lc = true;
-        }
-        KEEP(c);
       }
+      if (keepL) KEEP(left);
+      if (keepR) KEEP(right);
+      if (keepC) KEEP(c);
+      // lc: set to hasL when the scan moves on past the left, 1 when the left was cached,
+      // cleared by a new left
+      const bool lc_hasl = plus || firstR || farR || hangR || in_d;
+      const bool lc_one = dropL || in_a || in_b || (noov && hasL);
+      const bool lc_zero = newleft || hangL || in_c;
+      lc = lc_zero ? false : (lc_one ? true : (lc_hasl ? hasL : lc));
+      const bool setleft = newleft || hangL || in_c;
+      left = setleft ? c : left;
+      lce = setleft ? ce : lce;
+      ld = newleft ? d : ((hangL || in_c) ? 0 : ld);
+      const bool setright = firstR || hangR || in_a || in_d;
+      right = setright ? c : right;
+      rdist = firstR ? d : ((hangR || in_a || in_d) ? 0 : rdist);
+      if (plus || pos) break;
     }
-    if (c < 0 && left >= 0 && !lc) KEEP(left);
-    if (c < 0 && right >= 0) KEEP(right);
+    if (eof && left >= 0 && !lc) KEEP(left);
+    if (eof && right >= 0) KEEP(right);
 #undef KEEP
     // BedReader::PushBack(list): the list comes back out in list order
     if (ovf || S.n + nk > cap) return false;
