@@ -90,6 +90,39 @@ __device__ __forceinline__ void put_u64(Out& o, uint64_t v, int len) {
   o.adv(len);
 }
 
+// 4 ASCII digits of x (< 10000) as a little-endian dword, first digit in the low byte:
+// x/100 and x%100 into the two 16-bit halves, then /10 and %10 on both halves at once
+// (24-bit multiplies; the quotients are exact for these ranges)
+__device__ __forceinline__ uint32_t dig4_ascii(uint32_t x) {
+  const uint32_t h = __umul24(x, 5243u) >> 19;              // x / 100
+  const uint32_t v = h | ((x - 100u * h) << 16);             // pairs: hi | lo << 16
+  const uint32_t t = (__umul24(v, 103u) >> 10) & 0x000F000Fu;  // tens of both pairs
+  const uint32_t u = v - 10u * t;                            // units of both pairs
+  return (t | (u << 8)) + 0x30303030u;
+}
+
+// v (< 10^12) as exactly len digits into LDS: three 4-digit groups, then byte stores
+__device__ __forceinline__ void put_u64_lds(char* p, uint64_t v, int len) {
+  uint32_t hi, mid, lo;
+  if ((v >> 32) == 0) {
+    const uint32_t w = (uint32_t)v;
+    const uint32_t q = w / 10000u;
+    lo = w - q * 10000u;
+    hi = q / 10000u;
+    mid = q - hi * 10000u;
+  } else {
+    const uint64_t q = v / 10000u;
+    lo = (uint32_t)(v - q * 10000u);
+    hi = (uint32_t)(q / 10000u);
+    mid = (uint32_t)(q - (uint64_t)hi * 10000u);
+  }
+  const uint32_t g[3] = {dig4_ascii(hi), dig4_ascii(mid), dig4_ascii(lo)};
+  const int sk = 12 - len;  // leading zero characters to skip
+#pragma unroll
+  for (int i = 0; i < 12; ++i)
+    if (i >= sk) p[i - sk] = (char)(g[i >> 2] >> (8 * (i & 3)));
+}
+
 // exact %.{prec}f of |v| split as integer N = round_half_even(|v| * 10^prec) (< 2^64);
 // returns false if out of this path's range
 __device__ __forceinline__ bool fixed_digits(double v, int prec, uint64_t& N, bool& neg) {
@@ -156,6 +189,16 @@ struct LdsOut {
   __device__ __forceinline__ void adv(int k) { p += k; }
   __device__ __forceinline__ void put(char c) { *p++ = c; }
 };
+// coordinates (< 10^12, at most 12 digits): SWAR digit groups where the sink is memory
+__device__ __forceinline__ void put_coord(LdsOut& o, uint64_t v, int len) {
+  if (len <= 12) {
+    put_u64_lds(o.p, v, len);
+    o.adv(len);
+  } else {
+    put_u64(o, v, len);
+  }
+}
+__device__ __forceinline__ void put_coord(CountOut& o, uint64_t, int len) { o.adv(len); }
 
 template <typename Out>
 __device__ __forceinline__ void put_i64(Out& o, int64_t v) {
@@ -178,9 +221,9 @@ __device__ __forceinline__ void put_row(const FmtArgs& A, Out& o, int64_t s, int
   for (uint32_t q = 0; q < nl; ++q) o.put(nm[q]);
   o.put('\t');
   const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
-  put_u64(o, cs, dec_len_u64(cs));
+  put_coord(o, cs, dec_len_u64(cs));
   o.put('\t');
-  put_u64(o, ce, dec_len_u64(ce));
+  put_coord(o, ce, dec_len_u64(ce));
   for (uint32_t q = 0; q < rl; ++q) o.put(rest[q]);
 }
 
@@ -294,9 +337,9 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
   for (uint32_t q = 0; q < nl; ++q) o.put(nm[q]);
   o.put('\t');
   const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
-  put_u64(o, cs, dec_len_u64(cs));
+  put_coord(o, cs, dec_len_u64(cs));
   o.put('\t');
-  put_u64(o, ce, dec_len_u64(ce));
+  put_coord(o, ce, dec_len_u64(ce));
   if (KIND == RES_ROWS) {
     const uint32_t rl = A.rest_len[r];
     const char* rp = A.text + A.rest_off[r];
@@ -371,6 +414,73 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   }
   __syncthreads();
   // stream buf[skew, skew + tot) -> out[dst0, dst0 + tot)
+  const uint64_t a0 = dst0, a1 = dst0 + tot;
+  const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;
+  const char* bb = buf + skew;
+  if (al0 >= al1) {
+    for (uint64_t p = a0 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+    return;
+  }
+  for (uint64_t p = a0 + threadIdx.x; p < al0; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT)
+    *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
+}
+
+// RES_IVL rows ("%s\t%lu\t%lu\n"): thread t renders rows 2t and 2t+1 of the tile, both
+// loaded up front as 16-byte pairs, so one block scan of the per-thread byte counts places
+// them (k_fmt_write's general form scans once per row stripe and reloads each row to
+// render it)
+__device__ __forceinline__ uint32_t ivl_len(const FmtArgs& A, int64_t s, int64_t e) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  return A.name_len[g] + 3u + (uint32_t)dec_len_u64((uint64_t)(s & BG_COORD_MASK)) +
+         (uint32_t)dec_len_u64((uint64_t)(e & BG_COORD_MASK));
+}
+__device__ __forceinline__ void ivl_put(const FmtArgs& A, char* p, int64_t s, int64_t e) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  const uint32_t nl = A.name_len[g];
+  const char* nm = A.names + A.name_off[g];
+  for (uint32_t q = 0; q < nl; ++q) p[q] = nm[q];
+  p += nl;
+  *p++ = '\t';
+  const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
+  const int l1 = dec_len_u64(cs), l2 = dec_len_u64(ce);
+  put_u64_lds(p, cs, l1);
+  p += l1;
+  *p++ = '\t';
+  put_u64_lds(p, ce, l2);
+  p[l2] = '\n';
+}
+
+__global__ void __launch_bounds__(BG_NT) k_fmt_ivl_write(FmtArgs A, const uint64_t* __restrict__ toff,
+                                                         char* __restrict__ out) {
+  __shared__ uint32_t sh[BG_NT / 64 + 1];
+  __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
+  static_assert(FT_ROWS == 2, "two rows per thread");
+  const uint64_t r0 = (uint64_t)blockIdx.x * FT_TILE + 2ull * threadIdx.x;
+  int64_t s0 = 0, e0 = 0, s1 = 0, e1 = 0;
+  const bool v0 = r0 < A.n, v1 = r0 + 1 < A.n;
+  if (v1) {
+    const longlong2 S = reinterpret_cast<const longlong2*>(A.s)[r0 >> 1];
+    const longlong2 E = reinterpret_cast<const longlong2*>(A.e)[r0 >> 1];
+    s0 = S.x; s1 = S.y; e0 = E.x; e1 = E.y;
+  } else if (v0) {
+    s0 = A.s[r0];
+    e0 = A.e[r0];
+  }
+  const uint32_t l0 = v0 ? ivl_len(A, s0, e0) : 0u, l1 = v1 ? ivl_len(A, s1, e1) : 0u;
+  uint32_t tot;
+  const uint32_t my = block_excl_scan(l0 + l1, OpSum(), 0u, sh, &tot);
+  const uint64_t dst0 = toff[blockIdx.x];
+  if (tot > FT_LDS) {  // oversized tile (long names): render straight to HBM
+    if (v0) ivl_put(A, out + dst0 + my, s0, e0);
+    if (v1) ivl_put(A, out + dst0 + my + l0, s1, e1);
+    return;
+  }
+  const uint32_t skew = (uint32_t)(dst0 & 15);
+  if (v0) ivl_put(A, buf + skew + my, s0, e0);
+  if (v1) ivl_put(A, buf + skew + my + l0, s1, e1);
+  __syncthreads();
   const uint64_t a0 = dst0, a1 = dst0 + tot;
   const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;
   const char* bb = buf + skew;
@@ -479,7 +589,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!r->text) return BG_E_NOMEM;
   if (nb) {
     switch (A.kind) {
-      case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_IVL>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_write, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_MAP: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_MULTI: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MULTI>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
