@@ -494,6 +494,30 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_ivl_write(FmtArgs A, const uint64
     *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
 }
 
+// bytes of every FT_TILE-row tile of a RES_IVL result: the same two-rows-per-thread
+// layout as k_fmt_ivl_write, one block reduction per tile
+__global__ void __launch_bounds__(BG_NT) k_fmt_ivl_count(FmtArgs A, uint64_t* __restrict__ tb) {
+  __shared__ uint32_t sh[BG_NT / 64];
+  const uint64_t r0 = (uint64_t)blockIdx.x * FT_TILE + 2ull * threadIdx.x;
+  uint32_t l = 0;
+  if (r0 + 1 < A.n) {
+    const longlong2 S = reinterpret_cast<const longlong2*>(A.s)[r0 >> 1];
+    const longlong2 E = reinterpret_cast<const longlong2*>(A.e)[r0 >> 1];
+    l = ivl_len(A, S.x, E.x) + ivl_len(A, S.y, E.y);
+  } else if (r0 < A.n) {
+    l = ivl_len(A, A.s[r0], A.e[r0]);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) l += __shfl_xor(l, d, 64);
+  if (bg_lane() == 0) sh[bg_wave()] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int q = 0; q < BG_NT / 64; ++q) t += sh[q];
+    tb[blockIdx.x] = t;
+  }
+}
+
 static void fill_args(bg_result* r, FmtArgs& A) {
   memset(&A, 0, sizeof(A));
   bg_set* s = r->set;
@@ -570,7 +594,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   if (nb) {
     switch (A.kind) {
-      case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_IVL>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_ivl_count, dim3(nb), dim3(BG_NT), A, tb); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
       case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
       case RES_MULTI: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MULTI>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
