@@ -172,6 +172,40 @@ __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt
   }
 }
 
+// line_token's hash of the line at ls from three aligned 16-byte loads, when the line
+// starts with its token (no leading whitespace) of at most 16 bytes ending within 32
+// bytes; false: the caller takes the byte loop
+__device__ __forceinline__ bool token_hash_fast(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                int64_t ls, uint64_t& h) {
+  const int64_t a = ls & ~15LL;
+  if ((uint64_t)a + 48 > nb) return false;
+  const uint4 x = *reinterpret_cast<const uint4*>(txt + a);
+  const uint4 y = *reinterpret_cast<const uint4*>(txt + a + 16);
+  const uint4 z = *reinterpret_cast<const uint4*>(txt + a + 32);
+  const uint32_t d[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
+  const uint32_t o = (uint32_t)(ls - a);  // 0..15
+  const uint32_t wo = o >> 2, bo = o & 3;
+  uint32_t W[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // bytes [ls, ls + 32) as dwords
+    uint32_t lo = d[0], hi = d[1];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (wo == (uint32_t)k) { lo = d[i + k]; hi = d[i + k + 1]; }
+    if (wo == 0) { lo = d[i]; hi = d[i + 1]; }
+    W[i] = bgp_align(lo, hi, bo);
+  }
+  uint32_t WS, DG;
+  bgp_classify8(W, WS, DG);  // whitespace class includes '\n'
+  if (WS & 1u) return false;  // leading whitespace or a blank line
+  if (!(WS & 0x1FFFEu)) return false;  // token longer than 16 bytes (or no end in sight)
+  const uint32_t len = bgp_ctz(WS);
+  const uint64_t lo8 = (uint64_t)W[0] | ((uint64_t)W[1] << 32);
+  const uint64_t hi8 = (uint64_t)W[2] | ((uint64_t)W[3] << 32);
+  h = bgp_hash16(lo8, hi8, len);
+  return true;
+}
+
 // first owned line of each tile and the hash of its chromosome token (one thread per
 // tile, reads a few bytes). fnl: first '\n' per tile from k_scout, or nullptr: found here
 // by a forward scan (BG_BED3_SET loads have no scout pass)
@@ -204,7 +238,7 @@ __global__ void k_tokhash(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t
   else if (f + 1 < TT) ls = t0 + f + 1;
   if (ls >= 0 && (uint64_t)ls >= nb) ls = -1;
   uint64_t h = 0;
-  if (ls >= 0) {
+  if (ls >= 0 && !token_hash_fast(txt, nb, ls, h)) {
     TileText T{txt, txt, 0, 0, nb};  // global reads only
     int64_t tok;
     uint32_t len;
