@@ -6,8 +6,10 @@
  * with "--", the last one or two arguments are files, --delim/--prec/--sci/
  * --skip-unmapped/--bp-ovr/--chrom/--ec/--header/--faster/--sweep-all); output per
  * reference row is the operations' values in command-line order joined by --delim
- * (MultiVisitor.hpp:83-98). GPU path: --count and --mean with the default overlap
- * rule (--bp-ovr N); other operations and overlap criteria are reported as not
+ * (MultiVisitor.hpp:83-98). GPU path: --count --mean --sum --min --max --indicator
+ * --bases --bases-uniq --bases-uniq-f --echo --echo-ref-size --echo-ref-name under any
+ * overlap option (--bp-ovr --range --fraction-{ref,map,either,both} --exact; checks and
+ * messages of Input.hpp:143-215,330-345); other operations are reported as not
  * available in this build.
  */
 #include "cli_common.h"
@@ -25,11 +27,17 @@ static void usage(FILE* f) {
           "      --ec / --header       Error check / accept header lines.\n"
           "      --prec <int>          Change the post-decimal precision of scores to <int>.\n"
           "      --skip-unmapped       Print no output for a row with no mapped elements.\n\n"
-          "    Overlap Options:\n"
-          "      --bp-ovr <int>        Require <int> bp overlap (default 1).\n\n"
+          "    Overlap Options (At most, one may be selected.  By default, --bp-ovr 1 is used):\n"
+          "      --bp-ovr <int>           Require <int> bp overlap between elements of input files.\n"
+          "      --exact                  First 3 fields from <map-file> must be identical to <ref-file>'s.\n"
+          "      --fraction-both <val>    Both --fraction-ref <val> and --fraction-map <val> must be true.\n"
+          "      --fraction-either <val>  Either --fraction-ref <val> or --fraction-map <val> must be true.\n"
+          "      --fraction-map <val>     The fraction of the element's size from <map-file> that must overlap.\n"
+          "      --fraction-ref <val>     The fraction of the element's size from <ref-file> that must overlap.\n"
+          "      --range <int>            Grab <map-file> elements within <int> bp of <ref-file>'s element.\n\n"
           "    Operations (GPU path):\n"
-          "      --count               The number of overlapping elements in <map-file>.\n"
-          "      --mean                The average score from overlapping elements in <map-file>.\n",
+          "      --bases --bases-uniq --bases-uniq-f --count --echo --echo-ref-name --echo-ref-size\n"
+          "      --indicator --max --mean --min --sum\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -45,7 +53,13 @@ int main(int argc, char** argv) {
   o.overlap_bp = 1;
   o.precision = 6;
   strcpy(o.delim, "|");
-  int ec = 0, need5 = 0, set_prec = 0, set_delim = 0;
+  int ec = 0, need5 = 0, need_rest = 0, set_prec = 0, set_delim = 0;
+  int is_bp = 0, is_range = 0, range_alias = 0, is_exact = 0, is_frac[4] = {0, 0, 0, 0};
+  static const struct { const char* name; int op; } OPS[] = {
+      {"count", BG_MAP_COUNT}, {"mean", BG_MAP_MEAN}, {"sum", BG_MAP_SUM}, {"min", BG_MAP_MIN},
+      {"max", BG_MAP_MAX}, {"indicator", BG_MAP_INDICATOR}, {"bases", BG_MAP_BASES},
+      {"bases-uniq", BG_MAP_BASES_UNIQ}, {"bases-uniq-f", BG_MAP_BASES_UNIQ_F}, {"echo", BG_MAP_ECHO},
+      {"echo-ref-size", BG_MAP_ECHO_SIZE}, {"echo-ref-name", BG_MAP_ECHO_NAME}};
   const char* chrom = NULL;
   int a = 1;
   while (a < argc) {
@@ -85,6 +99,8 @@ int main(int argc, char** argv) {
       o.precision = atoi(v);
       set_prec = 1;
     } else if (!strcmp(k, "bp-ovr")) {
+      if (range_alias) arg_error("--range and --bp-ovr detected.  Choose one.");
+      if (is_bp) arg_error("multiple --bp-ovr's detected");
       if (a >= argc) arg_error("No arg for --bp-ovr");
       const char* v = argv[a++];
       if (strspn(v, "0123456789") != strlen(v)) {
@@ -94,20 +110,67 @@ int main(int argc, char** argv) {
       }
       o.overlap_bp = strtoull(v, NULL, 10);
       if (o.overlap_bp == 0) arg_error("--bp-ovr value must be > 0");
-    } else if (!strcmp(k, "count")) {
-      if (o.n_ops >= 16) arg_error("too many operations for this build");
-      o.ops[o.n_ops++] = BG_MAP_COUNT;
-    } else if (!strcmp(k, "mean")) {
-      if (o.n_ops >= 16) arg_error("too many operations for this build");
-      o.ops[o.n_ops++] = BG_MAP_MEAN;
-      need5 = 1;
-    } else {
+      is_bp = 1;
+    } else if (!strcmp(k, "range")) {
+      if (is_range || range_alias) arg_error("multiple --range's detected");
+      if (a >= argc) arg_error("No arg for --range");
+      const char* v = argv[a++];
+      if (strspn(v, "0123456789") != strlen(v)) {
+        char b[512];
+        snprintf(b, sizeof(b), "Non-positive-integer argument: %s for --range", v);
+        arg_error(b);
+      }
+      o.range_bp = strtoull(v, NULL, 10);
+      is_range = 1;
+      if (o.range_bp == 0) {  /* alias for --bp-ovr 1 (Input.hpp:165-171) */
+        if (is_bp) arg_error("--bp-ovr and --range detected.  Choose one.");
+        is_range = 0;
+        is_bp = 1;
+        range_alias = 1;
+        o.overlap_bp = 1;
+      }
+    } else if (!strncmp(k, "fraction-", 9) &&
+               (!strcmp(k + 9, "ref") || !strcmp(k + 9, "map") || !strcmp(k + 9, "either") || !strcmp(k + 9, "both"))) {
+      const int which = !strcmp(k + 9, "ref") ? 0 : !strcmp(k + 9, "map") ? 1 : !strcmp(k + 9, "either") ? 2 : 3;
       char b[512];
-      snprintf(b, sizeof(b), "--%s is not available in this build (GPU path: --count --mean, --bp-ovr)", k);
-      arg_error(b);
+      if (is_frac[which]) { snprintf(b, sizeof(b), "multiple --%s's detected", k); arg_error(b); }
+      if (a >= argc) { snprintf(b, sizeof(b), "No arg for --%s", k); arg_error(b); }
+      const char* v = argv[a++];
+      if (strspn(v, ".-0123456789") != strlen(v)) {
+        snprintf(b, sizeof(b), "Non-numeric argument: %s for --%s", v, k);
+        arg_error(b);
+      }
+      o.fraction = strtod(v, NULL);
+      if (!(o.fraction > 0 && o.fraction <= 1)) { snprintf(b, sizeof(b), "--%s value must be: >0-1.0", k); arg_error(b); }
+      is_frac[which] = 1;
+      static const int crit[4] = {BG_OVR_FRAC_REF, BG_OVR_FRAC_MAP, BG_OVR_FRAC_EITHER, BG_OVR_FRAC_BOTH};
+      o.criterion = crit[which];
+    } else if (!strcmp(k, "exact")) {
+      if (is_exact) arg_error("multiple --exact's detected - use one");
+      is_exact = 1;
+    } else {
+      int op = 0;
+      for (size_t q = 0; q < sizeof(OPS) / sizeof(OPS[0]); ++q)
+        if (!strcmp(k, OPS[q].name)) op = OPS[q].op;
+      if (!op) {
+        char b[512];
+        snprintf(b, sizeof(b), "--%s is not available in this build (GPU path: see --help)", k);
+        arg_error(b);
+      }
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.ops[o.n_ops++] = op;
+      if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX) need5 = 1;
+      if (op == BG_MAP_ECHO) need_rest = 1;
     }
   }
-  if (o.n_ops == 0) arg_error("No processing option specified (ie; --count).");
+  {  /* one overlap specification (Input.hpp:330-343) */
+    const int count = is_frac[0] + is_frac[1] + is_frac[2] + is_frac[3] + is_range + is_bp + is_exact;
+    if (count > 1) arg_error("More than one overlap specification used.");
+    if (is_range) o.criterion = BG_OVR_RANGE;
+    else if (is_exact) o.criterion = BG_OVR_EXACT;
+    else if (is_bp || count == 0) o.criterion = BG_OVR_BP;
+  }
+  if (o.n_ops == 0) arg_error("No processing option specified (ie; --max).");
   int nf = argc - a;
   if (nf < 1 || nf > 2) arg_error("Need one or two input files");
   for (int i = a; i < argc; ++i) {
@@ -129,7 +192,7 @@ int main(int argc, char** argv) {
   in[0].data = tr.data;
   in[0].nbytes = tr.n;
   in[0].on_device = 0;
-  in[0].kind = BG_BED3;
+  in[0].kind = need_rest ? BG_BED3_REST : BG_BED3;
   if (nf == 2) {
     if (read_text(argv[a + 1], &tm)) arg_error("Unable to read the map file");
     if (ec) apply_ec_header(&tm);

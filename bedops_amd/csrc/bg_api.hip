@@ -376,6 +376,10 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->rlen);
   bg_release(c, r->cnt);
   bg_release(c, r->isum);
+  bg_release(c, r->vmin);
+  bg_release(c, r->vmax);
+  bg_release(c, r->bases);
+  bg_release(c, r->uniq);
   bg_release(c, r->left);
   bg_release(c, r->right);
   bg_release(c, r->text);

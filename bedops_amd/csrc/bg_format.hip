@@ -38,6 +38,10 @@ struct FmtArgs {
   // map
   const int32_t* cnt;
   const int64_t* isum;
+  const double* vmin;
+  const double* vmax;
+  const uint64_t* bases;
+  const uint32_t* uniq;
   int nops;
   int ops[16];
   int prec;
@@ -308,23 +312,67 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
     return true;
   }
   if (KIND == RES_MAP) {
+    // one value per operation (MultiVisitor.hpp:83-98); formats: Count/Indicator "%d",
+    // OvrAggregate "%lu", OvrUnique "%u", Echo (ProcessBedVisitorRow.hpp:309-342), the rest
+    // "%.{p}lf" or "NAN" (PrintScorePrecision, Formats.hpp:42-50)
     const int32_t c = A.cnt[k];
     if (A.skip_unmapped && c == 0) return true;
     for (int q = 0; q < A.nops; ++q) {
-      if (q) for (int d = 0; d < A.dlen; ++d) o.put(A.delim[d]);
-      if (A.ops[q] == BG_MAP_COUNT) {
-        if (c < 0) { o.put('-'); put_u64(o, (uint64_t)(-(int64_t)c), dec_len_u64((uint64_t)(-(int64_t)c))); }
-        else put_u64(o, (uint64_t)c, dec_len_u64((uint64_t)c));
-      } else {
-        if (c <= 0) { o.put('N'); o.put('A'); o.put('N'); }
-        else {
-          const double mean = (double)A.isum[k] / (double)c;
-          uint64_t N;
-          bool neg;
-          if (!fixed_digits(mean, A.prec, N, neg)) return false;
-          put_fixed(o, N, neg, A.prec);
-        }
+      if (q) put_delim(A, o);
+      const int op = A.ops[q];
+      if (op == BG_MAP_COUNT) {
+        put_i64(o, (int64_t)c);
+        continue;
       }
+      if (op == BG_MAP_INDICATOR) {
+        o.put(c > 0 ? '1' : '0');
+        continue;
+      }
+      if (op == BG_MAP_BASES) {
+        put_u64(o, A.bases[k], dec_len_u64(A.bases[k]));
+        continue;
+      }
+      if (op == BG_MAP_BASES_UNIQ) {
+        put_u64(o, (uint64_t)A.uniq[k], dec_len_u64((uint64_t)A.uniq[k]));
+        continue;
+      }
+      if (op == BG_MAP_ECHO) {
+        put_row(A, o, A.s[k], A.e[k], A.text + A.rest_off[k], A.rest_len[k]);
+        continue;
+      }
+      if (op == BG_MAP_ECHO_SIZE) {
+        const uint64_t len = (uint64_t)(A.e[k] - A.s[k]);
+        put_u64(o, len, dec_len_u64(len));
+        continue;
+      }
+      if (op == BG_MAP_ECHO_NAME) {  // "chrom:start-end"
+        const uint32_t g = (uint32_t)(A.s[k] >> BG_KEY_SHIFT);
+        const char* nm = A.names + A.name_off[g];
+        for (uint32_t i = 0; i < A.name_len[g]; ++i) o.put(nm[i]);
+        o.put(':');
+        const uint64_t cs = (uint64_t)(A.s[k] & BG_COORD_MASK), ce = (uint64_t)(A.e[k] & BG_COORD_MASK);
+        put_u64(o, cs, dec_len_u64(cs));
+        o.put('-');
+        put_u64(o, ce, dec_len_u64(ce));
+        continue;
+      }
+      double v;
+      if (op == BG_MAP_BASES_UNIQ_F) {
+        v = (double)A.uniq[k] / (double)(A.e[k] - A.s[k]);
+      } else if (c <= 0) {
+        o.put('N'); o.put('A'); o.put('N');
+        continue;
+      } else if (op == BG_MAP_MEAN) {
+        v = (double)A.isum[k] / (double)c;
+      } else if (op == BG_MAP_SUM) {
+        v = (double)A.isum[k];
+      } else {
+        v = (op == BG_MAP_MIN) ? A.vmin[k] : A.vmax[k];
+      }
+      uint64_t N;
+      bool neg;
+      if (!fixed_digits(v, A.prec, N, neg)) return false;
+      put_fixed(o, N, neg, A.prec);
     }
     o.put('\n');
     return true;
@@ -567,6 +615,13 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.e = s->t[r->tab]->ke;
     A.cnt = r->cnt;
     A.isum = r->isum;
+    A.vmin = r->vmin;
+    A.vmax = r->vmax;
+    A.bases = r->bases;
+    A.uniq = r->uniq;
+    A.text = s->t[r->tab]->text;  // --echo: the reference rows' remainders
+    A.rest_off = s->t[r->tab]->rest_off;
+    A.rest_len = s->t[r->tab]->rest_len;
     A.nops = r->mopts.n_ops;
     for (int k = 0; k < A.nops; ++k) A.ops[k] = r->mopts.ops[k];
     A.prec = r->mopts.precision;

@@ -125,8 +125,12 @@ struct bg_result {
   uint32_t* rlen = nullptr;
   int tab = -1;
   // RES_MAP: per reference row columns
-  int32_t* cnt = nullptr;
-  int64_t* isum = nullptr;
+  int32_t* cnt = nullptr;    // rows in S(r) (Count, Indicator, --skip-unmapped)
+  int64_t* isum = nullptr;   // exact integer score sum (Average, Sum)
+  double* vmin = nullptr;    // Extreme (min / max score)
+  double* vmax = nullptr;
+  uint64_t* bases = nullptr; // OvrAggregate
+  uint32_t* uniq = nullptr;  // OvrUnique (unsigned int, as the reference)
   bg_map_opts mopts;
   // RES_CLOSEST: per row of table `tab`, the chosen rows of table `tab2` (-1: NA)
   int64_t* left = nullptr;

@@ -271,8 +271,19 @@ __device__ __forceinline__ uint32_t tile_line_starts(const uint4& v0, const uint
   for (int k = 0; k < 8; ++k) nlg |= bgp_group4(nl_mask4(w[k])) << (4 * k);
   // a '\n' on the tile's last byte starts a line in the next tile
   if (threadIdx.x == BG_NT - 1) nlg &= 0x7FFFFFFFu;
-  uint32_t tot;
-  uint32_t o = block_excl_scan((uint32_t)__popc(nlg), OpSum(), 0u, shs, &tot) + (has0 ? 1u : 0u);
+  // exclusive sum of the newline counts over the block: one barrier (every thread adds up
+  // the wave totals itself; the barrier at the end protects shs from its next use)
+  const uint32_t inc = wave_incl_scan((uint32_t)__popc(nlg), OpSum());
+  if (bg_lane() == 63) shs[bg_wave()] = inc;
+  __syncthreads();
+  uint32_t tot = 0, wpre = 0;
+#pragma unroll
+  for (int q = 0; q < BG_NT / 64; ++q) {
+    const uint32_t x = shs[q];
+    if (q < bg_wave()) wpre += x;
+    tot += x;
+  }
+  uint32_t o = wpre + inc - (uint32_t)__popc(nlg) + (has0 ? 1u : 0u);
   if (threadIdx.x == 0 && has0) ls[0] = 0;
   for (uint32_t m = nlg; m; m &= m - 1) {  // one iteration per line start
     if (o < cap) ls[o] = (uint16_t)(threadIdx.x * 32 + bgp_ctz(m) + 1);
@@ -1006,10 +1017,15 @@ __device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* ls
   }
 }
 
-// one tile per workgroup. (Measured on MI355X and dropped: a persistent grid streaming the
+// one tile per workgroup, 8 waves per SIMD (<= 64 VGPRs). (Measured on MI355X and dropped:
+// two lines per thread with one scan pass per tile instead of one per 256 lines — 1.53 ms
+// either way once held to 64 VGPRs, 1.59 at 67; a persistent grid streaming the
 // next tile into a second LDS buffer by LDS-DMA while parsing this one — 2.3-2.4 vs 1.83 ms
 // per 100M-row file: this kernel is VALU-issue bound, not load-latency bound.)
-__global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP k_parse_set(
+#ifndef BG_SET_WAVES
+#define BG_SET_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+__global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {

@@ -1,50 +1,194 @@
-// bg_map.hip — K5: bedmap <ops> ref map with the default overlap rule (--bp-ovr N).
+// bg_map.hip — K5: bedmap <operations> ref map, under every overlap criterion.
 //
 // Reference: WindowSweep::sweep overload 2 (interfaces/src/algorithm/sweep/
-// WindowSweepImpl.cpp:168-256) keeps a deque window of map rows; BedBaseVisitor::
-// fixWindow (algorithm/visitors/bed/BedBaseVisitor.hpp:184-215) re-tests the window
-// against each reference row with Overlapping(N) (data/bed/BedDistances.hpp:95-115),
-// and Count / Average (numerical/CountVisitor.hpp, AverageVisitor.hpp) accumulate.
-// For every reference row r that yields the multiset
-//   S(r) = { m : same chrom, min(r.e, m.e) - max(r.s, m.s) >= N }
-// (verified by randomized differential tests against the reference).
-// GPU form: map rows are start-sorted, so with L = max map length (computed by the
-// loader) every m in S(r)
-// has m.s in [r.s - L + 1, r.e): two binary searches bound the candidates, one
-// thread per reference row accumulates count and the exact integer score sum.
-// Exactness: the reference keeps ONE running double across the file
-// (AverageVisitor.hpp:46-54); it equals our exact per-row sum whenever scores are
-// integers and partial sums stay below 2^53. Other inputs are refused
-// (BG_E_UNSUPPORTED) rather than approximated; so are zero-length rows, on which the
-// reference's stream consumption differs from S(r).
+// WindowSweepImpl.cpp:168-256) keeps a deque window of map rows under the SWEEP distance
+// (Overlapping(0), or RangedDist(R) for --range: applications/bed/bedmap/src/Bedmap.cpp:
+// 95-155); BedBaseVisitor::fixWindow (algorithm/visitors/bed/BedBaseVisitor.hpp:184-215)
+// keeps the members whose VISITOR distance Map2Ref(map, ref) is 0, and the visitors
+// aggregate over that final window. For every reference row r that yields the multiset
+//   S(r) = { m : same chrom, m in the sweep window of r, criterion(r, m) }
+// with the criteria of data/bed/BedDistances.hpp (Overlapping :80-118, RangedDist :41-67,
+// PercentOverlapMapping/Reference/Either/Both :123-288 in the reference's double
+// arithmetic, Exact :293-317). Verified against the oracle's restatement of the sweep
+// (oracle/bedmap_oracle.c) by randomized differential tests (tests/test_gpu_parity.py).
+// GPU form: map rows are start-sorted, so with L = the longest map row every candidate
+// starts in [r.s - R - L + 1, r.e + R) (R = 0 except --range), clamped to r's chromosome.
+// Each workgroup bounds the candidate range of its 256 rows with two searches over the
+// whole map table; each row's own searches then run over that cache-resident slice, and
+// one thread per reference row walks its candidates in start order, accumulating
+//   count, exact integer score sum, min / max score, Σ overlap bp (OvrAggregate
+//   OvrAggregateVisitor.hpp:77-97) and the bp of r covered by the union of S(r)
+//   (OvrUnique, OvrUniqueVisitor.hpp:62-78: pieces merged in genomic order).
+// Exactness: Average/Sum keep ONE running double across the file (AverageVisitor.hpp:46-54,
+// SumVisitor.hpp:47-51); it equals the exact per-row integer sum whenever scores are
+// integers and partial sums stay below 2^53. Other inputs are refused (BG_E_UNSUPPORTED)
+// rather than approximated; so are zero-length rows. Min/max involve no
+// arithmetic and take any score.
+#include <cfloat>
 #include <climits>
 
 #include "bg_internal.h"
 
-__global__ void __launch_bounds__(BG_NT) k_map_count_sum(
-    const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
-    const int64_t* __restrict__ MS, const int64_t* __restrict__ ME, const double* __restrict__ SC,
-    uint64_t nm, int64_t L, int64_t ovr, int32_t* __restrict__ cnt, int64_t* __restrict__ isum,
-    bg_dstatus* st) {
-  const uint64_t r = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (r >= nr) return;
-  const int64_t s = RS[r], e = RE[r];
-  const uint64_t lo = lower_bound_i64(MS, nm, s - L + 1);
-  const uint64_t hi = lower_bound_i64(MS, nm, e);
+#define NEED_SUM 1u
+#define NEED_EXT 2u
+#define NEED_BASES 4u
+#define NEED_UNIQ 8u
+
+struct MapArgs {
+  const int64_t* RS;
+  const int64_t* RE;
+  uint64_t nr;
+  const int64_t* MS;
+  const int64_t* ME;
+  const double* SC;
+  uint64_t nm;
+  int64_t L;       // longest map row
+  int64_t ovr;     // --bp-ovr
+  int64_t range;   // --range R
+  double perc;     // PercentOverlapMapping::perc_ (set up on the host as its constructor does)
+  uint32_t need;   // NEED_* columns to compute
+  int32_t* cnt;
+  int64_t* isum;
+  double* vmin;
+  double* vmax;
+  uint64_t* bases;
+  uint32_t* uniq;
+  bg_dstatus* st;
+};
+
+__device__ __forceinline__ int64_t wmax64(int64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (int64_t)__shfl_xor(v, d, 64));
+  return v;
+}
+
+// m in S(r)? Keys of one chromosome: differences and comparisons are the coordinates'.
+template <int CRIT>
+__device__ __forceinline__ bool map_in(int64_t s, int64_t e, int64_t ms, int64_t me,
+                                       const MapArgs& A) {
+  if (CRIT == BG_OVR_RANGE) return (s < me) ? (e + A.range > ms) : (me + A.range > s);
+  const int64_t ov = min(e, me) - max(s, ms);
+  if (ov <= 0) return false;  // outside the sweep's Overlapping(0) window
+  if (CRIT == BG_OVR_BP) return ov >= A.ovr;
+  if (CRIT == BG_OVR_EXACT) return ms == s && me == e;
+  if (A.perc <= DBL_EPSILON) return true;
+  // sz of BedDistances.hpp:160-174 is the overlap length for overlapping rows
+  const bool fm = (double)ov / (double)(me - ms) >= A.perc;  // relative to the map row
+  const bool fr = (double)ov / (double)(e - s) >= A.perc;    // relative to the ref row
+  if (CRIT == BG_OVR_FRAC_MAP) return fm;
+  if (CRIT == BG_OVR_FRAC_REF) return fr;
+  if (CRIT == BG_OVR_FRAC_EITHER) return fm || fr;
+  return fm && fr;
+}
+
+// first index k in [lo, hi) with X[k] >= v, X in LDS
+__device__ __forceinline__ uint32_t lds_lower_bound(const int64_t* X, uint32_t lo, uint32_t hi,
+                                                    int64_t v) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (X[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+#define MAP_SLICE 3072  // map starts staged per workgroup (24 KiB of LDS)
+
+template <int CRIT>
+__global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
+  __shared__ int64_t wmax[BG_NT / 64];
+  __shared__ uint64_t bnd[2];
+  __shared__ int64_t xs[MAP_SLICE];  // the workgroup's candidate starts, when they fit
+  const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
+  const uint64_t r = r0 + threadIdx.x;
+  const bool live = r < A.nr;
+  const int64_t s = live ? A.RS[r] : 0, e = live ? A.RE[r] : 0;
+  const int64_t g = s & ~BG_COORD_MASK;  // the row's chromosome in key space
+  const int64_t pad = (CRIT == BG_OVR_RANGE) ? A.range : 0;
+  const int64_t klo = max(g, s - pad - A.L + 1);                   // non-decreasing in r
+  const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad);
+  const int64_t hm = wmax64(live ? khi : LLONG_MIN);
+  if (bg_lane() == 0) wmax[bg_wave()] = hm;
+  __syncthreads();
+  if (threadIdx.x == 0) bnd[0] = lower_bound_i64(A.MS, A.nm, klo);  // row r0 is live
+  if (threadIdx.x == 64) {
+    int64_t m = wmax[0];
+    for (int w = 1; w < BG_NT / 64; ++w) m = max(m, wmax[w]);
+    bnd[1] = lower_bound_i64(A.MS, A.nm, m);
+  }
+  __syncthreads();
+  const uint64_t blo = bnd[0], bhi = max(bnd[0], bnd[1]);
+  // the slice every row of this workgroup searches: staged in LDS when it fits (a search
+  // level then costs an LDS read instead of an L2 round trip)
+  const bool staged = bhi - blo <= MAP_SLICE;
+  if (staged) {
+    for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) xs[i] = A.MS[blo + i];
+    __syncthreads();
+  }
+  if (!live) return;
+  uint64_t lo, hi;
+  if (staged) {
+    const uint32_t n = (uint32_t)(bhi - blo);
+    const uint32_t l = lds_lower_bound(xs, 0, n, klo);
+    lo = blo + l;
+    hi = blo + lds_lower_bound(xs, l, n, khi);
+  } else {
+    lo = lower_bound_in(A.MS, blo, bhi, klo);
+    hi = lower_bound_in(A.MS, lo, bhi, khi);
+  }
   int32_t c = 0;
   int64_t sum = 0;
-  for (uint64_t m = lo; m < hi; ++m) {
-    const int64_t ov = min(e, ME[m]) - max(s, MS[m]);
-    if (ov >= ovr) {
+  double vmin = 0, vmax = 0;
+  uint64_t bases = 0;
+  uint32_t uniq = 0;                // unsigned int arithmetic, as OvrUnique's
+  int64_t us = 0, ue = LLONG_MIN;  // current union piece
+  // candidates in groups of MU: the group's loads are issued together (they are
+  // independent; one at a time, every candidate paid a cache round trip)
+  constexpr int MU = 4;
+  for (uint64_t m0 = lo; m0 < hi; m0 += MU) {
+    int64_t ms[MU], me[MU];
+    double sc[MU];
+#pragma unroll
+    for (int j = 0; j < MU; ++j) {
+      const uint64_t m = min(m0 + j, hi - 1);
+      ms[j] = staged ? xs[m - blo] : A.MS[m];
+      me[j] = A.ME[m];
+      if (A.need & (NEED_SUM | NEED_EXT)) sc[j] = A.SC[m];
+    }
+#pragma unroll
+    for (int j = 0; j < MU; ++j) {
+      if (m0 + j >= hi || !map_in<CRIT>(s, e, ms[j], me[j], A)) continue;
+      if (A.need & (NEED_SUM | NEED_EXT)) {
+        const double x = sc[j];
+        sum += (int64_t)x;
+        if (c == 0) vmin = vmax = x;
+        else {
+          if (x < vmin) vmin = x;
+          if (x > vmax) vmax = x;
+        }
+      }
       ++c;
-      if (SC) sum += (int64_t)SC[m];
+      if (A.need & NEED_BASES) bases += (uint64_t)max(min(e, me[j]) - max(s, ms[j]), (int64_t)0);
+      if (A.need & NEED_UNIQ) {
+        if (ms[j] < ue) {  // overlaps the current piece (rows come in start order)
+          ue = max(ue, me[j]);
+        } else {
+          if (ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
+          us = ms[j];
+          ue = me[j];
+        }
+      }
     }
   }
-  cnt[r] = c;
-  if (isum) {
-    isum[r] = sum;
-    if (sum >= (1LL << 53) || sum <= -(1LL << 53)) atomicOr(&st->flags, 4ULL);
+  if ((A.need & NEED_UNIQ) && ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
+  A.cnt[r] = c;
+  if (A.isum) {
+    A.isum[r] = sum;
+    if (sum >= (1LL << 53) || sum <= -(1LL << 53)) atomicOr(&A.st->flags, 4ULL);
   }
+  if (A.vmin) { A.vmin[r] = vmin; A.vmax[r] = vmax; }
+  if (A.bases) A.bases[r] = bases;
+  if (A.uniq) A.uniq[r] = uniq;
 }
 
 extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts* opts,
@@ -57,44 +201,116 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     int rc0 = bg_need_rows(c, set, f, 2, "bedmap");
     if (rc0) return rc0;
   }
-  bool need_score = false;
-  for (int k = 0; k < opts->n_ops; ++k) {
-    if (opts->ops[k] == BG_MAP_MEAN) need_score = true;
-    else if (opts->ops[k] != BG_MAP_COUNT) return bg_fail(c, BG_E_UNSUPPORTED, "bedmap operation not on the GPU path");
-  }
-  if (opts->scientific) return bg_fail(c, BG_E_UNSUPPORTED, "--sci is not on the GPU path yet");
-  if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
-  if (opts->overlap_bp < 1) return BG_E_ARG;
   bg_table* R = set->t[ref];
   bg_table* M = set->t[map];
-  if (need_score && (M->kind != BG_BED5 || !M->score)) return bg_fail(c, BG_E_ARG, "--mean needs the map file loaded as BG_BED5");
+  uint32_t need = 0;
+  bool need_sum = false, need_ext = false;
+  for (int k = 0; k < opts->n_ops; ++k) {
+    switch (opts->ops[k]) {
+      case BG_MAP_COUNT: case BG_MAP_INDICATOR: case BG_MAP_ECHO_SIZE: case BG_MAP_ECHO_NAME: break;
+      case BG_MAP_MEAN: case BG_MAP_SUM: need_sum = true; break;
+      case BG_MAP_MIN: case BG_MAP_MAX: need_ext = true; break;
+      case BG_MAP_BASES: need |= NEED_BASES; break;
+      case BG_MAP_BASES_UNIQ: case BG_MAP_BASES_UNIQ_F: need |= NEED_UNIQ; break;
+      case BG_MAP_ECHO:
+        if (!R->rest_off) return bg_fail(c, BG_E_ARG, "--echo needs the reference file loaded as BG_BED3_REST");
+        break;
+      default: return bg_fail(c, BG_E_UNSUPPORTED, "bedmap operation not on the GPU path");
+    }
+  }
+  if (need_sum) need |= NEED_SUM;
+  if (need_ext) need |= NEED_EXT;
+  if (opts->scientific) return bg_fail(c, BG_E_UNSUPPORTED, "--sci is not on the GPU path yet");
+  if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
+  const int crit = opts->criterion;
+  double perc = 1.0;
+  switch (crit) {
+    case BG_OVR_BP:
+      if (opts->overlap_bp < 1) return BG_E_ARG;
+      break;
+    case BG_OVR_RANGE:
+      if (opts->range_bp < 1 || opts->range_bp > (uint64_t)BG_COORD_MASK) return BG_E_ARG;
+      break;
+    case BG_OVR_FRAC_REF: case BG_OVR_FRAC_MAP: case BG_OVR_FRAC_EITHER: case BG_OVR_FRAC_BOTH:
+      if (!(opts->fraction > 0.0 && opts->fraction <= 1.0)) return BG_E_ARG;
+      // PercentOverlapMapping's constructor (BedDistances.hpp:126-136), same host doubles
+      perc = opts->fraction;
+      while (perc > 1) perc /= 10.0;
+      perc -= DBL_EPSILON;
+      if (perc <= 0.0) perc = DBL_EPSILON;
+      break;
+    case BG_OVR_EXACT: break;
+    default: return BG_E_ARG;
+  }
+  if ((need & (NEED_SUM | NEED_EXT)) && (M->kind != BG_BED5 || !M->score))
+    return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
   if (R->has_zero_len || M->has_zero_len)
     return bg_fail(c, BG_E_UNSUPPORTED, "zero-length elements (end == start) are not on the GPU path of bedmap");
-  if (need_score && !M->score_int)
-    return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean yet");
+  if (need_sum && !M->score_int)
+    return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean/--sum yet");
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
-  int32_t* cnt = (int32_t*)bg_alloc(c, 4 * (R->n ? R->n : 1));
-  int64_t* isum = need_score ? (int64_t*)bg_alloc(c, 8 * (R->n ? R->n : 1)) : nullptr;
-  if (!cnt || (need_score && !isum)) return BG_E_NOMEM;
-  const int64_t L = M->maxlen > 0 ? M->maxlen : 1;  // longest map row (from the loader)
-  if (R->n)
-    BG_LAUNCH(c, "k_map_count_sum", k_map_count_sum, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
-                       R->ks, R->ke, R->n, M->ks, M->ke, need_score ? M->score : nullptr, M->n, L,
-                       (int64_t)opts->overlap_bp, cnt, isum, c->dstat);
-  BG_HIP(c, hipGetLastError());
-  BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  if (c->hstat->flags & 4ULL)
-    return bg_fail(c, BG_E_UNSUPPORTED, "a window score sum reaches 2^53 (inexact in the reference too)");
+  const uint64_t n1 = R->n ? R->n : 1;
   bg_result* res = new bg_result();
   res->ctx = c;
   res->set = set;
   res->kind = RES_MAP;
   res->n = R->n;
-  res->cnt = cnt;
-  res->isum = isum;
   res->mopts = *opts;
   res->tab = ref;
+  res->cnt = (int32_t*)bg_alloc(c, 4 * n1);
+  if (need & NEED_SUM) res->isum = (int64_t*)bg_alloc(c, 8 * n1);
+  if (need & NEED_EXT) {
+    res->vmin = (double*)bg_alloc(c, 8 * n1);
+    res->vmax = (double*)bg_alloc(c, 8 * n1);
+  }
+  if (need & NEED_BASES) res->bases = (uint64_t*)bg_alloc(c, 8 * n1);
+  if (need & NEED_UNIQ) res->uniq = (uint32_t*)bg_alloc(c, 4 * n1);
+  if (!res->cnt || ((need & NEED_SUM) && !res->isum) || ((need & NEED_EXT) && (!res->vmin || !res->vmax)) ||
+      ((need & NEED_BASES) && !res->bases) || ((need & NEED_UNIQ) && !res->uniq)) {
+    bg_result_free(res);
+    return BG_E_NOMEM;
+  }
+  MapArgs A;
+  A.RS = R->ks;
+  A.RE = R->ke;
+  A.nr = R->n;
+  A.MS = M->ks;
+  A.ME = M->ke;
+  A.SC = (need & (NEED_SUM | NEED_EXT)) ? M->score : nullptr;
+  A.nm = M->n;
+  A.L = M->maxlen > 0 ? M->maxlen : 1;  // longest map row (from the loader)
+  A.ovr = (int64_t)opts->overlap_bp;
+  A.range = (int64_t)opts->range_bp;
+  A.perc = perc;
+  A.need = need;
+  A.cnt = res->cnt;
+  A.isum = res->isum;
+  A.vmin = res->vmin;
+  A.vmax = res->vmax;
+  A.bases = res->bases;
+  A.uniq = res->uniq;
+  A.st = c->dstat;
+  if (R->n) {
+    const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);
+    switch (crit) {
+      case BG_OVR_BP: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_BP>, g, b, A); break;
+      case BG_OVR_RANGE: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_RANGE>, g, b, A); break;
+      case BG_OVR_FRAC_REF: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_REF>, g, b, A); break;
+      case BG_OVR_FRAC_MAP: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_MAP>, g, b, A); break;
+      case BG_OVR_FRAC_EITHER: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_EITHER>, g, b, A); break;
+      case BG_OVR_FRAC_BOTH: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_BOTH>, g, b, A); break;
+      default: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_EXACT>, g, b, A); break;
+    }
+  }
+  int rc = bg_hip_ok(c, hipGetLastError());
+  if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  if (!rc && (c->hstat->flags & 4ULL))
+    rc = bg_fail(c, BG_E_UNSUPPORTED, "a window score sum reaches 2^53 (inexact in the reference too)");
+  if (rc) {
+    bg_result_free(res);
+    return rc;
+  }
   *out = res;
   bg_mark(c, "map");
   return 0;

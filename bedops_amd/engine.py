@@ -16,6 +16,13 @@ BED3, BED3_REST, BED5, BED3_SET = 0, 1, 2, 3
 SET_MODES = {"-m", "--merge", "-i", "--intersect", "-d", "--difference", "-e", "--element-of",
              "-n", "--not-element-of", "-c", "--complement", "-w", "--chop", "-s", "--symmdiff"}
 MAP_COUNT, MAP_MEAN = 1, 2
+# bedmap operations and overlap criteria (include/bedgpu.h BG_MAP_* / BG_OVR_*)
+MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, "bases": 7,
+           "bases-uniq": 8, "bases-uniq-f": 9, "echo": 10, "echo-ref-size": 11,
+           "echo-ref-name": 12}
+SCORE_OPS = ("mean", "sum", "min", "max")
+OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
+                "fraction-either": 4, "fraction-both": 5, "exact": 6}
 
 ERRORS = {-1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
           -7: "NOMEM", -8: "UNSUPPORTED", -9: "CHROM", -10: "IO"}
@@ -52,7 +59,8 @@ class _MapOpts(ctypes.Structure):
     _fields_ = [("overlap_bp", ctypes.c_uint64), ("n_ops", ctypes.c_int),
                 ("ops", ctypes.c_int * 16), ("precision", ctypes.c_int),
                 ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
-                ("delim", ctypes.c_char * 16)]
+                ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
+                ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double)]
 
 
 class _ClosestOpts(ctypes.Structure):
@@ -327,31 +335,38 @@ class Engine:
 
     # -------------------------------------------------------------- bedmap
     def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False):
-        """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result"""
-        names = {"count": MAP_COUNT, "mean": MAP_MEAN}
+               skip_unmapped=False, criterion="bp-ovr", value=None):
+        """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result.
+        criterion: "bp-ovr" (value = overlap_bp), "range" (value = bp), "fraction-ref",
+        "fraction-map", "fraction-either", "fraction-both" (value = fraction), "exact"."""
         o = _MapOpts()
         o.overlap_bp = overlap_bp
         o.n_ops = len(ops)
         for k, op in enumerate(ops):
-            o.ops[k] = names[op]
+            o.ops[k] = MAP_OPS[op]
         o.precision = precision
         o.scientific = 0
         o.skip_unmapped = 1 if skip_unmapped else 0
         o.delim = delim.encode()
+        o.criterion = OVR_CRITERIA[criterion]
+        if criterion == "range":
+            o.range_bp = int(value)
+        elif criterion.startswith("fraction"):
+            o.fraction = float(value)
         h = ctypes.c_void_p()
         self._check(self.L.bg_map(self.ctx, s.h, ref, map_, ctypes.byref(o), ctypes.byref(h)))
         return Result(self, h)
 
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, chrom=None):
-        need5 = "mean" in ops
-        s = self.load([(ref_text, BED3), (map_text if map_text is not None else ref_text,
-                                          BED5 if need5 else BED3)])
+               skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None):
+        need5 = any(op in SCORE_OPS for op in ops)
+        s = self.load([(ref_text, BED3_REST if "echo" in ops else BED3),
+                       (map_text if map_text is not None else ref_text, BED5 if need5 else BED3)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)
-            r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped)
+            r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped,
+                            criterion, value)
             try:
                 return r.text()
             finally:

@@ -109,7 +109,7 @@ def kernel_bytes(name, w):
         "k_fmt_count": 16 * out,
         "k_fmt_write": 16 * out + obytes,
         # bedmap: ref keys, map keys + score read; count + sum written
-        "k_map_count_sum": 28 * rows[0] + 24 * rows[-1],
+        "k_map_ops": 28 * rows[0] + 24 * rows[-1],
         # closest: every ref row and every candidate read once; left/right written
         "k_closest_chunks": 32 * rows[0] + 16 * rows[-1],
         # element-of: ref keys read + one flag per row; union prefix searched (cached)

@@ -86,9 +86,32 @@ typedef struct bg_map_opts {
   int scientific;      /* --sci                                                 */
   int skip_unmapped;   /* --skip-unmapped                                       */
   char delim[16];      /* --delim (default "|")                                 */
+  int criterion;       /* overlap option: BG_OVR_* (0 = --bp-ovr, the default)    */
+  uint64_t range_bp;   /* --range <int> (> 0; --range 0 is --bp-ovr 1)          */
+  double fraction;     /* --fraction-{ref,map,either,both} <val>, as given       */
 } bg_map_opts;
-#define BG_MAP_COUNT 1
-#define BG_MAP_MEAN 2
+/* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
+ * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */
+#define BG_MAP_COUNT 1         /* --count          Count<PrintScore>          "%d"     */
+#define BG_MAP_MEAN 2          /* --mean           Average<PrintScorePrecision>         */
+#define BG_MAP_SUM 3           /* --sum            Sum<PrintScorePrecision>             */
+#define BG_MAP_MIN 4           /* --min            Extreme<.., CompValueThenAddressLesser>  */
+#define BG_MAP_MAX 5           /* --max            Extreme<.., CompValueThenAddressGreater> */
+#define BG_MAP_INDICATOR 6     /* --indicator      Indicator<PrintScore>      "%d"     */
+#define BG_MAP_BASES 7         /* --bases          OvrAggregate               "%lu"    */
+#define BG_MAP_BASES_UNIQ 8    /* --bases-uniq     OvrUnique                  "%u"     */
+#define BG_MAP_BASES_UNIQ_F 9  /* --bases-uniq-f   OvrUniqueFract                      */
+#define BG_MAP_ECHO 10         /* --echo           Echo<Print> (ref row, BG_BED3_REST)  */
+#define BG_MAP_ECHO_SIZE 11    /* --echo-ref-size  Echo<PrintLength>          "%lu"    */
+#define BG_MAP_ECHO_NAME 12    /* --echo-ref-name  Echo<PrintSpanName>  chrom:start-end */
+/* overlap criteria (Bedmap.cpp:95-155 -> data/bed/BedDistances.hpp) */
+#define BG_OVR_BP 0            /* --bp-ovr N       Overlapping(N)            :80-118   */
+#define BG_OVR_RANGE 1         /* --range R        RangedDist(R)             :41-67    */
+#define BG_OVR_FRAC_REF 2      /* --fraction-ref   PercentOverlapReference   :196-218  */
+#define BG_OVR_FRAC_MAP 3      /* --fraction-map   PercentOverlapMapping     :123-190  */
+#define BG_OVR_FRAC_EITHER 4   /* --fraction-either PercentOverlapEither     :223-253  */
+#define BG_OVR_FRAC_BOTH 5     /* --fraction-both  PercentOverlapBoth        :258-288  */
+#define BG_OVR_EXACT 6         /* --exact          Exact                     :293-317  */
 
 typedef struct bg_closest_opts {
   int shortest;       /* --closest / --shortest: one element per row, ties to the left */

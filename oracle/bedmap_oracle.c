@@ -1,54 +1,132 @@
 /*
  * oracle/bedmap_oracle.c — TEST INFRASTRUCTURE ONLY.
  *
- * CPU restatement (plain C) of `bedmap [--bp-ovr N] [--delim D] [--prec P] [--sci]
- * [--skip-unmapped] <--count|--mean>... ref.bed map.bed` on the reference's exact
- * event order:
+ * CPU restatement (plain C) of `bedmap [overlap-option] [--delim D] [--prec P] [--sci]
+ * [--skip-unmapped] <operations>... ref.bed map.bed` on the reference's exact event order:
  *   two-file window sweep ........... interfaces/src/algorithm/sweep/WindowSweepImpl.cpp:168-256
- *   overlap "distance" .............. interfaces/general-headers/data/bed/BedDistances.hpp:80-118
+ *   sweep / visitor distances ....... applications/bed/bedmap/src/Bedmap.cpp:95-155 (the sweep
+ *                                     runs on Overlapping(0), or RangedDist(R) for --range;
+ *                                     the visitors filter with the chosen criterion)
+ *   criteria ........................ interfaces/general-headers/data/bed/BedDistances.hpp:
+ *                                     RangedDist :41-67, Overlapping :80-118,
+ *                                     PercentOverlapMapping/Reference/Either/Both :123-288,
+ *                                     Exact :293-317
  *   window repair (fixWindow) ....... algorithm/visitors/bed/BedBaseVisitor.hpp:131-215
  *   set order (start,end,rest,addr) . data/bed/BedCompare.hpp:143-194 (row index stands in
  *                                     for the heap address: allocation order)
  *   fan-out / row printing .......... algorithm/visitors/other/MultiVisitor.hpp:71-98
- *   Count ("%d") .................... algorithm/visitors/numerical/CountVisitor.hpp:34-64
- *   Average (running double) ........ algorithm/visitors/numerical/AverageVisitor.hpp:35-75,
- *                                     "%.{prec}lf"/"%.{prec}e" utility/Formats.hpp:42-50,
+ *   visitors ........................ numerical/CountVisitor.hpp ("%d"), AverageVisitor.hpp and
+ *                                     SumVisitor.hpp (running double), ExtremeVisitor.hpp (min/max),
+ *                                     IndicatorVisitor.hpp, bed/OvrAggregateVisitor.hpp ("%lu"),
+ *                                     bed/OvrUniqueVisitor.hpp ("%u"), bed/OvrUniqueFractionVisitor.hpp,
+ *                                     other/EchoVisitor.hpp with PrintAll / PrintLength /
+ *                                     PrintSpanName (helpers/ProcessBedVisitorRow.hpp:309-342);
+ *                                     option names: helpers/NamedVisitors.hpp:52-178
+ *   number formats .................. "%.{prec}lf"/"%.{prec}e" utility/Formats.hpp:42-50,
  *                                     "NAN" interfaces/src/data/measurement/NaN.cpp:26
  *   argv grammar (subset) ........... applications/bed/bedmap/src/Input.hpp:75-367
- * Map rows are read as BED5 (chrom start end id score) when --mean is requested
- * (bedmap/src/Input.hpp:395-410 MapFields), else as BED3.
+ * Map rows are read as BED5 (chrom start end id score) when a score operation is requested
+ * (bedmap/src/Input.hpp:395-410 MapFields), else as BED3; the reference file keeps its
+ * remainder (B3Rest) for --echo.
  * Only used by tests/ and bench.py's cpu_baseline; never linked into the product.
  */
+#include <float.h>
+
 #include "bedio.h"
 
 static chrom_pool_t POOL;
 static const bedfile_t *REF, *MAP;
 
-/* Overlapping(ovr)(a,b) for a map row vs a ref row (BedDistances.hpp:95-115);
- * sign convention: 0 = in range, <0 = a "before" b, >0 otherwise. */
-static int overlap_cmp(int ac, uint64_t as, uint64_t ae, int64_t aid, int bc, uint64_t bs,
-                       uint64_t be, int64_t bid, uint64_t ovr) {
-  if (ac != bc) {
-    int v = strcmp(POOL.names[ac], POOL.names[bc]);
-    if (v != 0) return v > 0 ? 1 : -1;
-  }
-  uint64_t mn = as > bs ? as : bs, mx = ae < be ? ae : be;
+enum { C_BP, C_RANGE, C_FREF, C_FMAP, C_FEITHER, C_FBOTH, C_EXACT };
+static int CRIT = C_BP;
+static uint64_t OVR = 1, RANGE = 0;
+static double PERC = 1.0; /* PercentOverlapMapping::perc_ after its constructor */
+
+typedef struct { int c; uint64_t s, e; int64_t id; } row_t;
+static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], -1 - r}; return x; }
+static row_t M_(int64_t m) { row_t x = {MAP->chrom[m], MAP->start[m], MAP->end[m], m}; return x; }
+static int chrom_cmp(int a, int b) {
+  if (a == b) return 0;
+  int v = strcmp(POOL.names[a], POOL.names[b]);
+  return v > 0 ? 1 : (v < 0 ? -1 : 0);
+}
+
+/* Overlapping(ovr)(a, b), BedDistances.hpp:97-115 */
+static int d_overlap(row_t a, row_t b, uint64_t ovr) {
+  int v = chrom_cmp(a.c, b.c);
+  if (v) return v;
+  uint64_t mn = a.s > b.s ? a.s : b.s, mx = a.e < b.e ? a.e : b.e;
   if (mx > mn) {
     if (mx - mn >= ovr) return 0;
-    if (as != bs) return as < bs ? -1 : 1;
-    if (ae != be) return ae < be ? -1 : 1;
-    return aid < bid ? -1 : 1;
+    if (a.s != b.s) return a.s < b.s ? -1 : 1;
+    if (a.e != b.e) return a.e < b.e ? -1 : 1;
+    return a.id < b.id ? -1 : 1;
   }
-  return as < bs ? -1 : 1;
+  return a.s < b.s ? -1 : 1;
 }
-/* Ref2Map(r, m) / Map2Ref(m, r) */
-static int r2m(int64_t r, int64_t m, uint64_t ovr) {
-  return overlap_cmp(REF->chrom[r], REF->start[r], REF->end[r], -1 - r, MAP->chrom[m],
-                     MAP->start[m], MAP->end[m], m, ovr);
+/* RangedDist(R)(a, b), BedDistances.hpp:57-64 */
+static int d_ranged(row_t a, row_t b) {
+  int v = chrom_cmp(a.c, b.c);
+  if (v) return v;
+  if (a.s < b.e) return (a.e + RANGE > b.s) ? 0 : -1;
+  return (b.e + RANGE > a.s) ? 0 : 1;
 }
-static int m2r(int64_t m, int64_t r, uint64_t ovr) {
-  return overlap_cmp(MAP->chrom[m], MAP->start[m], MAP->end[m], m, REF->chrom[r],
-                     REF->start[r], REF->end[r], -1 - r, ovr);
+/* PercentOverlapMapping::Ref2Map(ref, map), BedDistances.hpp:142-179 (fraction of map's size) */
+static int d_pmap(row_t ref, row_t map) {
+  int v = chrom_cmp(ref.c, map.c);
+  if (v) return v;
+  if (ref.e < map.s) return -1;
+  if (map.e < ref.s) return 1;
+  if (PERC <= DBL_EPSILON) return 0;
+  double sz, total = (double)(map.e - map.s);
+  int direction;
+  if (ref.s <= map.s) {
+    sz = (ref.e >= map.e) ? (double)(map.e - map.s) : (double)(ref.e - map.s);
+    direction = -1;
+  } else {
+    sz = (ref.e >= map.e) ? (double)(map.e - ref.s) : (double)(ref.e - ref.s);
+    direction = 1;
+  }
+  if (sz / total >= PERC) return 0;
+  return direction;
+}
+/* the visitor distance's Map2Ref(map, ref); fixWindow uses only its zero-ness */
+static int crit_m2r(int64_t m, int64_t r) {
+  row_t a = M_(m), b = R_(r);
+  switch (CRIT) {
+    case C_RANGE: return d_ranged(a, b);
+    case C_FMAP: return -d_pmap(b, a);          /* Mapping::Map2Ref = -Ref2Map(ref, map) */
+    case C_FREF: return d_pmap(a, b);           /* Reference::Map2Ref = -(-Base::Ref2Map(map, ref)) */
+    case C_FEITHER: {                           /* Either::Ref2Map, :233-241, negated */
+      int v1 = d_pmap(b, a);
+      if (v1 == 0) return 0;
+      int v2 = -d_pmap(a, b);
+      if (v2 == 0) return 0;
+      return -v1;
+    }
+    case C_FBOTH: {                             /* Both::Ref2Map, :268-276, negated */
+      int v1 = d_pmap(b, a);
+      if (v1 != 0) return -v1;
+      int v2 = -d_pmap(a, b);
+      if (v2 != 0) return -v2;
+      return 0;
+    }
+    case C_EXACT: {                             /* Exact::Ref2Map(ref, map), negated */
+      int v = chrom_cmp(b.c, a.c);
+      if (v) return -v;
+      if (b.s != a.s) return b.s < a.s ? 1 : -1;
+      if (b.e != a.e) return b.e < a.e ? 1 : -1;
+      return 0;
+    }
+    default: return d_overlap(a, b, OVR);
+  }
+}
+/* the sweep distance: Overlapping(0), or RangedDist(R) for --range */
+static int sweep_r2m(int64_t r, int64_t m) {
+  return CRIT == C_RANGE ? d_ranged(R_(r), M_(m)) : d_overlap(R_(r), M_(m), 0);
+}
+static int sweep_m2r(int64_t m, int64_t r) {
+  return CRIT == C_RANGE ? d_ranged(M_(m), R_(r)) : d_overlap(M_(m), R_(r), 0);
 }
 
 /* ordered set of map rows by (start, end, row) */
@@ -85,51 +163,154 @@ static int os_erase(oset_t* s, int64_t x) {
 }
 
 /* visitors */
-enum { V_COUNT = 1, V_MEAN = 2 };
+enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
+       V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME };
 static int VIS[64], NVIS;
-static int count_;
-static double sum_;
+static int count_;     /* Count / Indicator */
+static double sum_;    /* Average / Sum: one running double (they see the same events) */
 static int counter_;
-static long cnt_; /* MultiVisitor's own add/delete balance */
+static long cnt_;      /* MultiVisitor's own add/delete balance */
 static const char* DELIM = "|";
 static int PREC = 6, SCI = 0, SKIP_UNMAPPED = 0;
+static oset_t VWIN;    /* the visitor window (BedBaseVisitor::win_) */
 
 static void v_add(int64_t m) {
-  for (int i = 0; i < NVIS; ++i) {
-    if (VIS[i] == V_COUNT) ++count_;
-    else { sum_ += MAP->score[m]; ++counter_; }
-  }
+  ++count_;
+  if (MAP->score) { sum_ += MAP->score[m]; ++counter_; }
   ++cnt_;
 }
 static void v_del(int64_t m) {
-  for (int i = 0; i < NVIS; ++i) {
-    if (VIS[i] == V_COUNT) --count_;
-    else { sum_ -= MAP->score[m]; --counter_; }
-  }
+  --count_;
+  if (MAP->score) { sum_ -= MAP->score[m]; --counter_; }
   --cnt_;
 }
-static void v_done(void) {
-  if (SKIP_UNMAPPED && cnt_ == 0) return;
+static void put_real(double v) {
   char fmt[32];
   snprintf(fmt, sizeof(fmt), SCI ? "%%.%de" : "%%.%dlf", PREC);
+  printf(fmt, v);
+}
+/* OvrAggregate::coordCompare(ref, map), OvrAggregateVisitor.hpp:77-97 */
+static unsigned long ovr_agg(int64_t r, int64_t m) {
+  uint64_t ts = REF->start[r], te = REF->end[r], vs = MAP->start[m], ve = MAP->end[m];
+  if (ts >= vs) {
+    if (ve > ts) return ve > te ? te - ts : ve - ts;
+    return 0;
+  }
+  if (te > vs) return ve < te ? ve - vs : te - vs;
+  return 0;
+}
+/* BasicCoords::overlap length, Bed.hpp:172-190 */
+static uint64_t ovr_len(uint64_t as, uint64_t ae, uint64_t bs, uint64_t be) {
+  uint64_t mn = as > bs ? as : bs, mx = ae < be ? ae : be;
+  return mx > mn ? mx - mn : 0;
+}
+/* OvrUnique::DoneReference, OvrUniqueVisitor.hpp:62-78 (its set is in genomic order) */
+static unsigned int ovr_uniq(int64_t r) {
+  unsigned int ovr = 0;
+  if (VWIN.n == 0) return 0;
+  uint64_t ts = MAP->start[VWIN.v[0]], te = MAP->end[VWIN.v[0]];
+  const uint64_t rs = REF->start[r], re = REF->end[r];
+  for (int64_t i = 1; i < VWIN.n; ++i) {
+    const uint64_t s = MAP->start[VWIN.v[i]], e = MAP->end[VWIN.v[i]];
+    if (ovr_len(ts, te, s, e)) {
+      ts = ts < s ? ts : s;
+      te = te > e ? te : e;
+    } else {
+      ovr += (unsigned int)ovr_len(ts, te, rs, re);
+      ts = s;
+      te = e;
+    }
+  }
+  ovr += (unsigned int)ovr_len(ts, te, rs, re);
+  return ovr;
+}
+static void v_done(int64_t r) {
+  if (SKIP_UNMAPPED && cnt_ == 0) return;
   for (int i = 0; i < NVIS; ++i) {
     if (i) fputs(DELIM, stdout);
-    if (VIS[i] == V_COUNT) printf("%d", count_);
-    else if (counter_ > 0) printf(fmt, sum_ / counter_);
-    else fputs("NAN", stdout);
+    switch (VIS[i]) {
+      case V_COUNT: printf("%d", count_); break;
+      case V_INDICATOR: printf("%d", count_ > 0 ? 1 : 0); break;
+      case V_MEAN:
+        if (counter_ > 0) put_real(sum_ / counter_); else fputs("NAN", stdout);
+        break;
+      case V_SUM:
+        if (counter_ > 0) put_real(sum_); else fputs("NAN", stdout);
+        break;
+      case V_MIN:
+      case V_MAX: {
+        if (VWIN.n == 0) { fputs("NAN", stdout); break; }
+        double b = MAP->score[VWIN.v[0]];
+        for (int64_t k = 1; k < VWIN.n; ++k) {
+          const double x = MAP->score[VWIN.v[k]];
+          if (VIS[i] == V_MIN ? x < b : x > b) b = x;
+        }
+        put_real(b);
+        break;
+      }
+      case V_BASES: {
+        unsigned long o = 0;
+        for (int64_t k = 0; k < VWIN.n; ++k) o += ovr_agg(r, VWIN.v[k]);
+        printf("%lu", o);
+        break;
+      }
+      case V_BASES_UNIQ: printf("%u", ovr_uniq(r)); break;
+      case V_BASES_UNIQ_F:
+        put_real((double)ovr_uniq(r) / (double)(REF->end[r] - REF->start[r]));
+        break;
+      case V_ECHO:
+        printf("%s\t%" PRIu64 "\t%" PRIu64 "%s", POOL.names[REF->chrom[r]], REF->start[r], REF->end[r],
+               REF->rest ? REF->rest[r] : "");
+        break;
+      case V_ECHO_SIZE: printf("%" PRIu64, REF->end[r] - REF->start[r]); break;
+      case V_ECHO_NAME:
+        printf("%s:%" PRIu64 "-%" PRIu64, POOL.names[REF->chrom[r]], REF->start[r], REF->end[r]);
+        break;
+    }
   }
   fputc('\n', stdout);
 }
 
+/* PercentOverlapMapping's constructor, BedDistances.hpp:126-136 */
+static double parse_frac(const char* v) {
+  double p = strtod(v, NULL);
+  while (p > 1) p /= 10.0;
+  p -= DBL_EPSILON;
+  if (p <= 0.0) p = DBL_EPSILON;
+  return p;
+}
+
 int main(int argc, char** argv) {
-  uint64_t ovr = 1;
-  int a = 1, need5 = 0;
+  int a = 1, need5 = 0, rest = 0;
   const char* only_chrom = NULL;
+  static const struct { const char* name; int v; int score; } OPS[] = {
+      {"--count", V_COUNT, 0},         {"--mean", V_MEAN, 1},           {"--sum", V_SUM, 1},
+      {"--min", V_MIN, 1},             {"--max", V_MAX, 1},             {"--indicator", V_INDICATOR, 0},
+      {"--bases", V_BASES, 0},         {"--bases-uniq", V_BASES_UNIQ, 0},
+      {"--bases-uniq-f", V_BASES_UNIQ_F, 0},                            {"--echo", V_ECHO, 0},
+      {"--echo-ref-size", V_ECHO_SIZE, 0},                              {"--echo-ref-name", V_ECHO_NAME, 0}};
   while (a < argc - 2 || (a < argc && strncmp(argv[a], "--", 2) == 0)) {
     const char* o = argv[a++];
-    if (!strcmp(o, "--count")) VIS[NVIS++] = V_COUNT;
-    else if (!strcmp(o, "--mean")) { VIS[NVIS++] = V_MEAN; need5 = 1; }
-    else if (!strcmp(o, "--bp-ovr") && a < argc) ovr = strtoull(argv[a++], 0, 10);
+    int found = 0;
+    for (size_t k = 0; k < sizeof(OPS) / sizeof(OPS[0]); ++k)
+      if (!strcmp(o, OPS[k].name)) {
+        VIS[NVIS++] = OPS[k].v;
+        need5 |= OPS[k].score;
+        rest |= OPS[k].v == V_ECHO;
+        found = 1;
+      }
+    if (found) continue;
+    if (!strcmp(o, "--bp-ovr") && a < argc) { CRIT = C_BP; OVR = strtoull(argv[a++], 0, 10); }
+    else if (!strcmp(o, "--range") && a < argc) {
+      RANGE = strtoull(argv[a++], 0, 10);
+      if (RANGE == 0) { CRIT = C_BP; OVR = 1; } /* --range 0 == --bp-ovr 1, Input.hpp:165-171 */
+      else CRIT = C_RANGE;
+    }
+    else if (!strcmp(o, "--fraction-ref") && a < argc) { CRIT = C_FREF; PERC = parse_frac(argv[a++]); }
+    else if (!strcmp(o, "--fraction-map") && a < argc) { CRIT = C_FMAP; PERC = parse_frac(argv[a++]); }
+    else if (!strcmp(o, "--fraction-either") && a < argc) { CRIT = C_FEITHER; PERC = parse_frac(argv[a++]); }
+    else if (!strcmp(o, "--fraction-both") && a < argc) { CRIT = C_FBOTH; PERC = parse_frac(argv[a++]); }
+    else if (!strcmp(o, "--exact")) CRIT = C_EXACT;
     else if (!strcmp(o, "--delim") && a < argc) DELIM = argv[a++];
     else if (!strcmp(o, "--prec") && a < argc) PREC = atoi(argv[a++]);
     else if (!strcmp(o, "--chrom") && a < argc) only_chrom = argv[a++];
@@ -143,7 +324,7 @@ int main(int argc, char** argv) {
   FILE* fr = open_input(argv[a]);
   FILE* fm = open_input(argv[a + 1]);
   if (!fr || !fm) { fprintf(stderr, "bedmap_oracle: cannot open input\n"); return 2; }
-  read_bed3(fr, &POOL, &ref, 0);
+  read_bed3(fr, &POOL, &ref, rest);
   if (need5) read_bed5(fm, &POOL, &map);
   else read_bed3(fm, &POOL, &map, 0);
   if (only_chrom) {
@@ -155,6 +336,7 @@ int main(int argc, char** argv) {
         if (strcmp(POOL.names[f->chrom[j]], only_chrom) != 0) continue;
         f->chrom[k] = f->chrom[j]; f->start[k] = f->start[j]; f->end[k] = f->end[j];
         if (f->score) f->score[k] = f->score[j];
+        if (f->rest) f->rest[k] = f->rest[j];
         ++k;
       }
       f->n = k;
@@ -165,47 +347,47 @@ int main(int argc, char** argv) {
   static char obuf[1 << 20];
   setvbuf(stdout, obuf, _IOFBF, sizeof(obuf));
 
-  /* sweep() overload2 with Overlapping(0); visitor distance Overlapping(ovr) */
+  /* sweep() overload 2 with the sweep distance; fixWindow with the visitor distance */
   int64_t* win = (int64_t*)malloc(sizeof(int64_t) * (size_t)(map.n + 1));
   int64_t wh = 0, wt = 0; /* deque [wh, wt) */
   int64_t mi = 0, cache = -1;
-  oset_t vwin = {0}, vcache = {0}, lst = {0};
+  oset_t vcache = {0}, lst = {0};
   for (int64_t r = 0; r < ref.n; ++r) {
-    while (wt > wh && m2r(win[wh], r, 0) < 0) { /* OnDelete */
+    while (wt > wh && sweep_m2r(win[wh], r) < 0) { /* OnDelete */
       int64_t m = win[wh++];
-      if (os_erase(&vwin, m)) v_del(m);
+      if (os_erase(&VWIN, m)) v_del(m);
       else os_erase(&vcache, m);
     }
     while (cache >= 0 || mi < map.n) {
       int64_t m;
       if (cache >= 0) { m = cache; cache = -1; }
       else m = mi++;
-      int v = r2m(r, m, 0);
+      int v = sweep_r2m(r, m);
       if (v == 0) { win[wt++] = m; os_insert(&vcache, m); } /* OnAdd -> cache_ */
       else if (v < 0) { cache = m; break; }
     }
     /* OnDone: fixWindow (deletions first, then insertions), then DoneReference */
     lst.n = 0;
-    for (int64_t i = 0; i < vwin.n;) {
-      int64_t m = vwin.v[i];
-      if (m2r(m, r, ovr) != 0) {
+    for (int64_t i = 0; i < VWIN.n;) {
+      int64_t m = VWIN.v[i];
+      if (crit_m2r(m, r) != 0) {
         v_del(m);
         os_insert(&lst, m);
-        memmove(vwin.v + i, vwin.v + i + 1, (size_t)(vwin.n - i - 1) * 8);
-        vwin.n--;
+        memmove(VWIN.v + i, VWIN.v + i + 1, (size_t)(VWIN.n - i - 1) * 8);
+        VWIN.n--;
       } else ++i;
     }
     for (int64_t i = 0; i < vcache.n;) {
       int64_t m = vcache.v[i];
-      if (m2r(m, r, ovr) == 0) {
+      if (crit_m2r(m, r) == 0) {
         v_add(m);
-        os_insert(&vwin, m);
+        os_insert(&VWIN, m);
         memmove(vcache.v + i, vcache.v + i + 1, (size_t)(vcache.n - i - 1) * 8);
         vcache.n--;
       } else ++i;
     }
     for (int64_t i = 0; i < lst.n; ++i) os_insert(&vcache, lst.v[i]);
-    v_done();
+    v_done(r);
   }
   fflush(stdout);
   return 0;

@@ -109,6 +109,90 @@ def test_random_bedmap_vs_oracle(eng, oracle_bin, ovr, prec, skip):
                 assert got == want, (ops, trial)
 
 
+# every bedmap operation on the GPU path under every overlap criterion;
+# oracle = restatement of the sweep + fixWindow + visitors (oracle/bedmap_oracle.c)
+MAP_OPSETS = [["count", "sum", "min", "max", "indicator"],
+              ["bases", "bases-uniq", "bases-uniq-f", "mean"],
+              ["echo", "echo-ref-size", "echo-ref-name", "count"]]
+MAP_CRITS = [("bp-ovr", 1), ("bp-ovr", 7), ("range", 1), ("range", 25), ("fraction-ref", "0.5"),
+             ("fraction-map", "0.25"), ("fraction-map", "1"), ("fraction-either", "0.7"),
+             ("fraction-both", "0.3"), ("exact", None)]
+
+
+@pytest.mark.parametrize("crit,val", MAP_CRITS)
+def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
+    rng = random.Random(zlib.crc32(repr((crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(6):
+            ref = randbed.rows(rng, rng.choice([0, 1, 30, 500, 2000]), span=rng.choice([300, 3000]),
+                               maxlen=rng.choice([10, 80, 300]))
+            mp = randbed.rows(rng, rng.choice([0, 1, 50, 800, 3000]), span=rng.choice([300, 3000]),
+                              maxlen=rng.choice([10, 80, 300]))
+            if trial % 2:  # exact matches, duplicates and nesting
+                mp = sorted(mp + ref[::2] + ref[::3], key=lambda r: (r[0].encode(), r[1], r[2]))
+            rt = randbed.text(ref, rest="cols", rng=rng).encode()
+            mt = randbed.text(mp, rest="bed5", rng=rng).encode()
+            copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
+            kw = {"criterion": crit, "value": val}
+            if crit == "bp-ovr":
+                kw = {"overlap_bp": val}
+            for ops in MAP_OPSETS:
+                args = [f"--{o}" for o in ops] + copt
+                want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                got = eng.bedmap(ops, rt, mt, **kw)
+                assert got == want, (crit, val, ops, trial)
+
+
+def test_bedmap_dense_map_slice(eng, oracle_bin):
+    """a workgroup whose candidate slice exceeds the LDS stage (searches in HBM instead)"""
+    rng = random.Random(11)
+    ref = randbed.rows(rng, 300, chroms=["chr1"], span=2000, maxlen=60)
+    mp = randbed.rows(rng, 9000, chroms=["chr1"], span=2000, maxlen=60)
+    rt = randbed.text(ref).encode()
+    mt = randbed.text(mp, rest="bed5", rng=rng).encode()
+    with tempfile.TemporaryDirectory() as td:
+        want = run_oracle(oracle_bin["bedmap"], ["--count", "--mean", "--bases-uniq"], [rt, mt], td)
+        assert eng.bedmap(["count", "mean", "bases-uniq"], rt, mt) == want
+
+
+def test_bedmap_min_max_decimal_scores(eng, oracle_bin):
+    """min/max take any score (no arithmetic); sums of non-integer scores are refused"""
+    rng = random.Random(77)
+    ref = randbed.rows(rng, 400, span=2000, maxlen=80)
+    mp = randbed.rows(rng, 1500, span=2000, maxlen=80)
+    rt = randbed.text(ref).encode()
+    mt = "".join(f"{c}\t{s}\t{e}\tid{i}\t{rng.choice(['-', ''])}{rng.randint(0, 9999) / 100}\n"
+                 for i, (c, s, e) in enumerate(mp)).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for prec in (0, 2, 6):
+            want = run_oracle(oracle_bin["bedmap"], ["--min", "--max", "--count", "--prec", str(prec)],
+                              [rt, mt], td)
+            assert eng.bedmap(["min", "max", "count"], rt, mt, precision=prec) == want
+    from bedops_amd import BedgpuError
+    with pytest.raises(BedgpuError) as ei:
+        eng.bedmap(["sum"], rt, mt)
+    assert ei.value.code == -8
+
+
+def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
+    rng = random.Random(5)
+    ref = randbed.rows(rng, 300, span=3000, maxlen=100)
+    mp = randbed.rows(rng, 900, span=3000, maxlen=100)
+    r = randbed.write(str(tmp_path / "r.bed"), randbed.text(ref, rest="cols", rng=rng))
+    m = randbed.write(str(tmp_path / "m.bed"), randbed.text(mp, rest="bed5", rng=rng))
+    for args in (["--fraction-either", "0.4", "--echo", "--bases-uniq", "--max"],
+                 ["--range", "10", "--delim", ";", "--indicator", "--sum"],
+                 ["--range", "0", "--count"], ["--exact", "--skip-unmapped", "--echo-ref-name", "--count"]):
+        want = subprocess.run([oracle_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE,
+                              check=True).stdout
+        got = subprocess.run([gpu_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE,
+                             check=True).stdout
+        assert got == want, args
+    bad = subprocess.run([gpu_bin["bedmap"], "--bp-ovr", "3", "--exact", "--count", r, m],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    assert bad.returncode != 0 and b"More than one overlap specification used." in bad.stderr
+
+
 # ---------------------------------------------------------------------------------
 # I/O edge cases (Appendix B of SURVEY.md)
 # ---------------------------------------------------------------------------------

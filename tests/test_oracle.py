@@ -4,6 +4,8 @@ Appendix D, plus the synthetic generator's input hashes."""
 import hashlib
 import subprocess
 
+import pytest
+
 import testplan_runner
 
 
@@ -106,3 +108,34 @@ def test_closest_cache_free_model_is_not_the_reference(oracle_bin, tmp_path):
     assert out[1] == "chr1\t178\t202\tr2|chr1\t122\t148\tc1|NA"
     left, _ = model_closest.pick([(79, 156), (122, 148)], (178, 202), allow_overlaps=False)
     assert left == 0  # cache-free answer: c0
+
+
+# hand-worked bedmap answers for every operation and criterion on the oracle (computed by
+# hand from the reference's definitions: BedDistances.hpp, OvrAggregate/OvrUnique visitors)
+BEDMAP_HAND_REF = "chr1\t10\t100\ta\tx\nchr1\t50\t60\tb\nchr2\t5\t10\tc\n"
+BEDMAP_HAND_MAP = ("chr1\t0\t20\tm1\t5\nchr1\t15\t55\tm2\t-3\nchr1\t58\t70\tm3\t7.5\n"
+                   "chr1\t90\t200\tm4\t2\nchr2\t7\t9\tm5\t1\n")
+BEDMAP_HAND = [
+    (["--count", "--sum", "--min", "--max", "--indicator"],
+     "4|11.500000|-3.000000|7.500000|1\n2|4.500000|-3.000000|7.500000|1\n1|1.000000|1.000000|1.000000|1\n"),
+    (["--bases", "--bases-uniq", "--bases-uniq-f", "--echo"],
+     "72|67|0.744444|chr1\t10\t100\ta\tx\n7|7|0.700000|chr1\t50\t60\tb\n2|2|0.400000|chr2\t5\t10\tc\n"),
+    (["--range", "30", "--count", "--echo-ref-name", "--echo-ref-size"],
+     "4|chr1:10-100|90\n2|chr1:50-60|10\n1|chr2:5-10|5\n"),
+    (["--fraction-map", "0.5", "--count", "--bases"], "3|62\n0|0\n1|2\n"),
+    (["--fraction-ref", "0.2", "--count"], "1\n2\n1\n"),
+    (["--fraction-both", "0.3", "--count"], "1\n0\n1\n"),
+    (["--exact", "--count"], "0\n0\n0\n"),
+]
+
+
+@pytest.mark.parametrize("k", range(len(BEDMAP_HAND)))
+def test_bedmap_oracle_hand_cases(oracle_bin, tmp_path, k):
+    args, want = BEDMAP_HAND[k]
+    r = tmp_path / "r.bed"
+    m = tmp_path / "m.bed"
+    r.write_text(BEDMAP_HAND_REF)
+    m.write_text(BEDMAP_HAND_MAP)
+    out = subprocess.run([oracle_bin["bedmap"]] + args + [str(r), str(m)], stdout=subprocess.PIPE,
+                         check=True).stdout.decode()
+    assert out == want

@@ -1,0 +1,16 @@
+#!/bin/bash
+# A/B builds of libbedgpu: tools/ab_build.sh NAME "-DFLAG ..." -> build/ab/NAME/libbedgpu.so
+# (run here; the .so files travel with the tree). tools/ab_run.sh times them on the GPU.
+set -e
+cd "$(dirname "$0")/.."
+name=$1; shift
+out=build/ab/$name; mkdir -p $out
+objs=()
+for f in bedops_amd/csrc/*.hip; do
+  o=$out/$(basename $f .hip).o
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $* -c $f -o $o &
+  objs+=($o)
+done
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libbedgpu.so ${objs[@]} -Wl,-rpath,/opt/rocm/lib
+echo built $out/libbedgpu.so
