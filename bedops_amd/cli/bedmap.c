@@ -24,6 +24,7 @@ static void usage(FILE* f) {
           "    Process Flags:\n"
           "      --chrom <chromosome>  Jump to and process data only for <chromosome>.\n"
           "      --delim <delim>       Change output delimiter from '|' to <delim> between columns.\n"
+          "      --multidelim <delim>  Change delimiter of multi-value output columns from ';' to <delim>.\n"
           "      --ec / --header       Error check / accept header lines.\n"
           "      --prec <int>          Change the post-decimal precision of scores to <int>.\n"
           "      --skip-unmapped       Print no output for a row with no mapped elements.\n\n"
@@ -37,7 +38,8 @@ static void usage(FILE* f) {
           "      --range <int>            Grab <map-file> elements within <int> bp of <ref-file>'s element.\n\n"
           "    Operations (GPU path):\n"
           "      --bases --bases-uniq --bases-uniq-f --count --echo --echo-ref-name --echo-ref-size\n"
-          "      --indicator --max --mean --min --sum\n",
+          "      --echo-map --echo-map-id --echo-map-range --echo-map-score --echo-map-size\n"
+          "      --echo-overlap-size --indicator --max --mean --min --sum\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -53,13 +55,17 @@ int main(int argc, char** argv) {
   o.overlap_bp = 1;
   o.precision = 6;
   strcpy(o.delim, "|");
-  int ec = 0, need5 = 0, need_rest = 0, set_prec = 0, set_delim = 0;
+  strcpy(o.multidelim, ";");
+  int ec = 0, need5 = 0, need_rest = 0, map_rest = 0, set_prec = 0, set_delim = 0;
   int is_bp = 0, is_range = 0, range_alias = 0, is_exact = 0, is_frac[4] = {0, 0, 0, 0};
   static const struct { const char* name; int op; } OPS[] = {
       {"count", BG_MAP_COUNT}, {"mean", BG_MAP_MEAN}, {"sum", BG_MAP_SUM}, {"min", BG_MAP_MIN},
       {"max", BG_MAP_MAX}, {"indicator", BG_MAP_INDICATOR}, {"bases", BG_MAP_BASES},
       {"bases-uniq", BG_MAP_BASES_UNIQ}, {"bases-uniq-f", BG_MAP_BASES_UNIQ_F}, {"echo", BG_MAP_ECHO},
-      {"echo-ref-size", BG_MAP_ECHO_SIZE}, {"echo-ref-name", BG_MAP_ECHO_NAME}};
+      {"echo-ref-size", BG_MAP_ECHO_SIZE}, {"echo-ref-name", BG_MAP_ECHO_NAME},
+      {"echo-map", BG_MAP_ECHO_MAP}, {"echo-map-id", BG_MAP_ECHO_MAP_ID},
+      {"echo-map-score", BG_MAP_ECHO_MAP_SCORE}, {"echo-map-size", BG_MAP_ECHO_MAP_SIZE},
+      {"echo-overlap-size", BG_MAP_ECHO_OVERLAP_SIZE}, {"echo-map-range", BG_MAP_ECHO_MAP_RANGE}};
   const char* chrom = NULL;
   int a = 1;
   while (a < argc) {
@@ -81,6 +87,11 @@ int main(int argc, char** argv) {
       if (strlen(argv[a]) >= sizeof(o.delim)) arg_error("--delim value too long for this build");
       strcpy(o.delim, argv[a++]);
       set_delim = 1;
+    } else if (!strcmp(k, "multidelim")) {
+      if (strcmp(o.multidelim, ";")) arg_error("--multidelim specified multiple times");
+      if (a >= argc) arg_error("No multi-value column delimmiter given");
+      if (strlen(argv[a]) >= sizeof(o.multidelim)) arg_error("--multidelim value too long for this build");
+      strcpy(o.multidelim, argv[a++]);
     } else if (!strcmp(k, "chrom")) {
       if (a >= argc) arg_error("No chromosome name given");
       chrom = argv[a++];
@@ -159,8 +170,11 @@ int main(int argc, char** argv) {
       }
       if (o.n_ops >= 16) arg_error("too many operations for this build");
       o.ops[o.n_ops++] = op;
-      if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX) need5 = 1;
+      if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX ||
+          op == BG_MAP_ECHO_MAP_SCORE)
+        need5 = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
+      if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID) map_rest = 1;
     }
   }
   {  /* one overlap specification (Input.hpp:330-343) */
@@ -203,7 +217,7 @@ int main(int argc, char** argv) {
     in[1].nbytes = tr.n;
   }
   in[1].on_device = 0;
-  in[1].kind = need5 ? BG_BED5 : BG_BED3;
+  in[1].kind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
   free_text(&tr);

@@ -380,6 +380,8 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->vmax);
   bg_release(c, r->bases);
   bg_release(c, r->uniq);
+  bg_release(c, r->wlo);
+  bg_release(c, r->whi);
   bg_release(c, r->left);
   bg_release(c, r->right);
   bg_release(c, r->text);

@@ -42,6 +42,15 @@ struct FmtArgs {
   const double* vmax;
   const uint64_t* bases;
   const uint32_t* uniq;
+  // --echo-map*: the map table (s2/e2/text2/rest_off2/rest_len2 below), its scores, each
+  // row's candidate range and the overlap criterion
+  const double* score2;
+  const uint64_t* wlo;
+  const uint64_t* whi;
+  int crit, mapfields, mdlen;
+  int64_t ovr, range;
+  double perc;
+  char mdelim[16];
   int nops;
   int ops[16];
   int prec;
@@ -304,6 +313,81 @@ __device__ __forceinline__ void render_closest(const FmtArgs& A, uint64_t k, Out
   o.put('\n');
 }
 
+__device__ __forceinline__ bool fmt_isws(char ch) { return ch == ' ' || (ch >= '\t' && ch <= '\r'); }
+
+// map row m as the reference's map type prints it (Bed.hpp): B3Rest "%s\t%lu\t%lu%s",
+// B4Rest "%s\t%lu\t%lu\t%s%s" (id, then what follows it), B5Rest "...\t%s\t%lf%s"
+// (the score re-printed with "%lf", Formats.hpp:34)
+template <typename Out>
+__device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m) {
+  const char* rp = A.text2 + A.rest_off2[m];
+  const uint32_t rl = A.rest_len2[m];
+  if (A.mapfields == 3) {
+    put_row(A, o, A.s2[m], A.e2[m], rp, rl);
+    return true;
+  }
+  put_row(A, o, A.s2[m], A.e2[m], rp, 0);
+  uint32_t i = 0;
+  while (i < rl && fmt_isws(rp[i])) ++i;
+  o.put('\t');
+  for (; i < rl && !fmt_isws(rp[i]); ++i) o.put(rp[i]);  // id
+  if (A.mapfields == 5) {
+    while (i < rl && fmt_isws(rp[i])) ++i;
+    while (i < rl && !fmt_isws(rp[i])) ++i;  // the score's text, re-printed
+    o.put('\t');
+    uint64_t N;
+    bool neg;
+    if (!fixed_digits(A.score2[m], 6, N, neg)) return false;
+    put_fixed(o, N, neg, 6);
+  }
+  for (; i < rl; ++i) o.put(rp[i]);
+  return true;
+}
+
+// --echo-map* of reference row k: the window's rows in genomic order (EchoMapBed's set,
+// EchoMapBedVisitor.hpp:58-63) joined by --multidelim (PrintRangeDelim)
+template <typename Out>
+__device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t k, int op) {
+  const int64_t s = A.s[k], e = A.e[k];
+  bool first = true;
+  int64_t rs = 0, re = 0;
+  for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
+    const int64_t ms = A.s2[m], me = A.e2[m];
+    if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me)) continue;
+    if (op == BG_MAP_ECHO_MAP_RANGE) {  // PrintGenomicRange (ProcessBedVisitorRow.hpp:433-456)
+      if (first) { rs = ms; re = me; }
+      else { rs = min(rs, ms); re = max(re, me); }
+      first = false;
+      continue;
+    }
+    if (!first) for (int d = 0; d < A.mdlen; ++d) o.put(A.mdelim[d]);
+    first = false;
+    if (op == BG_MAP_ECHO_MAP) {
+      if (!put_map_row(A, o, m)) return false;
+    } else if (op == BG_MAP_ECHO_MAP_ID) {
+      const char* rp = A.text2 + A.rest_off2[m];
+      const uint32_t rl = A.rest_len2[m];
+      uint32_t i = 0;
+      while (i < rl && fmt_isws(rp[i])) ++i;
+      for (; i < rl && !fmt_isws(rp[i]); ++i) o.put(rp[i]);
+    } else if (op == BG_MAP_ECHO_MAP_SCORE) {
+      uint64_t N;
+      bool neg;
+      if (!fixed_digits(A.score2[m], A.prec, N, neg)) return false;
+      put_fixed(o, N, neg, A.prec);
+    } else if (op == BG_MAP_ECHO_MAP_SIZE) {
+      const uint64_t len = (uint64_t)(me - ms);
+      put_u64(o, len, dec_len_u64(len));
+    } else {  // BG_MAP_ECHO_OVERLAP_SIZE: |ref ∩ map row|, "%ld"
+      const int64_t ov = min(e, me) - max(s, ms);
+      const uint64_t len = ov > 0 ? (uint64_t)ov : 0;
+      put_u64(o, len, dec_len_u64(len));
+    }
+  }
+  if (op == BG_MAP_ECHO_MAP_RANGE && !first) put_row(A, o, rs, re, nullptr, 0);
+  return true;
+}
+
 // renders (or measures) line k; returns false on a value outside the GPU range
 template <int KIND, typename Out>
 __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
@@ -338,6 +422,10 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
       }
       if (op == BG_MAP_ECHO) {
         put_row(A, o, A.s[k], A.e[k], A.text + A.rest_off[k], A.rest_len[k]);
+        continue;
+      }
+      if (op >= BG_MAP_ECHO_MAP && op <= BG_MAP_ECHO_MAP_RANGE) {
+        if (!put_echo_map(A, o, k, op)) return false;
         continue;
       }
       if (op == BG_MAP_ECHO_SIZE) {
@@ -622,6 +710,24 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.text = s->t[r->tab]->text;  // --echo: the reference rows' remainders
     A.rest_off = s->t[r->tab]->rest_off;
     A.rest_len = s->t[r->tab]->rest_len;
+    if (r->wlo) {  // --echo-map*
+      const bg_table* M = s->t[r->map_tab];
+      A.s2 = M->ks;
+      A.e2 = M->ke;
+      A.text2 = M->text;
+      A.rest_off2 = M->rest_off;
+      A.rest_len2 = M->rest_len;
+      A.score2 = M->score;
+      A.wlo = r->wlo;
+      A.whi = r->whi;
+      A.crit = r->mopts.criterion;
+      A.ovr = (int64_t)r->mopts.overlap_bp;
+      A.range = (int64_t)r->mopts.range_bp;
+      A.perc = r->perc;
+      A.mapfields = r->mapfields;
+      A.mdlen = (int)strnlen(r->mopts.multidelim, 15);
+      memcpy(A.mdelim, r->mopts.multidelim, A.mdlen);
+    }
     A.nops = r->mopts.n_ops;
     for (int k = 0; k < A.nops; ++k) A.ops[k] = r->mopts.ops[k];
     A.prec = r->mopts.precision;

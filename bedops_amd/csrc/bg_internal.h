@@ -131,6 +131,11 @@ struct bg_result {
   double* vmax = nullptr;
   uint64_t* bases = nullptr; // OvrAggregate
   uint32_t* uniq = nullptr;  // OvrUnique (unsigned int, as the reference)
+  uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
+  uint64_t* whi = nullptr;
+  int map_tab = -1;          // the map table
+  int mapfields = 3;         // map row type printed by --echo-map (B3Rest / B4Rest / B5Rest)
+  double perc = 1.0;         // PercentOverlapMapping::perc_ of the criterion
   bg_map_opts mopts;
   // RES_CLOSEST: per row of table `tab`, the chosen rows of table `tab2` (-1: NA)
   int64_t* left = nullptr;
@@ -345,6 +350,26 @@ __device__ __forceinline__ uint64_t merge_path_xfirst(const int64_t* X, uint64_t
     else hi = mid;
   }
   return lo;
+}
+
+// bedmap: is map row [ms, me) in S(r) of reference row [s, e)? (keys of one chromosome;
+// criteria of data/bed/BedDistances.hpp, see bg_map.hip). Rows outside the sweep's
+// Overlapping(0) window never are, except under --range (RangedDist sweeps too).
+__device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, double perc,
+                                          int64_t s, int64_t e, int64_t ms, int64_t me) {
+  if (crit == BG_OVR_RANGE) return (s < me) ? (e + range > ms) : (me + range > s);
+  const int64_t ov = min(e, me) - max(s, ms);
+  if (ov <= 0) return false;
+  if (crit == BG_OVR_BP) return ov >= ovr;
+  if (crit == BG_OVR_EXACT) return ms == s && me == e;
+  if (perc <= 2.220446049250313e-16) return true;  // DBL_EPSILON
+  // sz of BedDistances.hpp:160-174 is the overlap length for overlapping rows
+  const bool fm = (double)ov / (double)(me - ms) >= perc;  // relative to the map row
+  const bool fr = (double)ov / (double)(e - s) >= perc;    // relative to the ref row
+  if (crit == BG_OVR_FRAC_MAP) return fm;
+  if (crit == BG_OVR_FRAC_REF) return fr;
+  if (crit == BG_OVR_FRAC_EITHER) return fm || fr;
+  return fm && fr;
 }
 
 // first index k in [0,n) with A[k] >= v (A sorted ascending); n if none

@@ -1187,7 +1187,7 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
 // host side
 // -------------------------------------------------------------------------------------
 static const char* kind_name(int k) {
-  return k == BG_BED5 ? "BED5" : (k == BG_BED3_REST ? "BED3+rest" : "BED3");
+  return (k == BG_BED5 || k == BG_BED5_REST) ? "BED5" : (k == BG_BED3_REST ? "BED3+rest" : "BED3");
 }
 
 static int report_status(bg_ctx* c, int file, const bg_dstatus& h) {
@@ -1394,12 +1394,12 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   T->ks = (int64_t*)bg_alloc(c, 8 * na);
   T->ke = (int64_t*)bg_alloc(c, 8 * na);
   if (!T->ks || !T->ke) return BG_E_NOMEM;
-  if (in.kind == BG_BED3_REST) {
+  if (in.kind == BG_BED3_REST || in.kind == BG_BED5_REST) {
     T->rest_off = (uint64_t*)bg_alloc(c, 8 * na);
     T->rest_len = (uint32_t*)bg_alloc(c, 4 * na);
     if (!T->rest_off || !T->rest_len) return BG_E_NOMEM;
   }
-  if (in.kind == BG_BED5) {
+  if (in.kind == BG_BED5 || in.kind == BG_BED5_REST) {
     T->score = (double*)bg_alloc(c, 8 * na);
     if (!T->score) return BG_E_NOMEM;
   }
@@ -1409,7 +1409,7 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   int rc = upload_runs(c, T, S, gid, R);
   if (rc) return rc;
   BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
-            S.rhi, in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
+            S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, st);
@@ -1480,7 +1480,7 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
   }
   int rc = report_status(c, idx, h);
   if (rc) return rc;
-  if (in.kind == BG_BED5 && (h.flags & 1ULL)) T->score_int = false;
+  if ((in.kind == BG_BED5 || in.kind == BG_BED5_REST) && (h.flags & 1ULL)) T->score_int = false;
   T->has_zero_len = (h.flags & 2ULL) != 0;
   T->maxlen = h.maxlen;
   // a trailing run may own only the dropped unterminated last line: no rows

@@ -26,6 +26,7 @@
 // arithmetic and take any score.
 #include <cfloat>
 #include <climits>
+#include <cstring>
 
 #include "bg_internal.h"
 
@@ -33,6 +34,7 @@
 #define NEED_EXT 2u
 #define NEED_BASES 4u
 #define NEED_UNIQ 8u
+#define NEED_WIN 16u  // --echo-map*: keep each row's candidate range for the formatter
 
 struct MapArgs {
   const int64_t* RS;
@@ -53,6 +55,8 @@ struct MapArgs {
   double* vmax;
   uint64_t* bases;
   uint32_t* uniq;
+  uint64_t* wlo;
+  uint64_t* whi;
   bg_dstatus* st;
 };
 
@@ -62,23 +66,11 @@ __device__ __forceinline__ int64_t wmax64(int64_t v) {
   return v;
 }
 
-// m in S(r)? Keys of one chromosome: differences and comparisons are the coordinates'.
+// m in S(r)? (bg_map_in with the criterion folded at compile time)
 template <int CRIT>
 __device__ __forceinline__ bool map_in(int64_t s, int64_t e, int64_t ms, int64_t me,
                                        const MapArgs& A) {
-  if (CRIT == BG_OVR_RANGE) return (s < me) ? (e + A.range > ms) : (me + A.range > s);
-  const int64_t ov = min(e, me) - max(s, ms);
-  if (ov <= 0) return false;  // outside the sweep's Overlapping(0) window
-  if (CRIT == BG_OVR_BP) return ov >= A.ovr;
-  if (CRIT == BG_OVR_EXACT) return ms == s && me == e;
-  if (A.perc <= DBL_EPSILON) return true;
-  // sz of BedDistances.hpp:160-174 is the overlap length for overlapping rows
-  const bool fm = (double)ov / (double)(me - ms) >= A.perc;  // relative to the map row
-  const bool fr = (double)ov / (double)(e - s) >= A.perc;    // relative to the ref row
-  if (CRIT == BG_OVR_FRAC_MAP) return fm;
-  if (CRIT == BG_OVR_FRAC_REF) return fr;
-  if (CRIT == BG_OVR_FRAC_EITHER) return fm || fr;
-  return fm && fr;
+  return bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, ms, me);
 }
 
 // first index k in [lo, hi) with X[k] >= v, X in LDS
@@ -135,6 +127,10 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   } else {
     lo = lower_bound_in(A.MS, blo, bhi, klo);
     hi = lower_bound_in(A.MS, lo, bhi, khi);
+  }
+  if (A.wlo) {
+    A.wlo[r] = lo;
+    A.whi[r] = hi;
   }
   int32_t c = 0;
   int64_t sum = 0;
@@ -205,6 +201,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   bg_table* M = set->t[map];
   uint32_t need = 0;
   bool need_sum = false, need_ext = false;
+  int mapfields = 3;  // map row type (bedmap/src/Input.hpp:401-418 MapFields)
   for (int k = 0; k < opts->n_ops; ++k) {
     switch (opts->ops[k]) {
       case BG_MAP_COUNT: case BG_MAP_INDICATOR: case BG_MAP_ECHO_SIZE: case BG_MAP_ECHO_NAME: break;
@@ -215,11 +212,24 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       case BG_MAP_ECHO:
         if (!R->rest_off) return bg_fail(c, BG_E_ARG, "--echo needs the reference file loaded as BG_BED3_REST");
         break;
+      case BG_MAP_ECHO_MAP: case BG_MAP_ECHO_MAP_ID:
+        if (!M->rest_off) return bg_fail(c, BG_E_ARG, "--echo-map/--echo-map-id need the map file loaded with its remainder (BG_BED3_REST / BG_BED5_REST)");
+        need |= NEED_WIN;
+        if (opts->ops[k] == BG_MAP_ECHO_MAP_ID && mapfields < 4) mapfields = 4;
+        break;
+      case BG_MAP_ECHO_MAP_SCORE:
+        need_ext = true;  // the map scores (no arithmetic)
+        need |= NEED_WIN;
+        break;
+      case BG_MAP_ECHO_MAP_SIZE: case BG_MAP_ECHO_OVERLAP_SIZE: case BG_MAP_ECHO_MAP_RANGE:
+        need |= NEED_WIN;
+        break;
       default: return bg_fail(c, BG_E_UNSUPPORTED, "bedmap operation not on the GPU path");
     }
   }
   if (need_sum) need |= NEED_SUM;
   if (need_ext) need |= NEED_EXT;
+  if (need_sum || need_ext) mapfields = 5;  // score operations read the map as B5Rest
   if (opts->scientific) return bg_fail(c, BG_E_UNSUPPORTED, "--sci is not on the GPU path yet");
   if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
   const int crit = opts->criterion;
@@ -242,7 +252,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     case BG_OVR_EXACT: break;
     default: return BG_E_ARG;
   }
-  if ((need & (NEED_SUM | NEED_EXT)) && (M->kind != BG_BED5 || !M->score))
+  if ((need & (NEED_SUM | NEED_EXT)) && !M->score)
     return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
   if (R->has_zero_len || M->has_zero_len)
     return bg_fail(c, BG_E_UNSUPPORTED, "zero-length elements (end == start) are not on the GPU path of bedmap");
@@ -256,6 +266,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   res->kind = RES_MAP;
   res->n = R->n;
   res->mopts = *opts;
+  if (!res->mopts.multidelim[0]) strcpy(res->mopts.multidelim, ";");  // unset: the default
   res->tab = ref;
   res->cnt = (int32_t*)bg_alloc(c, 4 * n1);
   if (need & NEED_SUM) res->isum = (int64_t*)bg_alloc(c, 8 * n1);
@@ -265,8 +276,16 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   if (need & NEED_BASES) res->bases = (uint64_t*)bg_alloc(c, 8 * n1);
   if (need & NEED_UNIQ) res->uniq = (uint32_t*)bg_alloc(c, 4 * n1);
+  if (need & NEED_WIN) {
+    res->wlo = (uint64_t*)bg_alloc(c, 8 * n1);
+    res->whi = (uint64_t*)bg_alloc(c, 8 * n1);
+  }
+  res->map_tab = map;
+  res->mapfields = mapfields;
+  res->perc = perc;
   if (!res->cnt || ((need & NEED_SUM) && !res->isum) || ((need & NEED_EXT) && (!res->vmin || !res->vmax)) ||
-      ((need & NEED_BASES) && !res->bases) || ((need & NEED_UNIQ) && !res->uniq)) {
+      ((need & NEED_BASES) && !res->bases) || ((need & NEED_UNIQ) && !res->uniq) ||
+      ((need & NEED_WIN) && (!res->wlo || !res->whi))) {
     bg_result_free(res);
     return BG_E_NOMEM;
   }
@@ -289,6 +308,8 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   A.vmax = res->vmax;
   A.bases = res->bases;
   A.uniq = res->uniq;
+  A.wlo = res->wlo;
+  A.whi = res->whi;
   A.st = c->dstat;
   if (R->n) {
     const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);

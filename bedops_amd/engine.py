@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
-BED3, BED3_REST, BED5, BED3_SET = 0, 1, 2, 3
+BED3, BED3_REST, BED5, BED3_SET, BED5_REST = 0, 1, 2, 3, 4
 # operations that read only each input's merged set (or, for element-of, only the
 # non-reference inputs' sets): their inputs may be loaded as BED3_SET
 SET_MODES = {"-m", "--merge", "-i", "--intersect", "-d", "--difference", "-e", "--element-of",
@@ -19,8 +19,10 @@ MAP_COUNT, MAP_MEAN = 1, 2
 # bedmap operations and overlap criteria (include/bedgpu.h BG_MAP_* / BG_OVR_*)
 MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, "bases": 7,
            "bases-uniq": 8, "bases-uniq-f": 9, "echo": 10, "echo-ref-size": 11,
-           "echo-ref-name": 12}
-SCORE_OPS = ("mean", "sum", "min", "max")
+           "echo-ref-name": 12, "echo-map": 13, "echo-map-id": 14, "echo-map-score": 15,
+           "echo-map-size": 16, "echo-overlap-size": 17, "echo-map-range": 18}
+SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score")
+MAP_REST_OPS = ("echo-map", "echo-map-id")  # the map rows' remainders are printed
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}
 
@@ -60,7 +62,8 @@ class _MapOpts(ctypes.Structure):
                 ("ops", ctypes.c_int * 16), ("precision", ctypes.c_int),
                 ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
                 ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
-                ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double)]
+                ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double),
+                ("multidelim", ctypes.c_char * 16)]
 
 
 class _ClosestOpts(ctypes.Structure):
@@ -335,7 +338,7 @@ class Engine:
 
     # -------------------------------------------------------------- bedmap
     def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, criterion="bp-ovr", value=None):
+               skip_unmapped=False, criterion="bp-ovr", value=None, multidelim=";"):
         """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result.
         criterion: "bp-ovr" (value = overlap_bp), "range" (value = bp), "fraction-ref",
         "fraction-map", "fraction-either", "fraction-both" (value = fraction), "exact"."""
@@ -348,6 +351,7 @@ class Engine:
         o.scientific = 0
         o.skip_unmapped = 1 if skip_unmapped else 0
         o.delim = delim.encode()
+        o.multidelim = multidelim.encode()
         o.criterion = OVR_CRITERIA[criterion]
         if criterion == "range":
             o.range_bp = int(value)
@@ -358,15 +362,17 @@ class Engine:
         return Result(self, h)
 
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None):
+               skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None, multidelim=";"):
         need5 = any(op in SCORE_OPS for op in ops)
+        mrest = any(op in MAP_REST_OPS for op in ops)
+        mkind = (BED5_REST if mrest else BED5) if need5 else (BED3_REST if mrest else BED3)
         s = self.load([(ref_text, BED3_REST if "echo" in ops else BED3),
-                       (map_text if map_text is not None else ref_text, BED5 if need5 else BED3)])
+                       (map_text if map_text is not None else ref_text, mkind)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)
             r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped,
-                            criterion, value)
+                            criterion, value, multidelim)
             try:
                 return r.text()
             finally:

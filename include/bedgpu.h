@@ -66,6 +66,9 @@ extern "C" {
  * files; operations that need rows (element-of's reference, partition, everything,
  * bedmap, closest-features, --chrom, --range) refuse such a table with BG_E_ARG. */
 #define BG_BED3_SET 3
+/* BED5 with the remainder after `end` kept too (bedmap map files under --echo-map*: the
+ * id and the verbatim row are printed, Bed::B5Rest)                                    */
+#define BG_BED5_REST 4
 
 typedef struct bg_ctx bg_ctx;
 typedef struct bg_set bg_set;       /* N parsed inputs sharing one chromosome dictionary */
@@ -89,6 +92,7 @@ typedef struct bg_map_opts {
   int criterion;       /* overlap option: BG_OVR_* (0 = --bp-ovr, the default)    */
   uint64_t range_bp;   /* --range <int> (> 0; --range 0 is --bp-ovr 1)          */
   double fraction;     /* --fraction-{ref,map,either,both} <val>, as given       */
+  char multidelim[16]; /* --multidelim between --echo-map* items ("" = the default ";") */
 } bg_map_opts;
 /* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
  * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */
@@ -104,6 +108,14 @@ typedef struct bg_map_opts {
 #define BG_MAP_ECHO 10         /* --echo           Echo<Print> (ref row, BG_BED3_REST)  */
 #define BG_MAP_ECHO_SIZE 11    /* --echo-ref-size  Echo<PrintLength>          "%lu"    */
 #define BG_MAP_ECHO_NAME 12    /* --echo-ref-name  Echo<PrintSpanName>  chrom:start-end */
+/* per map row of the window, in genomic order, joined by multidelim (EchoMapBed,
+ * algorithm/visitors/bed/EchoMapBedVisitor.hpp:38-64 + PrintRangeDelim) */
+#define BG_MAP_ECHO_MAP 13           /* --echo-map          the map row verbatim     */
+#define BG_MAP_ECHO_MAP_ID 14        /* --echo-map-id       its 4th column (id)      */
+#define BG_MAP_ECHO_MAP_SCORE 15     /* --echo-map-score    its score, "%.{p}lf"     */
+#define BG_MAP_ECHO_MAP_SIZE 16      /* --echo-map-size     its length               */
+#define BG_MAP_ECHO_OVERLAP_SIZE 17  /* --echo-overlap-size |ref ∩ map row| (EchoMapIntersectLength) */
+#define BG_MAP_ECHO_MAP_RANGE 18     /* --echo-map-range    chrom\tmin start\tmax end (PrintGenomicRange) */
 /* overlap criteria (Bedmap.cpp:95-155 -> data/bed/BedDistances.hpp) */
 #define BG_OVR_BP 0            /* --bp-ovr N       Overlapping(N)            :80-118   */
 #define BG_OVR_RANGE 1         /* --range R        RangedDist(R)             :41-67    */

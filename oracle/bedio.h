@@ -44,7 +44,8 @@ typedef struct {
   int* chrom;
   uint64_t* start;
   uint64_t* end;
-  char** rest;      /* NULL unless read with keep_rest */
+  char** rest;      /* NULL unless read with keep_rest (BED5 / BED4: after score / id) */
+  char** id;        /* NULL unless read as BED4 / BED5 */
   double* score;    /* NULL unless read as BED5 */
   int64_t n, cap;
 } bedfile_t;
@@ -65,6 +66,10 @@ static void bf_push(bedfile_t* f, int c, uint64_t s, uint64_t e, const char* res
   if (keep_rest) f->rest[f->n] = strdup(rest ? rest : "");
   if (keep_score) f->score[f->n] = score;
   f->n++;
+}
+static void bf_set_id(bedfile_t* f, const char* id) {
+  f->id = (char**)realloc(f->id, (size_t)f->cap * sizeof(char*));
+  f->id[f->n - 1] = strdup(id);
 }
 
 #define ORACLE_CHR_MAX 127
@@ -105,7 +110,27 @@ static int read_bed5(FILE* fp, chrom_pool_t* pool, bedfile_t* f) {
                  id, &sc, rest);
     (void)fgetc(fp);
     if (feof(fp)) break;
-    bf_push(f, pool_intern(pool, chr), s, e, NULL, 0, sc, 1);
+    bf_push(f, pool_intern(pool, chr), s, e, rest, 1, sc, 1);
+    bf_set_id(f, id);
+  }
+  return 0;
+}
+
+/* Read a BED4 file: chrom start end id [rest] (Bed::Bed4 with rest, Bed.hpp:
+ * "%s\t%lu\t%lu\t%s%[^\n]s\n"); rest keeps what follows the id. */
+static int read_bed4(FILE* fp, chrom_pool_t* pool, bedfile_t* f) {
+  static char chr[ORACLE_CHR_MAX + 1];
+  static char id[16384];
+  static char rest[ORACLE_REST_MAX + 1];
+  memset(f, 0, sizeof(*f));
+  for (;;) {
+    uint64_t s = 0, e = 0;
+    chr[0] = id[0] = rest[0] = '\0';
+    (void)fscanf(fp, "%127s\t%" SCNu64 "\t%" SCNu64 "\t%16383s%1048576[^\n]s\n", chr, &s, &e, id, rest);
+    (void)fgetc(fp);
+    if (feof(fp)) break;
+    bf_push(f, pool_intern(pool, chr), s, e, rest, 1, 0.0, 0);
+    bf_set_id(f, id);
   }
   return 0;
 }

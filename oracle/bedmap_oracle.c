@@ -164,13 +164,16 @@ static int os_erase(oset_t* s, int64_t x) {
 
 /* visitors */
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
-       V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME };
+       V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
+       V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE };
 static int VIS[64], NVIS;
 static int count_;     /* Count / Indicator */
 static double sum_;    /* Average / Sum: one running double (they see the same events) */
 static int counter_;
 static long cnt_;      /* MultiVisitor's own add/delete balance */
 static const char* DELIM = "|";
+static const char* MULTIDELIM = ";";
+static int MAPFIELDS = 3; /* map row type: B3Rest / B4Rest / B5Rest (Bedmap.cpp:601-655) */
 static int PREC = 6, SCI = 0, SKIP_UNMAPPED = 0;
 static oset_t VWIN;    /* the visitor window (BedBaseVisitor::win_) */
 
@@ -224,6 +227,39 @@ static unsigned int ovr_uniq(int64_t r) {
   ovr += (unsigned int)ovr_len(ts, te, rs, re);
   return ovr;
 }
+/* one map row as its type prints it: B3Rest "%s\t%lu\t%lu%s", B4Rest "...\t%s%s",
+ * B5Rest "...\t%s\t%lf%s" (Bed.hpp; Formats.hpp:34 "%lf") */
+static void print_map_row(int64_t m) {
+  printf("%s\t%" PRIu64 "\t%" PRIu64, POOL.names[MAP->chrom[m]], MAP->start[m], MAP->end[m]);
+  if (MAPFIELDS >= 4) printf("\t%s", MAP->id[m]);
+  if (MAPFIELDS >= 5) printf("\t%lf", MAP->score[m]);
+  fputs(MAP->rest ? MAP->rest[m] : "", stdout);
+}
+static void echo_map(int how, int64_t r) {
+  if (how == V_ECHO_MAP_RANGE) { /* PrintGenomicRange<PrintBED3>, ProcessBedVisitorRow.hpp:433-456 */
+    if (VWIN.n == 0) return;
+    uint64_t s = MAP->start[VWIN.v[0]], e = MAP->end[VWIN.v[0]];
+    for (int64_t k = 1; k < VWIN.n; ++k) {
+      if (s > MAP->start[VWIN.v[k]]) s = MAP->start[VWIN.v[k]];
+      if (e < MAP->end[VWIN.v[k]]) e = MAP->end[VWIN.v[k]];
+    }
+    printf("%s\t%" PRIu64 "\t%" PRIu64, POOL.names[MAP->chrom[VWIN.v[0]]], s, e);
+    return;
+  }
+  for (int64_t k = 0; k < VWIN.n; ++k) { /* PrintRangeDelim: genomic (set) order */
+    const int64_t m = VWIN.v[k];
+    if (k) fputs(MULTIDELIM, stdout);
+    switch (how) {
+      case V_ECHO_MAP: print_map_row(m); break;
+      case V_ECHO_MAP_ID: fputs(MAP->id[m], stdout); break;
+      case V_ECHO_MAP_SCORE: put_real(MAP->score[m]); break;
+      case V_ECHO_MAP_SIZE: printf("%" PRIu64, MAP->end[m] - MAP->start[m]); break;
+      case V_ECHO_OVERLAP_SIZE: /* EchoMapIntersectLengthVisitor.hpp:66-75, "%ld" */
+        printf("%ld", (long)ovr_len(REF->start[r], REF->end[r], MAP->start[m], MAP->end[m]));
+        break;
+    }
+  }
+}
 static void v_done(int64_t r) {
   if (SKIP_UNMAPPED && cnt_ == 0) return;
   for (int i = 0; i < NVIS; ++i) {
@@ -263,6 +299,8 @@ static void v_done(int64_t r) {
                REF->rest ? REF->rest[r] : "");
         break;
       case V_ECHO_SIZE: printf("%" PRIu64, REF->end[r] - REF->start[r]); break;
+      case V_ECHO_MAP: case V_ECHO_MAP_ID: case V_ECHO_MAP_SCORE: case V_ECHO_MAP_SIZE:
+      case V_ECHO_OVERLAP_SIZE: case V_ECHO_MAP_RANGE: echo_map(VIS[i], r); break;
       case V_ECHO_NAME:
         printf("%s:%" PRIu64 "-%" PRIu64, POOL.names[REF->chrom[r]], REF->start[r], REF->end[r]);
         break;
@@ -281,14 +319,17 @@ static double parse_frac(const char* v) {
 }
 
 int main(int argc, char** argv) {
-  int a = 1, need5 = 0, rest = 0;
+  int a = 1, need5 = 0, need4 = 0, rest = 0;
   const char* only_chrom = NULL;
   static const struct { const char* name; int v; int score; } OPS[] = {
       {"--count", V_COUNT, 0},         {"--mean", V_MEAN, 1},           {"--sum", V_SUM, 1},
       {"--min", V_MIN, 1},             {"--max", V_MAX, 1},             {"--indicator", V_INDICATOR, 0},
       {"--bases", V_BASES, 0},         {"--bases-uniq", V_BASES_UNIQ, 0},
       {"--bases-uniq-f", V_BASES_UNIQ_F, 0},                            {"--echo", V_ECHO, 0},
-      {"--echo-ref-size", V_ECHO_SIZE, 0},                              {"--echo-ref-name", V_ECHO_NAME, 0}};
+      {"--echo-ref-size", V_ECHO_SIZE, 0},                              {"--echo-ref-name", V_ECHO_NAME, 0},
+      {"--echo-map", V_ECHO_MAP, 0},   {"--echo-map-id", V_ECHO_MAP_ID, 0}, {"--echo-map-score", V_ECHO_MAP_SCORE, 1},
+      {"--echo-map-size", V_ECHO_MAP_SIZE, 0}, {"--echo-overlap-size", V_ECHO_OVERLAP_SIZE, 0},
+      {"--echo-map-range", V_ECHO_MAP_RANGE, 0}};
   while (a < argc - 2 || (a < argc && strncmp(argv[a], "--", 2) == 0)) {
     const char* o = argv[a++];
     int found = 0;
@@ -296,6 +337,7 @@ int main(int argc, char** argv) {
       if (!strcmp(o, OPS[k].name)) {
         VIS[NVIS++] = OPS[k].v;
         need5 |= OPS[k].score;
+        if (OPS[k].v == V_ECHO_MAP_ID) need4 = 1;
         rest |= OPS[k].v == V_ECHO;
         found = 1;
       }
@@ -312,6 +354,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(o, "--fraction-both") && a < argc) { CRIT = C_FBOTH; PERC = parse_frac(argv[a++]); }
     else if (!strcmp(o, "--exact")) CRIT = C_EXACT;
     else if (!strcmp(o, "--delim") && a < argc) DELIM = argv[a++];
+    else if (!strcmp(o, "--multidelim") && a < argc) MULTIDELIM = argv[a++];
     else if (!strcmp(o, "--prec") && a < argc) PREC = atoi(argv[a++]);
     else if (!strcmp(o, "--chrom") && a < argc) only_chrom = argv[a++];
     else if (!strcmp(o, "--sci")) SCI = 1;
@@ -325,8 +368,10 @@ int main(int argc, char** argv) {
   FILE* fm = open_input(argv[a + 1]);
   if (!fr || !fm) { fprintf(stderr, "bedmap_oracle: cannot open input\n"); return 2; }
   read_bed3(fr, &POOL, &ref, rest);
+  MAPFIELDS = need5 ? 5 : (need4 ? 4 : 3);
   if (need5) read_bed5(fm, &POOL, &map);
-  else read_bed3(fm, &POOL, &map, 0);
+  else if (need4) read_bed4(fm, &POOL, &map);
+  else read_bed3(fm, &POOL, &map, 1);
   if (only_chrom) {
     bedfile_t* fs[2] = {&ref, &map};
     for (int q = 0; q < 2; ++q) {
@@ -337,6 +382,7 @@ int main(int argc, char** argv) {
         f->chrom[k] = f->chrom[j]; f->start[k] = f->start[j]; f->end[k] = f->end[j];
         if (f->score) f->score[k] = f->score[j];
         if (f->rest) f->rest[k] = f->rest[j];
+        if (f->id) f->id[k] = f->id[j];
         ++k;
       }
       f->n = k;

@@ -113,7 +113,10 @@ def test_random_bedmap_vs_oracle(eng, oracle_bin, ovr, prec, skip):
 # oracle = restatement of the sweep + fixWindow + visitors (oracle/bedmap_oracle.c)
 MAP_OPSETS = [["count", "sum", "min", "max", "indicator"],
               ["bases", "bases-uniq", "bases-uniq-f", "mean"],
-              ["echo", "echo-ref-size", "echo-ref-name", "count"]]
+              ["echo", "echo-ref-size", "echo-ref-name", "count"],
+              ["echo-map", "echo-map-id", "echo-map-size"],
+              ["echo-map", "mean", "echo-map-score"],
+              ["echo-overlap-size", "echo-map-range", "count"]]
 MAP_CRITS = [("bp-ovr", 1), ("bp-ovr", 7), ("range", 1), ("range", 25), ("fraction-ref", "0.5"),
              ("fraction-map", "0.25"), ("fraction-map", "1"), ("fraction-either", "0.7"),
              ("fraction-both", "0.3"), ("exact", None)]
@@ -131,7 +134,8 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
             if trial % 2:  # exact matches, duplicates and nesting
                 mp = sorted(mp + ref[::2] + ref[::3], key=lambda r: (r[0].encode(), r[1], r[2]))
             rt = randbed.text(ref, rest="cols", rng=rng).encode()
-            mt = randbed.text(mp, rest="bed5", rng=rng).encode()
+            mt = "".join(f"{c}\t{s}\t{e}\tid{i}\t{rng.randint(0, 999)}" + ("\tx\t+" if i % 3 == 0 else "")
+                         + "\n" for i, (c, s, e) in enumerate(mp)).encode()
             copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
             kw = {"criterion": crit, "value": val}
             if crit == "bp-ovr":
@@ -181,6 +185,7 @@ def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
     r = randbed.write(str(tmp_path / "r.bed"), randbed.text(ref, rest="cols", rng=rng))
     m = randbed.write(str(tmp_path / "m.bed"), randbed.text(mp, rest="bed5", rng=rng))
     for args in (["--fraction-either", "0.4", "--echo", "--bases-uniq", "--max"],
+                 ["--multidelim", "::", "--echo-map-id", "--echo-map", "--prec", "2", "--echo-map-score"],
                  ["--range", "10", "--delim", ";", "--indicator", "--sum"],
                  ["--range", "0", "--count"], ["--exact", "--skip-unmapped", "--echo-ref-name", "--count"]):
         want = subprocess.run([oracle_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE,
