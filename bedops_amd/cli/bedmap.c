@@ -39,7 +39,8 @@ static void usage(FILE* f) {
           "    Operations (GPU path):\n"
           "      --bases --bases-uniq --bases-uniq-f --count --echo --echo-ref-name --echo-ref-size\n"
           "      --echo-map --echo-map-id --echo-map-range --echo-map-score --echo-map-size\n"
-          "      --echo-overlap-size --indicator --max --mean --min --sum\n",
+          "      --echo-overlap-size --indicator --max --mean --min --sum\n"
+          "      --cv --kth <val> --median --stdev --variance\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -65,7 +66,8 @@ int main(int argc, char** argv) {
       {"echo-ref-size", BG_MAP_ECHO_SIZE}, {"echo-ref-name", BG_MAP_ECHO_NAME},
       {"echo-map", BG_MAP_ECHO_MAP}, {"echo-map-id", BG_MAP_ECHO_MAP_ID},
       {"echo-map-score", BG_MAP_ECHO_MAP_SCORE}, {"echo-map-size", BG_MAP_ECHO_MAP_SIZE},
-      {"echo-overlap-size", BG_MAP_ECHO_OVERLAP_SIZE}, {"echo-map-range", BG_MAP_ECHO_MAP_RANGE}};
+      {"echo-overlap-size", BG_MAP_ECHO_OVERLAP_SIZE}, {"echo-map-range", BG_MAP_ECHO_MAP_RANGE},
+      {"median", BG_MAP_MEDIAN}, {"variance", BG_MAP_VARIANCE}, {"stdev", BG_MAP_STDEV}, {"cv", BG_MAP_CV}};
   const char* chrom = NULL;
   int a = 1;
   while (a < argc) {
@@ -156,6 +158,20 @@ int main(int argc, char** argv) {
       is_frac[which] = 1;
       static const int crit[4] = {BG_OVR_FRAC_REF, BG_OVR_FRAC_MAP, BG_OVR_FRAC_EITHER, BG_OVR_FRAC_BOTH};
       o.criterion = crit[which];
+    } else if (!strcmp(k, "kth")) {  /* Input.hpp:290-302; 0 / 1 are Min / Max (Bedmap.cpp:490-501) */
+      char b[512];
+      if (a >= argc) arg_error("No arg for --kth");
+      const char* v = argv[a++];
+      if (strspn(v, ".-0123456789") != strlen(v)) {
+        snprintf(b, sizeof(b), "Non-numeric argument: %s for --kth", v);
+        arg_error(b);
+      }
+      const double kv = strtod(v, NULL);
+      if (!(kv >= 0 && kv <= 1)) arg_error("--kth Expect 0 <= val <= 1");
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.op_arg[o.n_ops] = kv;
+      o.ops[o.n_ops++] = kv == 0 ? BG_MAP_MIN : (kv == 1 ? BG_MAP_MAX : BG_MAP_KTH);
+      need5 = 1;
     } else if (!strcmp(k, "exact")) {
       if (is_exact) arg_error("multiple --exact's detected - use one");
       is_exact = 1;
@@ -171,7 +187,7 @@ int main(int argc, char** argv) {
       if (o.n_ops >= 16) arg_error("too many operations for this build");
       o.ops[o.n_ops++] = op;
       if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX ||
-          op == BG_MAP_ECHO_MAP_SCORE)
+          op == BG_MAP_ECHO_MAP_SCORE || op >= BG_MAP_MEDIAN)
         need5 = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
       if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID) map_rest = 1;

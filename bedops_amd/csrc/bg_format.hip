@@ -44,6 +44,8 @@ struct FmtArgs {
   const uint32_t* uniq;
   // --echo-map*: the map table (s2/e2/text2/rest_off2/rest_len2 below), its scores, each
   // row's candidate range and the overlap criterion
+  const int64_t* isq;
+  double op_arg[16];
   const double* score2;
   const uint64_t* wlo;
   const uint64_t* whi;
@@ -388,6 +390,40 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
   return true;
 }
 
+// value at sorted position p of the window's scores (a multiset: x is at positions
+// [#{< x}, #{<= x}) ), by counting; windows are small, and this keeps no per-row buffer
+__device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint32_t p) {
+  const int64_t s = A.s[k], e = A.e[k];
+  for (uint64_t i = A.wlo[k]; i < A.whi[k]; ++i) {
+    if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[i], A.e2[i])) continue;
+    const double x = A.score2[i];
+    uint32_t lt = 0, le = 0;
+    for (uint64_t j = A.wlo[k]; j < A.whi[k]; ++j) {
+      if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[j], A.e2[j])) continue;
+      const double y = A.score2[j];
+      lt += y < x;
+      le += y <= x;
+    }
+    if (lt <= p && p < le) return x;
+  }
+  return 0.0;  // not reached for p < window size
+}
+
+// RollingKthAverage::DoneReference (numerical/RollingKthAverageVisitor.hpp:61-92): with
+// up = ceil(kth*n), down = floor(kth*n), each made zero-based when > 0, the average of the
+// elements at up and up+1 when up == down, else the element at up
+__device__ __forceinline__ double window_kth(const FmtArgs& A, uint64_t k, uint32_t n, double kth) {
+  if (n == 1) return window_rank(A, k, 0);
+  uint64_t up = (uint64_t)ceil(kth * (double)n), down = (uint64_t)floor(kth * (double)n);
+  if (up > 0) --up;
+  if (down > 0) --down;
+  if (up == down) {
+    const double one = window_rank(A, k, (uint32_t)up), two = window_rank(A, k, (uint32_t)up + 1);
+    return (one + two) / 2.0;
+  }
+  return window_rank(A, k, (uint32_t)up);
+}
+
 // renders (or measures) line k; returns false on a value outside the GPU range
 template <int KIND, typename Out>
 __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
@@ -454,6 +490,22 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         v = (double)A.isum[k] / (double)c;
       } else if (op == BG_MAP_SUM) {
         v = (double)A.isum[k];
+      } else if (op == BG_MAP_VARIANCE || op == BG_MAP_STDEV || op == BG_MAP_CV) {
+        // Variance / StdDev / CoeffVariation DoneReference (VarianceVisitor.hpp, StdevVisitor.hpp,
+        // CoeffVariationVisitor.hpp:60-74) on the exact running sums, in their double order
+        if (c <= 1) { o.put('N'); o.put('A'); o.put('N'); continue; }
+        const double cnt = (double)c, sum = (double)A.isum[k], sq = (double)A.isq[k];
+        const double numer = (cnt * sq) - (sum * sum);
+        const double denom = (cnt * (cnt - 1));
+        v = numer / denom;
+        if (op != BG_MAP_VARIANCE) v = sqrt(v);
+        if (op == BG_MAP_CV) {
+          const double mean = sum / cnt;
+          if (mean == 0) { o.put('N'); o.put('A'); o.put('N'); continue; }
+          v = v / mean;
+        }
+      } else if (op == BG_MAP_MEDIAN || op == BG_MAP_KTH) {
+        v = window_kth(A, k, (uint32_t)c, op == BG_MAP_MEDIAN ? 0.5 : A.op_arg[q]);
       } else {
         v = (op == BG_MAP_MIN) ? A.vmin[k] : A.vmax[k];
       }
@@ -703,6 +755,8 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.e = s->t[r->tab]->ke;
     A.cnt = r->cnt;
     A.isum = r->isum;
+    A.isq = r->isq;
+    for (int q = 0; q < 16; ++q) A.op_arg[q] = r->mopts.op_arg[q];
     A.vmin = r->vmin;
     A.vmax = r->vmax;
     A.bases = r->bases;

@@ -131,6 +131,7 @@ struct bg_result {
   double* vmax = nullptr;
   uint64_t* bases = nullptr; // OvrAggregate
   uint32_t* uniq = nullptr;  // OvrUnique (unsigned int, as the reference)
+  int64_t* isq = nullptr;    // exact integer sum of squared scores (Variance, StdDev, CV)
   uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
   uint64_t* whi = nullptr;
   int map_tab = -1;          // the map table

@@ -34,6 +34,7 @@
 #define NEED_EXT 2u
 #define NEED_BASES 4u
 #define NEED_UNIQ 8u
+#define NEED_SQ 32u   // sum of squares (Variance, StdDev, CV)
 #define NEED_WIN 16u  // --echo-map*: keep each row's candidate range for the formatter
 
 struct MapArgs {
@@ -55,6 +56,7 @@ struct MapArgs {
   double* vmax;
   uint64_t* bases;
   uint32_t* uniq;
+  int64_t* isq;
   uint64_t* wlo;
   uint64_t* whi;
   bg_dstatus* st;
@@ -133,7 +135,7 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
     A.whi[r] = hi;
   }
   int32_t c = 0;
-  int64_t sum = 0;
+  int64_t sum = 0, sq = 0;
   double vmin = 0, vmax = 0;
   uint64_t bases = 0;
   uint32_t uniq = 0;                // unsigned int arithmetic, as OvrUnique's
@@ -157,6 +159,7 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
       if (A.need & (NEED_SUM | NEED_EXT)) {
         const double x = sc[j];
         sum += (int64_t)x;
+        if (A.need & NEED_SQ) sq += (int64_t)x * (int64_t)x;
         if (c == 0) vmin = vmax = x;
         else {
           if (x < vmin) vmin = x;
@@ -181,6 +184,10 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   if (A.isum) {
     A.isum[r] = sum;
     if (sum >= (1LL << 53) || sum <= -(1LL << 53)) atomicOr(&A.st->flags, 4ULL);
+  }
+  if (A.isq) {
+    A.isq[r] = sq;
+    if (sq >= (1LL << 53) || sq < 0) atomicOr(&A.st->flags, 4ULL);
   }
   if (A.vmin) { A.vmin[r] = vmin; A.vmax[r] = vmax; }
   if (A.bases) A.bases[r] = bases;
@@ -223,6 +230,18 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
         break;
       case BG_MAP_ECHO_MAP_SIZE: case BG_MAP_ECHO_OVERLAP_SIZE: case BG_MAP_ECHO_MAP_RANGE:
         need |= NEED_WIN;
+        break;
+      case BG_MAP_KTH:
+        if (!(opts->op_arg[k] > 0.0 && opts->op_arg[k] < 1.0))
+          return bg_fail(c, BG_E_ARG, "--kth on the GPU path takes 0 < val < 1 (0 is --min, 1 is --max)");
+        [[fallthrough]];
+      case BG_MAP_MEDIAN:  // order statistics of the window's scores, taken by the formatter
+        need_ext = true;
+        need |= NEED_WIN;
+        break;
+      case BG_MAP_VARIANCE: case BG_MAP_STDEV: case BG_MAP_CV:
+        need_sum = true;
+        need |= NEED_SQ;
         break;
       default: return bg_fail(c, BG_E_UNSUPPORTED, "bedmap operation not on the GPU path");
     }
@@ -276,6 +295,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   if (need & NEED_BASES) res->bases = (uint64_t*)bg_alloc(c, 8 * n1);
   if (need & NEED_UNIQ) res->uniq = (uint32_t*)bg_alloc(c, 4 * n1);
+  if (need & NEED_SQ) res->isq = (int64_t*)bg_alloc(c, 8 * n1);
   if (need & NEED_WIN) {
     res->wlo = (uint64_t*)bg_alloc(c, 8 * n1);
     res->whi = (uint64_t*)bg_alloc(c, 8 * n1);
@@ -285,7 +305,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   res->perc = perc;
   if (!res->cnt || ((need & NEED_SUM) && !res->isum) || ((need & NEED_EXT) && (!res->vmin || !res->vmax)) ||
       ((need & NEED_BASES) && !res->bases) || ((need & NEED_UNIQ) && !res->uniq) ||
-      ((need & NEED_WIN) && (!res->wlo || !res->whi))) {
+      ((need & NEED_WIN) && (!res->wlo || !res->whi)) || ((need & NEED_SQ) && !res->isq)) {
     bg_result_free(res);
     return BG_E_NOMEM;
   }
@@ -308,6 +328,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   A.vmax = res->vmax;
   A.bases = res->bases;
   A.uniq = res->uniq;
+  A.isq = res->isq;
   A.wlo = res->wlo;
   A.whi = res->whi;
   A.st = c->dstat;
@@ -327,7 +348,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
   if (!rc && (c->hstat->flags & 4ULL))
-    rc = bg_fail(c, BG_E_UNSUPPORTED, "a window score sum reaches 2^53 (inexact in the reference too)");
+    rc = bg_fail(c, BG_E_UNSUPPORTED, "a window score sum (or sum of squares) reaches 2^53 (inexact in the reference too)");
   if (rc) {
     bg_result_free(res);
     return rc;

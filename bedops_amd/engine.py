@@ -20,8 +20,10 @@ MAP_COUNT, MAP_MEAN = 1, 2
 MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, "bases": 7,
            "bases-uniq": 8, "bases-uniq-f": 9, "echo": 10, "echo-ref-size": 11,
            "echo-ref-name": 12, "echo-map": 13, "echo-map-id": 14, "echo-map-score": 15,
-           "echo-map-size": 16, "echo-overlap-size": 17, "echo-map-range": 18}
-SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score")
+           "echo-map-size": 16, "echo-overlap-size": 17, "echo-map-range": 18, "median": 19,
+           "kth": 20, "variance": 21, "stdev": 22, "cv": 23}
+SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score", "median", "kth", "variance", "stdev",
+             "cv")
 MAP_REST_OPS = ("echo-map", "echo-map-id")  # the map rows' remainders are printed
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}
@@ -63,7 +65,7 @@ class _MapOpts(ctypes.Structure):
                 ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
                 ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
                 ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double),
-                ("multidelim", ctypes.c_char * 16)]
+                ("multidelim", ctypes.c_char * 16), ("op_arg", ctypes.c_double * 16)]
 
 
 class _ClosestOpts(ctypes.Structure):
@@ -345,8 +347,10 @@ class Engine:
         o = _MapOpts()
         o.overlap_bp = overlap_bp
         o.n_ops = len(ops)
-        for k, op in enumerate(ops):
-            o.ops[k] = MAP_OPS[op]
+        for k, op in enumerate(ops):  # an op is a name, or (name, argument) for "kth"
+            name, arg = (op if isinstance(op, tuple) else (op, 0.0))
+            o.ops[k] = MAP_OPS[name]
+            o.op_arg[k] = float(arg)
         o.precision = precision
         o.scientific = 0
         o.skip_unmapped = 1 if skip_unmapped else 0
@@ -363,10 +367,11 @@ class Engine:
 
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
                skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None, multidelim=";"):
-        need5 = any(op in SCORE_OPS for op in ops)
-        mrest = any(op in MAP_REST_OPS for op in ops)
+        names = [op[0] if isinstance(op, tuple) else op for op in ops]
+        need5 = any(op in SCORE_OPS for op in names)
+        mrest = any(op in MAP_REST_OPS for op in names)
         mkind = (BED5_REST if mrest else BED5) if need5 else (BED3_REST if mrest else BED3)
-        s = self.load([(ref_text, BED3_REST if "echo" in ops else BED3),
+        s = self.load([(ref_text, BED3_REST if "echo" in names else BED3),
                        (map_text if map_text is not None else ref_text, mkind)])
         try:
             if chrom:

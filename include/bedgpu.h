@@ -93,6 +93,7 @@ typedef struct bg_map_opts {
   uint64_t range_bp;   /* --range <int> (> 0; --range 0 is --bp-ovr 1)          */
   double fraction;     /* --fraction-{ref,map,either,both} <val>, as given       */
   char multidelim[16]; /* --multidelim between --echo-map* items ("" = the default ";") */
+  double op_arg[16];   /* argument of ops[k] (--kth <val>)                         */
 } bg_map_opts;
 /* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
  * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */
@@ -116,6 +117,12 @@ typedef struct bg_map_opts {
 #define BG_MAP_ECHO_MAP_SIZE 16      /* --echo-map-size     its length               */
 #define BG_MAP_ECHO_OVERLAP_SIZE 17  /* --echo-overlap-size |ref ∩ map row| (EchoMapIntersectLength) */
 #define BG_MAP_ECHO_MAP_RANGE 18     /* --echo-map-range    chrom\tmin start\tmax end (PrintGenomicRange) */
+/* order statistics and moments of the window scores (algorithm/visitors/numerical) */
+#define BG_MAP_MEDIAN 19       /* --median         Median = RollingKthAverage(0.5)     */
+#define BG_MAP_KTH 20          /* --kth <val>      RollingKthAverage(val), 0 < val < 1 */
+#define BG_MAP_VARIANCE 21     /* --variance       Variance (running double sums)      */
+#define BG_MAP_STDEV 22        /* --stdev          StdDev                              */
+#define BG_MAP_CV 23           /* --cv             CoeffVariation                      */
 /* overlap criteria (Bedmap.cpp:95-155 -> data/bed/BedDistances.hpp) */
 #define BG_OVR_BP 0            /* --bp-ovr N       Overlapping(N)            :80-118   */
 #define BG_OVR_RANGE 1         /* --range R        RangedDist(R)             :41-67    */

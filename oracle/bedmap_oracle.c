@@ -21,6 +21,8 @@
  *                                     bed/OvrUniqueVisitor.hpp ("%u"), bed/OvrUniqueFractionVisitor.hpp,
  *                                     other/EchoVisitor.hpp with PrintAll / PrintLength /
  *                                     PrintSpanName (helpers/ProcessBedVisitorRow.hpp:309-342);
+ *                                     VarianceVisitor.hpp / StdevVisitor.hpp / CoeffVariationVisitor.hpp
+ *                                     (running double sums), Median / RollingKthAverageVisitor.hpp:61-92;
  *                                     option names: helpers/NamedVisitors.hpp:52-178
  *   number formats .................. "%.{prec}lf"/"%.{prec}e" utility/Formats.hpp:42-50,
  *                                     "NAN" interfaces/src/data/measurement/NaN.cpp:26
@@ -31,6 +33,7 @@
  * Only used by tests/ and bench.py's cpu_baseline; never linked into the product.
  */
 #include <float.h>
+#include <math.h>
 
 #include "bedio.h"
 
@@ -165,7 +168,10 @@ static int os_erase(oset_t* s, int64_t x) {
 /* visitors */
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
        V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
-       V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE };
+       V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE, V_MEDIAN,
+       V_KTH, V_VARIANCE, V_STDEV, V_CV };
+static double VARG[64];      /* --kth argument per visitor */
+static double sq_;           /* Variance-family running sum of squares */
 static int VIS[64], NVIS;
 static int count_;     /* Count / Indicator */
 static double sum_;    /* Average / Sum: one running double (they see the same events) */
@@ -179,12 +185,12 @@ static oset_t VWIN;    /* the visitor window (BedBaseVisitor::win_) */
 
 static void v_add(int64_t m) {
   ++count_;
-  if (MAP->score) { sum_ += MAP->score[m]; ++counter_; }
+  if (MAP->score) { sum_ += MAP->score[m]; sq_ += MAP->score[m] * MAP->score[m]; ++counter_; }
   ++cnt_;
 }
 static void v_del(int64_t m) {
   --count_;
-  if (MAP->score) { sum_ -= MAP->score[m]; --counter_; }
+  if (MAP->score) { sum_ -= MAP->score[m]; sq_ -= MAP->score[m] * MAP->score[m]; --counter_; }
   --cnt_;
 }
 static void put_real(double v) {
@@ -260,6 +266,25 @@ static void echo_map(int how, int64_t r) {
     }
   }
 }
+static int dcmp(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+/* RollingKthAverage::DoneReference on the window's sorted scores (RollingKthAverageVisitor.hpp:61-92) */
+static void put_kth(double kth) {
+  const size_t n = (size_t)VWIN.n;
+  if (n == 0) { fputs("NAN", stdout); return; }
+  double* v = (double*)malloc(n * sizeof(double));
+  for (size_t i = 0; i < n; ++i) v[i] = MAP->score[VWIN.v[i]];
+  qsort(v, n, sizeof(double), dcmp);
+  size_t up = (size_t)ceil(kth * (double)n), down = (size_t)floor(kth * (double)n);
+  if (up > 0) --up;
+  if (down > 0) --down;
+  if (n == 1) put_real(v[0]);
+  else if (up == down) put_real((v[up] + v[up + 1]) / 2.0);
+  else put_real(v[up]);
+  free(v);
+}
 static void v_done(int64_t r) {
   if (SKIP_UNMAPPED && cnt_ == 0) return;
   for (int i = 0; i < NVIS; ++i) {
@@ -299,6 +324,23 @@ static void v_done(int64_t r) {
                REF->rest ? REF->rest[r] : "");
         break;
       case V_ECHO_SIZE: printf("%" PRIu64, REF->end[r] - REF->start[r]); break;
+      case V_MEDIAN: put_kth(0.5); break;
+      case V_KTH: put_kth(VARG[i]); break;
+      case V_VARIANCE: case V_STDEV: case V_CV: {
+        const double count = (double)counter_;
+        if (count <= 1) { fputs("NAN", stdout); break; }
+        const double numer = (count * sq_) - (sum_ * sum_);
+        const double denom = (count * (count - 1));
+        double v = numer / denom;
+        if (VIS[i] != V_VARIANCE) v = sqrt(v);
+        if (VIS[i] == V_CV) {
+          const double mean = sum_ / count;
+          if (mean == 0) { fputs("NAN", stdout); break; }
+          v = v / mean;
+        }
+        put_real(v);
+        break;
+      }
       case V_ECHO_MAP: case V_ECHO_MAP_ID: case V_ECHO_MAP_SCORE: case V_ECHO_MAP_SIZE:
       case V_ECHO_OVERLAP_SIZE: case V_ECHO_MAP_RANGE: echo_map(VIS[i], r); break;
       case V_ECHO_NAME:
@@ -329,7 +371,8 @@ int main(int argc, char** argv) {
       {"--echo-ref-size", V_ECHO_SIZE, 0},                              {"--echo-ref-name", V_ECHO_NAME, 0},
       {"--echo-map", V_ECHO_MAP, 0},   {"--echo-map-id", V_ECHO_MAP_ID, 0}, {"--echo-map-score", V_ECHO_MAP_SCORE, 1},
       {"--echo-map-size", V_ECHO_MAP_SIZE, 0}, {"--echo-overlap-size", V_ECHO_OVERLAP_SIZE, 0},
-      {"--echo-map-range", V_ECHO_MAP_RANGE, 0}};
+      {"--echo-map-range", V_ECHO_MAP_RANGE, 0}, {"--median", V_MEDIAN, 1},
+      {"--variance", V_VARIANCE, 1},   {"--stdev", V_STDEV, 1},         {"--cv", V_CV, 1}};
   while (a < argc - 2 || (a < argc && strncmp(argv[a], "--", 2) == 0)) {
     const char* o = argv[a++];
     int found = 0;
@@ -342,6 +385,12 @@ int main(int argc, char** argv) {
         found = 1;
       }
     if (found) continue;
+    if (!strcmp(o, "--kth") && a < argc) {
+      VARG[NVIS] = strtod(argv[a++], NULL);
+      VIS[NVIS++] = V_KTH;
+      need5 = 1;
+      continue;
+    }
     if (!strcmp(o, "--bp-ovr") && a < argc) { CRIT = C_BP; OVR = strtoull(argv[a++], 0, 10); }
     else if (!strcmp(o, "--range") && a < argc) {
       RANGE = strtoull(argv[a++], 0, 10);

@@ -116,7 +116,8 @@ MAP_OPSETS = [["count", "sum", "min", "max", "indicator"],
               ["echo", "echo-ref-size", "echo-ref-name", "count"],
               ["echo-map", "echo-map-id", "echo-map-size"],
               ["echo-map", "mean", "echo-map-score"],
-              ["echo-overlap-size", "echo-map-range", "count"]]
+              ["echo-overlap-size", "echo-map-range", "count"],
+              ["median", "variance", "stdev", "cv", ("kth", 0.3), ("kth", 0.05)]]
 MAP_CRITS = [("bp-ovr", 1), ("bp-ovr", 7), ("range", 1), ("range", 25), ("fraction-ref", "0.5"),
              ("fraction-map", "0.25"), ("fraction-map", "1"), ("fraction-either", "0.7"),
              ("fraction-both", "0.3"), ("exact", None)]
@@ -141,7 +142,8 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
             if crit == "bp-ovr":
                 kw = {"overlap_bp": val}
             for ops in MAP_OPSETS:
-                args = [f"--{o}" for o in ops] + copt
+                args = [a for o in ops for a in ([f"--{o[0]}", str(o[1])] if isinstance(o, tuple)
+                                                 else [f"--{o}"])] + copt
                 want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
                 got = eng.bedmap(ops, rt, mt, **kw)
                 assert got == want, (crit, val, ops, trial)
@@ -169,9 +171,10 @@ def test_bedmap_min_max_decimal_scores(eng, oracle_bin):
                  for i, (c, s, e) in enumerate(mp)).encode()
     with tempfile.TemporaryDirectory() as td:
         for prec in (0, 2, 6):
-            want = run_oracle(oracle_bin["bedmap"], ["--min", "--max", "--count", "--prec", str(prec)],
-                              [rt, mt], td)
-            assert eng.bedmap(["min", "max", "count"], rt, mt, precision=prec) == want
+            want = run_oracle(oracle_bin["bedmap"], ["--min", "--max", "--count", "--median", "--kth",
+                                                     "0.7", "--prec", str(prec)], [rt, mt], td)
+            assert eng.bedmap(["min", "max", "count", "median", ("kth", 0.7)], rt, mt,
+                              precision=prec) == want
     from bedops_amd import BedgpuError
     with pytest.raises(BedgpuError) as ei:
         eng.bedmap(["sum"], rt, mt)
