@@ -288,8 +288,26 @@ __global__ void __launch_bounds__(BG_NT) k_lengths(const int64_t* __restrict__ S
 }
 
 // One thread per reference row; the workgroup first bounds the component range its rows
-// can touch (two searches over the whole list), so each row's own searches run over a
-// few hundred cache-resident components instead of the whole list.
+// can touch (two searches over the whole list), stages that slice of component starts and
+// ends in LDS when it fits (it nearly always does: 256 consecutive rows span few
+// components), and each row's own two searches run there instead of in L2.
+#define EF_SLICE 1024
+__device__ __forceinline__ uint32_t lds_lower(const int64_t* X, uint32_t lo, uint32_t hi, int64_t v) {
+  while (lo < hi) {  // first k in [lo, hi) with X[k] >= v
+    const uint32_t mid = (lo + hi) >> 1;
+    if (X[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint32_t lds_upper(const int64_t* X, uint32_t lo, uint32_t hi, int64_t v) {
+  while (lo < hi) {  // first k in [lo, hi) with X[k] > v
+    const uint32_t mid = (lo + hi) >> 1;
+    if (X[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
 __global__ void __launch_bounds__(BG_NT) k_element_flags(
     const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
     const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
@@ -297,6 +315,7 @@ __global__ void __launch_bounds__(BG_NT) k_element_flags(
     uint8_t* __restrict__ flag) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
+  __shared__ int64_t xs[EF_SLICE], xe[EF_SLICE];
   const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
   const uint64_t r = r0 + threadIdx.x;
   const bool live = r < nr;
@@ -311,22 +330,35 @@ __global__ void __launch_bounds__(BG_NT) k_element_flags(
     bnd[1] = lower_bound_i64(OS_, no, m);  // no row ends after m
   }
   __syncthreads();
-  if (!live) return;
   const uint64_t blo = bnd[0], bhi = max(bnd[0], bnd[1]);
+  const bool staged = bhi - blo <= EF_SLICE;  // block-uniform
+  if (staged) {
+    for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) {
+      xs[i] = OS_[blo + i];
+      xe[i] = OE_[blo + i];
+    }
+    __syncthreads();
+  }
+  if (!live) return;
   // exact within [blo, bhi]: a row's first component ending after s is >= blo, and its
   // first component starting at/after e is <= bhi; a clamped lo == bhi means no overlap,
   // which decides like "nothing left" below (keep = invert)
-  const uint64_t lo = upper_bound_in(OE_, blo, bhi, s);  // first component ending after s
+  const uint32_t n = (uint32_t)(bhi - blo);
+  const uint64_t lo = staged ? blo + lds_upper(xe, 0, n, s)
+                             : upper_bound_in(OE_, blo, bhi, s);  // first component ending after s
   bool keep;
   if (lo >= no) {
     keep = invert;  // nothing left to be an element of (Bedops.cpp:1044-1048)
   } else {
-    const uint64_t hi = lower_bound_in(OS_, blo, bhi, e);  // first component starting at/after e
+    const uint64_t hi = staged ? blo + lds_lower(xs, (uint32_t)(lo - blo), n, e)
+                               : lower_bound_in(OS_, blo, bhi, e);  // first component starting at/after e
     uint64_t ov = 0;
     if (lo < hi) {
       ov = P[hi] - P[lo];
-      if (s > OS_[lo]) ov -= (uint64_t)(s - OS_[lo]);
-      if (OE_[hi - 1] > e) ov -= (uint64_t)(OE_[hi - 1] - e);
+      const int64_t slo = staged ? xs[lo - blo] : OS_[lo];
+      const int64_t ehi = staged ? xe[hi - 1 - blo] : OE_[hi - 1];
+      if (s > slo) ov -= (uint64_t)(s - slo);
+      if (ehi > e) ov -= (uint64_t)(ehi - e);
     }
     const double rov = (double)ov, range = (double)(e - s);
     const bool is_el = use_pct ? (rov / range >= thres) : (rov >= thres);

@@ -82,6 +82,21 @@ def test_random_bedops_vs_oracle(eng, oracle_bin, mode, nfiles, zero_frac):
                 assert got == want, (mode, spec, trial, n)
 
 
+def test_element_of_wide_rows_slice(eng, oracle_bin):
+    """reference rows spanning more components than a workgroup stages in LDS"""
+    rng = random.Random(21)
+    ref = sorted([("chr1", 0, 90000), ("chr1", 5, 60000), ("chr1", 100, 101)] +
+                 randbed.rows(rng, 600, chroms=["chr1"], span=100000, maxlen=50),
+                 key=lambda r: (r[1], r[2]))
+    other = randbed.rows(rng, 6000, chroms=["chr1"], span=100000, maxlen=8)
+    rt = randbed.text(ref, rest="cols", rng=rng).encode()
+    ot = randbed.text(other).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for spec in ("1", "30%", "100%"):
+            want = run_oracle(oracle_bin["bedops"], ["-e", spec], [rt, ot], td)
+            assert eng.bedops("-e", [rt, ot], spec=spec) == want, spec
+
+
 def _fields(t):
     for ln in t.decode().splitlines():
         f = ln.split()
