@@ -40,7 +40,7 @@ static void usage(FILE* f) {
           "      --bases --bases-uniq --bases-uniq-f --count --echo --echo-ref-name --echo-ref-size\n"
           "      --echo-map --echo-map-id --echo-map-range --echo-map-score --echo-map-size\n"
           "      --echo-overlap-size --indicator --max --mean --min --sum\n"
-          "      --cv --kth <val> --median --stdev --variance\n",
+          "      --cv --kth <val> --median --stdev --variance --echo-map-id-uniq --echo-ref-row-id\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -67,7 +67,8 @@ int main(int argc, char** argv) {
       {"echo-map", BG_MAP_ECHO_MAP}, {"echo-map-id", BG_MAP_ECHO_MAP_ID},
       {"echo-map-score", BG_MAP_ECHO_MAP_SCORE}, {"echo-map-size", BG_MAP_ECHO_MAP_SIZE},
       {"echo-overlap-size", BG_MAP_ECHO_OVERLAP_SIZE}, {"echo-map-range", BG_MAP_ECHO_MAP_RANGE},
-      {"median", BG_MAP_MEDIAN}, {"variance", BG_MAP_VARIANCE}, {"stdev", BG_MAP_STDEV}, {"cv", BG_MAP_CV}};
+      {"median", BG_MAP_MEDIAN}, {"variance", BG_MAP_VARIANCE}, {"stdev", BG_MAP_STDEV}, {"cv", BG_MAP_CV},
+      {"echo-map-id-uniq", BG_MAP_ECHO_MAP_ID_UNIQ}, {"echo-ref-row-id", BG_MAP_ECHO_REF_ROW_ID}};
   const char* chrom = NULL;
   int a = 1;
   while (a < argc) {
@@ -187,10 +188,10 @@ int main(int argc, char** argv) {
       if (o.n_ops >= 16) arg_error("too many operations for this build");
       o.ops[o.n_ops++] = op;
       if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX ||
-          op == BG_MAP_ECHO_MAP_SCORE || op >= BG_MAP_MEDIAN)
+          op == BG_MAP_ECHO_MAP_SCORE || (op >= BG_MAP_MEDIAN && op <= BG_MAP_CV))
         need5 = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
-      if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID) map_rest = 1;
+      if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) map_rest = 1;
     }
   }
   {  /* one overlap specification (Input.hpp:330-343) */

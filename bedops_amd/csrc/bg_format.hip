@@ -45,6 +45,8 @@ struct FmtArgs {
   // --echo-map*: the map table (s2/e2/text2/rest_off2/rest_len2 below), its scores, each
   // row's candidate range and the overlap criterion
   const int64_t* isq;
+  const uint64_t* rrank;  // --echo-ref-row-id under --skip-unmapped (else the row index)
+  int nrid;               // --echo-ref-row-id operations per line
   double op_arg[16];
   const double* score2;
   const uint64_t* wlo;
@@ -390,6 +392,49 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
   return true;
 }
 
+// the id (4th column) of map row m: the first token of its remainder
+__device__ __forceinline__ const char* map_id(const FmtArgs& A, uint64_t m, uint32_t& len) {
+  const char* rp = A.text2 + A.rest_off2[m];
+  const uint32_t rl = A.rest_len2[m];
+  uint32_t i = 0;
+  while (i < rl && fmt_isws(rp[i])) ++i;
+  uint32_t j = i;
+  while (j < rl && !fmt_isws(rp[j])) ++j;
+  len = j - i;
+  return rp + i;
+}
+// std::string ordering (char_traits<char>::compare: bytes as unsigned char, then length)
+__device__ __forceinline__ int id_cmp(const char* a, uint32_t la, const char* b, uint32_t lb) {
+  const uint32_t n = la < lb ? la : lb;
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return (uint8_t)a[i] < (uint8_t)b[i] ? -1 : 1;
+  return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+// --echo-map-id-uniq: the window's ids as a sorted set (PrintUniqueRangeIDs,
+// ProcessBedVisitorRow.hpp:361-385), by repeated selection of the next larger id
+template <typename Out>
+__device__ __forceinline__ void put_unique_ids(const FmtArgs& A, Out& o, uint64_t k) {
+  const int64_t s = A.s[k], e = A.e[k];
+  const char* prev = nullptr;
+  uint32_t plen = 0;
+  for (;;) {
+    const char* best = nullptr;
+    uint32_t blen = 0;
+    for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
+      if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m])) continue;
+      uint32_t l;
+      const char* id = map_id(A, m, l);
+      if (prev && id_cmp(id, l, prev, plen) <= 0) continue;
+      if (!best || id_cmp(id, l, best, blen) < 0) { best = id; blen = l; }
+    }
+    if (!best) return;
+    if (prev) for (int d = 0; d < A.mdlen; ++d) o.put(A.mdelim[d]);
+    for (uint32_t i = 0; i < blen; ++i) o.put(best[i]);
+    prev = best;
+    plen = blen;
+  }
+}
+
 // value at sorted position p of the window's scores (a multiset: x is at positions
 // [#{< x}, #{<= x}) ), by counting; windows are small, and this keeps no per-row buffer
 __device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint32_t p) {
@@ -458,6 +503,19 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
       }
       if (op == BG_MAP_ECHO) {
         put_row(A, o, A.s[k], A.e[k], A.text + A.rest_off[k], A.rest_len[k]);
+        continue;
+      }
+      if (op == BG_MAP_ECHO_MAP_ID_UNIQ) {
+        put_unique_ids(A, o, k);
+        continue;
+      }
+      if (op == BG_MAP_ECHO_REF_ROW_ID) {  // PrintRowID: "id-" ++rowID (a static shared by all)
+        const uint64_t line = A.rrank ? A.rrank[k] : k;
+        uint64_t j = 0;
+        for (int q2 = 0; q2 < q; ++q2) j += A.ops[q2] == BG_MAP_ECHO_REF_ROW_ID;
+        const uint64_t id = line * (uint64_t)A.nrid + j + 1;
+        o.put('i'); o.put('d'); o.put('-');
+        put_u64(o, id, dec_len_u64(id));
         continue;
       }
       if (op >= BG_MAP_ECHO_MAP && op <= BG_MAP_ECHO_MAP_RANGE) {
@@ -756,6 +814,9 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.cnt = r->cnt;
     A.isum = r->isum;
     A.isq = r->isq;
+    A.rrank = r->rrank;
+    A.nrid = 0;
+    for (int q = 0; q < r->mopts.n_ops; ++q) A.nrid += r->mopts.ops[q] == BG_MAP_ECHO_REF_ROW_ID;
     for (int q = 0; q < 16; ++q) A.op_arg[q] = r->mopts.op_arg[q];
     A.vmin = r->vmin;
     A.vmax = r->vmax;

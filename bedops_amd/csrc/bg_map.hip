@@ -194,6 +194,12 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   if (A.uniq) A.uniq[r] = uniq;
 }
 
+// 1 per reference row that prints a line (MultiVisitor.hpp:83-84 skips rows without maps)
+__global__ void k_map_printed(const int32_t* __restrict__ cnt, uint64_t n, uint64_t* __restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = cnt[i] > 0 ? 1 : 0;
+}
+
 extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts* opts,
                       bg_result** out) {
   if (!c || !set || !opts || !out || ref < 0 || map < 0 || ref >= (int)set->t.size() ||
@@ -209,6 +215,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   uint32_t need = 0;
   bool need_sum = false, need_ext = false;
   int mapfields = 3;  // map row type (bedmap/src/Input.hpp:401-418 MapFields)
+  bool need_rrank = false;
   for (int k = 0; k < opts->n_ops; ++k) {
     switch (opts->ops[k]) {
       case BG_MAP_COUNT: case BG_MAP_INDICATOR: case BG_MAP_ECHO_SIZE: case BG_MAP_ECHO_NAME: break;
@@ -219,10 +226,11 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       case BG_MAP_ECHO:
         if (!R->rest_off) return bg_fail(c, BG_E_ARG, "--echo needs the reference file loaded as BG_BED3_REST");
         break;
-      case BG_MAP_ECHO_MAP: case BG_MAP_ECHO_MAP_ID:
+      case BG_MAP_ECHO_REF_ROW_ID: need_rrank = opts->skip_unmapped != 0; break;
+      case BG_MAP_ECHO_MAP: case BG_MAP_ECHO_MAP_ID: case BG_MAP_ECHO_MAP_ID_UNIQ:
         if (!M->rest_off) return bg_fail(c, BG_E_ARG, "--echo-map/--echo-map-id need the map file loaded with its remainder (BG_BED3_REST / BG_BED5_REST)");
         need |= NEED_WIN;
-        if (opts->ops[k] == BG_MAP_ECHO_MAP_ID && mapfields < 4) mapfields = 4;
+        if (opts->ops[k] != BG_MAP_ECHO_MAP && mapfields < 4) mapfields = 4;
         break;
       case BG_MAP_ECHO_MAP_SCORE:
         need_ext = true;  // the map scores (no arithmetic)
@@ -347,6 +355,16 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   int rc = bg_hip_ok(c, hipGetLastError());
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  if (!rc && need_rrank && R->n) {  // printed-line ranks for --echo-ref-row-id
+    res->rrank = (uint64_t*)bg_alloc(c, 8 * n1);
+    if (!res->rrank) rc = BG_E_NOMEM;
+    if (!rc) {
+      BG_LAUNCH(c, "k_map_printed", k_map_printed, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT), res->cnt,
+                R->n, res->rrank);
+      rc = bg_hip_ok(c, hipGetLastError());
+    }
+    if (!rc) rc = bg_scan_sum_u64(c, res->rrank, res->rrank, R->n, nullptr);
+  }
   if (!rc && (c->hstat->flags & 4ULL))
     rc = bg_fail(c, BG_E_UNSUPPORTED, "a window score sum (or sum of squares) reaches 2^53 (inexact in the reference too)");
   if (rc) {

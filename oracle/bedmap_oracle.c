@@ -169,7 +169,7 @@ static int os_erase(oset_t* s, int64_t x) {
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
        V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
        V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE, V_MEDIAN,
-       V_KTH, V_VARIANCE, V_STDEV, V_CV };
+       V_KTH, V_VARIANCE, V_STDEV, V_CV, V_ECHO_MAP_ID_UNIQ, V_ECHO_REF_ROW_ID };
 static double VARG[64];      /* --kth argument per visitor */
 static double sq_;           /* Variance-family running sum of squares */
 static int VIS[64], NVIS;
@@ -285,6 +285,21 @@ static void put_kth(double kth) {
   else put_real(v[up]);
   free(v);
 }
+static int scmp(const void* a, const void* b) { return strcmp(*(char* const*)a, *(char* const*)b); }
+/* PrintUniqueRangeIDs (ProcessBedVisitorRow.hpp:361-385): std::set<std::string> of the ids */
+static void put_unique_ids(void) {
+  if (VWIN.n == 0) return;
+  char** v = (char**)malloc((size_t)VWIN.n * sizeof(char*));
+  for (int64_t i = 0; i < VWIN.n; ++i) v[i] = MAP->id[VWIN.v[i]];
+  qsort(v, (size_t)VWIN.n, sizeof(char*), scmp);
+  for (int64_t i = 0; i < VWIN.n; ++i) {
+    if (i && !strcmp(v[i], v[i - 1])) continue;
+    if (i) fputs(MULTIDELIM, stdout);
+    fputs(v[i], stdout);
+  }
+  free(v);
+}
+static unsigned long ROWID; /* PrintRowID's static counter (ProcessBedVisitorRow.hpp:347-355) */
 static void v_done(int64_t r) {
   if (SKIP_UNMAPPED && cnt_ == 0) return;
   for (int i = 0; i < NVIS; ++i) {
@@ -324,6 +339,8 @@ static void v_done(int64_t r) {
                REF->rest ? REF->rest[r] : "");
         break;
       case V_ECHO_SIZE: printf("%" PRIu64, REF->end[r] - REF->start[r]); break;
+      case V_ECHO_MAP_ID_UNIQ: put_unique_ids(); break;
+      case V_ECHO_REF_ROW_ID: printf("id-%lu", ++ROWID); break;
       case V_MEDIAN: put_kth(0.5); break;
       case V_KTH: put_kth(VARG[i]); break;
       case V_VARIANCE: case V_STDEV: case V_CV: {
@@ -372,7 +389,8 @@ int main(int argc, char** argv) {
       {"--echo-map", V_ECHO_MAP, 0},   {"--echo-map-id", V_ECHO_MAP_ID, 0}, {"--echo-map-score", V_ECHO_MAP_SCORE, 1},
       {"--echo-map-size", V_ECHO_MAP_SIZE, 0}, {"--echo-overlap-size", V_ECHO_OVERLAP_SIZE, 0},
       {"--echo-map-range", V_ECHO_MAP_RANGE, 0}, {"--median", V_MEDIAN, 1},
-      {"--variance", V_VARIANCE, 1},   {"--stdev", V_STDEV, 1},         {"--cv", V_CV, 1}};
+      {"--variance", V_VARIANCE, 1},   {"--stdev", V_STDEV, 1},         {"--cv", V_CV, 1},
+      {"--echo-map-id-uniq", V_ECHO_MAP_ID_UNIQ, 0}, {"--echo-ref-row-id", V_ECHO_REF_ROW_ID, 0}};
   while (a < argc - 2 || (a < argc && strncmp(argv[a], "--", 2) == 0)) {
     const char* o = argv[a++];
     int found = 0;
@@ -380,7 +398,7 @@ int main(int argc, char** argv) {
       if (!strcmp(o, OPS[k].name)) {
         VIS[NVIS++] = OPS[k].v;
         need5 |= OPS[k].score;
-        if (OPS[k].v == V_ECHO_MAP_ID) need4 = 1;
+        if (OPS[k].v == V_ECHO_MAP_ID || OPS[k].v == V_ECHO_MAP_ID_UNIQ) need4 = 1;
         rest |= OPS[k].v == V_ECHO;
         found = 1;
       }

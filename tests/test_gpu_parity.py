@@ -132,7 +132,8 @@ MAP_OPSETS = [["count", "sum", "min", "max", "indicator"],
               ["echo-map", "echo-map-id", "echo-map-size"],
               ["echo-map", "mean", "echo-map-score"],
               ["echo-overlap-size", "echo-map-range", "count"],
-              ["median", "variance", "stdev", "cv", ("kth", 0.3), ("kth", 0.05)]]
+              ["median", "variance", "stdev", "cv", ("kth", 0.3), ("kth", 0.05)],
+              ["echo-ref-row-id", "echo-map-id-uniq", "echo-ref-row-id", "count"]]
 MAP_CRITS = [("bp-ovr", 1), ("bp-ovr", 7), ("range", 1), ("range", 25), ("fraction-ref", "0.5"),
              ("fraction-map", "0.25"), ("fraction-map", "1"), ("fraction-either", "0.7"),
              ("fraction-both", "0.3"), ("exact", None)]
@@ -150,7 +151,7 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
             if trial % 2:  # exact matches, duplicates and nesting
                 mp = sorted(mp + ref[::2] + ref[::3], key=lambda r: (r[0].encode(), r[1], r[2]))
             rt = randbed.text(ref, rest="cols", rng=rng).encode()
-            mt = "".join(f"{c}\t{s}\t{e}\tid{i}\t{rng.randint(0, 999)}" + ("\tx\t+" if i % 3 == 0 else "")
+            mt = "".join(f"{c}\t{s}\t{e}\tid{i % 37}\t{rng.randint(0, 999)}" + ("\tx\t+" if i % 3 == 0 else "")
                          + "\n" for i, (c, s, e) in enumerate(mp)).encode()
             copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
             kw = {"criterion": crit, "value": val}
@@ -205,7 +206,8 @@ def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
     for args in (["--fraction-either", "0.4", "--echo", "--bases-uniq", "--max"],
                  ["--multidelim", "::", "--echo-map-id", "--echo-map", "--prec", "2", "--echo-map-score"],
                  ["--range", "10", "--delim", ";", "--indicator", "--sum"],
-                 ["--range", "0", "--count"], ["--exact", "--skip-unmapped", "--echo-ref-name", "--count"]):
+                 ["--range", "0", "--count"], ["--exact", "--skip-unmapped", "--echo-ref-name", "--count"],
+                 ["--skip-unmapped", "--echo-ref-row-id", "--echo-map-id-uniq"]):
         want = subprocess.run([oracle_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE,
                               check=True).stdout
         got = subprocess.run([gpu_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE,
