@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
   o.precision = 6;
   strcpy(o.delim, "|");
   strcpy(o.multidelim, ";");
-  int ec = 0, need5 = 0, need_rest = 0, map_rest = 0, set_prec = 0, set_delim = 0;
+  int ec = 0, check = 0, need4 = 0, need5 = 0, need_rest = 0, map_rest = 0, set_prec = 0, set_delim = 0;
   int is_bp = 0, is_range = 0, range_alias = 0, is_exact = 0, is_frac[4] = {0, 0, 0, 0};
   static const struct { const char* name; int op; } OPS[] = {
       {"count", BG_MAP_COUNT}, {"mean", BG_MAP_MEAN}, {"sum", BG_MAP_SUM}, {"min", BG_MAP_MIN},
@@ -82,7 +82,10 @@ int main(int argc, char** argv) {
     const char* k = nx + 2;
     if (!strcmp(k, "help")) { usage(stdout); return EXIT_SUCCESS; }
     else if (!strcmp(k, "version")) { printf("bedmap\n  version:  %s\n", BEDOPS_AMD_VERSION); return EXIT_SUCCESS; }
-    else if (!strcmp(k, "ec") || !strcmp(k, "header")) ec = 1;
+    else if (!strcmp(k, "ec") || !strcmp(k, "header")) {
+      ec = 1;
+      if (!strcmp(k, "ec")) check = 1;
+    }
     else if (!strcmp(k, "faster") || !strcmp(k, "sweep-all")) {}
     else if (!strcmp(k, "delim")) {
       if (set_delim) arg_error("--delim specified multiple times");
@@ -192,6 +195,7 @@ int main(int argc, char** argv) {
         need5 = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
       if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) map_rest = 1;
+      if (op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) need4 = 1;
     }
   }
   {  /* one overlap specification (Input.hpp:330-343) */
@@ -218,6 +222,10 @@ int main(int argc, char** argv) {
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   text_buf_t tr = {0}, tm = {0};
   if (read_text(argv[a], &tr)) arg_error("Unable to read the reference file");
+  /* --ec: the reference file is B3Rest, the map file B3Rest/B4Rest/B5Rest by the
+   * operations' MapFields (Input.hpp:401-418, Bedmap.cpp:601-655) */
+  const int mapfields = need5 ? 5 : (need4 ? 4 : 3);
+  if (check) ec_check(PROG, ctx, argv[a], &tr, nf == 1 ? mapfields : 3, 1);
   if (ec) apply_ec_header(&tr);
   bg_input in[2];
   in[0].data = tr.data;
@@ -226,6 +234,7 @@ int main(int argc, char** argv) {
   in[0].kind = need_rest ? BG_BED3_REST : BG_BED3;
   if (nf == 2) {
     if (read_text(argv[a + 1], &tm)) arg_error("Unable to read the map file");
+    if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1);
     if (ec) apply_ec_header(&tm);
     in[1].data = tm.data;
     in[1].nbytes = tm.n;

@@ -151,7 +151,7 @@ int main(int argc, char** argv) {
     usage(stderr);
     return EXIT_FAILURE;
   }
-  int ec = 0, has_op = 0, has_chrom = 0, has_range = 0, lpad = 0, rpad = 0;
+  int ec = 0, check = 0, has_op = 0, has_chrom = 0, has_range = 0, lpad = 0, rpad = 0;
   int full_left = 0, chop_x = 0;
   long chop_bp = 1, chop_stagger = 0;
   char mode = 0;
@@ -163,6 +163,7 @@ int main(int argc, char** argv) {
     const char* nx = argv[a];
     if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) {
       ec = 1;
+      if (!strcmp(nx, "--ec")) check = 1;
     } else if (!strcmp(nx, "--chrom")) {
       if (has_chrom) bad_input("--chrom specified multiple times.");
       if (++a >= argc) bad_input("No value for --chrom given.");
@@ -314,6 +315,8 @@ int main(int argc, char** argv) {
       snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
       die_msg(PROG, b);
     }
+    const int keep_rest = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0));
+    if (check) ec_check(PROG, ctx, argv[a + i], &tx[i], 3, keep_rest);
     if (ec) apply_ec_header(&tx[i]);
     in[i].data = tx[i].data;
     in[i].nbytes = tx[i].n;

@@ -108,6 +108,26 @@ static void apply_ec_header(text_buf_t* t) {
   if (t->n > 0 && t->data[t->n - 1] != '\n') t->data[t->n++] = '\n'; /* capacity has +16 */
 }
 
+/* --ec (Bed::bed_check_iterator, BedCheckIterator.hpp): every line of `t` checked on the
+ * GPU before anything else reads it; the first failing line ends the program with the
+ * reference's "in <file>\n<message>\nSee row: <n>" */
+static void ec_check(const char* prog, bg_ctx* ctx, const char* fn, const text_buf_t* t, int nfields,
+                     int has_rest) {
+  bg_input in;
+  in.data = t->data;
+  in.nbytes = t->n;
+  in.on_device = 0;
+  in.kind = BG_BED3;
+  bg_check_result cr;
+  int rc = bg_check(ctx, &in, nfields, has_rest, &cr);
+  if (rc) die_ctx(prog, ctx, rc);
+  if (!cr.row) return;
+  char m[2048], b[4096];
+  bg_check_message(t->data + cr.line_off, cr.line_len, cr.code, nfields, has_rest, m, sizeof(m));
+  snprintf(b, sizeof(b), "in %s\n%s\nSee row: %llu", fn, m, (unsigned long long)cr.row);
+  die_msg(prog, b);
+}
+
 static int env_device(void) {
   const char* d = getenv("BEDGPU_DEVICE");
   return d ? atoi(d) : 0;

@@ -48,14 +48,17 @@ int main(int argc, char** argv) {
   bg_closest_opts o;
   memset(&o, 0, sizeof(o));
   strcpy(o.delim, "|");
-  int ec = 0, outopt = 0;
+  int ec = 0, check = 0, outopt = 0;
   const char* chrom = NULL;
   int a = 1;
   for (; a < argc; ++a) {
     const char* nx = argv[a];
     if (!strcmp(nx, "--help")) { usage(stdout); return EXIT_SUCCESS; }
     if (!strcmp(nx, "--version")) { printf("closest-features\n  version:  %s\n", BEDOPS_AMD_VERSION); return EXIT_SUCCESS; }
-    if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) ec = 1;
+    if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) {
+      ec = 1;
+      if (!strcmp(nx, "--ec")) check = 1;
+    }
     else if (!strcmp(nx, "--no-overlaps")) o.no_overlaps = 1;
     else if (!strcmp(nx, "--delim")) {
       if (++a >= argc) arg_error("No value given for --delim.");
@@ -100,6 +103,7 @@ int main(int argc, char** argv) {
   bg_input in[2];
   for (int k = 0; k < 2; ++k) {
     if (read_text(argv[a + k], &t[k])) arg_error("Unable to read an input file");
+    if (check) ec_check(PROG, ctx, argv[a + k], &t[k], 3, 1);
     if (ec) apply_ec_header(&t[k]);
     in[k].data = t[k].data;
     in[k].nbytes = t[k].n;

@@ -40,7 +40,13 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_stats", "bg_host_alloc", "bg_host_free", "bg_prof_enable", "bg_prof_read",
            "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
            "bg_set_chrom_name", "bg_closest", "bg_complement", "bg_chop", "bg_partition",
-           "bg_symmdiff", "bg_everything", "bg_set_pad"]
+           "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message"]
+
+
+class _CheckResult(ctypes.Structure):
+    _fields_ = [("row", ctypes.c_uint64), ("code", ctypes.c_int), ("line_off", ctypes.c_uint64),
+                ("line_len", ctypes.c_uint64), ("prev_off", ctypes.c_uint64),
+                ("prev_len", ctypes.c_uint64)]
 
 
 def lib_path():
@@ -111,6 +117,8 @@ def load_library():
     for fn in (L.bg_partition, L.bg_symmdiff, L.bg_everything):
         fn.argtypes = [vp, vp, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
     L.bg_set_pad.argtypes = [vp, vp, i32, i32, i32]
+    L.bg_check.argtypes = [vp, vp, i32, i32, vp]
+    L.bg_check_message.argtypes = [ctypes.c_char_p, u64, i32, i32, i32, ctypes.c_char_p, u64]
     L.bg_map.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_MapOpts), ctypes.POINTER(vp)]
     L.bg_closest.argtypes = [vp, vp, i32, i32, ctypes.POINTER(_ClosestOpts), ctypes.POINTER(vp)]
     L.bg_result_rows.argtypes = [vp, ctypes.POINTER(u64)]
@@ -338,6 +346,23 @@ class Engine:
                 r.free()
         finally:
             s.free()
+
+    # -------------------------------------------------------------- --ec
+    def check(self, text, nfields=3, has_rest=False, name="-"):
+        """--ec validation of one input on the GPU (bg_check): None if it passes, else the
+        reference's exception text "in <name>\n<message>\nSee row: <n>"."""
+        buf = ctypes.create_string_buffer(bytes(text), len(text) or 1)
+        i = _Input(ctypes.cast(buf, ctypes.c_void_p), len(text), 0, BED3)
+        r = _CheckResult()
+        self._check(self.L.bg_check(self.ctx, ctypes.byref(i), nfields, 1 if has_rest else 0,
+                                    ctypes.byref(r)))
+        if not r.row:
+            return None
+        line = bytes(text[r.line_off:r.line_off + r.line_len])
+        msg = ctypes.create_string_buffer(4096)
+        self._check(self.L.bg_check_message(line, len(line), r.code, nfields, 1 if has_rest else 0,
+                                            msg, 4096))
+        return f"in {name}\n".encode() + msg.value + f"\nSee row: {r.row}".encode()
 
     # -------------------------------------------------------------- bedmap
     def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",

@@ -174,6 +174,21 @@ int bg_symmdiff(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_resul
 int bg_everything(bg_ctx* ctx, bg_set* set, const int* files, int nfiles, bg_result** out);
 /* --range L:R applied to one loaded file (in place; before the operation) */
 int bg_set_pad(bg_ctx* ctx, bg_set* set, int file, int lpad, int rpad);
+/* --ec validation (replaces Bed::bed_check_iterator::check and its order checks,
+ * interfaces/general-headers/data/bed/BedCheckIterator.hpp:215-634): every line of one
+ * input checked on the GPU; row = 0 when the file passes, else the first failing line
+ * (1-based, headers counted), its code and byte range (and the line before it).
+ * nfields: 3 (BED3 types), 5 (bedmap's map file under score operations); has_rest: the
+ * reader keeps the remainder (B3Rest). */
+typedef struct bg_check_result {
+  uint64_t row;
+  int code;
+  uint64_t line_off, line_len, prev_off, prev_len;
+} bg_check_result;
+int bg_check(bg_ctx* ctx, const bg_input* in, int nfields, int has_rest, bg_check_result* out);
+/* the reference's message for `code` on `line` (host): the text after "in <file>\n" */
+int bg_check_message(const char* line, uint64_t len, int code, int nfields, int has_rest,
+                     char* buf, uint64_t cap);
 int bg_map(bg_ctx* ctx, bg_set* set, int ref, int map, const bg_map_opts* opts,
            bg_result** out);
 /* closest-features <input-file> <query-file>: `ref` = the <input-file> table, `query` =
