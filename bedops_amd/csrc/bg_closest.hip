@@ -110,6 +110,18 @@ __device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, i
 __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, uint32_t* kept,
                        bool emit) {
   const uint32_t cap = A.cap;
+  // the next CPF file candidates, loaded ahead: the scan's loads are independent of its
+  // decisions, so the file stream is software-pipelined (one candidate at a time each
+  // lane waited an L2 round trip per candidate; lanes read disjoint regions)
+  constexpr int CPF = 4;
+  int64_t pcs[CPF], pce[CPF];
+  const uint64_t nc1 = A.nc ? A.nc - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < CPF; ++i) {
+    const uint64_t j = min(S.fp + i, nc1);
+    pcs[i] = A.nc ? A.cs[j] : 0;
+    pce[i] = A.nc ? A.ce[j] : 0;
+  }
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
     const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
@@ -124,11 +136,27 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
     else kept[nk++] = (uint32_t)(x); \
   } while (0)
     for (;;) {
-      int64_t c;
-      if (S.n) c = S.c[--S.n];
-      else if (S.fp < A.nc) c = (int64_t)S.fp++;
-      else { eof = true; break; }
-      const int64_t cs = A.cs[c], ce = A.ce[c];
+      int64_t c, cs, ce;
+      if (S.n) {
+        c = S.c[--S.n];
+        cs = A.cs[c];
+        ce = A.ce[c];
+      } else if (S.fp < A.nc) {
+        c = (int64_t)S.fp++;
+        cs = pcs[0];
+        ce = pce[0];
+#pragma unroll
+        for (int i = 0; i + 1 < CPF; ++i) {
+          pcs[i] = pcs[i + 1];
+          pce[i] = pce[i + 1];
+        }
+        const uint64_t j = min(S.fp + (CPF - 1), nc1);
+        pcs[CPF - 1] = A.cs[j];
+        pce[CPF - 1] = A.ce[j];
+      } else {
+        eof = true;
+        break;
+      }
       const int64_t d = cl_dist(cs, ce, bs, be);
       if (d == D_MINUS) continue;  // earlier chromosome: dropped
       const bool hasL = left >= 0, hasR = right >= 0;
@@ -144,11 +172,14 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
       const bool hangL = ovl && cs <= bs;
       const bool hangR = ovl && !hangL && be <= ce;
       const bool inside = ovl && !hangL && !hangR;
-      const double cst = (double)(cs & BG_COORD_MASK);
-      const double prop =
-          cen < cst ? 0.0
-                    : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
-      const bool half = prop < 0.5;
+      bool half = false;
+      if (inside) {  // rare: the double division is skipped by every wave without such a row
+        const double cst = (double)(cs & BG_COORD_MASK);
+        const double prop =
+            cen < cst ? 0.0
+                      : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
+        half = prop < 0.5;
+      }
       const bool in_a = inside && ld == 0 && half;    // keepL(!lc), lc = 1, keepR, right = c
       const bool in_b = inside && ld == 0 && !half;   // keepL(!lc), lc = 1, keepC
       const bool in_c = inside && ld != 0 && !half;   // reset, left = c, ld = 0, lc = 0
