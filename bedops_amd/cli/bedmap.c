@@ -40,7 +40,8 @@ static void usage(FILE* f) {
           "      --bases --bases-uniq --bases-uniq-f --count --echo --echo-ref-name --echo-ref-size\n"
           "      --echo-map --echo-map-id --echo-map-range --echo-map-score --echo-map-size\n"
           "      --echo-overlap-size --indicator --max --mean --min --sum\n"
-          "      --cv --kth <val> --median --stdev --variance --echo-map-id-uniq --echo-ref-row-id\n",
+          "      --cv --kth <val> --mad [mult] --median --stdev --variance --echo-map-id-uniq\n"
+          "      --echo-ref-row-id\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -162,6 +163,17 @@ int main(int argc, char** argv) {
       is_frac[which] = 1;
       static const int crit[4] = {BG_OVR_FRAC_REF, BG_OVR_FRAC_MAP, BG_OVR_FRAC_EITHER, BG_OVR_FRAC_BOTH};
       o.criterion = crit[which];
+    } else if (!strcmp(k, "mad")) {  /* optional multiplier (Input.hpp:275-288) */
+      double mult = 0;
+      if (a < argc && strspn(argv[a], ".-0123456789") == strlen(argv[a])) {
+        const char* v = argv[a++];
+        mult = strtod(v, NULL);
+        if (!(mult > 0)) arg_error("--mad Expect 0 < val");
+      }
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.op_arg[o.n_ops] = mult;
+      o.ops[o.n_ops++] = BG_MAP_MAD;
+      need5 = 1;
     } else if (!strcmp(k, "kth")) {  /* Input.hpp:290-302; 0 / 1 are Min / Max (Bedmap.cpp:490-501) */
       char b[512];
       if (a >= argc) arg_error("No arg for --kth");

@@ -437,15 +437,21 @@ __device__ __forceinline__ void put_unique_ids(const FmtArgs& A, Out& o, uint64_
 
 // value at sorted position p of the window's scores (a multiset: x is at positions
 // [#{< x}, #{<= x}) ), by counting; windows are small, and this keeps no per-row buffer
-__device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint32_t p) {
+// (dev: of the absolute deviations |x - med| instead, MedianAbsoluteDeviationVisitor.hpp:43-49)
+__device__ __forceinline__ double mad_dev(double x, double med) {
+  const double d = x - med;
+  return d < 0 ? -d : d;
+}
+__device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint32_t p,
+                                              bool dev = false, double med = 0.0) {
   const int64_t s = A.s[k], e = A.e[k];
   for (uint64_t i = A.wlo[k]; i < A.whi[k]; ++i) {
     if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[i], A.e2[i])) continue;
-    const double x = A.score2[i];
+    const double x = dev ? mad_dev(A.score2[i], med) : A.score2[i];
     uint32_t lt = 0, le = 0;
     for (uint64_t j = A.wlo[k]; j < A.whi[k]; ++j) {
       if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[j], A.e2[j])) continue;
-      const double y = A.score2[j];
+      const double y = dev ? mad_dev(A.score2[j], med) : A.score2[j];
       lt += y < x;
       le += y <= x;
     }
@@ -562,6 +568,19 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
           if (mean == 0) { o.put('N'); o.put('A'); o.put('N'); continue; }
           v = v / mean;
         }
+      } else if (op == BG_MAP_MAD) {  // MedianAbsoluteDeviation::DoneReference (:70-110)
+        if (c <= 1) { o.put('N'); o.put('A'); o.put('N'); continue; }
+        const double med = window_kth(A, k, (uint32_t)c, 0.5);
+        const uint32_t sz = (uint32_t)c;
+        double mad;
+        if (sz % 2 == 0) {
+          mad = window_rank(A, k, sz / 2 - 1, true, med);
+          mad += window_rank(A, k, sz / 2, true, med);
+          mad /= 2.0;
+        } else {
+          mad = window_rank(A, k, sz / 2, true, med);
+        }
+        v = mad * (A.op_arg[q] > 0 ? A.op_arg[q] : 1.0);
       } else if (op == BG_MAP_MEDIAN || op == BG_MAP_KTH) {
         v = window_kth(A, k, (uint32_t)c, op == BG_MAP_MEDIAN ? 0.5 : A.op_arg[q]);
       } else {

@@ -243,6 +243,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
         if (!(opts->op_arg[k] > 0.0 && opts->op_arg[k] < 1.0))
           return bg_fail(c, BG_E_ARG, "--kth on the GPU path takes 0 < val < 1 (0 is --min, 1 is --max)");
         [[fallthrough]];
+      case BG_MAP_MAD:
       case BG_MAP_MEDIAN:  // order statistics of the window's scores, taken by the formatter
         need_ext = true;
         need |= NEED_WIN;

@@ -21,10 +21,10 @@ MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, 
            "bases-uniq": 8, "bases-uniq-f": 9, "echo": 10, "echo-ref-size": 11,
            "echo-ref-name": 12, "echo-map": 13, "echo-map-id": 14, "echo-map-score": 15,
            "echo-map-size": 16, "echo-overlap-size": 17, "echo-map-range": 18, "median": 19,
-           "kth": 20, "variance": 21, "stdev": 22, "cv": 23, "echo-map-id-uniq": 25,
+           "kth": 20, "variance": 21, "stdev": 22, "cv": 23, "echo-map-id-uniq": 25, "mad": 24,
            "echo-ref-row-id": 26}
 SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score", "median", "kth", "variance", "stdev",
-             "cv")
+             "cv", "mad")
 MAP_REST_OPS = ("echo-map", "echo-map-id", "echo-map-id-uniq")  # the map rows' remainders are printed
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}

@@ -123,6 +123,7 @@ typedef struct bg_map_opts {
 #define BG_MAP_VARIANCE 21     /* --variance       Variance (running double sums)      */
 #define BG_MAP_STDEV 22        /* --stdev          StdDev                              */
 #define BG_MAP_CV 23           /* --cv             CoeffVariation                      */
+#define BG_MAP_MAD 24          /* --mad [mult]     MedianAbsoluteDeviation (op_arg = mult, 0 = 1) */
 #define BG_MAP_ECHO_MAP_ID_UNIQ 25  /* --echo-map-id-uniq  the window's ids, sorted (strcmp) and unique */
 #define BG_MAP_ECHO_REF_ROW_ID 26   /* --echo-ref-row-id   "id-<n>", n = printed-line counter (PrintRowID) */
 /* overlap criteria (Bedmap.cpp:95-155 -> data/bed/BedDistances.hpp) */

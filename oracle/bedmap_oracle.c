@@ -169,7 +169,7 @@ static int os_erase(oset_t* s, int64_t x) {
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
        V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
        V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE, V_MEDIAN,
-       V_KTH, V_VARIANCE, V_STDEV, V_CV, V_ECHO_MAP_ID_UNIQ, V_ECHO_REF_ROW_ID };
+       V_KTH, V_VARIANCE, V_STDEV, V_CV, V_ECHO_MAP_ID_UNIQ, V_ECHO_REF_ROW_ID, V_MAD };
 static double VARG[64];      /* --kth argument per visitor */
 static double sq_;           /* Variance-family running sum of squares */
 static int VIS[64], NVIS;
@@ -271,19 +271,41 @@ static int dcmp(const void* a, const void* b) {
   return x < y ? -1 : (x > y ? 1 : 0);
 }
 /* RollingKthAverage::DoneReference on the window's sorted scores (RollingKthAverageVisitor.hpp:61-92) */
-static void put_kth(double kth) {
+static double kth_value(double kth) {
   const size_t n = (size_t)VWIN.n;
-  if (n == 0) { fputs("NAN", stdout); return; }
   double* v = (double*)malloc(n * sizeof(double));
   for (size_t i = 0; i < n; ++i) v[i] = MAP->score[VWIN.v[i]];
   qsort(v, n, sizeof(double), dcmp);
   size_t up = (size_t)ceil(kth * (double)n), down = (size_t)floor(kth * (double)n);
   if (up > 0) --up;
   if (down > 0) --down;
-  if (n == 1) put_real(v[0]);
-  else if (up == down) put_real((v[up] + v[up + 1]) / 2.0);
-  else put_real(v[up]);
+  double r;
+  if (n == 1) r = v[0];
+  else if (up == down) r = (v[up] + v[up + 1]) / 2.0;
+  else r = v[up];
   free(v);
+  return r;
+}
+static void put_kth(double kth) {
+  if (VWIN.n == 0) { fputs("NAN", stdout); return; }
+  put_real(kth_value(kth));
+}
+/* MedianAbsoluteDeviation::DoneReference (MedianAbsoluteDeviationVisitor.hpp:70-110) */
+static void put_mad(double mult) {
+  const size_t n = (size_t)VWIN.n;
+  if (n <= 1) { fputs("NAN", stdout); return; }
+  const double med = kth_value(0.5);
+  double* v = (double*)malloc(n * sizeof(double));
+  for (size_t i = 0; i < n; ++i) {
+    const double d = MAP->score[VWIN.v[i]] - med;
+    v[i] = d < 0 ? -d : d;
+  }
+  qsort(v, n, sizeof(double), dcmp);
+  double mad;
+  if (n % 2 == 0) { mad = v[n / 2 - 1]; mad += v[n / 2]; mad /= 2.0; }
+  else mad = v[n / 2];
+  free(v);
+  put_real(mad * mult);
 }
 static int scmp(const void* a, const void* b) { return strcmp(*(char* const*)a, *(char* const*)b); }
 /* PrintUniqueRangeIDs (ProcessBedVisitorRow.hpp:361-385): std::set<std::string> of the ids */
@@ -343,6 +365,7 @@ static void v_done(int64_t r) {
       case V_ECHO_REF_ROW_ID: printf("id-%lu", ++ROWID); break;
       case V_MEDIAN: put_kth(0.5); break;
       case V_KTH: put_kth(VARG[i]); break;
+      case V_MAD: put_mad(VARG[i]); break;
       case V_VARIANCE: case V_STDEV: case V_CV: {
         const double count = (double)counter_;
         if (count <= 1) { fputs("NAN", stdout); break; }
@@ -403,6 +426,13 @@ int main(int argc, char** argv) {
         found = 1;
       }
     if (found) continue;
+    if (!strcmp(o, "--mad")) { /* optional multiplier when the next argument is all reals (Input.hpp:275-288) */
+      VARG[NVIS] = 1.0;
+      if (a < argc && argv[a][0] && strspn(argv[a], ".-0123456789") == strlen(argv[a])) VARG[NVIS] = strtod(argv[a++], NULL);
+      VIS[NVIS++] = V_MAD;
+      need5 = 1;
+      continue;
+    }
     if (!strcmp(o, "--kth") && a < argc) {
       VARG[NVIS] = strtod(argv[a++], NULL);
       VIS[NVIS++] = V_KTH;
