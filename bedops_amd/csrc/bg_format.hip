@@ -58,6 +58,7 @@ struct FmtArgs {
   int nops;
   int ops[16];
   int prec;
+  int sci;  // --sci
   int skip_unmapped;
   int dlen;
   char delim[16];
@@ -173,6 +174,59 @@ __device__ __forceinline__ bool fixed_digits(double v, int prec, uint64_t& N, bo
   return true;
 }
 
+// exact "%.{prec}e" of v (glibc: the binary value rounded half-to-even at prec+1
+// significant digits), for 1e-16 <= |v| < 2^128 (and 0); false outside that range.
+// N = round(|v| * 10^s) with s = prec - E must land in [10^prec, 10^(prec+1)); E starts
+// from log10 and is corrected by one step when the rounding says so.
+__device__ __forceinline__ bool sci_digits(double v, int prec, uint64_t& N, int& E, bool& neg) {
+  typedef unsigned __int128 u128;
+  uint64_t bits = __double_as_longlong(v);
+  neg = (bits >> 63) != 0;
+  const int bexp = (int)((bits >> 52) & 0x7ff);
+  uint64_t m = bits & ((1ULL << 52) - 1);
+  if (bexp == 0x7ff) return false;
+  if (bexp == 0 && m == 0) { N = 0; E = 0; return true; }
+  int ex;
+  if (bexp == 0) ex = -1074;
+  else { m |= 1ULL << 52; ex = bexp - 1075; }
+  const double a = neg ? -v : v;
+  if (a < 1e-16) return false;
+  uint64_t P = 1;
+  for (int k = 0; k < prec; ++k) P *= 10;
+  E = (int)floor(log10(a));
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    const int sc = prec - E;  // N = round(m * 2^ex * 10^sc)
+    u128 num = m, den = 1;
+    if (sc >= 0) {
+      for (int k = 0; k < sc; ++k) {
+        if (num > (~(u128)0) / 10) return false;
+        num *= 10;
+      }
+    } else {
+      for (int k = 0; k < -sc; ++k) den *= 10;  // -sc <= 38 + prec: fits while |v| < 2^128
+      if (-sc > 38) return false;
+    }
+    if (ex >= 0) {
+      for (int k = 0; k < ex; ++k) {
+        if (num >> 127) return false;
+        num <<= 1;
+      }
+    } else {
+      if (-ex >= 128) return false;
+      if ((den >> (127 + ex)) != 0) return false;
+      den <<= -ex;
+    }
+    const u128 q = num / den, r = num - q * den;
+    u128 qq = q;
+    if (r * 2 > den || (r * 2 == den && (q & 1))) ++qq;
+    if (qq >= (u128)P * 10) { ++E; continue; }
+    if (qq < (u128)P) { --E; continue; }
+    N = (uint64_t)qq;
+    return true;
+  }
+  return false;
+}
+
 __device__ __forceinline__ int fixed_len(uint64_t N, bool neg, int prec) {
   uint64_t P = 1;
   for (int k = 0; k < prec; ++k) P *= 10;
@@ -192,6 +246,38 @@ __device__ __forceinline__ void put_fixed(Out& o, uint64_t N, bool neg, int prec
     o.adv(1);
     put_u64(o, fp, prec);
   }
+}
+
+// "%.{prec}e": d[.ddd]e±XX (at least two exponent digits)
+template <typename Out>
+__device__ __forceinline__ void put_sci(Out& o, uint64_t N, int E, bool neg, int prec) {
+  uint64_t P = 1;
+  for (int k = 0; k < prec; ++k) P *= 10;
+  if (neg) o.put('-');
+  o.put((char)('0' + N / P));
+  if (prec > 0) {
+    o.put('.');
+    put_u64(o, N % P, prec);
+  }
+  o.put('e');
+  o.put(E < 0 ? '-' : '+');
+  const uint64_t ae = (uint64_t)(E < 0 ? -E : E);
+  put_u64(o, ae, ae < 10 ? 2 : dec_len_u64(ae));
+}
+// a score-precision value (PrintScorePrecision: "%.{p}lf", or "%.{p}e" under --sci)
+template <typename Out>
+__device__ __forceinline__ bool put_real(Out& o, double v, int prec, bool sci) {
+  uint64_t N;
+  bool neg;
+  if (sci) {
+    int E;
+    if (!sci_digits(v, prec, N, E, neg)) return false;
+    put_sci(o, N, E, neg, prec);
+    return true;
+  }
+  if (!fixed_digits(v, prec, N, neg)) return false;
+  put_fixed(o, N, neg, prec);
+  return true;
 }
 
 struct CountOut {  // measures only
@@ -375,10 +461,7 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
       while (i < rl && fmt_isws(rp[i])) ++i;
       for (; i < rl && !fmt_isws(rp[i]); ++i) o.put(rp[i]);
     } else if (op == BG_MAP_ECHO_MAP_SCORE) {
-      uint64_t N;
-      bool neg;
-      if (!fixed_digits(A.score2[m], A.prec, N, neg)) return false;
-      put_fixed(o, N, neg, A.prec);
+      if (!put_real(o, A.score2[m], A.prec, A.sci)) return false;
     } else if (op == BG_MAP_ECHO_MAP_SIZE) {
       const uint64_t len = (uint64_t)(me - ms);
       put_u64(o, len, dec_len_u64(len));
@@ -586,10 +669,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
       } else {
         v = (op == BG_MAP_MIN) ? A.vmin[k] : A.vmax[k];
       }
-      uint64_t N;
-      bool neg;
-      if (!fixed_digits(v, A.prec, N, neg)) return false;
-      put_fixed(o, N, neg, A.prec);
+      if (!put_real(o, v, A.prec, A.sci)) return false;
     }
     o.put('\n');
     return true;
@@ -865,6 +945,7 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.nops = r->mopts.n_ops;
     for (int k = 0; k < A.nops; ++k) A.ops[k] = r->mopts.ops[k];
     A.prec = r->mopts.precision;
+    A.sci = r->mopts.scientific;
     A.skip_unmapped = r->mopts.skip_unmapped;
     A.dlen = (int)strnlen(r->mopts.delim, 15);
     memcpy(A.delim, r->mopts.delim, A.dlen);

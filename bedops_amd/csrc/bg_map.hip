@@ -258,7 +258,6 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (need_sum) need |= NEED_SUM;
   if (need_ext) need |= NEED_EXT;
   if (need_sum || need_ext) mapfields = 5;  // score operations read the map as B5Rest
-  if (opts->scientific) return bg_fail(c, BG_E_UNSUPPORTED, "--sci is not on the GPU path yet");
   if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
   const int crit = opts->criterion;
   double perc = 1.0;

@@ -366,7 +366,7 @@ class Engine:
 
     # -------------------------------------------------------------- bedmap
     def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, criterion="bp-ovr", value=None, multidelim=";"):
+               skip_unmapped=False, criterion="bp-ovr", value=None, multidelim=";", sci=False):
         """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result.
         criterion: "bp-ovr" (value = overlap_bp), "range" (value = bp), "fraction-ref",
         "fraction-map", "fraction-either", "fraction-both" (value = fraction), "exact"."""
@@ -378,7 +378,7 @@ class Engine:
             o.ops[k] = MAP_OPS[name]
             o.op_arg[k] = float(arg)
         o.precision = precision
-        o.scientific = 0
+        o.scientific = 1 if sci else 0
         o.skip_unmapped = 1 if skip_unmapped else 0
         o.delim = delim.encode()
         o.multidelim = multidelim.encode()
@@ -392,7 +392,8 @@ class Engine:
         return Result(self, h)
 
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None, multidelim=";"):
+               skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None, multidelim=";",
+               sci=False):
         names = [op[0] if isinstance(op, tuple) else op for op in ops]
         need5 = any(op in SCORE_OPS for op in names)
         mrest = any(op in MAP_REST_OPS for op in names)
@@ -403,7 +404,7 @@ class Engine:
             if chrom:
                 s.restrict_chrom(chrom)
             r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped,
-                            criterion, value, multidelim)
+                            criterion, value, multidelim, sci)
             try:
                 return r.text()
             finally:

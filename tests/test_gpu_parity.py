@@ -169,6 +169,25 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
                 assert got == want, (crit, val, ops, trial)
 
 
+@pytest.mark.parametrize("prec", [0, 3, 6, 12])
+def test_bedmap_sci(eng, oracle_bin, prec):
+    """--sci: every score-precision value as exact "%.{p}e" (glibc's rounding)"""
+    rng = random.Random(prec + 40)
+    ref = randbed.rows(rng, 300, span=3000, maxlen=80)
+    mp = randbed.rows(rng, 1200, span=3000, maxlen=80)
+    rt = randbed.text(ref).encode()
+    ints = "".join(f"{c}\t{s}\t{e}\tid{i}\t{rng.choice([0, 1, 7, 999, 123456, -42])}\n"
+                   for i, (c, s, e) in enumerate(mp)).encode()
+    decs = "".join(f"{c}\t{s}\t{e}\tid{i}\t{rng.choice(['0.5', '-2.25', '0.001', '3.14159', '0.0001', '95'])}\n"
+                   for i, (c, s, e) in enumerate(mp)).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for mt, ops in ((ints, ["mean", "sum", "variance", "stdev", "cv", "bases-uniq-f", "min"]),
+                        (decs, ["min", "max", "median", "echo-map-score", "mad"])):
+            want = run_oracle(oracle_bin["bedmap"], [f"--{o}" for o in ops] + ["--sci", "--prec", str(prec)],
+                              [rt, mt], td)
+            assert eng.bedmap(ops, rt, mt, precision=prec, sci=True) == want, ops
+
+
 def test_bedmap_dense_map_slice(eng, oracle_bin):
     """a workgroup whose candidate slice exceeds the LDS stage (searches in HBM instead)"""
     rng = random.Random(11)
