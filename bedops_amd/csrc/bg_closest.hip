@@ -113,7 +113,10 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
   // the next CPF file candidates, loaded ahead: the scan's loads are independent of its
   // decisions, so the file stream is software-pipelined (one candidate at a time each
   // lane waited an L2 round trip per candidate; lanes read disjoint regions)
-  constexpr int CPF = 4;
+#ifndef BG_CPF
+#define BG_CPF 4
+#endif
+  constexpr int CPF = BG_CPF;
   int64_t pcs[CPF], pce[CPF];
   const uint64_t nc1 = A.nc ? A.nc - 1 : 0;
 #pragma unroll
@@ -260,7 +263,10 @@ __device__ __forceinline__ void cl_own(const ClArgs& A, uint32_t k) {
   A.st_n[w] = S.n;
 }
 
-__global__ void __launch_bounds__(BG_NT) k_closest_chunks(ClArgs A) {
+#ifndef BG_CL_WAVES
+#define BG_CL_WAVES
+#endif
+__global__ void __launch_bounds__(BG_NT) BG_CL_WAVES k_closest_chunks(ClArgs A) {
   const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
   if (k >= A.nchunks) return;
   const uint64_t q0 = (uint64_t)k * A.cq;
