@@ -539,9 +539,18 @@ struct Fast {
   uint32_t toklen;
   uint32_t rest;  // local offset (from the line start) of the rest
 };
+// 8 bytes of LDS starting at byte offset q
+__device__ __forceinline__ uint64_t lds8(const uint8_t* buf, uint32_t q) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(buf + (q & ~3u));
+  const uint32_t o = q & 3u;
+  const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+  return (uint64_t)bgp_align(x0, x1, o) | ((uint64_t)bgp_align(x1, x2, o) << 32);
+}
+// short8: the caller only accepts tokens of <= 8 bytes (its run's token is that short), so
+// 8 bytes of the token are read instead of 16
 __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32_t* wsm,
                                                 const uint32_t* dgm, uint32_t q, uint32_t len,
-                                                Fast& L) {
+                                                Fast& L, bool short8 = false) {
   BgpFields F;
   const int r = bgp_fields_masks(mask_window(wsm, q), mask_window(dgm, q), len, F);
   if (r != 1) return false;  // blank lines and errors take the byte path (messages)
@@ -554,7 +563,13 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   lds12_end(buf, b + F.e1, d1, d2, d3);
   L.end = bgp_digits_r(d1, d2, d3, (int)(F.e1 - F.e0));
   uint64_t lo, hi;
-  lds16(buf, b + F.a0, lo, hi);
+  if (short8) {
+    if (toklen > 8) return false;
+    lo = lds8(buf, b + F.a0);
+    hi = 0;
+  } else {
+    lds16(buf, b + F.a0, lo, hi);
+  }
   if (toklen < 16) {
     if (toklen <= 8) {
       hi = 0;
@@ -747,7 +762,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
       const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
       const RunInfo& I = R.info[run];
       double sc = 0;
-      if (parse_line_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F) &&
+      if (parse_line_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
           F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi &&
           (kind != BG_BED5 ||
            parse_score_fast(buf, wsm, dgm, lst[k], (uint32_t)(le - ls), F.rest, sc))) {
@@ -860,7 +875,7 @@ __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, 
 #if defined(BG_EXP) && BG_EXP == 2
   if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F)) {
 #else
-  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F) &&
+  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
       F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
 #endif
     start = F.start;
