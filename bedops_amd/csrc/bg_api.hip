@@ -384,6 +384,8 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->rrank);
   bg_release(c, r->wlo);
   bg_release(c, r->whi);
+  bg_release(c, r->zin);
+  bg_release(c, r->zout);
   bg_release(c, r->left);
   bg_release(c, r->right);
   bg_release(c, r->text);

@@ -51,6 +51,8 @@ struct FmtArgs {
   const double* score2;
   const uint64_t* wlo;
   const uint64_t* whi;
+  const int64_t* zin;  // zero-length rows: sweep-window membership (bg_map_live)
+  const int64_t* zout;
   int crit, mapfields, mdlen;
   int64_t ovr, range;
   double perc;
@@ -443,7 +445,8 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
   int64_t rs = 0, re = 0;
   for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
     const int64_t ms = A.s2[m], me = A.e2[m];
-    if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me)) continue;
+    if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me))
+      continue;
     if (op == BG_MAP_ECHO_MAP_RANGE) {  // PrintGenomicRange (ProcessBedVisitorRow.hpp:433-456)
       if (first) { rs = ms; re = me; }
       else { rs = min(rs, ms); re = max(re, me); }
@@ -504,7 +507,9 @@ __device__ __forceinline__ void put_unique_ids(const FmtArgs& A, Out& o, uint64_
     const char* best = nullptr;
     uint32_t blen = 0;
     for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
-      if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m])) continue;
+      if (!bg_map_live(A.zin, A.zout, k, m) ||
+          !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]))
+        continue;
       uint32_t l;
       const char* id = map_id(A, m, l);
       if (prev && id_cmp(id, l, prev, plen) <= 0) continue;
@@ -529,11 +534,15 @@ __device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint
                                               bool dev = false, double med = 0.0) {
   const int64_t s = A.s[k], e = A.e[k];
   for (uint64_t i = A.wlo[k]; i < A.whi[k]; ++i) {
-    if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[i], A.e2[i])) continue;
+    if (!bg_map_live(A.zin, A.zout, k, i) ||
+        !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[i], A.e2[i]))
+      continue;
     const double x = dev ? mad_dev(A.score2[i], med) : A.score2[i];
     uint32_t lt = 0, le = 0;
     for (uint64_t j = A.wlo[k]; j < A.whi[k]; ++j) {
-      if (!bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[j], A.e2[j])) continue;
+      if (!bg_map_live(A.zin, A.zout, k, j) ||
+          !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[j], A.e2[j]))
+        continue;
       const double y = dev ? mad_dev(A.score2[j], med) : A.score2[j];
       lt += y < x;
       le += y <= x;
@@ -934,6 +943,8 @@ static void fill_args(bg_result* r, FmtArgs& A) {
       A.score2 = M->score;
       A.wlo = r->wlo;
       A.whi = r->whi;
+      A.zin = r->zin;
+      A.zout = r->zout;
       A.crit = r->mopts.criterion;
       A.ovr = (int64_t)r->mopts.overlap_bp;
       A.range = (int64_t)r->mopts.range_bp;

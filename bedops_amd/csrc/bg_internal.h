@@ -135,6 +135,10 @@ struct bg_result {
   uint64_t* rrank = nullptr; // --echo-ref-row-id with --skip-unmapped: printed lines before row r
   uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
   uint64_t* whi = nullptr;
+  // zero-length rows in a bedmap input: map row m is in the sweep window of reference rows
+  // [zin[m], zout[m]) only (bg_map.hip, k_mz_member); null otherwise
+  int64_t* zin = nullptr;
+  int64_t* zout = nullptr;
   int map_tab = -1;          // the map table
   int mapfields = 3;         // map row type printed by --echo-map (B3Rest / B4Rest / B5Rest)
   double perc = 1.0;         // PercentOverlapMapping::perc_ of the criterion
@@ -372,6 +376,12 @@ __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, 
   if (crit == BG_OVR_FRAC_REF) return fr;
   if (crit == BG_OVR_FRAC_EITHER) return fm || fr;
   return fm && fr;
+}
+
+// bedmap with zero-length rows: is map row m in reference row r's sweep window at all?
+__device__ __forceinline__ bool bg_map_live(const int64_t* zin, const int64_t* zout, uint64_t r,
+                                            uint64_t m) {
+  return !zin || (zin[m] <= (int64_t)r && (int64_t)r < zout[m]);
 }
 
 // first index k in [0,n) with A[k] >= v (A sorted ascending); n if none

@@ -22,8 +22,14 @@
 // Exactness: Average/Sum keep ONE running double across the file (AverageVisitor.hpp:46-54,
 // SumVisitor.hpp:47-51); it equals the exact per-row integer sum whenever scores are
 // integers and partial sums stay below 2^53. Other inputs are refused (BG_E_UNSUPPORTED)
-// rather than approximated; so are zero-length rows. Min/max involve no
-// arithmetic and take any score.
+// rather than approximated. Min/max involve no arithmetic and take any score.
+// Zero-length rows (k_mz_*): under Overlapping(0) a zero-length row overlaps nothing, and
+// the sweep then (a) deletes every unread map row starting at or before a zero-length
+// reference row, (b) pops every window row starting before it, and (c) stops reading at a
+// zero-length map row starting after the current reference start (it is cached, and hides
+// the rows behind it). The window is then no longer "every overlapping map row": each map
+// row m is a window member of the reference rows [zin[m], zout[m]) only, computed from the
+// map-stream position after each reference row (k_mz_walk) — see k_mz_member.
 #include <cfloat>
 #include <climits>
 #include <cstring>
@@ -59,6 +65,8 @@ struct MapArgs {
   int64_t* isq;
   uint64_t* wlo;
   uint64_t* whi;
+  const int64_t* zin;  // zero-length rows: window membership (bg_map_live), else null
+  const int64_t* zout;
   bg_dstatus* st;
 };
 
@@ -88,7 +96,7 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const int64_t* X, uint32_t l
 
 #define MAP_SLICE 3072  // map starts staged per workgroup (24 KiB of LDS)
 
-template <int CRIT>
+template <int CRIT, bool ZM>
 __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
@@ -146,16 +154,18 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   for (uint64_t m0 = lo; m0 < hi; m0 += MU) {
     int64_t ms[MU], me[MU];
     double sc[MU];
+    bool live_m[MU];
 #pragma unroll
     for (int j = 0; j < MU; ++j) {
       const uint64_t m = min(m0 + j, hi - 1);
       ms[j] = staged ? xs[m - blo] : A.MS[m];
       me[j] = A.ME[m];
       if (A.need & (NEED_SUM | NEED_EXT)) sc[j] = A.SC[m];
+      live_m[j] = !ZM || bg_map_live(A.zin, A.zout, r, m);
     }
 #pragma unroll
     for (int j = 0; j < MU; ++j) {
-      if (m0 + j >= hi || !map_in<CRIT>(s, e, ms[j], me[j], A)) continue;
+      if (m0 + j >= hi || !live_m[j] || !map_in<CRIT>(s, e, ms[j], me[j], A)) continue;
       if (A.need & (NEED_SUM | NEED_EXT)) {
         const double x = sc[j];
         sum += (int64_t)x;
@@ -169,7 +179,10 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
       ++c;
       if (A.need & NEED_BASES) bases += (uint64_t)max(min(e, me[j]) - max(s, ms[j]), (int64_t)0);
       if (A.need & NEED_UNIQ) {
-        if (ms[j] < ue) {  // overlaps the current piece (rows come in start order)
+        // OvrUnique merges a row into the current piece only when they overlap by > 0 bp
+        // (BasicCoords::overlap, Bed.hpp:172-190): a zero-length row closes the piece
+        if (min(ue, me[j]) > max(us, ms[j])) {
+          us = min(us, ms[j]);
           ue = max(ue, me[j]);
         } else {
           if (ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
@@ -192,6 +205,120 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   if (A.vmin) { A.vmin[r] = vmin; A.vmax[r] = vmax; }
   if (A.bases) A.bases[r] = bases;
   if (A.uniq) A.uniq[r] = uniq;
+}
+
+// ------------------------------- zero-length rows ---------------------------------
+// The map-stream position p_i after reference row i (the index of the row it leaves
+// cached, WindowSweepImpl.cpp:214-234): starting from p_{i-1}, rows are consumed until one
+// starts after r.start without overlapping r, i.e. (map rows start-sorted)
+//   p_i = min(max(p_{i-1}, A_i), Z(max(p_{i-1}, C_i)))
+// with C_i = first map row starting after r.start, A_i = first starting at or after r.end
+// (= C_i for a zero-length r) and Z(x) = first zero-length map row at index >= x. When no
+// earlier reference row ends past r.start + 1, p_{i-1} <= C_i and p_i = min(A_i, Z(C_i))
+// does not depend on the past: those rows start the segments k_mz_walk replays, one thread
+// per segment.
+__global__ void k_mz_flags(const int64_t* __restrict__ S, const int64_t* __restrict__ E,
+                           const int64_t* __restrict__ PM, uint64_t n, uint8_t* __restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  f[i] = PM ? (S[i] + 1 >= PM[i]) : (S[i] == E[i]);  // segment start | zero-length row
+}
+
+__device__ __forceinline__ uint64_t mz_next_zero(const uint64_t* zm, uint64_t nz, uint64_t nm,
+                                                 uint64_t x) {
+  uint64_t lo = 0, hi = nz;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (zm[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < nz ? zm[lo] : nm;
+}
+
+__global__ void k_mz_walk(const int64_t* __restrict__ RS, const int64_t* __restrict__ RE,
+                          uint64_t nr, const int64_t* __restrict__ MS, uint64_t nm,
+                          const uint64_t* __restrict__ zm, uint64_t nz,
+                          const uint64_t* __restrict__ seg, uint64_t nseg, int64_t* __restrict__ P) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nseg) return;
+  const uint64_t i0 = seg[k], i1 = k + 1 < nseg ? seg[k + 1] : nr;
+  uint64_t p = 0;
+  for (uint64_t i = i0; i < i1; ++i) {
+    const int64_t s = RS[i], e = RE[i];
+    const uint64_t pp = (i == i0) ? 0 : p;
+    const uint64_t C = upper_bound_in(MS, min(pp, nm), nm, s);
+    const uint64_t A = (e > s) ? lower_bound_in(MS, C, nm, e) : C;
+    p = min(max(pp, A), mz_next_zero(zm, nz, nm, max(pp, C)));
+    P[i] = (int64_t)p;
+  }
+}
+
+// Map row m is consumed by reference row i* = first i with p_i > m, and enters the window
+// iff it overlaps r_{i*} (else it is deleted, :232-233). It leaves at the first
+// zero-length reference row after i* that starts after m.start (which pops every window
+// row starting before it, :207-211); a non-empty reference row only pops rows that end at
+// or before its start, which no later row overlaps. zin = i* (INT64_MAX: never a member),
+// zout = that zero-length row (nr: none).
+__global__ void k_mz_member(const int64_t* __restrict__ RS, const int64_t* __restrict__ RE,
+                            uint64_t nr, const int64_t* __restrict__ MS,
+                            const int64_t* __restrict__ ME, uint64_t nm,
+                            const int64_t* __restrict__ P, const uint64_t* __restrict__ zr,
+                            uint64_t nzr, int64_t* __restrict__ zin, int64_t* __restrict__ zout) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const int64_t ms = MS[m], me = ME[m];
+  const uint64_t is = upper_bound_i64(P, nr, (int64_t)m);
+  const bool added = is < nr && min(RE[is], me) > max(RS[is], ms);
+  zin[m] = added ? (int64_t)is : LLONG_MAX;
+  uint64_t lo = 0, hi = nzr;  // first zero-length row index > is
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (zr[mid] <= is) lo = mid + 1;
+    else hi = mid;
+  }
+  uint64_t lo2 = 0, hi2 = nzr;  // first zero-length row starting after ms
+  while (lo2 < hi2) {
+    const uint64_t mid = (lo2 + hi2) >> 1;
+    if (RS[zr[mid]] <= ms) lo2 = mid + 1;
+    else hi2 = mid;
+  }
+  const uint64_t k = max(lo, lo2);
+  zout[m] = k < nzr ? (int64_t)zr[k] : (int64_t)nr;
+}
+
+static int map_zero_prep(bg_ctx* c, const bg_table* R, const bg_table* M, bg_result* res) {
+  const uint64_t nr = R->n, nm = M->n;
+  if (!nr || !nm) return 0;
+  res->zin = (int64_t*)bg_alloc(c, 8 * nm);
+  res->zout = (int64_t*)bg_alloc(c, 8 * nm);
+  int64_t* PM = (int64_t*)bg_alloc(c, 8 * nr);
+  int64_t* P = (int64_t*)bg_alloc(c, 8 * nr);
+  uint8_t* f = (uint8_t*)bg_alloc(c, max(nr, nm));
+  if (!res->zin || !res->zout || !PM || !P || !f) return BG_E_NOMEM;
+  int rc = bg_scan_max_i64(c, R->ke, PM, nr, LLONG_MIN);
+  if (rc) return rc;
+  uint64_t *seg = nullptr, *zm = nullptr, *zr = nullptr, nseg = 0, nz = 0, nzr = 0;
+  BG_LAUNCH(c, "k_mz_flags", k_mz_flags, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), R->ks, R->ke, PM, nr, f);
+  if ((rc = bg_compact_flags(c, f, nr, &seg, &nseg))) return rc;
+  BG_LAUNCH(c, "k_mz_flags", k_mz_flags, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), M->ks, M->ke,
+            (const int64_t*)nullptr, nm, f);
+  if ((rc = bg_compact_flags(c, f, nm, &zm, &nz))) return rc;
+  BG_LAUNCH(c, "k_mz_flags", k_mz_flags, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), R->ks, R->ke,
+            (const int64_t*)nullptr, nr, f);
+  if ((rc = bg_compact_flags(c, f, nr, &zr, &nzr))) return rc;
+  if (nseg)
+    BG_LAUNCH(c, "k_mz_walk", k_mz_walk, dim3(bg_blocks(nseg, BG_NT)), dim3(BG_NT), R->ks, R->ke, nr,
+              M->ks, nm, zm, nz, seg, nseg, P);
+  BG_LAUNCH(c, "k_mz_member", k_mz_member, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), R->ks, R->ke, nr,
+            M->ks, M->ke, nm, P, zr, nzr, res->zin, res->zout);
+  BG_HIP(c, hipGetLastError());
+  bg_release(c, PM);
+  bg_release(c, P);
+  bg_release(c, f);
+  bg_release(c, seg);
+  bg_release(c, zm);
+  bg_release(c, zr);
+  return 0;
 }
 
 // 1 per reference row that prints a line (MultiVisitor.hpp:83-84 skips rows without maps)
@@ -281,8 +408,6 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   if ((need & (NEED_SUM | NEED_EXT)) && !M->score)
     return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
-  if (R->has_zero_len || M->has_zero_len)
-    return bg_fail(c, BG_E_UNSUPPORTED, "zero-length elements (end == start) are not on the GPU path of bedmap");
   if (need_sum && !M->score_int)
     return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean/--sum yet");
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
@@ -317,6 +442,15 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     bg_result_free(res);
     return BG_E_NOMEM;
   }
+  // zero-length rows change the sweep window under Overlapping(0); RangedDist (--range)
+  // treats them as ordinary rows
+  if (crit != BG_OVR_RANGE && (R->has_zero_len || M->has_zero_len)) {
+    int rz = map_zero_prep(c, R, M, res);
+    if (rz) {
+      bg_result_free(res);
+      return rz;
+    }
+  }
   MapArgs A;
   A.RS = R->ks;
   A.RE = R->ke;
@@ -339,18 +473,26 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   A.isq = res->isq;
   A.wlo = res->wlo;
   A.whi = res->whi;
+  A.zin = res->zin;
+  A.zout = res->zout;
   A.st = c->dstat;
   if (R->n) {
     const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);
+#define BG_MAP_LAUNCH(K)                                                                   \
+  do {                                                                                     \
+    if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true>), g, b, A);                   \
+    else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false>), g, b, A);                        \
+  } while (0)
     switch (crit) {
-      case BG_OVR_BP: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_BP>, g, b, A); break;
-      case BG_OVR_RANGE: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_RANGE>, g, b, A); break;
-      case BG_OVR_FRAC_REF: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_REF>, g, b, A); break;
-      case BG_OVR_FRAC_MAP: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_MAP>, g, b, A); break;
-      case BG_OVR_FRAC_EITHER: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_EITHER>, g, b, A); break;
-      case BG_OVR_FRAC_BOTH: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_FRAC_BOTH>, g, b, A); break;
-      default: BG_LAUNCH(c, "k_map_ops", k_map_ops<BG_OVR_EXACT>, g, b, A); break;
+      case BG_OVR_BP: BG_MAP_LAUNCH(BG_OVR_BP); break;
+      case BG_OVR_RANGE: BG_MAP_LAUNCH(BG_OVR_RANGE); break;
+      case BG_OVR_FRAC_REF: BG_MAP_LAUNCH(BG_OVR_FRAC_REF); break;
+      case BG_OVR_FRAC_MAP: BG_MAP_LAUNCH(BG_OVR_FRAC_MAP); break;
+      case BG_OVR_FRAC_EITHER: BG_MAP_LAUNCH(BG_OVR_FRAC_EITHER); break;
+      case BG_OVR_FRAC_BOTH: BG_MAP_LAUNCH(BG_OVR_FRAC_BOTH); break;
+      default: BG_MAP_LAUNCH(BG_OVR_EXACT); break;
     }
+#undef BG_MAP_LAUNCH
   }
   int rc = bg_hip_ok(c, hipGetLastError());
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));

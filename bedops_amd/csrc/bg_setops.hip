@@ -401,6 +401,133 @@ __global__ void __launch_bounds__(BG_NT) k_compact_flags(const uint8_t* __restri
   }
 }
 
+// ------------------------------- intersect: zero-length pieces --------------------
+// A file's zero-length piece [t, t) (an isolated zero-length row) never contributes to the
+// set intersection, but nextIntersectLine (Bedops.cpp:1105-1181) prints it as "chr t t"
+// when its stream reaches it in a particular state. The state between two calls is just
+// one head piece per file, and after a call that printed [s, e) with marker file q it is
+// canonical: every file's head is its first piece ending after s, except q's, which is its
+// first piece ending after e (the final pass left each head overlapping [s, e); the
+// marker's piece, the first one ending at e, was consumed, :1178). Zero-length pieces
+// never change which non-empty pieces are printed (they only pop pieces that end at or
+// before t, none of which can meet a piece on the far side of t), so: the non-empty
+// output is the set intersection (k_mp_tile), and for every non-empty output O[m] that
+// has a zero-length piece t with O[m-1].s < t <= O[m].s, one thread replays the calls
+// from the canonical state after O[m-1] until the next non-empty print, which must be
+// O[m], collecting the zero-length prints in call order. tests/model_setops.py holds the
+// same construction; both are compared with oracle/bedops_oracle.c (next_intersect).
+struct ZFile {
+  const int64_t* s;
+  const int64_t* e;
+  uint64_t n;
+};
+
+// first index >= h with E[index] > v, galloping from h (heads move forward a little)
+__device__ __forceinline__ uint64_t zi_pop(const int64_t* E, uint64_t n, uint64_t h, int64_t v) {
+  if (h >= n || E[h] > v) return h;
+  uint64_t lo = h + 1, step = 1;
+  while (lo + step <= n && E[lo + step - 1] <= v) { lo += step; step <<= 1; }
+  return upper_bound_in(E, lo, min(n, lo + step), v);
+}
+
+// k_zi_mark: flag[m] = 1 for the first output m starting at or after some zero-length piece
+__global__ void __launch_bounds__(BG_NT) k_zi_mark(const int64_t* __restrict__ S,
+                                                   const int64_t* __restrict__ E, uint64_t n,
+                                                   const int64_t* __restrict__ OS, uint64_t no,
+                                                   uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (i >= n) return;
+  const int64_t t = S[i];
+  if (E[i] != t) return;
+  flag[lower_bound_i64(OS, no, t)] = 1;
+}
+
+// One thread per anchor m (from k_zi_mark): replay calls from the state after O[m-1]
+// (the initial state for m == 0). COUNT: cnt[a] = zero-length prints. WRITE: store them
+// at m + off[a] + k. H is per-thread scratch (nf heads); bad[0] != 0 flags an internal
+// inconsistency (the replay did not reach O[m]) or the iteration bound.
+template <bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_zi_replay(
+    const ZFile* __restrict__ F, int nf, const int64_t* __restrict__ OS,
+    const int64_t* __restrict__ OE, uint64_t no, const uint64_t* __restrict__ anchors, uint64_t na,
+    uint64_t* __restrict__ H, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+    int64_t* __restrict__ ZS, int64_t* __restrict__ ZE, uint64_t cap,
+    unsigned long long* __restrict__ bad) {
+  const uint64_t a = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (a >= na) return;
+  const uint64_t m = anchors[a];
+  uint64_t* h = H + a * (uint64_t)nf;
+  if (m == 0) {
+    for (int f = 0; f < nf; ++f) h[f] = 0;
+  } else {
+    const int64_t s = OS[m - 1], e = OE[m - 1];
+    int q = -1;
+    for (int f = 0; f < nf; ++f) {
+      h[f] = upper_bound_i64(F[f].e, F[f].n, s);
+      if (q < 0 && h[f] < F[f].n && F[f].e[h[f]] == e) q = f;
+    }
+    if (q < 0) { atomicOr(bad, 1ULL); return; }
+    h[q] += 1;
+  }
+  uint64_t k = 0, steps = 0;
+  const uint64_t base = WRITE ? m + off[a] : 0;
+  for (;;) {  // one iteration = one nextIntersectLine call
+    bool stop = false;
+    int mj = 0;
+    for (int f = 0; f < nf && !stop; ++f) {
+      if (h[f] >= F[f].n) stop = true;
+      else if (f > 0 && F[f].s[h[f]] > F[mj].s[h[mj]]) mj = f;
+    }
+    if (stop) break;
+    int64_t cs = F[mj].s[h[mj]], ce = F[mj].e[h[mj]];
+    int marker = -1;
+    int64_t minE = LLONG_MAX;
+    for (int f = 0; f < nf;) {
+      if (++steps > cap) { atomicOr(bad, 2ULL); return; }
+      h[f] = zi_pop(F[f].e, F[f].n, h[f], cs);
+      if (h[f] >= F[f].n) { stop = true; break; }
+      const int64_t ps = F[f].s[h[f]], pe = F[f].e[h[f]];
+      if (ps >= ce) {  // no overlap: restart from this piece (:1161-1168)
+        cs = ps; ce = pe; marker = -1; minE = LLONG_MAX; f = 0;
+        continue;
+      }
+      cs = max(cs, ps);
+      ce = min(ce, pe);
+      if (pe < minE) { minE = pe; marker = f; }
+      ++f;
+    }
+    if (stop) break;
+    h[marker] += 1;
+    if (cs != ce) {  // the next non-empty print: must be O[m]
+      if (m >= no || OS[m] != cs || OE[m] != ce) atomicOr(bad, 4ULL);
+      break;
+    }
+    if (WRITE) { ZS[base + k] = cs; ZE[base + k] = ce; }
+    ++k;
+  }
+  if (!WRITE) cnt[a] = k;
+}
+
+// O[m] -> position m + (zero-length prints anchored at or before m)
+__global__ void __launch_bounds__(BG_NT) k_zi_place(const int64_t* __restrict__ OS,
+                                                    const int64_t* __restrict__ OE, uint64_t no,
+                                                    const uint64_t* __restrict__ anchors,
+                                                    uint64_t na, const uint64_t* __restrict__ off,
+                                                    int64_t* __restrict__ ZS,
+                                                    int64_t* __restrict__ ZE) {
+  const uint64_t m = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (m >= no) return;
+  uint64_t lo = 0, hi = na;  // anchors <= m
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (anchors[mid] <= m) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint64_t p = m + off[lo];
+  ZS[p] = OS[m];
+  ZE[p] = OE[m];
+}
+
 // =====================================================================================
 // host drivers
 // =====================================================================================
@@ -600,29 +727,95 @@ extern "C" int bg_merge(bg_ctx* c, bg_set* set, const int* files, int nf, bg_res
   return 0;
 }
 
+// the zero-length prints of nextIntersectLine (see k_zi_replay) merged into `acc`
+static int intersect_zero_len(bg_ctx* c, const std::vector<Ivl>& F, Ivl& acc) {
+  const int nf = (int)F.size();
+  const uint64_t no = acc.n;
+  uint8_t* flag = (uint8_t*)bg_alloc(c, no + 1);
+  if (!flag) return BG_E_NOMEM;
+  BG_HIP(c, hipMemsetAsync(flag, 0, no + 1, c->stream));
+  uint64_t npieces = 0;
+  for (const Ivl& f : F) {
+    npieces += f.n;
+    if (f.n)
+      BG_LAUNCH(c, "k_zi_mark", k_zi_mark, dim3(bg_blocks(f.n, BG_NT)), dim3(BG_NT), f.s, f.e, f.n,
+                acc.s, no, flag);
+  }
+  BG_HIP(c, hipGetLastError());
+  uint64_t* anchors = nullptr;
+  uint64_t na = 0;
+  int rc = bg_compact_flags(c, flag, no + 1, &anchors, &na);
+  bg_release(c, flag);
+  if (rc) return rc;
+  if (na == 0) {
+    bg_release(c, anchors);
+    return 0;
+  }
+  std::vector<ZFile> hf(nf);
+  for (int f = 0; f < nf; ++f) hf[f] = ZFile{F[f].s, F[f].e, F[f].n};
+  ZFile* dF = (ZFile*)bg_alloc(c, sizeof(ZFile) * nf);
+  uint64_t* H = (uint64_t*)bg_alloc(c, 8ull * na * nf);
+  uint64_t* cnt = (uint64_t*)bg_alloc(c, 8ull * (na + 1));
+  uint64_t* bad = (uint64_t*)bg_alloc(c, 8);
+  if (!dF || !H || !cnt || !bad) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(dF, hf.data(), sizeof(ZFile) * nf, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemsetAsync(bad, 0, 8, c->stream));
+  // every loop iteration of a replay advances a head or restarts from a later piece
+  const uint64_t cap = 8ull * (npieces + 16) * (uint64_t)(nf + 1);
+  const unsigned nb = bg_blocks(na, BG_NT);
+  BG_LAUNCH(c, "k_zi_replay_count", k_zi_replay<false>, dim3(nb), dim3(BG_NT), dF, nf, acc.s, acc.e,
+            no, anchors, na, H, cnt, (const uint64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr,
+            cap, (unsigned long long*)bad);
+  BG_HIP(c, hipGetLastError());
+  if ((rc = bg_scan_sum_u64(c, cnt, cnt, na, cnt + na))) return rc;
+  uint64_t total = 0, hbad = 0;
+  if ((rc = bg_fetch_u64(c, cnt + na, &total)) || (rc = bg_fetch_u64(c, bad, &hbad))) return rc;
+  if (hbad)
+    return bg_fail(c, BG_E_INTERNAL, "intersect: zero-length replay inconsistent (code " +
+                                         std::to_string(hbad) + ")");
+  Ivl out;
+  if ((rc = ivl_alloc(c, out, no + total))) return rc;
+  BG_LAUNCH(c, "k_zi_replay_write", k_zi_replay<true>, dim3(nb), dim3(BG_NT), dF, nf, acc.s, acc.e,
+            no, anchors, na, H, (uint64_t*)nullptr, (const uint64_t*)cnt, out.s, out.e, cap,
+            (unsigned long long*)bad);
+  if (no)
+    BG_LAUNCH(c, "k_zi_place", k_zi_place, dim3(bg_blocks(no, BG_NT)), dim3(BG_NT), acc.s, acc.e, no,
+              anchors, na, (const uint64_t*)cnt, out.s, out.e);
+  BG_HIP(c, hipGetLastError());
+  BG_HIP(c, hipStreamSynchronize(c->stream));  // hf/dF copy and the scratch below
+  bg_release(c, dF);
+  bg_release(c, H);
+  bg_release(c, cnt);
+  bg_release(c, bad);
+  bg_release(c, anchors);
+  ivl_free(c, acc);
+  acc = out;
+  return 0;
+}
+
 extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
   int rc = bg_check_files(c, set, files, nf, 2);
   if (rc) return rc;
-  // Zero-length rows (end == start; rejected by the reference's own --ec checker,
-  // BedCheckIterator.hpp:619-620) make nextIntersectLine's output depend on its
-  // stream state (a zero-length piece is emitted only when reached while skipping
-  // a stale head); that is not reproduced here, so such inputs are refused.
-  for (int k = 0; k < nf; ++k)
-    if (set->t[files[k]]->has_zero_len)
-      return bg_fail(c, BG_E_UNSUPPORTED,
-                     "zero-length elements (end == start) are not supported by --intersect on "
-                     "the GPU path (BEDOPS --ec rejects them: End coordinates must be greater "
-                     "than start coordinates)");
-  Ivl acc;
-  if ((rc = bg_table_components(c, set->t[files[0]], acc))) return rc;
+  // Each file's pieces (getNextFileMergedCoords); the non-empty output is the set
+  // intersection, folded pairwise. Files with zero-length pieces add nextIntersectLine's
+  // zero-length prints afterwards (intersect_zero_len).
+  bool zero = false;
+  std::vector<Ivl> comp(nf);
+  for (int k = 0; k < nf; ++k) {
+    zero = zero || set->t[files[k]]->has_zero_len;
+    if ((rc = bg_table_components(c, set->t[files[k]], comp[k]))) return rc;
+  }
+  Ivl acc = comp[0];
+  acc.owned = false;  // comp[0] keeps ownership
   for (int k = 1; k < nf; ++k) {
-    Ivl ck, p;
-    if ((rc = bg_table_components(c, set->t[files[k]], ck))) return rc;
-    if ((rc = mp_op<MP_INTERSECT>(c, acc, ck, p, "k_intersect_count", "k_intersect_write"))) return rc;
+    Ivl p;
+    if ((rc = mp_op<MP_INTERSECT>(c, acc, comp[k], p, "k_intersect_count", "k_intersect_write")))
+      return rc;
     ivl_free(c, acc);
-    ivl_free(c, ck);
     acc = p;
   }
+  if (zero && (rc = intersect_zero_len(c, comp, acc))) return rc;
+  for (Ivl& v : comp) ivl_free(c, v);
   *out = bg_new_ivl_result(c, set, acc);
   bg_mark(c, "intersect");
   return 0;

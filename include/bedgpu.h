@@ -55,6 +55,7 @@ extern "C" {
 #define BG_E_UNSUPPORTED (-8) /* input/option outside the GPU path (message says which) */
 #define BG_E_CHROM (-9)       /* chromosome name longer than 127 bytes */
 #define BG_E_IO (-10)         /* read/write failure */
+#define BG_E_INTERNAL (-11)   /* a kernel-side consistency check failed (a bug: please report) */
 
 /* kinds of input, decided by the operation (Bedops.cpp:402-429, Bedmap.cpp:643-654) */
 #define BG_BED3 0      /* chrom start end; remainder ignored            (Bed::B3NoRest) */

@@ -106,3 +106,101 @@ def element_of(ref, comps, thres, use_pct, invert):
         if k:
             keep.append(idx)
     return keep
+
+
+def intersect_zero_len(files):
+    """--intersect including nextIntersectLine's zero-length prints (Bedops.cpp:1105-1181),
+    as k_zi_mark / k_zi_replay / k_zi_place compute it: the non-empty output is the set
+    intersection; zero-length prints come from replaying the calls that follow the
+    canonical state after O[m-1] (every head = first piece ending after O[m-1].s, the
+    marker file's = first piece ending after O[m-1].e) until O[m] is printed again."""
+    import bisect
+    P = [components(f) for f in files]
+    normal = P[0]
+    for f in P[1:]:
+        normal = intersect2(normal, f)
+    nf = len(P)
+    ends = [[p[1] for p in Pi] for Pi in P]
+
+    def call(h):
+        if any(h[j] >= len(P[j]) for j in range(nf)):
+            return None
+        mj = 0
+        for j in range(1, nf):
+            if P[j][h[j]][0] > P[mj][h[mj]][0]:
+                mj = j
+        cur = P[mj][h[mj]]
+        i, marker, min_e = 0, -1, None
+        while i < nf:
+            h[i] = max(h[i], bisect.bisect_right(ends[i], cur[0]))
+            if h[i] >= len(P[i]):
+                return None
+            p = P[i][h[i]]
+            if p[0] >= cur[1]:
+                cur, i, marker, min_e = p, 0, -1, None
+                continue
+            cur = (max(cur[0], p[0]), min(cur[1], p[1]))
+            if min_e is None or p[1] < min_e:
+                min_e, marker = p[1], i
+            i += 1
+        h[marker] += 1
+        return cur
+
+    zs = sorted({p[0] for Pi in P for p in Pi if p[0] == p[1]})
+    starts = [o[0] for o in normal]
+    extra = {}
+    for m in sorted({bisect.bisect_left(starts, t) for t in zs}):
+        if m == 0:
+            h = [0] * nf
+        else:
+            s, e = normal[m - 1]
+            h = [bisect.bisect_right(ends[j], s) for j in range(nf)]
+            q = next(j for j in range(nf) if h[j] < len(P[j]) and P[j][h[j]][1] == e)
+            h[q] += 1
+        em = []
+        while True:
+            c = call(h)
+            if c is None:
+                break
+            if c[0] == c[1]:
+                em.append(c)
+                continue
+            assert m < len(normal) and c == normal[m]
+            break
+        extra[m] = em
+    out = []
+    for m in range(len(normal) + 1):
+        out += extra.get(m, [])
+        if m < len(normal):
+            out.append(normal[m])
+    return out
+
+
+def bedmap_zero_len_window(ref, mp):
+    """Sweep-window membership of each map row with zero-length rows present, as
+    k_mz_walk / k_mz_member compute it (bg_map.hip): map row j is a window member of
+    reference rows [zin[j], zout[j]). ref, mp: keyed (start, end), start-sorted."""
+    import bisect
+    nr, nm = len(ref), len(mp)
+    ms_ = [m[0] for m in mp]
+    zmap = [j for j, m in enumerate(mp) if m[0] == m[1]]
+
+    def next_zero(x):
+        k = bisect.bisect_left(zmap, x)
+        return zmap[k] if k < len(zmap) else nm
+    P, p = [], 0
+    for s, e in ref:
+        c = bisect.bisect_right(ms_, s)
+        a = bisect.bisect_left(ms_, e) if e > s else c
+        p = min(max(p, a), next_zero(max(p, c)))
+        P.append(p)
+    zref = [i for i, r in enumerate(ref) if r[0] == r[1]]
+    zt = [ref[i][0] for i in zref]
+    zin, zout = [], []
+    for j, (ms, me) in enumerate(mp):
+        i = bisect.bisect_right(P, j)
+        added = i < nr and min(ref[i][1], me) > max(ref[i][0], ms)
+        zin.append(i if added else None)
+        k = max(bisect.bisect_right(zref, i), bisect.bisect_right(zt, ms))
+        zout.append(zref[k] if k < len(zref) else nr)
+    return zin, zout

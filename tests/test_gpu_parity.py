@@ -68,18 +68,31 @@ def test_random_bedops_vs_oracle(eng, oracle_bin, mode, nfiles, zero_frac):
                                   zero_frac=zero_frac)
                 rest = "cols" if (f == 0 and mode in ("-e", "-n")) else None
                 texts.append(randbed.text(rs, rest=rest, rng=rng).encode())
-            has_zero = any(s == e for t in texts for (_, s, e) in _fields(t))
             for spec in SPECS.get(mode, [None]):
                 args = [mode] + ([spec] if spec else [])
-                if mode == "-i" and has_zero:  # refused loudly, never approximated
-                    from bedops_amd import BedgpuError
-                    with pytest.raises(BedgpuError) as ei:
-                        eng.bedops(mode, texts, spec=spec)
-                    assert ei.value.code == -8
-                    continue
                 want = run_oracle(oracle_bin["bedops"], args, texts, td)
                 got = eng.bedops(mode, texts, spec=spec)
                 assert got == want, (mode, spec, trial, n)
+
+
+@pytest.mark.parametrize("nfiles", [2, 3, 4])
+def test_intersect_zero_length_rows_vs_oracle(eng, oracle_bin, nfiles):
+    """nextIntersectLine prints some isolated zero-length pieces ("chr t t") depending on
+    its stream state (Bedops.cpp:1105-1181): the GPU replays those calls (k_zi_replay)"""
+    rng = random.Random(1000 + nfiles)
+    nzero = 0
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(40):
+            texts = []
+            for f in range(nfiles):
+                rs = randbed.rows(rng, rng.choice([0, 1, 5, 40, 300, 3000]),
+                                  span=rng.choice([40, 300, 5000]), maxlen=rng.choice([3, 12, 60]),
+                                  zero_frac=rng.choice([0.05, 0.3, 0.7]))
+                texts.append(randbed.text(rs).encode())
+            want = run_oracle(oracle_bin["bedops"], ["-i"], texts, td)
+            nzero += sum(1 for ln in want.splitlines() if ln.split(b"\t")[1] == ln.split(b"\t")[2])
+            assert eng.bedops("-i", texts) == want, trial
+    assert nzero > 0  # the trials did exercise the zero-length prints
 
 
 def test_element_of_wide_rows_slice(eng, oracle_bin):
@@ -167,6 +180,32 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
                 want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
                 got = eng.bedmap(ops, rt, mt, **kw)
                 assert got == want, (crit, val, ops, trial)
+
+
+@pytest.mark.parametrize("crit,val", MAP_CRITS)
+def test_bedmap_zero_length_rows_vs_oracle(eng, oracle_bin, crit, val):
+    """zero-length reference/map rows change the reference's sweep window (deleted, popped and
+    hiding rows; WindowSweepImpl.cpp:195-237): k_mz_* reproduce it, byte-equal to the oracle"""
+    rng = random.Random(zlib.crc32(repr(("zero", crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(8):
+            zr, zm = rng.choice([(0.0, 0.2), (0.2, 0.0), (0.1, 0.1), (0.4, 0.3)])
+            ref = randbed.rows(rng, rng.choice([1, 30, 400, 2000]), span=rng.choice([300, 3000]),
+                               maxlen=rng.choice([10, 80]), zero_frac=zr)
+            mp = randbed.rows(rng, rng.choice([1, 50, 800, 3000]), span=rng.choice([300, 3000]),
+                              maxlen=rng.choice([10, 80, 300]), zero_frac=zm)
+            rt = randbed.text(ref, rest="cols", rng=rng).encode()
+            mt = "".join(f"{c}\t{s}\t{e}\tid{i % 37}\t{rng.randint(0, 999)}\n"
+                         for i, (c, s, e) in enumerate(mp)).encode()
+            copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
+            kw = {"overlap_bp": val} if crit == "bp-ovr" else {"criterion": crit, "value": val}
+            for ops in (["count", "sum", "min", "max", "indicator"], ["bases", "bases-uniq", "mean"],
+                        ["echo-map", "echo-map-id", "echo-overlap-size"], ["median", "stdev"],
+                        ["echo-ref-row-id", "echo-map-id-uniq", "count"]):
+                if ops[0] == "median" and len(mp) > 1500:
+                    continue
+                want = run_oracle(oracle_bin["bedmap"], [f"--{o}" for o in ops] + copt, [rt, mt], td)
+                assert eng.bedmap(ops, rt, mt, **kw) == want, (crit, val, ops, trial)
 
 
 @pytest.mark.parametrize("prec", [0, 3, 6, 12])
@@ -265,11 +304,6 @@ def test_io_edge_cases(eng, oracle_bin, k, mode):
     b = b"chr1\t4\t8\nchr1\t9\t25\nchr2\t0\t5\n"
     texts = [a] if mode == "-m" else [a, b]
     spec = "1" if mode == "-e" else None
-    if mode == "-i" and any(s == e for (_, s, e) in _fields(a)):
-        from bedops_amd import BedgpuError
-        with pytest.raises(BedgpuError):  # refused, see bg_intersect
-            eng.bedops(mode, texts)
-        return
     with tempfile.TemporaryDirectory() as td:
         want = run_oracle(oracle_bin["bedops"], [mode] + ([spec] if spec else []), texts, td)
     assert eng.bedops(mode, texts, spec=spec) == want
