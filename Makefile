@@ -3,7 +3,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CC ?= gcc
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-value -Wno-unused-result
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-value -Wno-unused-result
 CFLAGS ?= -O2 -std=gnu11 -Wall -Wno-unused-result
 
 SRC := bedops_amd/csrc

@@ -207,6 +207,11 @@ int main(int argc, char** argv) {
         need5 = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
       if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) map_rest = 1;
+      // running-double operations order equal rows by their id and remainder
+      // (CoordRestAddressCompare, BedCompare.hpp:143-194) when the scores are decimals
+      if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_VARIANCE || op == BG_MAP_STDEV ||
+          op == BG_MAP_CV)
+        map_rest = 1;
       if (op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) need4 = 1;
     }
   }

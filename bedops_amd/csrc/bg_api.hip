@@ -381,6 +381,8 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->bases);
   bg_release(c, r->uniq);
   bg_release(c, r->isq);
+  bg_release(c, r->dsum);
+  bg_release(c, r->dsq);
   bg_release(c, r->rrank);
   bg_release(c, r->wlo);
   bg_release(c, r->whi);

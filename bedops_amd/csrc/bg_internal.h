@@ -132,6 +132,8 @@ struct bg_result {
   uint64_t* bases = nullptr; // OvrAggregate
   uint32_t* uniq = nullptr;  // OvrUnique (unsigned int, as the reference)
   int64_t* isq = nullptr;    // exact integer sum of squared scores (Variance, StdDev, CV)
+  double* dsum = nullptr;    // decimal scores: the reference's running sum_ at each row
+  double* dsq = nullptr;     //   and squareSum_ (bg_map.hip, k_mev_*), replacing isum / isq
   uint64_t* rrank = nullptr; // --echo-ref-row-id with --skip-unmapped: printed lines before row r
   uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
   uint64_t* whi = nullptr;

@@ -412,42 +412,76 @@ __device__ __forceinline__ bool parse_u64(const TileText& T, int64_t& p, int64_t
   return nd > 0;
 }
 
-// strtod subset, exact where it claims to be: [+-]digits[.digits] with <= 19
-// significant digits; integers are flagged. Anything else -> ERR_SCORE.
+// strtod subset, correctly rounded where it accepts: [+-]digits[.digits][(e|E)[+-]digits]
+// with <= 19 significant digits m and value m * 10^p, |p| <= 22 (Clinger's fast path: one
+// rounding of exact operands), or p up to 37 when m * 10^(p-22) stays an exact integer
+// <= 2^53. Integers up to 2^53 are flagged (exact sums). Anything else -> ERR_SCORE.
 __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64_t le,
                                             double& out, int& isint) {
   bool neg = false;
   if (p < le && (T.at(p) == '+' || T.at(p) == '-')) neg = T.at(p++) == '-';
   uint64_t m = 0;
   int nd = 0, frac = 0, sig = 0;
-  bool dot = false, fracnz = false;
+  bool dot = false;
   while (p < le) {
     const uint8_t ch = T.at(p);
     if (ch == '.' && !dot) { dot = true; ++p; continue; }
     if (ch < '0' || ch > '9') break;
     ++nd;
-    if (dot) {
-      ++frac;
-      if (ch != '0') fracnz = true;
-    }
+    if (dot) ++frac;
     if (m != 0 || ch != '0') ++sig;
     if (sig <= 19) m = m * 10 + (ch - '0');
     else return false;
     ++p;
   }
   if (nd == 0 || sig > 19) return false;
-  if (p < le && !bg_isws(T.at(p))) return false;  // exponent / junk: not on the GPU path
-  isint = !fracnz;
-  if (!fracnz) {
-    for (int k = 0; k < frac; ++k) m /= 10;
-    if (m > (1ULL << 53)) return false;
-    out = neg ? -(double)m : (double)m;
+  int ex = 0;
+  if (p < le && (T.at(p) == 'e' || T.at(p) == 'E')) {  // strtod takes the exponent only if digits follow
+    int64_t q = p + 1;
+    bool eneg = false;
+    if (q < le && (T.at(q) == '+' || T.at(q) == '-')) eneg = T.at(q++) == '-';
+    int ed = 0;
+    while (q < le && T.at(q) >= '0' && T.at(q) <= '9') {
+      if (ex < 10000) ex = ex * 10 + (T.at(q) - '0');
+      ++ed;
+      ++q;
+    }
+    if (ed == 0) return false;  // "1e" / "1e+": not a plain number for this path
+    if (eneg) ex = -ex;
+    p = q;
+  }
+  if (p < le && !bg_isws(T.at(p))) return false;  // junk after the number
+  int pw = ex - frac;  // value = m * 10^pw
+  while (pw < 0 && m != 0 && m % 10 == 0) { m /= 10; ++pw; }  // trailing zeros
+  const double P10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                          1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  if (m == 0) {
+    isint = 1;
+    out = neg ? -0.0 : 0.0;
     return true;
   }
-  if (m > (1ULL << 53) || frac > 22) return false;  // Clinger fast path: exact
-  double s = 1.0;
-  for (int k = 0; k < frac; ++k) s *= 10.0;
-  out = (double)m / s;
+  if (m > (1ULL << 53)) return false;
+  if (pw < 0) {
+    if (pw < -22) return false;
+    isint = 0;
+    out = (double)m / P10[-pw];
+  } else {
+    if (pw > 22) {  // m * 10^(pw-22) exact and <= 2^53, then one rounding by 1e22
+      for (; pw > 22; --pw) {
+        if (m > (1ULL << 53) / 10) return false;
+        m *= 10;
+      }
+    }
+    // an integer: exact sums need |value| <= 2^53
+    uint64_t v = m;
+    bool small = true;
+    for (int k = 0; k < pw && small; ++k) {
+      if (v > (1ULL << 53) / 10) small = false;
+      else v *= 10;
+    }
+    isint = small ? 1 : 0;
+    out = (double)m * P10[pw];
+  }
   if (neg) out = -out;
   return true;
 }

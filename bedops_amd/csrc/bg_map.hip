@@ -321,6 +321,274 @@ static int map_zero_prep(bg_ctx* c, const bg_table* R, const bg_table* M, bg_res
   return 0;
 }
 
+// ------------------------------- running doubles (decimal scores) ------------------
+// Average / Sum / Variance keep ONE running double (sum_, squareSum_) for the whole file
+// (AverageVisitor.hpp:46-54, SumVisitor.hpp:47-51, VarianceVisitor.hpp:45-55): with
+// non-integer scores every printed value depends on the exact order of all earlier Add and
+// Delete calls, and two runs that start from different sums never re-converge (measured:
+// DESIGN.md §5.2), so the sums are replayed exactly, in the reference's event order:
+//   at reference row i (after row i-1 left S(r_{i-1}) as BedBaseVisitor::win_):
+//   (a) the sweep pops the deque front while Map2Ref(front, r_i) < 0 (WindowSweepImpl.cpp:
+//       207-211): members of S(r_{i-1}) popped there are Deleted in file order; a member m
+//       is popped iff it is poppable (ends R or more before r_i.start, or lies on an
+//       earlier chromosome) and no earlier row still in the deque is not, i.e. m < f_i, the
+//       first candidate of r_i that is not poppable (a row before it that is not poppable
+//       would overlap r_i, and every row overlapping r_i was added to the deque);
+//   (b) fixWindow Deletes the other members of S(r_{i-1}) that fail the criterion for r_i,
+//   (c) then Adds the rows of S(r_i) \ S(r_{i-1}) — both in set order
+//       (CoordRestAddressCompare: start, end, id + remainder, address ~ row index).
+// k_mev counts and writes that event stream (+score / -score, and +-fl(score^2) for the
+// Variance family); k_mev_chain folds it with one wavefront in order (the only sequential
+// step: one FP64 add per event on the critical path), and k_mev_pick reads each row's sums
+// after its last event.
+struct EvArgs {
+  const int64_t* RS;
+  const int64_t* RE;
+  uint64_t nr;
+  const int64_t* MS;
+  const int64_t* ME;
+  const double* SC;
+  uint64_t nm;
+  const uint64_t* wlo;
+  const uint64_t* whi;
+  int64_t ovr, range;
+  double perc;
+  const char* text;  // map text + remainder spans: full_rest() for the set order
+  const uint64_t* rest_off;
+  const uint32_t* rest_len;
+  int mapfields;
+};
+
+__device__ __forceinline__ bool ev_ws(char c) {
+  return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
+}
+// full_rest() of map row m as up to two byte ranges: B3Rest the remainder after `end`,
+// B4Rest id + remainder after it, B5Rest id + remainder after the score (Bed.hpp:301,
+// 537, 788; the score itself is not part of it)
+__device__ __forceinline__ void ev_frest(const EvArgs& A, uint64_t m, const char*& p1, uint32_t& l1,
+                                         const char*& p2, uint32_t& l2) {
+  const char* rp = A.text + A.rest_off[m];
+  const uint32_t rl = A.rest_len[m];
+  l2 = 0;
+  p2 = rp;
+  if (A.mapfields == 3) { p1 = rp; l1 = rl; return; }
+  uint32_t i = 0;
+  while (i < rl && ev_ws(rp[i])) ++i;
+  p1 = rp + i;
+  if (A.mapfields == 4) { l1 = rl - i; return; }
+  uint32_t j = i;
+  while (j < rl && !ev_ws(rp[j])) ++j;
+  l1 = j - i;
+  uint32_t k = j;
+  while (k < rl && ev_ws(rp[k])) ++k;
+  while (k < rl && !ev_ws(rp[k])) ++k;
+  p2 = rp + k;
+  l2 = rl - k;
+}
+// strcmp of the two full_rest strings
+__device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
+  const char *a1, *a2, *b1, *b2;
+  uint32_t la1, la2, lb1, lb2;
+  ev_frest(A, a, a1, la1, a2, la2);
+  ev_frest(A, b, b1, lb1, b2, lb2);
+  const uint32_t la = la1 + la2, lb = lb1 + lb2;
+  for (uint32_t q = 0; q < la && q < lb; ++q) {
+    const uint8_t x = (uint8_t)(q < la1 ? a1[q] : a2[q - la1]);
+    const uint8_t y = (uint8_t)(q < lb1 ? b1[q] : b2[q - lb1]);
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+// CoordRestAddressCompare for two rows of equal start
+__device__ __forceinline__ bool ev_less(const EvArgs& A, uint64_t a, uint64_t b) {
+  if (A.ME[a] != A.ME[b]) return A.ME[a] < A.ME[b];
+  const int c = ev_rest_cmp(A, a, b);
+  if (c != 0) return c < 0;
+  return a < b;
+}
+// the rows of [a, b) that satisfy `pred`, in set order (rows are start-sorted: only runs of
+// equal starts need ordering, by selection)
+template <typename Pred, typename Emit>
+__device__ __forceinline__ void ev_walk(const EvArgs& A, uint64_t a, uint64_t b, Pred pred, Emit emit) {
+  uint64_t m = a;
+  while (m < b) {
+    uint64_t g1 = m + 1;
+    while (g1 < b && A.MS[g1] == A.MS[m]) ++g1;
+    if (g1 - m == 1) {
+      if (pred(m)) emit(m);
+    } else {
+      uint64_t last = ~0ULL;
+      for (;;) {
+        uint64_t best = ~0ULL;
+        for (uint64_t t = m; t < g1; ++t) {
+          if (!pred(t)) continue;
+          if (last != ~0ULL && !ev_less(A, last, t)) continue;
+          if (best == ~0ULL || ev_less(A, t, best)) best = t;
+        }
+        if (best == ~0ULL) break;
+        emit(best);
+        last = best;
+      }
+    }
+    m = g1;
+  }
+}
+
+template <int CRIT, bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_mev(EvArgs A, uint64_t* __restrict__ cnt,
+                                               const uint64_t* __restrict__ off,
+                                               double* __restrict__ X, double* __restrict__ X2) {
+  const uint64_t i = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (i >= A.nr) return;
+  const int64_t s = A.RS[i], e = A.RE[i];
+  const int64_t g = s & ~BG_COORD_MASK;
+  const int64_t R = (CRIT == BG_OVR_RANGE) ? A.range : 0;
+  const uint64_t lo = A.wlo[i], hi = A.whi[i];
+  const bool hp = i > 0;
+  const int64_t ps = hp ? A.RS[i - 1] : 0, pe = hp ? A.RE[i - 1] : 0;
+  const uint64_t plo = hp ? A.wlo[i - 1] : 0, phi = hp ? A.whi[i - 1] : 0;
+  uint64_t f = lo;  // first candidate of r_i that the sweep cannot pop
+  while (f < hi && A.ME[f] + R <= s) ++f;
+  auto in_prev = [&](uint64_t m) {
+    return hp && m >= plo && m < phi && bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m]);
+  };
+  auto in_cur = [&](uint64_t m) {
+    return (A.MS[m] & ~BG_COORD_MASK) == g &&
+           bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]);
+  };
+  auto popped = [&](uint64_t m) {
+    return m < f && ((A.ME[m] & ~BG_COORD_MASK) != g || A.ME[m] + R <= s);
+  };
+  uint64_t k = 0;
+  const uint64_t base = WRITE ? off[i] : 0;
+  auto emit_del = [&](uint64_t m) {
+    if (WRITE) {
+      const double x = A.SC[m];
+      X[base + k] = -x;
+      if (X2) X2[base + k] = -(x * x);
+    }
+    ++k;
+  };
+  auto emit_add = [&](uint64_t m) {
+    if (WRITE) {
+      const double x = A.SC[m];
+      X[base + k] = x;
+      if (X2) X2[base + k] = x * x;
+    }
+    ++k;
+  };
+  if (hp) {
+    for (uint64_t m = plo; m < phi; ++m)  // (a) in deque (file) order
+      if (in_prev(m) && popped(m)) emit_del(m);
+    ev_walk(A, plo, phi, [&](uint64_t m) { return in_prev(m) && !popped(m) && !in_cur(m); }, emit_del);
+  }
+  ev_walk(A, lo, hi, [&](uint64_t m) { return in_cur(m) && !in_prev(m); }, emit_add);  // (c)
+  if (!WRITE) cnt[i] = k;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int j) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), j);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// one wavefront folds the whole event stream in order: SA[k] = sum_ after event k
+// (QA: squareSum_); `s += x` with x = -score for a Delete is exactly `sum_ -= score`
+__global__ void __launch_bounds__(64) k_mev_chain(const double* __restrict__ X,
+                                                  const double* __restrict__ X2, uint64_t E,
+                                                  double* __restrict__ SA, double* __restrict__ QA) {
+  const int lane = threadIdx.x;
+  double s = 0.0, q = 0.0;
+  for (uint64_t b = 0; b < E; b += 64) {
+    const uint64_t k = b + lane;
+    const double x = k < E ? X[k] : 0.0;
+    const double x2 = (X2 && k < E) ? X2[k] : 0.0;
+    double ms = 0.0, mq = 0.0;
+    if (b + 64 <= E) {
+      if (X2) {
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+          s += readlane_f64(x, j);
+          q += readlane_f64(x2, j);
+          if (lane == j) { ms = s; mq = q; }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+          s += readlane_f64(x, j);
+          if (lane == j) ms = s;
+        }
+      }
+    } else {
+      const int nb = (int)(E - b);
+      for (int j = 0; j < nb; ++j) {
+        s += readlane_f64(x, j);
+        if (X2) q += readlane_f64(x2, j);
+        if (lane == j) { ms = s; mq = q; }
+      }
+    }
+    if (k < E) {
+      SA[k] = ms;
+      if (QA) QA[k] = mq;
+    }
+  }
+}
+
+// each row's running sums after its last event (0 before any event: the visitors start at 0)
+__global__ void k_mev_pick(const uint64_t* __restrict__ off, uint64_t nr, const double* __restrict__ SA,
+                           const double* __restrict__ QA, double* __restrict__ dsum,
+                           double* __restrict__ dsq) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nr) return;
+  const uint64_t end = off[i + 1];
+  dsum[i] = end ? SA[end - 1] : 0.0;
+  if (dsq) dsq[i] = end ? QA[end - 1] : 0.0;
+}
+
+template <int CRIT>
+static int map_running_sums_t(bg_ctx* c, const EvArgs& A, bool need_sq, bg_result* res) {
+  const uint64_t nr = A.nr;
+  const unsigned nb = bg_blocks(nr, BG_NT);
+  uint64_t* off = (uint64_t*)bg_alloc(c, 8 * (nr + 1));
+  if (!off) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_mev_count", (k_mev<CRIT, false>), dim3(nb), dim3(BG_NT), A, off,
+            (const uint64_t*)nullptr, (double*)nullptr, (double*)nullptr);
+  BG_HIP(c, hipGetLastError());
+  int rc = bg_scan_sum_u64(c, off, off, nr, off + nr);
+  uint64_t E = 0;
+  if (rc || (rc = bg_fetch_u64(c, off + nr, &E))) return rc;
+  const uint64_t E1 = E ? E : 1;
+  double* X = (double*)bg_alloc(c, 8 * E1);
+  double* X2 = need_sq ? (double*)bg_alloc(c, 8 * E1) : nullptr;
+  double* SA = (double*)bg_alloc(c, 8 * E1);
+  double* QA = need_sq ? (double*)bg_alloc(c, 8 * E1) : nullptr;
+  if (!X || !SA || (need_sq && (!X2 || !QA))) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_mev_write", (k_mev<CRIT, true>), dim3(nb), dim3(BG_NT), A, (uint64_t*)nullptr,
+            (const uint64_t*)off, X, X2);
+  if (E) BG_LAUNCH(c, "k_mev_chain", k_mev_chain, dim3(1), dim3(64), X, X2, E, SA, QA);
+  BG_LAUNCH(c, "k_mev_pick", k_mev_pick, dim3(nb), dim3(BG_NT), off, nr, SA, QA, res->dsum, res->dsq);
+  BG_HIP(c, hipGetLastError());
+  bg_release(c, off);
+  bg_release(c, X);
+  bg_release(c, X2);
+  bg_release(c, SA);
+  bg_release(c, QA);
+  return 0;
+}
+
+static int map_running_sums(bg_ctx* c, int crit, const EvArgs& A, bool need_sq, bg_result* res) {
+  switch (crit) {
+    case BG_OVR_BP: return map_running_sums_t<BG_OVR_BP>(c, A, need_sq, res);
+    case BG_OVR_RANGE: return map_running_sums_t<BG_OVR_RANGE>(c, A, need_sq, res);
+    case BG_OVR_FRAC_REF: return map_running_sums_t<BG_OVR_FRAC_REF>(c, A, need_sq, res);
+    case BG_OVR_FRAC_MAP: return map_running_sums_t<BG_OVR_FRAC_MAP>(c, A, need_sq, res);
+    case BG_OVR_FRAC_EITHER: return map_running_sums_t<BG_OVR_FRAC_EITHER>(c, A, need_sq, res);
+    case BG_OVR_FRAC_BOTH: return map_running_sums_t<BG_OVR_FRAC_BOTH>(c, A, need_sq, res);
+    default: return map_running_sums_t<BG_OVR_EXACT>(c, A, need_sq, res);
+  }
+}
+
 // 1 per reference row that prints a line (MultiVisitor.hpp:83-84 skips rows without maps)
 __global__ void k_map_printed(const int32_t* __restrict__ cnt, uint64_t n, uint64_t* __restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -408,8 +676,17 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   if ((need & (NEED_SUM | NEED_EXT)) && !M->score)
     return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
-  if (need_sum && !M->score_int)
-    return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores are not on the GPU path of bedmap --mean/--sum yet");
+  // decimal scores: the running doubles are replayed in event order (map_running_sums)
+  const bool decimal = need_sum && !M->score_int;
+  const bool need_sq = (need & NEED_SQ) != 0;
+  if (decimal) {
+    if (R->has_zero_len || M->has_zero_len)
+      return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores with zero-length rows are not on the GPU path of bedmap --mean/--sum/--variance/--stdev/--cv");
+    if (!M->rest_off)
+      return bg_fail(c, BG_E_ARG, "non-integer scores under --mean/--sum/--variance/--stdev/--cv need the map file loaded as BG_BED5_REST (equal rows are ordered by id and remainder)");
+    need &= ~(NEED_SUM | NEED_SQ);
+    need |= NEED_WIN;
+  }
   BG_HIP(c, hipMemsetAsync(c->dstat, 0, sizeof(bg_dstatus), c->stream));
   const uint64_t n1 = R->n ? R->n : 1;
   bg_result* res = new bg_result();
@@ -429,6 +706,14 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (need & NEED_BASES) res->bases = (uint64_t*)bg_alloc(c, 8 * n1);
   if (need & NEED_UNIQ) res->uniq = (uint32_t*)bg_alloc(c, 4 * n1);
   if (need & NEED_SQ) res->isq = (int64_t*)bg_alloc(c, 8 * n1);
+  if (decimal) {
+    res->dsum = (double*)bg_alloc(c, 8 * n1);
+    if (need_sq) res->dsq = (double*)bg_alloc(c, 8 * n1);
+    if (!res->dsum || (need_sq && !res->dsq)) {
+      bg_result_free(res);
+      return BG_E_NOMEM;
+    }
+  }
   if (need & NEED_WIN) {
     res->wlo = (uint64_t*)bg_alloc(c, 8 * n1);
     res->whi = (uint64_t*)bg_alloc(c, 8 * n1);
@@ -495,6 +780,26 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
 #undef BG_MAP_LAUNCH
   }
   int rc = bg_hip_ok(c, hipGetLastError());
+  if (!rc && decimal && R->n) {
+    EvArgs E;
+    E.RS = R->ks;
+    E.RE = R->ke;
+    E.nr = R->n;
+    E.MS = M->ks;
+    E.ME = M->ke;
+    E.SC = M->score;
+    E.nm = M->n;
+    E.wlo = res->wlo;
+    E.whi = res->whi;
+    E.ovr = A.ovr;
+    E.range = A.range;
+    E.perc = perc;
+    E.text = M->text;
+    E.rest_off = M->rest_off;
+    E.rest_len = M->rest_len;
+    E.mapfields = mapfields;
+    rc = map_running_sums(c, crit, E, need_sq, res);
+  }
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
   if (!rc && need_rrank && R->n) {  // printed-line ranks for --echo-ref-row-id

@@ -25,11 +25,14 @@ MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, 
            "echo-ref-row-id": 26}
 SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score", "median", "kth", "variance", "stdev",
              "cv", "mad")
-MAP_REST_OPS = ("echo-map", "echo-map-id", "echo-map-id-uniq")  # the map rows' remainders are printed
+# the map rows' remainders are printed, or order equal rows for the running-double
+# operations (CoordRestAddressCompare: id + remainder)
+MAP_REST_OPS = ("echo-map", "echo-map-id", "echo-map-id-uniq", "mean", "sum", "variance", "stdev",
+                "cv")
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}
 
-ERRORS = {-1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
+ERRORS = {-11: "INTERNAL", -1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
           -7: "NOMEM", -8: "UNSUPPORTED", -9: "CHROM", -10: "IO"}
 
 # exported symbols of include/bedgpu.h (checked by tests/test_abi.py)

@@ -165,6 +165,48 @@ static int os_erase(oset_t* s, int64_t x) {
   return 0;
 }
 
+/* BedBaseVisitor's set order (CoordRestAddressCompare, BedCompare.hpp:143-194): start, end,
+ * then strcmp of full_rest() (B3Rest: the remainder after end; B4Rest/B5Rest: id + the
+ * remainder after id / score, Bed.hpp:301,537,788), then the address (row index here).
+ * Add/Delete calls of fixWindow come in this order; it decides the running doubles'
+ * rounding for rows of equal coordinates. */
+static int MAPFIELDS = 3; /* map row type: B3Rest / B4Rest / B5Rest (Bedmap.cpp:601-655) */
+static const char* frest_part(int64_t m, int part) {
+  if (MAPFIELDS >= 4) return part == 0 ? MAP->id[m] : (MAP->rest ? MAP->rest[m] : "");
+  return part == 0 ? (MAP->rest ? MAP->rest[m] : "") : "";
+}
+static int frest_cmp(int64_t a, int64_t b) {
+  const char *pa = frest_part(a, 0), *pb = frest_part(b, 0);
+  int ia = 0, ib = 0;
+  for (;;) {
+    if (!*pa && ia == 0) { pa = frest_part(a, 1); ia = 1; continue; }
+    if (!*pb && ib == 0) { pb = frest_part(b, 1); ib = 1; continue; }
+    const unsigned char x = (unsigned char)*pa, y = (unsigned char)*pb;
+    if (x != y) return x < y ? -1 : 1;
+    if (!x) return 0;
+    ++pa;
+    ++pb;
+  }
+}
+static int rless(int64_t a, int64_t b) {
+  if (MAP->start[a] != MAP->start[b]) return MAP->start[a] < MAP->start[b];
+  if (MAP->end[a] != MAP->end[b]) return MAP->end[a] < MAP->end[b];
+  int v = frest_cmp(a, b);
+  if (v) return v < 0;
+  return a < b;
+}
+static void ev_push(oset_t* s, int64_t x) {
+  if (s->n == s->cap) { s->cap = s->cap ? 2 * s->cap : 64; s->v = (int64_t*)realloc(s->v, (size_t)s->cap * 8); }
+  s->v[s->n++] = x;
+}
+static void sort_rless(int64_t* v, int64_t n) { /* insertion sort: runs are short */
+  for (int64_t i = 1; i < n; ++i) {
+    int64_t x = v[i], j = i;
+    while (j > 0 && rless(x, v[j - 1])) { v[j] = v[j - 1]; --j; }
+    v[j] = x;
+  }
+}
+
 /* visitors */
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
        V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
@@ -179,7 +221,6 @@ static int counter_;
 static long cnt_;      /* MultiVisitor's own add/delete balance */
 static const char* DELIM = "|";
 static const char* MULTIDELIM = ";";
-static int MAPFIELDS = 3; /* map row type: B3Rest / B4Rest / B5Rest (Bedmap.cpp:601-655) */
 static int PREC = 6, SCI = 0, SKIP_UNMAPPED = 0;
 static oset_t VWIN;    /* the visitor window (BedBaseVisitor::win_) */
 
@@ -494,7 +535,7 @@ int main(int argc, char** argv) {
   int64_t* win = (int64_t*)malloc(sizeof(int64_t) * (size_t)(map.n + 1));
   int64_t wh = 0, wt = 0; /* deque [wh, wt) */
   int64_t mi = 0, cache = -1;
-  oset_t vcache = {0}, lst = {0};
+  oset_t vcache = {0}, lst = {0}, ev = {0};
   for (int64_t r = 0; r < ref.n; ++r) {
     while (wt > wh && sweep_m2r(win[wh], r) < 0) { /* OnDelete */
       int64_t m = win[wh++];
@@ -511,24 +552,30 @@ int main(int argc, char** argv) {
     }
     /* OnDone: fixWindow (deletions first, then insertions), then DoneReference */
     lst.n = 0;
+    ev.n = 0;
     for (int64_t i = 0; i < VWIN.n;) {
       int64_t m = VWIN.v[i];
       if (crit_m2r(m, r) != 0) {
-        v_del(m);
+        ev_push(&ev, m);
         os_insert(&lst, m);
         memmove(VWIN.v + i, VWIN.v + i + 1, (size_t)(VWIN.n - i - 1) * 8);
         VWIN.n--;
       } else ++i;
     }
+    sort_rless(ev.v, ev.n);
+    for (int64_t i = 0; i < ev.n; ++i) v_del(ev.v[i]);
+    ev.n = 0;
     for (int64_t i = 0; i < vcache.n;) {
       int64_t m = vcache.v[i];
       if (crit_m2r(m, r) == 0) {
-        v_add(m);
+        ev_push(&ev, m);
         os_insert(&VWIN, m);
         memmove(vcache.v + i, vcache.v + i + 1, (size_t)(vcache.n - i - 1) * 8);
         vcache.n--;
       } else ++i;
     }
+    sort_rless(ev.v, ev.n);
+    for (int64_t i = 0; i < ev.n; ++i) v_add(ev.v[i]);
     for (int64_t i = 0; i < lst.n; ++i) os_insert(&vcache, lst.v[i]);
     v_done(r);
   }

@@ -240,7 +240,7 @@ def test_bedmap_dense_map_slice(eng, oracle_bin):
 
 
 def test_bedmap_min_max_decimal_scores(eng, oracle_bin):
-    """min/max take any score (no arithmetic); sums of non-integer scores are refused"""
+    """min/max/order statistics take any score (no arithmetic)"""
     rng = random.Random(77)
     ref = randbed.rows(rng, 400, span=2000, maxlen=80)
     mp = randbed.rows(rng, 1500, span=2000, maxlen=80)
@@ -253,10 +253,58 @@ def test_bedmap_min_max_decimal_scores(eng, oracle_bin):
                                                      "0.7", "--mad", "--prec", str(prec)], [rt, mt], td)
             assert eng.bedmap(["min", "max", "count", "median", ("kth", 0.7), "mad"], rt, mt,
                               precision=prec) == want
-    from bedops_amd import BedgpuError
-    with pytest.raises(BedgpuError) as ei:
-        eng.bedmap(["sum"], rt, mt)
-    assert ei.value.code == -8
+
+
+def _decimal_map(rng, rows):
+    out = []
+    for i, (c, s, e) in enumerate(rows):
+        kind = rng.random()
+        if kind < 0.05:
+            sc = f"{rng.choice(['', '-'])}{rng.randint(1, 9)}e{rng.randint(8, 16)}"  # mixed magnitudes
+        elif kind < 0.5:
+            sc = f"{rng.choice(['', '-'])}{rng.randint(0, 99999) / 1000}"
+        else:
+            sc = f"{rng.randint(0, 10 ** 6) / 10 ** rng.randint(1, 6)}"
+        out.append(f"{c}\t{s}\t{e}\tid{rng.randint(0, 5)}\t{sc}" + ("\tx" if i % 4 == 0 else "") + "\n")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("crit,val", [("bp-ovr", 1), ("bp-ovr", 9), ("range", 15), ("fraction-map", "0.5"),
+                                      ("fraction-either", "0.3"), ("exact", None)])
+def test_bedmap_decimal_running_sums_vs_oracle(eng, oracle_bin, crit, val):
+    """decimal scores: the reference's one running double per visitor, replayed in its event
+    order (sweep pops in file order, then fixWindow deletes and adds in
+    CoordRestAddressCompare order) by k_mev / k_mev_chain; byte-equal to the oracle"""
+    rng = random.Random(zlib.crc32(repr(("dec", crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(6):
+            ref = randbed.rows(rng, rng.choice([1, 40, 600, 2500]), span=rng.choice([300, 3000]),
+                               maxlen=rng.choice([10, 80]))
+            mp = randbed.rows(rng, rng.choice([1, 60, 900, 4000]), span=rng.choice([300, 3000]),
+                              maxlen=rng.choice([10, 80, 300]))
+            if trial % 2:  # equal coordinates with different ids and scores
+                mp = sorted(mp + mp[::3] + mp[::5], key=lambda r: (r[0].encode(), r[1], r[2]))
+            rt = randbed.text(ref).encode()
+            mt = _decimal_map(rng, mp)
+            copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
+            kw = {"overlap_bp": val} if crit == "bp-ovr" else {"criterion": crit, "value": val}
+            for ops, prec in ((["count", "mean", "sum"], 6), (["variance", "stdev", "cv", "mean"], 9),
+                              (["sum"], 0), (["mean", "min"], 17)):
+                args = [f"--{o}" for o in ops] + copt + ["--prec", str(prec)]
+                want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                assert eng.bedmap(ops, rt, mt, precision=prec, **kw) == want, (crit, ops, trial)
+
+
+def test_bedmap_decimal_drift_fixture(eng):
+    """tests/golden/bedmap_drift.json: running-double drift (2|0.350001 where the exact mean
+    is 0.35) and CoordRestAddressCompare order of equal rows"""
+    import json
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bedmap_drift.json")))
+    for c in cases:
+        ops = [a[2:] for a in c["args"] if a.startswith("--") and a != "--prec"]
+        prec = int(c["args"][c["args"].index("--prec") + 1]) if "--prec" in c["args"] else 6
+        got = eng.bedmap(ops, c["ref"].encode(), c["map"].encode(), precision=prec)
+        assert got == c["expect"].encode(), c["name"]
 
 
 def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):

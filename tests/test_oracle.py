@@ -2,6 +2,7 @@
 the reference's own KATs and the reference-produced output hashes of SURVEY.md
 Appendix D, plus the synthetic generator's input hashes."""
 import hashlib
+import os
 import subprocess
 
 import pytest
@@ -139,3 +140,17 @@ def test_bedmap_oracle_hand_cases(oracle_bin, tmp_path, k):
     out = subprocess.run([oracle_bin["bedmap"]] + args + [str(r), str(m)], stdout=subprocess.PIPE,
                          check=True).stdout.decode()
     assert out == want
+
+
+def test_oracle_bedmap_drift_fixture(oracle_bin, tmp_path):
+    """the committed running-double fixture (tests/golden/make_bedmap_drift_fixture.py)"""
+    import json
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bedmap_drift.json")))
+    assert any(c["expect"].endswith("2|0.350001\n") for c in cases)
+    for c in cases:
+        pr, pm = tmp_path / "r.bed", tmp_path / "m.bed"
+        pr.write_text(c["ref"])
+        pm.write_text(c["map"])
+        got = subprocess.run([oracle_bin["bedmap"], *c["args"], str(pr), str(pm)],
+                             stdout=subprocess.PIPE, check=True).stdout.decode()
+        assert got == c["expect"], c["name"]

@@ -71,7 +71,7 @@ typedef struct {
   uint64_t n;        /* rows */
   uint32_t* start;
   uint8_t* length;
-  uint16_t* score;   /* BED5 only */
+  uint32_t* score;   /* BED5 only */
 } cgen_t;
 
 /* Number of contigs and their names/lengths (for sharding by chromosome). */
@@ -85,7 +85,8 @@ uint64_t bedgen_contig_len(int c) { return (c >= 0 && c < 25) ? HG38[c].len : 0;
 int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uint64_t mask,
                          char** out, uint64_t* out_len, uint64_t* out_rows);
 
-/* Generate a whole file into a malloc'ed buffer. mode: 3 = BED3, 5 = BED5.
+/* Generate a whole file into a malloc'ed buffer. mode: 3 = BED3, 5 = BED5,
+ * 6 = BED5 with decimal scores ("<d>.<ddd>": draw % 100000 / 1000; not in SURVEY App. D).
  * Returns 0 on success; *out must be freed with bedgen_free(). */
 int bedgen_buffer(uint64_t N, uint64_t seed, int mode, int chr1_only,
                   char** out, uint64_t* out_len, uint64_t* out_rows) {
@@ -103,7 +104,7 @@ int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uin
   for (int c = 0; c < nc; ++c) {
     g[c].c = c;
     g[c].n = (uint64_t)((double)N * ((double)HG38[c].len / total) + 0.5);
-    base[c + 1] = base[c] + g[c].n * (mode == 5 ? 3 : 2);
+    base[c + 1] = base[c] + g[c].n * (mode >= 5 ? 3 : 2);
   }
   for (int c = 0; c < nc; ++c) { /* unselected contigs keep their draw offsets, emit nothing */
     if (!((mask >> c) & 1ULL)) g[c].n = 0;
@@ -133,9 +134,9 @@ int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uin
     }
     free(tmp);
     g[c].start = st; g[c].length = ln;
-    if (mode == 5) {
-      uint16_t* sc = (uint16_t*)malloc((n ? n : 1) * sizeof(uint16_t));
-      for (uint64_t i = 0; i < n; ++i) sc[i] = (uint16_t)(draw(seed, k++) % 1000);
+    if (mode >= 5) {
+      uint32_t* sc = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+      for (uint64_t i = 0; i < n; ++i) sc[i] = (uint32_t)(draw(seed, k++) % (mode == 6 ? 100000 : 1000));
       g[c].score = sc;
     }
   }
@@ -158,6 +159,7 @@ int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uin
       uint64_t s = G->start[i], e = s + G->length[i];
       bytes += nl + 1 + (uint64_t)u64_len(s) + 1 + (uint64_t)u64_len(e) + 1;
       if (mode == 5) bytes += 3 + (uint64_t)u64_len(i) + 1 + (uint64_t)u64_len(G->score[i]);
+      if (mode == 6) bytes += 3 + (uint64_t)u64_len(i) + 1 + (uint64_t)u64_len(G->score[i] / 1000) + 4;
     }
     ck_off[t + 1] = bytes;
   }
@@ -178,6 +180,12 @@ int bedgen_buffer_subset(uint64_t N, uint64_t seed, int mode, int chr1_only, uin
       if (mode == 5) {
         *p++ = '\t'; *p++ = 'i'; *p++ = 'd'; p = put_u64(p, i);
         *p++ = '\t'; p = put_u64(p, G->score[i]);
+      }
+      if (mode == 6) {
+        const uint32_t f = G->score[i] % 1000;
+        *p++ = '\t'; *p++ = 'i'; *p++ = 'd'; p = put_u64(p, i);
+        *p++ = '\t'; p = put_u64(p, G->score[i] / 1000);
+        *p++ = '.'; *p++ = (char)('0' + f / 100); *p++ = (char)('0' + f / 10 % 10); *p++ = (char)('0' + f % 10);
       }
       *p++ = '\n';
     }
@@ -201,6 +209,7 @@ int main(int argc, char** argv) {
   int mode = 3, chr1 = 0;
   for (int i = 3; i < argc; ++i) {
     if (!strcmp(argv[i], "--bed5")) mode = 5;
+    if (!strcmp(argv[i], "--bed5-decimal")) mode = 6;
     else if (!strcmp(argv[i], "--chr1")) chr1 = 1;
   }
   char* buf; uint64_t len, rows;
