@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CC ?= gcc
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-value -Wno-unused-result
-CFLAGS ?= -O2 -std=gnu11 -Wall -Wno-unused-result
+CFLAGS ?= -O2 -std=gnu11 -pthread -Wall -Wno-unused-result
 
 SRC := bedops_amd/csrc
 OBJ := build/obj
@@ -26,9 +26,9 @@ $(OBJ)/%.o: $(SRC)/%.hip $(SRC)/bg_internal.h include/bedgpu.h
 
 $(LIB): $(HIPOBJS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-$(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h include/bedgpu.h $(LIB)
+$(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
 

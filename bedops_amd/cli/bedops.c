@@ -13,6 +13,7 @@
 #include <ctype.h>
 
 #include "cli_common.h"
+#include "cli_shard.h"
 
 static const char* PROG = "bedops";
 
@@ -144,6 +145,47 @@ static void parse_range(const char* v, int* lpad, int* rpad) {
     *lpad = -r;
     *rpad = r;
   }
+}
+
+/* how each input is parsed (Bedops.cpp:402-421): --everything keeps all columns of every
+ * file, element-of those of the reference file; the other inputs of the set operations
+ * are read only as merged sets (getNextFileMergedCoords, Bedops.cpp:792-814), so they are
+ * parsed straight to their components unless --chrom/--range need the rows */
+static int input_kind(int mode, int i, const char* chrom, int has_range) {
+  if (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0)) return BG_BED3_REST;
+  if (strchr("midencws", mode) && !chrom && !has_range && !env_no_set()) return BG_BED3_SET;
+  return BG_BED3;
+}
+
+typedef struct {
+  int mode, full_left;
+  double thres;
+  int use_pct;
+  uint64_t chop_bp, chop_stagger;
+  int chop_x;
+} op_args_t;
+
+/* selectWork (Bedops.cpp:1524-1577): the operation on every loaded file */
+static int run_op(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
+  const op_args_t* o = (const op_args_t*)arg;
+  int nf = 0;
+  while (bg_set_rows(set, nf, &(uint64_t){0}) == 0) ++nf;
+  int idx[4096];
+  if (nf > 4096) return BG_E_ARG;
+  for (int i = 0; i < nf; ++i) idx[i] = i;
+  switch (o->mode) {
+    case 'm': return bg_merge(ctx, set, idx, nf, res);
+    case 'i': return bg_intersect(ctx, set, idx, nf, res);
+    case 'd': return bg_difference(ctx, set, 0, idx + 1, nf - 1, res);
+    case 'e': return bg_element_of(ctx, set, 0, idx + 1, nf - 1, o->thres, o->use_pct, 0, res);
+    case 'n': return bg_element_of(ctx, set, 0, idx + 1, nf - 1, o->thres, o->use_pct, 1, res);
+    case 'c': return bg_complement(ctx, set, idx, nf, o->full_left, res);
+    case 'w': return bg_chop(ctx, set, idx, nf, o->chop_bp, o->chop_stagger, o->chop_x, res);
+    case 's': return bg_symmdiff(ctx, set, idx, nf, res);
+    case 'p': return bg_partition(ctx, set, idx, nf, res);
+    case 'u': return bg_everything(ctx, set, idx, nf, res);
+  }
+  return BG_E_ARG;
 }
 
 int main(int argc, char** argv) {
@@ -304,13 +346,27 @@ int main(int argc, char** argv) {
   }
   if (nf < minfiles) bad_input("Not enough files");
 
+  text_buf_t* tx = (text_buf_t*)calloc((size_t)nf, sizeof(text_buf_t));
+  bg_input* in = (bg_input*)calloc((size_t)nf, sizeof(bg_input));
+  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h); every mode is
+   * chromosome-local except --range padding, which looks across the whole file */
+  if (!check && !ec && !chrom && !has_range && getenv("BEDGPU_DEVICES")) {
+    for (int i = 0; i < nf; ++i) {
+      if (read_text(argv[a + i], &tx[i])) {
+        char b[1024];
+        snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
+        die_msg(PROG, b);
+      }
+      in[i].kind = input_kind(mode, i, chrom, has_range);
+    }
+    op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
+    if (shard_run(PROG, nf, in, tx, run_op, &oa) == 0) return EXIT_SUCCESS;
+  }
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
-  text_buf_t* tx = (text_buf_t*)calloc((size_t)nf, sizeof(text_buf_t));
-  bg_input* in = (bg_input*)calloc((size_t)nf, sizeof(bg_input));
   for (int i = 0; i < nf; ++i) {
-    if (read_text(argv[a + i], &tx[i])) {
+    if (!tx[i].data && read_text(argv[a + i], &tx[i])) {
       char b[1024];
       snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
       die_msg(PROG, b);
@@ -325,9 +381,7 @@ int main(int argc, char** argv) {
      * file (Bedops.cpp:402-421); the other inputs of the set operations are read only as
      * merged sets (getNextFileMergedCoords, Bedops.cpp:792-814), so they are parsed
      * straight to their components unless --chrom/--range need the rows */
-    in[i].kind = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0)) ? BG_BED3_REST
-                 : (strchr("midencws", mode) && !chrom && !has_range && !env_no_set()) ? BG_BED3_SET
-                                                                                       : BG_BED3;
+    in[i].kind = input_kind(mode, i, chrom, has_range);
   }
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);
@@ -337,28 +391,14 @@ int main(int argc, char** argv) {
   for (int i = 0; has_range && i < nf; ++i)
     if (!((mode == 'e' || mode == 'n') && i == 0) && (rc = bg_set_pad(ctx, set, i, lpad, rpad)))
       die_ctx(PROG, ctx, rc);
-  int* idx = (int*)calloc((size_t)nf, sizeof(int));
-  for (int i = 0; i < nf; ++i) idx[i] = i;
   bg_result* res = NULL;
-  switch (mode) {
-    case 'm': rc = bg_merge(ctx, set, idx, nf, &res); break;
-    case 'i': rc = bg_intersect(ctx, set, idx, nf, &res); break;
-    case 'd': rc = bg_difference(ctx, set, 0, idx + 1, nf - 1, &res); break;
-    case 'e': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 0, &res); break;
-    case 'n': rc = bg_element_of(ctx, set, 0, idx + 1, nf - 1, thres, use_pct, 1, &res); break;
-    case 'c': rc = bg_complement(ctx, set, idx, nf, full_left, &res); break;
-    case 'w': rc = bg_chop(ctx, set, idx, nf, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x, &res); break;
-    case 's': rc = bg_symmdiff(ctx, set, idx, nf, &res); break;
-    case 'p': rc = bg_partition(ctx, set, idx, nf, &res); break;
-    case 'u': rc = bg_everything(ctx, set, idx, nf, &res); break;
-  }
-  if (rc) die_ctx(PROG, ctx, rc);
+  op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
+  if ((rc = run_op(&oa, ctx, set, &res))) die_ctx(PROG, ctx, rc);
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
   maybe_stats(ctx);
   bg_result_free(res);
   bg_set_free(set);
   bg_close(ctx);
-  free(idx);
   free(in);
   free(tx);
   return EXIT_SUCCESS;

@@ -10,13 +10,6 @@
 
 #include "bg_internal.h"
 
-namespace {
-struct LiveMap {
-  std::unordered_map<void*, size_t> m;
-};
-std::unordered_map<bg_ctx*, LiveMap> g_live;  // one entry per context
-}  // namespace
-
 int bg_fail(bg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
@@ -29,6 +22,7 @@ int bg_hip_fail(bg_ctx* c, hipError_t e, const char* what) {
 }
 
 void* bg_alloc(bg_ctx* c, size_t bytes) {
+  bg_bind(c);  // the calling thread may drive several devices (bg_group)
   bytes = (bytes + 255) & ~(size_t)255;
   if (bytes == 0) bytes = 256;
   // best fit among cached blocks no larger than 2x the request
@@ -57,13 +51,13 @@ void* bg_alloc(bg_ctx* c, size_t bytes) {
       }
     }
   }
-  g_live[c].m[p] = got;
+  c->live[p] = got;
   return p;
 }
 
 void bg_release(bg_ctx* c, void* p) {
   if (!c || !p) return;
-  auto& L = g_live[c].m;
+  auto& L = c->live;
   auto it = L.find(p);
   if (it == L.end()) return;
   c->free_list.push_back({p, it->second});
@@ -175,8 +169,7 @@ extern "C" void bg_close(bg_ctx* c) {
   if (!c) return;
   hipStreamSynchronize(c->stream);
   for (auto& b : c->free_list) hipFree(b.p);
-  for (auto& kv : g_live[c].m) hipFree(kv.first);
-  g_live.erase(c);
+  for (auto& kv : c->live) hipFree(kv.first);
   for (auto& m : c->marks) hipEventDestroy(m.second);
   for (auto& p : c->prof_pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   for (auto e : c->prof_events) hipEventDestroy(e);
@@ -317,44 +310,78 @@ static int write_all(int fd, const char* p, uint64_t n) {
   return 0;
 }
 
-// formats on the device, then streams the text to fd through two pinned buffers so
-// the D2H copy of chunk k+1 overlaps write(2) of chunk k
+// streams n bytes of device memory to fd through two pinned buffers, so the D2H copy of
+// chunk k+1 overlaps write(2) of chunk k; every exit path frees the buffers and events
+extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
+  if (!c || (!d && n)) return BG_E_ARG;
+  if (n == 0) return 0;
+  bg_bind(c);
+  const uint64_t CH = 64ull << 20;
+  char* hb[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = 0;
+  for (int k = 0; k < 2 && !rc; ++k) {
+    hipError_t e = hipHostMalloc((void**)&hb[k], CH, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device buffers");
+  }
+  const char* src = (const char*)d;
+  const uint64_t nch = (n + CH - 1) / CH;
+  auto issue = [&](uint64_t k) -> int {
+    const uint64_t off = k * CH, len = std::min(CH, n - off);
+    hipError_t e = hipMemcpyAsync(hb[k & 1], src + off, len, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(ev[k & 1], c->stream);
+    return e == hipSuccess ? 0 : bg_hip_fail(c, e, "bg_write_device copy");
+  };
+  if (!rc) rc = issue(0);
+  for (uint64_t k = 0; k < nch && !rc; ++k) {
+    hipError_t e = hipEventSynchronize(ev[k & 1]);
+    if (e != hipSuccess) { rc = bg_hip_fail(c, e, "bg_write_device sync"); break; }
+    if (k + 1 < nch && (rc = issue(k + 1))) break;
+    const uint64_t off = k * CH, len = std::min(CH, n - off);
+    if (write_all(fd, hb[k & 1], len)) rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
+  }
+  hipStreamSynchronize(c->stream);
+  for (int k = 0; k < 2; ++k) {
+    if (hb[k]) hipHostFree(hb[k]);
+    if (ev[k]) hipEventDestroy(ev[k]);
+  }
+  bg_mark(c, "write");
+  return rc;
+}
+
+// formats on the device, then streams the text to fd
 extern "C" int bg_result_write(bg_ctx* c, bg_result* r, int fd) {
   uint64_t n = 0;
   int rc = bg_result_format(c, r, &n);
   if (rc) return rc;
-  if (n == 0) return 0;
-  const uint64_t CH = 64ull << 20;
-  char* hb[2] = {nullptr, nullptr};
-  hipEvent_t ev[2];
-  for (int k = 0; k < 2; ++k) {
-    BG_HIP(c, hipHostMalloc((void**)&hb[k], CH, hipHostMallocDefault));
-    BG_HIP(c, hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+  return bg_write_device(c, r->text, n, fd);
+}
+
+// host parts (pinned for async DMA) copied back to back into one new device buffer: a
+// chromosome shard of a file assembled on the GPU that will parse it (bg_input.on_device)
+extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts, const uint64_t* lens,
+                                     void** out, uint64_t* total) {
+  if (!c || n < 0 || !out || !total || (n && (!parts || !lens))) return BG_E_ARG;
+  uint64_t t = 0;
+  for (int k = 0; k < n; ++k) t += lens[k];
+  char* d = (char*)bg_alloc(c, t + 64);
+  if (!d) return BG_E_NOMEM;
+  uint64_t o = 0;
+  for (int k = 0; k < n; ++k) {
+    if (lens[k]) BG_HIP(c, hipMemcpyAsync(d + o, parts[k], lens[k], hipMemcpyHostToDevice, c->stream));
+    o += lens[k];
   }
-  const uint64_t nch = (n + CH - 1) / CH;
-  auto issue = [&](uint64_t k) -> int {
-    const uint64_t off = k * CH, len = std::min(CH, n - off);
-    BG_HIP(c, hipMemcpyAsync(hb[k & 1], r->text + off, len, hipMemcpyDeviceToHost, c->stream));
-    BG_HIP(c, hipEventRecord(ev[k & 1], c->stream));
-    return 0;
-  };
-  if ((rc = issue(0))) return rc;
-  for (uint64_t k = 0; k < nch; ++k) {
-    BG_HIP(c, hipEventSynchronize(ev[k & 1]));
-    if (k + 1 < nch && (rc = issue(k + 1))) return rc;
-    const uint64_t off = k * CH, len = std::min(CH, n - off);
-    if (write_all(fd, hb[k & 1], len)) {
-      rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
-      break;
-    }
-  }
-  BG_HIP(c, hipStreamSynchronize(c->stream));
-  for (int k = 0; k < 2; ++k) {
-    hipHostFree(hb[k]);
-    hipEventDestroy(ev[k]);
-  }
-  bg_mark(c, "write");
-  return rc;
+  *out = d;
+  *total = t;
+  return 0;
+}
+
+extern "C" int bg_bind(bg_ctx* c) {
+  if (!c) return BG_E_ARG;
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess || d != c->device) BG_HIP(c, hipSetDevice(c->device));
+  return 0;
 }
 
 extern "C" void* bg_host_alloc(uint64_t bytes) {

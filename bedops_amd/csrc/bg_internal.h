@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/bedgpu.h"
@@ -57,9 +58,10 @@ struct bg_ctx {
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
   bg_dstatus* hstat = nullptr;  // pinned host mirror
-  // caching allocator: free blocks by size
+  // caching allocator: free blocks by size; live blocks -> their size (per context, so
+  // contexts on different devices can be driven from different host threads)
   std::vector<bg_buf> free_list;
-  std::vector<bg_buf> live;
+  std::unordered_map<void*, size_t> live;
   // stage timing
   bool stats = false;
   std::vector<std::pair<std::string, hipEvent_t>> marks;

@@ -43,7 +43,11 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_stats", "bg_host_alloc", "bg_host_free", "bg_prof_enable", "bg_prof_read",
            "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
            "bg_set_chrom_name", "bg_closest", "bg_complement", "bg_chop", "bg_partition",
-           "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message"]
+           "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message",
+           "bg_write_device", "bg_bind", "bg_group_uid", "bg_group_open", "bg_group_open_rank",
+           "bg_group_size", "bg_group_ctx", "bg_group_close", "bg_group_gather", "bg_device_free",
+           "bg_device_gather_host"]
+UID_BYTES = 128
 
 
 class _CheckResult(ctypes.Structure):
@@ -143,6 +147,22 @@ def load_library():
     L.bg_set_chroms.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     L.bg_set_chrom_name.argtypes = [vp, ctypes.c_uint32]
     L.bg_set_chrom_name.restype = ctypes.c_char_p
+    L.bg_write_device.argtypes = [vp, vp, u64, i32]
+    L.bg_bind.argtypes = [vp]
+    L.bg_group_uid.argtypes = [vp]
+    L.bg_group_open.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(i32), i32]
+    L.bg_group_open_rank.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32]
+    L.bg_group_size.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.bg_group_ctx.argtypes = [vp, i32]
+    L.bg_group_ctx.restype = vp
+    L.bg_group_close.argtypes = [vp]
+    L.bg_group_close.restype = None
+    L.bg_group_gather.argtypes = [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                  ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    L.bg_device_free.argtypes = [vp, vp]
+    L.bg_device_free.restype = None
+    L.bg_device_gather_host.argtypes = [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(u64),
+                                        ctypes.POINTER(vp), ctypes.POINTER(u64)]
     _LIB = L
     return L
 
@@ -245,8 +265,12 @@ class InputSet:
 class Engine:
     """One libbedgpu context (one device, one HIP stream)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, ctx=None):
         self.L = load_library()
+        self._owns = ctx is None
+        if ctx is not None:  # a member of a Group (the group owns the context)
+            self.ctx = ctypes.c_void_p(ctx)
+            return
         self.ctx = ctypes.c_void_p()
         rc = self.L.bg_open(ctypes.byref(self.ctx), int(device))
         if rc:
@@ -257,9 +281,15 @@ class Engine:
             raise BedgpuError(rc, self.L.bg_last_error(self.ctx).decode(errors="replace"))
 
     def close(self):
-        if self.ctx:
+        if self.ctx and self._owns:
             self.L.bg_close(self.ctx)
-            self.ctx = None
+        self.ctx = None
+
+    def write_device(self, dptr, nbytes, fd):
+        self._check(self.L.bg_write_device(self.ctx, ctypes.c_void_p(dptr), nbytes, fd))
+
+    def device_free(self, dptr):
+        self.L.bg_device_free(self.ctx, ctypes.c_void_p(dptr))
 
     def stream(self):
         return self.L.bg_stream(self.ctx)
@@ -459,3 +489,62 @@ class Engine:
         buf = ctypes.create_string_buffer(8192)
         self._check(self.L.bg_stats(self.ctx, buf, 8192))
         return buf.value.decode()
+
+
+def group_uid():
+    """ncclGetUniqueId on this process (rank 0 of a multi-process group): 128 bytes."""
+    L = load_library()
+    buf = ctypes.create_string_buffer(UID_BYTES)
+    rc = L.bg_group_uid(buf)
+    if rc:
+        raise BedgpuError(rc, "bg_group_uid failed (RCCL)")
+    return buf.raw
+
+
+class Group:
+    """Several devices working on chromosome shards (include/bedgpu.h bg_group_*):
+    Group(devices=[0, 1, ...]) in one process, or Group(device=d, uid=..., nranks=N,
+    rank=r) as one rank of a multi-process group. gather() reassembles every member's
+    per-chromosome text on rank 0 over RCCL."""
+
+    def __init__(self, devices=None, device=None, uid=None, nranks=1, rank=0):
+        self.L = load_library()
+        self.h = ctypes.c_void_p()
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = self.L.bg_group_open(ctypes.byref(self.h), arr, len(devices))
+        else:
+            rc = self.L.bg_group_open_rank(ctypes.byref(self.h), int(device), uid, int(nranks), int(rank))
+        if rc:
+            raise BedgpuError(rc, "bg_group_open failed")
+        nl, nr, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self.L.bg_group_size(self.h, ctypes.byref(nl), ctypes.byref(nr), ctypes.byref(r0))
+        self.nlocal, self.nranks, self.rank0 = nl.value, nr.value, r0.value
+        self.engines = [Engine(ctx=self.L.bg_group_ctx(self.h, k)) for k in range(self.nlocal)]
+
+    def gather(self, nchrom, parts):
+        """parts: per local member (text_devptr, offsets[nchrom], lengths[nchrom]) over the
+        GLOBAL chromosome list. Returns (devptr, nbytes) on rank 0, (None, 0) elsewhere."""
+        n = len(parts)
+        texts = (ctypes.c_void_p * n)(*[p[0] for p in parts])
+        keep = []
+        offs, lens = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+        for k, (_, o, ln) in enumerate(parts):
+            ao = (ctypes.c_uint64 * max(nchrom, 1))(*o)
+            al = (ctypes.c_uint64 * max(nchrom, 1))(*ln)
+            keep += [ao, al]
+            offs[k] = ctypes.cast(ao, ctypes.c_void_p)
+            lens[k] = ctypes.cast(al, ctypes.c_void_p)
+        out, nb = ctypes.c_void_p(), ctypes.c_uint64()
+        rc = self.L.bg_group_gather(self.h, int(nchrom), texts, offs, lens, ctypes.byref(out),
+                                    ctypes.byref(nb))
+        if rc:
+            raise BedgpuError(rc, self.L.bg_last_error(self.engines[0].ctx).decode(errors="replace"))
+        return (out.value, nb.value) if out.value else (None, 0)
+
+    def close(self):
+        if self.h:
+            for e in self.engines:
+                e.ctx = None
+            self.L.bg_group_close(self.h)
+            self.h = None

@@ -213,6 +213,40 @@ int bg_set_chroms(const bg_set* set, uint32_t* n);
 const char* bg_set_chrom_name(const bg_set* set, uint32_t g);
 void bg_result_free(bg_result* res);
 
+/* stream n bytes of device memory (on ctx's device) to fd: double-buffered D2H + write */
+int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
+/* make ctx's device current on the calling thread (a host thread per device in a group) */
+int bg_bind(bg_ctx* ctx);
+
+/* ---- multi-GPU: chromosome shards reassembled over RCCL ------------
+ * Replaces the reference's per-chromosome process fan-out (`--chrom` per process,
+ * docs/content/reference/set-operations/bedops.rst:721-726; comparators start with
+ * strcmp(chrom), BedCompare.hpp:42-43): each member of a group processes whole
+ * chromosomes on its own GPU; bg_group_gather puts their formatted texts on member 0 in
+ * strcmp chromosome order with grouped ncclSend/ncclRecv over xGMI. */
+typedef struct bg_group bg_group;
+#define BG_UID_BYTES 128
+int bg_group_uid(void* uid); /* ncclGetUniqueId: rank 0 of a multi-process group */
+/* one process driving n devices (ncclCommInitAll); a device listed twice gets no
+ * communicator (transfers become device copies: tests on one GPU) */
+int bg_group_open(bg_group** g, const int* devices, int n);
+/* one rank of a multi-process group (one process per GPU; uid from rank 0) */
+int bg_group_open_rank(bg_group** g, int device, const void* uid, int nranks, int rank);
+int bg_group_size(const bg_group* g, int* nlocal, int* nranks, int* rank0);
+bg_ctx* bg_group_ctx(bg_group* g, int local);
+void bg_group_close(bg_group* g);
+/* nchrom: the GLOBAL chromosome list (identical on every rank, strcmp order). For each
+ * local member k: text[k] its formatted text (device), off[k][q] / len[k][q] the bytes of
+ * global chromosome q in it (len 0: none). Rank 0 gets *out = a device buffer on member
+ * 0's device with every chromosome's text in order (free with bg_device_free). */
+int bg_group_gather(bg_group* g, int nchrom, const char* const* text, const uint64_t* const* off,
+                    const uint64_t* const* len, char** out, uint64_t* out_len);
+void bg_device_free(bg_ctx* ctx, void* dptr);
+/* host byte ranges copied back to back into one new device buffer of ctx's device (a
+ * file's chromosome shard, then loaded with bg_input.on_device = 1) */
+int bg_device_gather_host(bg_ctx* ctx, int n, const void* const* parts, const uint64_t* lens,
+                          void** out, uint64_t* total);
+
 /* per-stage device timings of the last call sequence (ms), for BEDGPU_STATS */
 int bg_stats(const bg_ctx* ctx, char* buf, uint64_t cap);
 

@@ -1,0 +1,124 @@
+"""Multi-GPU path on one GPU: chromosome shards run as separate group members on cuda:0.
+
+The C front-ends under BEDGPU_DEVICES=0,0[,0] split every input by chromosome (bisection),
+run each shard on its own member (host thread, context, stream) and reassemble the texts
+with bg_group_gather (bedops_amd/cli/cli_shard.h, bedops_amd/csrc/bg_group.hip); with a
+device listed twice the members get no RCCL communicator and the transfers are device
+copies — the plan, the spans and the reassembly are the code the RCCL path runs. The output
+must be byte-identical to the one-device run and to the oracle. The engine-level test drives
+engine.Group.gather the way bench.py does under torch.distributed.run.
+"""
+import os
+import random
+import subprocess
+import tempfile
+import zlib
+
+import pytest
+
+import randbed
+
+pytestmark = pytest.mark.gpu
+
+CHROMS = ["chr1", "chr10", "chr11", "chr2", "chr20", "chr3", "chrM", "chrX", "chrY"]
+MODES = [["-m"], ["-i"], ["-d"], ["-e", "1"], ["-n", "30%"], ["-c"], ["-c", "-L"], ["-w", "7"],
+         ["-s"], ["-p"], ["-u"]]
+
+
+def _cli(exe, args, env_devices):
+    env = dict(os.environ)
+    env.pop("BEDGPU_DEVICES", None)
+    if env_devices:
+        env["BEDGPU_DEVICES"] = env_devices
+    return subprocess.run([exe, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
+                          timeout=120)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_cli_sharded_equals_single_device(gpu_bin, oracle_bin, mode):
+    rng = random.Random(zlib.crc32(repr(mode).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(4):
+            files = []
+            for f in range(3 if mode[0] in ("-m", "-i", "-u") else 2):
+                rows = randbed.rows(rng, rng.choice([1, 40, 600, 3000]),
+                                    chroms=rng.sample(CHROMS, rng.choice([1, 4, 9])),
+                                    span=rng.choice([500, 5000]), maxlen=rng.choice([10, 120]),
+                                    zero_frac=0.05 if mode[0] in ("-i", "-d", "-e", "-n") else 0.0)
+                p = os.path.join(td, f"f{trial}_{f}.bed")
+                randbed.write(p, randbed.text(rows, rest="cols" if f == 0 else None, rng=rng))
+                files.append(p)
+            one = _cli(gpu_bin["bedops"], mode + files, None)
+            assert one.returncode == 0, one.stderr
+            want = subprocess.run([oracle_bin["bedops"], *mode, *files], stdout=subprocess.PIPE,
+                                  check=True).stdout
+            assert one.stdout == want
+            for devs in ("0,0", "0,0,0"):
+                got = _cli(gpu_bin["bedops"], mode + files, devs)
+                assert got.returncode == 0, got.stderr
+                assert got.stdout == want, (mode, trial, devs)
+
+
+def test_cli_sharded_errors_match_single_device(gpu_bin, tmp_path):
+    """an error inside a shard falls back to the one-device run: same message, same line"""
+    a = tmp_path / "a.bed"
+    b = tmp_path / "b.bed"
+    a.write_text("chr1\t1\t5\nchr2\t3\t9\nchr2\t4\tx\nchr3\t1\t2\n")
+    b.write_text("chr1\t2\t8\nchr3\t0\t9\n")
+    one = _cli(gpu_bin["bedops"], ["-i", str(a), str(b)], None)
+    two = _cli(gpu_bin["bedops"], ["-i", str(a), str(b)], "0,0")
+    assert one.returncode != 0
+    assert (two.returncode, two.stderr, two.stdout) == (one.returncode, one.stderr, one.stdout)
+
+
+def test_engine_group_gather_equals_single_run(oracle_bin):
+    """bench.py's multi-rank step on one GPU: each member loads only its chromosomes,
+    intersects, formats; Group.gather reassembles on member 0"""
+    from bedops_amd.engine import BED3_SET, Group
+    from bedops_amd.shard import assign, member_spans, strcmp_order
+
+    rng = random.Random(5)
+    texts = [randbed.text(randbed.rows(rng, 4000, chroms=CHROMS, span=20000, maxlen=90)).encode()
+             for _ in range(2)]
+    weights = {}
+    for t in texts:
+        for ln in t.splitlines(keepends=True):
+            c = ln.split(b"\t", 1)[0].decode()
+            weights[c] = weights.get(c, 0) + len(ln)
+    gnames = strcmp_order(weights)
+    for world in (2, 3):
+        owner, _ = assign(weights, world)
+        g = Group(devices=[0] * world)
+        try:
+            parts, keep = [], []
+            for m, eng in enumerate(g.engines):
+                shard = [b"".join(ln for ln in t.splitlines(keepends=True)
+                                  if owner[ln.split(b"\t", 1)[0].decode()] == m) for t in texts]
+                s = eng.load([(x, BED3_SET) for x in shard])
+                r = eng.op("-i", s, [0, 1])
+                r.format()
+                dptr, _ = r.device_text()
+                names = s.chroms()
+                offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
+                parts.append((dptr, offs, lens))
+                keep.append((s, r))
+            out, n = g.gather(len(gnames), parts)
+            with tempfile.TemporaryFile() as fo:  # member 0 streams its buffer to a file
+                g.engines[0].write_device(out, n, fo.fileno())
+                fo.seek(0)
+                got = fo.read()
+            g.engines[0].device_free(out)
+            for s, r in keep:
+                r.free()
+                s.free()
+        finally:
+            g.close()
+        with tempfile.TemporaryDirectory() as td:
+            paths = []
+            for i, t in enumerate(texts):
+                p = os.path.join(td, f"{i}.bed")
+                open(p, "wb").write(t)
+                paths.append(p)
+            want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE,
+                                  check=True).stdout
+        assert got == want, world

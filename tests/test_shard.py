@@ -1,9 +1,13 @@
-"""Per-chromosome sharding + rank-0 reassembly (bedops_amd/shard.py), world size 2 and 3 on
-CPU with gloo. Each rank computes its chromosomes' output with the oracle (the GPU engine
-is exercised by bench.py on the box; the shard logic is the same code), the texts are
-gathered with bedops_amd.shard.gather_text, and rank 0's bytes must equal the single-run
-output — the reference's documented per-chromosome scale-out property
-(SURVEY.md §8(e))."""
+"""Per-chromosome sharding plan + rank-0 reassembly model, world size 2 and 3 on CPU with gloo.
+
+Each rank reads the inputs, builds the plan (bedops_amd.shard.assign), runs the oracle on its
+own chromosomes only, and describes its output over the global chromosome list with
+shard.member_spans — the bookkeeping bg_group_gather does in C (bedops_amd/csrc/
+bg_group.hip). The plans are exchanged and must be identical on every rank; rank 0
+reassembles with shard.reassemble and must equal the single-run output: the reference's
+documented per-chromosome scale-out property. The same path on the GPU
+(C sharding in the front-ends, the engine's Group.gather) is tests/test_gpu_shard.py.
+"""
 import os
 import random
 import socket
@@ -25,86 +29,103 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, files, mode, exe, outdir, pipelined=False):
-    import torch
+def _names_of(text):
+    out = []
+    for ln in text.splitlines():
+        c = ln.split(b"\t", 1)[0].decode()
+        if not out or out[-1] != c:
+            out.append(c)
+    return out
+
+
+def _offsets(text, names):
+    """bg_result_chrom_spans of a formatted text: first byte of each chromosome + total"""
+    offs, pos, seen = [], 0, {}
+    for ln in text.splitlines(keepends=True):
+        c = ln.split(b"\t", 1)[0].decode()
+        if c not in seen:
+            seen[c] = pos
+        pos += len(ln)
+    for c in names:
+        offs.append(seen.get(c, pos))
+    return offs + [pos]
+
+
+def _worker(rank, world, port, files, mode, exe, outdir):
     import torch.distributed as dist
-    from bedops_amd.shard import assign, gather_text, gather_text_async, spans_from_text
+    from bedops_amd.shard import assign, member_spans, reassemble, strcmp_order
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
-        weights = {c: 0 for c in CHROMS}
         texts = [open(f, "rb").read() for f in files]
-        for t in texts:
-            for line in t.splitlines():
-                weights[line.split(b"\t", 1)[0].decode()] += 1
+        weights = {}
+        for t in texts:  # bytes per chromosome over all inputs (the C front-ends' weight)
+            for line in t.splitlines(keepends=True):
+                c = line.split(b"\t", 1)[0].decode()
+                weights[c] = weights.get(c, 0) + len(line)
         owner, _ = assign(weights, world)
+        plans = [None] * world
+        dist.all_gather_object(plans, sorted(owner.items()))
+        assert all(p == plans[0] for p in plans), "ranks disagree on the shard plan"
         mine = []
-        for i, t in enumerate(texts):  # this rank's chromosomes only
-            keep = b"".join(ln + b"\n" for ln in t.splitlines()
+        for i, t in enumerate(texts):  # this rank's chromosomes only (no input exchange)
+            keep = b"".join(ln for ln in t.splitlines(keepends=True)
                             if owner[ln.split(b"\t", 1)[0].decode()] == rank)
             p = os.path.join(outdir, f"in{rank}_{i}.bed")
             open(p, "wb").write(keep)
             mine.append(p)
         out = subprocess.run([exe, *mode, *mine], capture_output=True, check=True).stdout
-        spans = spans_from_text(out)
-        buf = torch.frombuffer(bytearray(out), dtype=torch.uint8) if out else \
-            torch.empty(0, dtype=torch.uint8)
-        if pipelined:  # two batches in flight before either is waited for (bench.py's loop)
-            sg = dist.new_group(backend="gloo")
-            p1 = gather_text_async(dist, buf, spans, CHROMS, owner, rank, world, sg)
-            p2 = gather_text_async(dist, buf.clone(), spans, CHROMS, owner, rank, world, sg)
-            got, got2 = p1.wait(), p2.wait()
-            if rank == 0:
-                assert bytes(got.numpy()) == bytes(got2.numpy())
-        else:
-            got = gather_text(dist, buf, spans, CHROMS, owner, rank, world)
+        global_names = strcmp_order(weights)
+        local = _names_of(out)
+        offs, lens = member_spans(local, _offsets(out, local), global_names)
+        pieces = [None] * world
+        dist.all_gather_object(pieces, (out, offs, lens))
         if rank == 0:
-            open(os.path.join(outdir, "gathered.bed"), "wb").write(bytes(got.numpy()))
+            got = reassemble(pieces, global_names, owner)
+            open(os.path.join(outdir, "gathered.bed"), "wb").write(got)
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, files, mode, exe, outdir, pipelined=False):
+def _run(world, mode, nfiles, seed, oracle_bin):
     import torch.multiprocessing as mp
-    mp.start_processes(_worker, args=(world, _free_port(), files, mode, exe, outdir, pipelined),
-                       nprocs=world, start_method="spawn", join=True)
-    return open(os.path.join(outdir, "gathered.bed"), "rb").read()
+
+    rng = random.Random(seed)
+    with tempfile.TemporaryDirectory() as td:
+        files = []
+        for f in range(nfiles):
+            rows = randbed.rows(rng, rng.choice([50, 400, 1500]), chroms=CHROMS, span=3000,
+                                maxlen=rng.choice([20, 150]))
+            p = os.path.join(td, f"f{f}.bed")
+            randbed.write(p, randbed.text(rows, rest="cols" if f == 0 else None, rng=rng))
+            files.append(p)
+        exe = oracle_bin["bedops"]
+        want = subprocess.run([exe, *mode, *files], capture_output=True, check=True).stdout
+        mp.start_processes(_worker, args=(world, _free_port(), files, mode, exe, td), nprocs=world,
+                           join=True, start_method="spawn")
+        got = open(os.path.join(td, "gathered.bed"), "rb").read()
+    return want, got
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode", [["-i"], ["-m"], ["-d"], ["-e", "1"], ["-n", "50%"]])
+def test_sharded_reassembly_equals_single_run(oracle_bin, world, mode):
+    want, got = _run(world, mode, 2 if mode != ["-m"] else 3, hash((world, tuple(mode))) & 0xffff,
+                     oracle_bin)
+    assert got == want
 
 
 def test_assign_is_lpt_and_deterministic():
     from bedops_amd.shard import assign
-    w = {"chr1": 249, "chr2": 242, "chr3": 198, "chrX": 156, "chrM": 0, "chr10": 134}
-    owner, load = assign(w, 2)
-    assert sorted(owner) == sorted(w)
-    assert sum(load) == sum(w.values())
-    assert max(load) - min(load) <= max(w.values())
-    assert assign(w, 2) == (owner, load)
-    assert set(assign(w, 1)[0].values()) == {0}
-    assert set(assign(w, 8)[0].values()) <= set(range(8))
+    w = {"chr1": 249, "chr2": 242, "chr3": 198, "chrX": 156, "chrM": 1, "chr21": 46}
+    owner, load = assign(w, 3)
+    assert owner == assign(dict(reversed(list(w.items()))), 3)[0]
+    assert sorted(load) == sorted([249 + 46, 242 + 1, 198 + 156]) or max(load) <= 249 + 156
+    assert set(owner.values()) == {0, 1, 2}
 
 
-def test_spans_from_text():
-    from bedops_amd.shard import spans_from_text
-    t = b"chr1\t1\t2\nchr1\t3\t4\nchr10\t1\t2\nchrX\t5\t6\n"
-    assert spans_from_text(t) == {"chr1": (0, 18), "chr10": (18, 28), "chrX": (28, 37)}
-    assert spans_from_text(b"") == {}
-
-
-@pytest.mark.parametrize("world,mode,pipelined", [(2, ["-i"], False), (2, ["-m"], False),
-                                                  (3, ["-d"], False), (2, ["-e", "1"], False),
-                                                  (3, ["-n", "50%"], False), (2, ["-i"], True),
-                                                  (3, ["-m"], True)])
-def test_sharded_equals_single_run(oracle_bin, world, mode, pipelined):
-    rng = random.Random(1000 + world)
-    with tempfile.TemporaryDirectory() as td:
-        files = []
-        for i in range(2):
-            chroms = CHROMS if i == 0 else CHROMS[:-2]  # chrX/chrY only in file 0
-            p = os.path.join(td, f"f{i}.bed")
-            randbed.write(p, randbed.text(randbed.rows(rng, 3000, chroms=chroms, span=20000)))
-            files.append(p)
-        exe = oracle_bin["bedops"]
-        want = subprocess.run([exe, *mode, *files], capture_output=True, check=True).stdout
-        got = _run(world, files, mode, exe, td, pipelined)
-        assert got == want
+def test_member_spans_rejects_unsorted_global_list():
+    from bedops_amd.shard import member_spans
+    with pytest.raises(ValueError):
+        member_spans(["chr1"], [0, 5], ["chr2", "chr1"])
