@@ -2,16 +2,29 @@
 """bench.py — headline benchmark of the bedops_amd sweep path on MI355X.
 
 Metric (BASELINE.json): intervals/sec of `bedops --intersect A.bed B.bed`, 100M x 100M
-sorted BED3 (SURVEY.md Appendix D generator, seeds 42/43).
+sorted BED3 (SURVEY.md Appendix D generator, seeds 42/43), at 1/2/4/8 GPUs.
 
 One step = one whole pass of the GPU path over the input text already resident in HBM:
-load both files (k_scout, k_tokhash, run/dictionary kernels, k_parse) -> per-file merge
-(k_tile_max, k_components_*) -> intersect (k_mp_partition, k_intersect_*) -> render the
-sorted BED text back into HBM (k_fmt_*). With N GPUs (one process per GPU,
-torch.distributed over RCCL) the dataset is N x 100M rows per file (weak scaling),
-chromosomes go to ranks by bedops_amd.shard.assign (LPT), every rank runs the step on its
-shard and bedops_amd.shard.gather_text sends the per-chromosome texts to rank 0 over xGMI,
-where they land in strcmp chromosome order — the one exchange the path has.
+load both files (k_scout, k_tokhash, run/dictionary kernels, k_parse_set) -> per-file
+components -> intersect (k_mp_partition, k_mp_tile) -> render the sorted BED text back into
+HBM (k_fmt_*). With N GPUs (one process per GPU; `--gpus N` starts them itself, or
+torch.distributed.run does) the chromosomes are assigned to ranks by
+bedops_amd.shard.assign (LPT), every rank runs the step on its chromosomes only, and the
+per-chromosome texts are reassembled on rank 0 in strcmp order by bg_group_gather
+(bedops_amd/csrc/bg_group.hip: grouped ncclSend/ncclRecv over xGMI) inside the step.
+Strong scaling by default: the dataset is the fixed 100M x 100M at every N (`--weak`: N x
+100M rows per file). After the timed steps rank 0 hashes the reassembled output against the
+reference binary's hash at every N.
+
+Rank 0, N = 1, also times:
+  e2e_intervals_per_s  the drop-in CLI `bedops_amd/bin/bedops --intersect A B > out`, input
+                       files in page cache -> output file (process start and HIP init
+                       included), best of two runs;
+  cpu_baseline         the oracle (plain-C restatement of the reference) on the same full
+                       inputs, fanned out per chromosome over the host cores — the
+                       reference's own documented scale-out (`--chrom` per process,
+                       bedops.rst:721-726) — file -> file, outputs concatenated in order;
+  gpu_vs_cpu           e2e_intervals_per_s / cpu_baseline (both file -> file).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -20,6 +33,7 @@ import ctypes
 import hashlib
 import json
 import os
+import socket
 import subprocess
 import sys
 import tempfile
@@ -32,7 +46,7 @@ METRIC = "intervals/sec, bedops --intersect 100M×100M BED3 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # reference bedops output for A100M x B100M
 REF_INTERSECT = {"rows": 38507974, "bytes": 917848625, "sha16": "2495074965b49d74"}
-
+REF_BEDMAP_R5M = {"rows": 4999998, "bytes": 54515904, "sha16": "899ec7973e166e2d"}
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
@@ -58,14 +72,8 @@ def bedgen_lib():
     return L
 
 
-def contig_shards(L, world):
-    """contig index -> rank: bedops_amd.shard.assign (LPT) on contig length, which is
-    proportional to the generator's rows per contig"""
-    from bedops_amd.shard import assign
-    n = L.bedgen_ncontigs()
-    owner, load = assign({L.bedgen_contig_name(c).decode(): L.bedgen_contig_len(c)
-                          for c in range(n)}, world)
-    return {c: owner[L.bedgen_contig_name(c).decode()] for c in range(n)}, load
+def contigs(L):
+    return [(L.bedgen_contig_name(c).decode(), L.bedgen_contig_len(c)) for c in range(L.bedgen_ncontigs())]
 
 
 def gen(L, n, seed, mask, mode=3):
@@ -77,7 +85,11 @@ def gen(L, n, seed, mask, mode=3):
     return p, nb.value, rows.value
 
 
-def to_device(torch, L, p, nb, dev):
+def host_bytes(p, nb):
+    return memoryview((ctypes.c_char * max(nb, 1)).from_address(p.value))[:nb]
+
+
+def to_device(torch, p, nb, dev):
     import numpy as np
     host = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(max(nb, 1),))
     t = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
@@ -91,7 +103,7 @@ def kernel_bytes(name, w):
     (what each kernel must read and write at minimum)."""
     texts, rows, kinds = w["texts"], w["rows"], w["kinds"]
     nf = len(texts)
-    col = {0: 16, 1: 28, 2: 24, 3: 0}  # keyed start/end (+ rest span 12 B | score 8 B) per row
+    col = {0: 16, 1: 28, 2: 24, 3: 0, 4: 36}  # keyed start/end (+ rest span 12 B | score 8 B) per row
     out, obytes, comps = w["out"], w["out_bytes"], w["comps"]
     table = {
         # one launch per input file: text read + columns written (mean over the files)
@@ -118,67 +130,31 @@ def kernel_bytes(name, w):
     return table.get(name)
 
 
-# ----------------------------------------------------------------------------- cpu baseline
-def cpu_baseline(L, W, target_s=15.0):
-    """Time the CPU oracle (plain-C restatement of the reference; the reference itself is
-    not buildable in this image) on a bounded sample of the same workload:
-    the leading whole contigs (strcmp order) of every input, about `target_s` seconds of
-    single-thread work at the oracle's expected rate."""
-    exe = os.path.join(ROOT, "oracle", "build", W["oracle"])
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-s", "oracle"], cwd=ROOT, check=True)
-    n = L.bedgen_ncontigs()
-    lens = [L.bedgen_contig_len(c) for c in range(n)]
-    total = float(sum(lens))
-    budget = W["cpu_rate"] * target_s
-    rows_all = sum(W["rows"])
-    mask, used = 0, 0.0
-    for c in range(n):  # contigs in strcmp order
-        share = rows_all * lens[c] / total
-        if mask and used + share > budget:
-            break
-        mask |= 1 << c
-        used += share
-    last = L.bedgen_contig_name(max(c for c in range(n) if (mask >> c) & 1)).decode()
-    with tempfile.TemporaryDirectory() as td:
-        paths, nrows = [], 0
-        for i, (seed, mode) in enumerate(W["gen"]):
-            p, nb, r = gen(L, W["rows"][i], seed, mask, mode)
-            path = os.path.join(td, f"in{i}.bed")
-            with open(path, "wb") as f:
-                f.write(memoryview((ctypes.c_char * nb).from_address(p.value)))
-            L.bedgen_free(p)
-            paths.append(path)
-            nrows += r
-        with open(os.path.join(td, "out.bed"), "wb") as fo:
-            t0 = time.perf_counter()
-            subprocess.run([exe, *W["cpu_args"], *paths], stdout=fo, check=True)
-            dt = time.perf_counter() - t0
-    return {"value": nrows / dt, "unit": "intervals/s", "cores": 1, "kind": "port",
-            "sample": f"{W['oracle']} {' '.join(W['cpu_args'])} on contigs chr1..{last} (strcmp "
-                      f"order) of the same inputs: {nrows} rows, file->file, {dt:.2f} s, 1 thread"}
-
-
 # ----------------------------------------------------------------------------- workloads
 # BASELINE.json configs on the GPU path. "intersect" (configs[1]) is the headline metric
 # and the default; the others are measured with --workload for DESIGN.md.
-# gen: (seed, 3 = BED3 | 5 = BED5) per input; rows: per input at N = 1.
+# gen: (seed, 3 = BED3 | 5 = BED5 | 6 = BED5 decimal scores) per input; rows: per input.
 WORKLOADS = {
     "intersect": {"gen": [(42, 3), (43, 3)], "rows": [100_000_000, 100_000_000],
-                  "kinds": [3, 3], "oracle": "bedops_oracle", "cpu_args": ["-i"],
-                  "cpu_rate": 8.5e6, "ref": REF_INTERSECT,
+                  "kinds": [3, 3], "oracle": "bedops_oracle", "args": ["-i"], "cli": "bedops",
+                  "ref": REF_INTERSECT,
                   "desc": "bedops --intersect A.bed B.bed: BED3 text in HBM -> parse -> merge -> "
                           "intersect -> BED text in HBM"},
     "element-of": {"gen": [(44, 3), (45, 3)], "rows": [200_000_000, 200_000_000],
-                   "kinds": [1, 3], "oracle": "bedops_oracle", "cpu_args": ["-e", "1"],
-                   "cpu_rate": 3e6, "ref": None,
+                   "kinds": [1, 3], "oracle": "bedops_oracle", "args": ["-e", "1"], "cli": "bedops",
+                   "ref": None,
                    "desc": "bedops --element-of 1 A.bed B.bed (configs[3] shape, 200M x 200M)"},
     "bedmap": {"gen": [(7, 3), (8, 5)], "rows": [50_000_000, 500_000_000], "kinds": [0, 2],
-               "oracle": "bedmap_oracle", "cpu_args": ["--count", "--mean"], "cpu_rate": 2e6,
+               "oracle": "bedmap_oracle", "args": ["--count", "--mean"], "cli": "bedmap",
                "ref": None, "desc": "bedmap --count --mean ref.bed map.bed (configs[2], 50M x 500M "
                                     "BED5 map)"},
+    "bedmap-decimal": {"gen": [(7, 3), (8, 6)], "rows": [5_000_000, 50_000_000], "kinds": [0, 4],
+                       "oracle": "bedmap_oracle", "args": ["--count", "--mean"], "cli": "bedmap",
+                       "ref": None,
+                       "desc": "bedmap --count --mean ref.bed map.bed, decimal scores (running "
+                               "double replayed in the reference's event order; 5M x 50M)"},
     "closest": {"gen": [(46, 3), (47, 3)], "rows": [10_000_000, 1_000_000_000], "kinds": [1, 1],
-                "oracle": "closest_oracle", "cpu_args": ["--closest"], "cpu_rate": 4e6,
+                "oracle": "closest_oracle", "args": ["--closest"], "cli": "closest-features",
                 "ref": None, "desc": "closest-features --closest query.bed ref.bed (configs[4], "
                                      "10M x 1B)"},
 }
@@ -189,9 +165,130 @@ def run_op(eng, name, s):
         return eng.op("-i", s, [0, 1])
     if name == "element-of":
         return eng.op("-e", s, [0, 1], "1")
-    if name == "bedmap":
+    if name.startswith("bedmap"):
         return eng.map_op(s, ["count", "mean"], 0, 1)
     return eng.closest_op(s, 0, 1, shortest=True)
+
+
+# ----------------------------------------------------------------------------- process launch
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N rank processes of this script (before any GPU
+    call in this process) and exit with the first failing child's status."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    sys.exit(rc)
+
+
+# ----------------------------------------------------------------------------- baselines
+def write_inputs(L, W, td):
+    """the full inputs as files (page cache) for the CLI and the CPU fan-out"""
+    paths, rows = [], 0
+    for i, (seed, mode) in enumerate(W["gen"]):
+        p, nb, r = gen(L, W["rows"][i], seed, ~0 & ((1 << 64) - 1), mode)
+        path = os.path.join(td, f"in{i}.bed")
+        with open(path, "wb") as f:
+            f.write(host_bytes(p, nb))
+        L.bedgen_free(p)
+        paths.append(path)
+        rows += r
+    return paths, rows
+
+
+def e2e_cli(W, paths, rows, td):
+    """drop-in CLI, file -> file (BEDGPU_DEVICES unset: one GPU), best of two runs"""
+    exe = os.path.join(ROOT, "bedops_amd", "bin", W["cli"])
+    out = os.path.join(td, "cli_out.bed")
+    args = W["args"] if W["cli"] != "closest-features" else ["--closest"]
+    env = {k: v for k, v in os.environ.items() if k != "BEDGPU_DEVICES"}
+    best = None
+    for _ in range(2):
+        with open(out, "wb") as fo:
+            t0 = time.perf_counter()
+            subprocess.run([exe, *args, *paths], stdout=fo, check=True, env=env)
+            dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    h = hashlib.sha256()
+    with open(out, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 26), b""):
+            h.update(chunk)
+    nbytes = os.path.getsize(out)
+    os.unlink(out)
+    return {"value": rows / best, "unit": "intervals/s", "seconds": round(best, 3),
+            "command": f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> > out",
+            "output_sha16": h.hexdigest()[:16], "output_bytes": nbytes}
+
+
+def cpu_fanout(L, W, td, workers):
+    """The oracle (test infrastructure: plain-C restatement of the reference; the reference
+    is not buildable in this image) on the full inputs, one process per
+    chromosome, `workers` at a time (the reference's documented `--chrom` fan-out). Each
+    chromosome's inputs are written as their own files first (untimed: what the reference's
+    --chrom seek reads); the timed region runs the processes and concatenates their outputs
+    in strcmp chromosome order, file -> file."""
+    exe = os.path.join(ROOT, "oracle", "build", W["oracle"])
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "oracle"], cwd=ROOT, check=True)
+    cs = contigs(L)
+    jobs, rows = [], 0
+    for c, (name, ln) in enumerate(cs):
+        files = []
+        for i, (seed, mode) in enumerate(W["gen"]):
+            p, nb, r = gen(L, W["rows"][i], seed, 1 << c, mode)
+            path = os.path.join(td, f"c{c}_in{i}.bed")
+            with open(path, "wb") as f:
+                f.write(host_bytes(p, nb))
+            L.bedgen_free(p)
+            files.append(path)
+            rows += r
+        jobs.append((ln, c, files))
+    jobs.sort(key=lambda j: -j[0])  # longest first
+    outs = {c: os.path.join(td, f"c{c}_out.bed") for _, c, _ in jobs}
+    t0 = time.perf_counter()
+    running, pending = [], list(jobs)
+    while pending or running:
+        while pending and len(running) < workers:
+            _, c, files = pending.pop(0)
+            fo = open(outs[c], "wb")
+            running.append((subprocess.Popen([exe, *W["args"], *files], stdout=fo), fo))
+        p, fo = running.pop(0)
+        if p.wait() != 0:
+            raise RuntimeError("oracle failed in the CPU baseline")
+        fo.close()
+    final = os.path.join(td, "cpu_out.bed")
+    with open(final, "wb") as fo:
+        for c in range(len(cs)):
+            with open(outs[c], "rb") as fi:
+                while True:
+                    b = fi.read(1 << 26)
+                    if not b:
+                        break
+                    fo.write(b)
+    dt = time.perf_counter() - t0
+    for _, c, files in jobs:
+        for f in files + [outs[c]]:
+            os.unlink(f)
+    os.unlink(final)
+    return {"value": rows / dt, "unit": "intervals/s", "cores": workers, "kind": "port",
+            "sample": f"full inputs ({rows} rows): {W['oracle']} {' '.join(W['args'])} per "
+                      f"chromosome ({len(cs)} contigs, {workers} processes at a time), outputs "
+                      f"concatenated in strcmp order, file->file, {dt:.2f} s"}
 
 
 # ----------------------------------------------------------------------------- main
@@ -201,10 +298,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="intersect")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: N x the workload's rows per file (default: strong)")
     ap.add_argument("--scale", type=float, default=1.0,
-                    help="rows per input per GPU = scale x the workload's size (tests/smoke)")
+                    help="rows per input = scale x the workload's size (tests/smoke)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=16,
+                    help="host processes of the CPU fan-out (capped at os.cpu_count())")
     ap.add_argument("--load-only", action="store_true",
                     help="time the loader stage alone (text in HBM -> keyed columns)")
     ap.add_argument("--profile-all", action="store_true",
@@ -212,31 +314,48 @@ def main():
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        spawn_ranks(args.gpus)  # does not return
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+            f"{world}-GPU run as {args.gpus} GPUs")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    from bedops_amd.engine import Group, group_uid
+    from bedops_amd.shard import assign, member_spans, strcmp_order
+
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        # a first collective over every rank initialises the RCCL communicator, so the
-        # later batched point-to-point transfers may involve only a subset of the ranks
-        dist.barrier(device_ids=[local])
+        # host-side coordination only (uid, barriers, the max over ranks); the data path's
+        # exchange is RCCL inside libbedgpu (bg_group_gather)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        uidl = [group_uid() if rank == 0 else None]
+        dist.broadcast_object_list(uidl, src=0)
+        uid = uidl[0]
+    else:
+        uid = bytes(128)
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    from bedops_amd import Engine
+    grp = Group(device=local, uid=uid, nranks=world, rank=rank)
+    eng = grp.engines[0]
 
     L = bedgen_lib()
-    owner, _ = contig_shards(L, world)
-    mask = sum(1 << c for c, r in owner.items() if r == rank)
-    per_gpu = [int(r * args.scale) for r in W["rows"]]
+    cs = contigs(L)
+    owner, _ = assign({nm: ln for nm, ln in cs}, world)  # rows per contig ∝ its length
+    gnames = strcmp_order([nm for nm, _ in cs])
+    mask = sum(1 << c for c, (nm, _) in enumerate(cs) if owner[nm] == rank)
+    per_file = [int(r * args.scale) * (world if args.weak else 1) for r in W["rows"]]
     t0 = time.perf_counter()
     bufs, texts, rows = [], [], []
-    for (seed, mode), n in zip(W["gen"], per_gpu):
-        p, nb, r = gen(L, n * world, seed, mask, mode)
-        bufs.append(to_device(torch, L, p, nb, dev))
+    for (seed, mode), n in zip(W["gen"], per_file):
+        p, nb, r = gen(L, n, seed, mask, mode)
+        bufs.append(to_device(torch, p, nb, dev))
         L.bedgen_free(p)
         texts.append(nb)
         rows.append(r)
@@ -244,8 +363,6 @@ def main():
         f"{time.perf_counter() - t0:.1f}s")
     torch.cuda.synchronize(dev)
 
-    eng = Engine(local)
-    ncontigs = L.bedgen_ncontigs()
     state = {}
     inputs = [((t.data_ptr(), nb), k) for t, nb, k in zip(bufs, texts, W["kinds"])]
 
@@ -259,39 +376,33 @@ def main():
         nbytes = r.format()
         state["out_rows"] = r.rows()
         state["out_bytes"] = nbytes
-        if world > 1:
-            gather_to_rank0(r, s, nbytes)
-        if "keep" in state:
+        if world > 1:  # the path's one exchange: per-chromosome text -> rank 0 (RCCL)
+            names = s.chroms()
+            dptr, _ = r.device_text()
+            offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
+            out, n = grp.gather(len(gnames), [(dptr, offs, lens)])
+            if rank == 0:
+                if "keep" in state:
+                    state["text"] = read_device(out, n)
+                    del state["keep"]
+                eng.device_free(out)
+        elif "keep" in state:
             state["text"] = r.text()
             del state["keep"]
         r.free()
         s.free()
 
-    contig_names = [L.bedgen_contig_name(c).decode() for c in range(ncontigs)]
-    chrom_owner = {contig_names[c]: owner[c] for c in range(ncontigs)}
+    def read_device(dptr, n):
+        with tempfile.TemporaryFile() as fo:
+            eng.write_device(dptr, n, fo.fileno())
+            fo.seek(0)
+            return fo.read()
 
-    size_pg = dist.new_group(backend="gloo") if world > 1 else None
-
-    def gather_to_rank0(r, s, nbytes):
-        # the path's one exchange: per-chromosome text -> rank 0 over RCCL, in strcmp order.
-        # Pipelined: this batch's transfers are posted and run on RCCL's stream while the
-        # next batch is computed; the previous batch's are waited for here.
-        from bedops_amd.shard import gather_text_async
-        names = s.chroms()
-        sp = r.chrom_spans(len(names))
-        spans = {nm: (sp[g], sp[g + 1]) for g, nm in enumerate(names) if sp[g + 1] > sp[g]}
-        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-        r.copy_to_device(buf.data_ptr(), max(nbytes, 1))
-        pend = gather_text_async(dist, buf, spans, contig_names, chrom_owner, rank, world, size_pg)
-        drain()
-        state["pending"] = pend
-
-    def drain():
-        p = state.pop("pending", None)
-        if p is not None:
-            out = p.wait()
-            if rank == 0:
-                state["gathered"] = int(out.numel())
+    def barrier():
+        eng.sync()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
 
     # warmup; the first warmup step profiles every kernel to find the dominant one
     eng.prof_enable("*")
@@ -310,34 +421,44 @@ def main():
             m.free()
         s.free()
     eng.prof_enable("*" if args.profile_all else dominant)
-    drain()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    barrier()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-    drain()  # the last batch's transfers are inside the timed region
     eng.sync()
     torch.cuda.synchronize(dev)
     t_end = time.perf_counter()
     if dist:
         dist.barrier()
     elapsed = t_end - t_start
+    total_rows = sum(rows)
     if dist:
-        et = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        et = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(et, op=dist.ReduceOp.MAX)
         elapsed = float(et.item())
-        rows_all = torch.tensor([sum(rows)], dtype=torch.int64, device=dev)
-        dist.all_reduce(rows_all)
-        total_rows = int(rows_all.item())
-    else:
-        total_rows = sum(rows)
+        rt = torch.tensor([sum(rows)], dtype=torch.int64)
+        dist.all_reduce(rt)
+        total_rows = int(rt.item())
     prof = eng.prof_read()
 
+    # parity after timing: the reassembled output against the reference hash, at every N
+    verify = None
+    if not args.no_verify and not args.load_only and args.scale == 1.0 and not args.weak:
+        if rank == 0:
+            state["keep"] = True
+        step()
+        if rank == 0:
+            txt = state.pop("text")
+            verify = {"rows": txt.count(b"\n"), "bytes": len(txt),
+                      "sha16": hashlib.sha256(txt).hexdigest()[:16]}
+            if W["ref"]:
+                verify["matches_reference"] = all(verify[k] == W["ref"][k] for k in W["ref"])
+            del txt
+    if dist:
+        dist.barrier()
+
     if rank != 0:
-        eng.close()
+        grp.close()
         dist.destroy_process_group()
         return
 
@@ -345,38 +466,36 @@ def main():
     sizes = {"texts": texts, "rows": rows, "kinds": W["kinds"], "out": state["out_rows"],
              "out_bytes": state["out_bytes"], "comps": comps}
     roof = None
-    pick = dominant
-    per_launch = kernel_bytes(pick, sizes)
-    if per_launch is not None and pick in prof:
-        calls, ms = prof[pick]  # launches inside the timed region only
+    per_launch = kernel_bytes(dominant, sizes)
+    if per_launch is not None and dominant in prof:
+        calls, ms = prof[dominant]  # launches inside the timed region only
         avg_s = ms / 1e3 / max(calls, 1)
         gbs = per_launch / avg_s / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and args.workload == "intersect":
+        if os.path.exists(pmc) and args.workload == "intersect" and world == 1:
             try:
-                traffic = json.load(open(pmc)).get(PMC_NAME.get(pick, pick), {}).get("bytes")
+                traffic = json.load(open(pmc)).get(PMC_NAME.get(dominant, dominant), {}).get("bytes")
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": pick,
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dominant,
                 "avg_ms": round(avg_s * 1e3, 4), "launches": calls,
-                "bytes_per_launch": int(per_launch)}
+                "bytes_per_launch": int(per_launch), "rank": 0}
 
-    verify = None
-    if world == 1 and not args.no_verify and not args.load_only and args.scale == 1.0:
-        state["keep"] = True
-        step()
-        txt = state.pop("text")
-        verify = {"rows": txt.count(b"\n"), "bytes": len(txt),
-                  "sha16": hashlib.sha256(txt).hexdigest()[:16]}
-        if W["ref"]:
-            verify["matches_reference"] = all(verify[k] == W["ref"][k] for k in W["ref"])
-        del txt
-
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline and rank == 0:
-        cpu = cpu_baseline(L, W)
+    e2e = cpu = None
+    if world == 1 and args.scale == 1.0 and not args.load_only and (
+            not args.no_e2e or not args.no_cpu_baseline):
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as td:
+            if not args.no_e2e:
+                paths, nrows = write_inputs(L, W, td)
+                e2e = e2e_cli(W, paths, nrows, td)
+                if W["ref"]:
+                    e2e["matches_reference"] = e2e["output_sha16"] == W["ref"]["sha16"]
+                for p in paths:
+                    os.unlink(p)
+            if not args.no_cpu_baseline:
+                cpu = cpu_fanout(L, W, td, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
 
     ms_per_step = elapsed / args.steps * 1e3
     value = total_rows * args.steps / elapsed
@@ -385,17 +504,22 @@ def main():
         f"intervals/sec, {W['desc'].split(' (')[0]}",
         "value": round(value, 1), "unit": "intervals/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "higher_is_better": True, "scaling": "weak" if args.weak else "strong",
+        "vs_baseline": None, "dtype": "int64",
         "data": "synthetic (SURVEY.md App. D generator, seeds "
                 f"{'/'.join(str(g[0]) for g in W['gen'])}; BED text resident in HBM)",
         "config": {"workload": W["desc"] + (" (loader only)" if args.load_only else ""),
-                   "rows_per_input": [r * world for r in per_gpu],
-                   "rows_per_gpu_per_input": per_gpu,
+                   "rows_per_input": [r * (world if args.weak else 1) for r in
+                                      [int(x * args.scale) for x in W["rows"]]],
                    "parallelism": "single GPU" if world == 1 else
-                   f"{world} GPUs, chromosome shards (LPT) + RCCL gather to rank 0",
+                   f"{world} GPUs (one process each), chromosome shards (LPT) + RCCL gather "
+                   "to rank 0 inside every step",
                    "output_rows": state["out_rows"] if world == 1 else None},
         "roofline": roof, "cpu_baseline": cpu,
-        "gpu_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+        "e2e_intervals_per_s": round(e2e["value"], 1) if e2e else None,
+        "e2e": e2e,
+        "gpu_vs_cpu": round(e2e["value"] / cpu["value"], 2) if (cpu and e2e) else None,
+        "gpu_vs_cpu_scope": "file->file CLI vs file->file CPU fan-out" if (cpu and e2e) else None,
         "parity": verify,
         "kernels_first_step_ms": {k: round(v[1], 4) for k, v in
                                   sorted(first.items(), key=lambda kv: -kv[1][1])},
@@ -404,7 +528,7 @@ def main():
         line["kernels_ms_per_step"] = {k: round(v[1] / args.steps, 4) for k, v in
                                        sorted(prof.items(), key=lambda kv: -kv[1][1])}
     print(json.dumps(line), flush=True)
-    eng.close()
+    grp.close()
     if dist:
         dist.destroy_process_group()
 
