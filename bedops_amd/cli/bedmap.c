@@ -238,28 +238,30 @@ int main(int argc, char** argv) {
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   text_buf_t tr = {0}, tm = {0};
-  if (read_text(argv[a], &tr)) arg_error("Unable to read the reference file");
+  bg_input in[2];
+  memset(in, 0, sizeof(in));
+  if (read_input(ctx, argv[a], check || ec, &tr, &in[0])) arg_error("Unable to read the reference file");
   /* --ec: the reference file is B3Rest, the map file B3Rest/B4Rest/B5Rest by the
    * operations' MapFields (Input.hpp:401-418, Bedmap.cpp:601-655) */
   const int mapfields = need5 ? 5 : (need4 ? 4 : 3);
   if (check) ec_check(PROG, ctx, argv[a], &tr, nf == 1 ? mapfields : 3, 1);
-  if (ec) apply_ec_header(&tr);
-  bg_input in[2];
-  in[0].data = tr.data;
-  in[0].nbytes = tr.n;
-  in[0].on_device = 0;
+  if (ec) {
+    apply_ec_header(&tr);
+    in[0].data = tr.data;
+    in[0].nbytes = tr.n;
+  }
   in[0].kind = need_rest ? BG_BED3_REST : BG_BED3;
   if (nf == 2) {
-    if (read_text(argv[a + 1], &tm)) arg_error("Unable to read the map file");
+    if (read_input(ctx, argv[a + 1], check || ec, &tm, &in[1])) arg_error("Unable to read the map file");
     if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1);
-    if (ec) apply_ec_header(&tm);
-    in[1].data = tm.data;
-    in[1].nbytes = tm.n;
+    if (ec) {
+      apply_ec_header(&tm);
+      in[1].data = tm.data;
+      in[1].nbytes = tm.n;
+    }
   } else { /* single-file mode: the reference file is also the map file */
-    in[1].data = tr.data;
-    in[1].nbytes = tr.n;
+    in[1] = in[0];
   }
-  in[1].on_device = 0;
   in[1].kind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
@@ -270,8 +272,11 @@ int main(int argc, char** argv) {
   if ((rc = bg_map(ctx, set, 0, 1, &o, &res))) die_ctx(PROG, ctx, rc);
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
   maybe_stats(ctx);
+  fast_exit();
   bg_result_free(res);
   bg_set_free(set);
+  free_input(ctx, &tr);
+  free_input(ctx, &tm);
   bg_close(ctx);
   return EXIT_SUCCESS;
 }

@@ -362,29 +362,38 @@ int main(int argc, char** argv) {
     op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
     if (shard_run(PROG, nf, in, tx, run_op, &oa) == 0) return EXIT_SUCCESS;
   }
+  cli_mark("start");
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
+  cli_mark("open");
   for (int i = 0; i < nf; ++i) {
-    if (!tx[i].data && read_text(argv[a + i], &tx[i])) {
+    if (tx[i].data) { /* read for the sharded attempt */
+      in[i].data = tx[i].data;
+      in[i].nbytes = tx[i].n;
+      in[i].on_device = 0;
+    } else if (read_input(ctx, argv[a + i], check || ec, &tx[i], &in[i])) {
       char b[1024];
       snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
       die_msg(PROG, b);
     }
     const int keep_rest = (mode == 'u' || ((mode == 'e' || mode == 'n') && i == 0));
     if (check) ec_check(PROG, ctx, argv[a + i], &tx[i], 3, keep_rest);
-    if (ec) apply_ec_header(&tx[i]);
-    in[i].data = tx[i].data;
-    in[i].nbytes = tx[i].n;
-    in[i].on_device = 0;
+    if (ec) {
+      apply_ec_header(&tx[i]);
+      in[i].data = tx[i].data;
+      in[i].nbytes = tx[i].n;
+    }
     /* --everything keeps all columns of every file, element-of those of the reference
      * file (Bedops.cpp:402-421); the other inputs of the set operations are read only as
      * merged sets (getNextFileMergedCoords, Bedops.cpp:792-814), so they are parsed
      * straight to their components unless --chrom/--range need the rows */
     in[i].kind = input_kind(mode, i, chrom, has_range);
   }
+  cli_mark("read");
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);
+  cli_mark("load");
   for (int i = 0; i < nf; ++i) free_text(&tx[i]);
   if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
   /* --range pads every file but the element-of reference (Bedops.cpp:230-236) */
@@ -394,10 +403,14 @@ int main(int argc, char** argv) {
   bg_result* res = NULL;
   op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
   if ((rc = run_op(&oa, ctx, set, &res))) die_ctx(PROG, ctx, rc);
+  cli_mark("operation");
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
+  cli_mark("write");
   maybe_stats(ctx);
+  fast_exit();
   bg_result_free(res);
   bg_set_free(set);
+  for (int i = 0; i < nf; ++i) free_input(ctx, &tx[i]);
   bg_close(ctx);
   free(in);
   free(tx);

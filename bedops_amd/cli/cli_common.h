@@ -26,6 +26,7 @@ typedef struct {
   char* data;     /* pinned host buffer */
   uint64_t n;     /* bytes of BED text */
   int pinned;
+  void* ddata;    /* the text on the device instead (read_input), freed by free_input */
 } text_buf_t;
 
 static void die_msg(const char* prog, const char* msg) {
@@ -78,10 +79,46 @@ static int read_text(const char* path, text_buf_t* out) {
   return 0;
 }
 
+/* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
+ * go straight to device memory (bg_read_file_device: parallel page-cache reads through a
+ * small pinned ring, no whole-file pinning); stdin, pipes and checked inputs are read
+ * into host memory. Returns 0 or -1 (unreadable). */
+static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, text_buf_t* t, bg_input* in) {
+  struct stat st;
+  memset(t, 0, sizeof(*t));
+  if (!host_needed && strcmp(path, "-") != 0 && stat(path, &st) == 0 && S_ISREG(st.st_mode)) {
+    void* d = NULL;
+    uint64_t n = 0;
+    const int rc = bg_read_file_device(ctx, path, &d, &n);
+    if (rc == 0) {
+      t->ddata = d;
+      t->n = n;
+      in->data = d;
+      in->nbytes = n;
+      in->on_device = 1;
+      return 0;
+    }
+    const char* s = getenv("BEDGPU_STATS");
+    if (s && *s && strcmp(s, "0") != 0)
+      fprintf(stderr, "bedgpu: device read of %s failed (%d: %s); reading into host memory\n", path, rc,
+              bg_last_error(ctx));
+  }
+  if (read_text(path, t)) return -1;
+  in->data = t->data;
+  in->nbytes = t->n;
+  in->on_device = 0;
+  return 0;
+}
+
 static void free_text(text_buf_t* t) {
   if (!t->data) return;
   if (t->pinned) bg_host_free(t->data); else free(t->data);
   t->data = NULL;
+}
+static inline void free_input(bg_ctx* ctx, text_buf_t* t) {
+  free_text(t);
+  if (t->ddata) bg_device_free(ctx, t->ddata);
+  t->ddata = NULL;
 }
 
 /* --header / --ec: drop leading UCSC/VCF/SAM header lines ("browser", "track", '#',
@@ -140,11 +177,37 @@ static inline int env_no_set(void) {
   return s && strcmp(s, "0") == 0;
 }
 
+#include <time.h>
+/* BEDGPU_STATS=1: host wall-clock marks on stderr (never stdout) */
+static inline double cli_now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static inline void cli_mark(const char* what) {
+  static double t0 = 0, last = 0;
+  const char* s = getenv("BEDGPU_STATS");
+  if (!s || !*s || strcmp(s, "0") == 0) return;
+  const double t = cli_now();
+  if (t0 == 0) t0 = last = t;
+  fprintf(stderr, "bedgpu host  %-12s %10.3f ms (+%.3f)\n", what, 1e3 * (t - t0), 1e3 * (t - last));
+  last = t;
+}
+
 static void maybe_stats(bg_ctx* ctx) {
   const char* s = getenv("BEDGPU_STATS");
   if (!s || !*s || strcmp(s, "0") == 0) return;
   char buf[4096];
   if (bg_stats(ctx, buf, sizeof(buf)) == 0) fputs(buf, stderr);
+}
+
+/* after the output is written: leave without tearing down the device state (freeing
+ * every HBM block, the pinned ring and the HIP runtime costs ~0.3 s; the kernel driver
+ * reclaims a process's GPU resources at exit). Output went through write(2) only. */
+static inline void fast_exit(void) {
+  fflush(stdout);
+  fflush(stderr);
+  _exit(EXIT_SUCCESS);
 }
 
 #endif

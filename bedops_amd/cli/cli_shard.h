@@ -294,6 +294,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const text
     if (rc) die_ctx(prog, c0, rc);
     if ((rc = bg_write_device(c0, out, n, 1))) die_ctx(prog, c0, rc);
     maybe_stats(c0);
+    fast_exit();
     bg_device_free(c0, out);
     free(texts);
     free(offs);

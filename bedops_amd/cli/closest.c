@@ -102,12 +102,13 @@ int main(int argc, char** argv) {
   text_buf_t t[2] = {{0}, {0}};
   bg_input in[2];
   for (int k = 0; k < 2; ++k) {
-    if (read_text(argv[a + k], &t[k])) arg_error("Unable to read an input file");
+    if (read_input(ctx, argv[a + k], check || ec, &t[k], &in[k])) arg_error("Unable to read an input file");
     if (check) ec_check(PROG, ctx, argv[a + k], &t[k], 3, 1);
-    if (ec) apply_ec_header(&t[k]);
-    in[k].data = t[k].data;
-    in[k].nbytes = t[k].n;
-    in[k].on_device = 0;
+    if (ec) {
+      apply_ec_header(&t[k]);
+      in[k].data = t[k].data;
+      in[k].nbytes = t[k].n;
+    }
     in[k].kind = BG_BED3_REST;
   }
   bg_set* set = NULL;
@@ -119,8 +120,11 @@ int main(int argc, char** argv) {
   if ((rc = bg_closest(ctx, set, 0, 1, &o, &res))) die_ctx(PROG, ctx, rc);
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
   maybe_stats(ctx);
+  fast_exit();
   bg_result_free(res);
   bg_set_free(set);
+  free_input(ctx, &t[0]);
+  free_input(ctx, &t[1]);
   bg_close(ctx);
   return EXIT_SUCCESS;
 }

@@ -5,7 +5,12 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <unordered_map>
 
 #include "bg_internal.h"
@@ -176,6 +181,9 @@ extern "C" void bg_close(bg_ctx* c) {
   hipFree(c->dstat);
   hipHostFree(c->hstat);
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
+  for (auto s : c->rd_stream) { hipStreamSynchronize(s); hipStreamDestroy(s); }
+  for (auto e : c->rd_ev) hipEventDestroy(e);
+  for (auto p : c->rd_slot) hipHostFree(p);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -374,6 +382,89 @@ extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts,
   }
   *out = d;
   *total = t;
+  return 0;
+}
+
+// A regular file straight into a new device buffer: RD_THREADS readers pread interleaved
+// 16 MiB chunks into their own two pinned slots and copy each to HBM on their own stream
+// while reading the next, so the page-cache reads run in parallel and overlap the H2D
+// copies; only 2 x RD_THREADS x 16 MiB of host memory is ever pinned (pinning the whole
+// file costs more than reading it). The context's stream waits for every copy.
+#define RD_THREADS 8
+#define RD_CHUNK (16ull << 20)
+extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint64_t* nbytes) {
+  if (!c || !path || !out || !nbytes) return BG_E_ARG;
+  *out = nullptr;
+  *nbytes = 0;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return bg_fail(c, BG_E_IO, std::string("cannot open ") + path);
+  struct stat st;
+  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+    close(fd);
+    return bg_fail(c, BG_E_ARG, std::string(path) + " is not a regular file");
+  }
+  const uint64_t n = (uint64_t)st.st_size;
+  bg_bind(c);
+  char* d = (char*)bg_alloc(c, n + 64);
+  if (!d) {
+    close(fd);
+    return BG_E_NOMEM;
+  }
+  if (c->rd_slot.empty()) {
+    for (int k = 0; k < 2 * RD_THREADS; ++k) {
+      char* p = nullptr;
+      hipEvent_t e = nullptr;
+      BG_HIP(c, hipHostMalloc((void**)&p, RD_CHUNK, hipHostMallocDefault));
+      BG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->rd_slot.push_back(p);
+      c->rd_ev.push_back(e);
+    }
+    for (int t = 0; t < RD_THREADS; ++t) {
+      hipStream_t s = nullptr;
+      BG_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      c->rd_stream.push_back(s);
+    }
+  }
+  const uint64_t nch = (n + RD_CHUNK - 1) / RD_CHUNK;
+  std::atomic<int> bad{0};
+  auto reader = [&](int t) {
+    if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
+    uint64_t j = 0;
+    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += RD_THREADS, ++j) {
+      const int slot = 2 * t + (int)(j & 1);
+      if (hipEventSynchronize(c->rd_ev[slot]) != hipSuccess) { bad = 1; return; }
+      const uint64_t off = k * RD_CHUNK, len = std::min<uint64_t>(RD_CHUNK, n - off);
+      uint64_t got = 0;
+      while (got < len) {
+        const ssize_t r = pread(fd, c->rd_slot[slot] + got, len - got, (off_t)(off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) { bad = 2; return; }
+        got += (uint64_t)r;
+      }
+      if (hipMemcpyAsync(d + off, c->rd_slot[slot], len, hipMemcpyHostToDevice, c->rd_stream[t]) != hipSuccess ||
+          hipEventRecord(c->rd_ev[slot], c->rd_stream[t]) != hipSuccess) {
+        bad = 1;
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  const int nt = (int)std::min<uint64_t>(RD_THREADS, nch);
+  for (int t = 0; t < nt; ++t) th.emplace_back(reader, t);
+  for (auto& x : th) x.join();
+  close(fd);
+  for (int t = 0; t < nt; ++t) {  // the context's stream (the loader) waits for the copies
+    BG_HIP(c, hipEventRecord(c->rd_ev[2 * t], c->rd_stream[t]));
+    BG_HIP(c, hipStreamWaitEvent(c->stream, c->rd_ev[2 * t], 0));
+  }
+  if (bad) {
+    hipStreamSynchronize(c->stream);
+    bg_release(c, d);
+    return bad == 2 ? bg_fail(c, BG_E_IO, std::string("read failed: ") + path)
+                    : bg_fail(c, BG_E_HIP, std::string("copy failed: ") + path);
+  }
+  *out = d;
+  *nbytes = n;
   return 0;
 }
 

@@ -215,6 +215,10 @@ void bg_result_free(bg_result* res);
 
 /* stream n bytes of device memory (on ctx's device) to fd: double-buffered D2H + write */
 int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
+/* read a regular file into a new device buffer of ctx's device (parallel page-cache reads
+ * through a small pinned ring, overlapped with the H2D copies; ordered before later work on
+ * ctx's stream); load it with bg_input.on_device = 1, free with bg_device_free */
+int bg_read_file_device(bg_ctx* ctx, const char* path, void** dptr, uint64_t* nbytes);
 /* make ctx's device current on the calling thread (a host thread per device in a group) */
 int bg_bind(bg_ctx* ctx);
 
