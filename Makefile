@@ -12,7 +12,7 @@ LIB := bedops_amd/lib/libbedgpu.so
 BIN := bedops_amd/bin
 HIPSRCS := $(wildcard $(SRC)/*.hip)
 HIPOBJS := $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(HIPSRCS))
-CLIS := $(BIN)/bedops $(BIN)/bedmap $(BIN)/closest-features
+CLIS := $(BIN)/bedops $(BIN)/bedmap $(BIN)/closest-features $(BIN)/sort-bed
 
 all: lib cli tools oracle
 
@@ -29,6 +29,10 @@ $(LIB): $(HIPOBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h include/bedgpu.h $(LIB)
+	@mkdir -p $(BIN)
+	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
+
+$(BIN)/sort-bed: bedops_amd/cli/sortbed.c bedops_amd/cli/cli_common.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
 

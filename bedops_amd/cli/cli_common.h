@@ -124,7 +124,7 @@ static inline void free_input(bg_ctx* ctx, text_buf_t* t) {
 /* --header / --ec: drop leading UCSC/VCF/SAM header lines ("browser", "track", '#',
  * '@'; BedCheckIterator.hpp:315-350) and keep an unterminated final line (the error
  * checking reader keeps it, the plain reader drops it). */
-static void apply_ec_header(text_buf_t* t) {
+static inline void apply_ec_header(text_buf_t* t) {
   uint64_t p = 0;
   for (;;) {
     uint64_t e = p;
@@ -148,7 +148,7 @@ static void apply_ec_header(text_buf_t* t) {
 /* --ec (Bed::bed_check_iterator, BedCheckIterator.hpp): every line of `t` checked on the
  * GPU before anything else reads it; the first failing line ends the program with the
  * reference's "in <file>\n<message>\nSee row: <n>" */
-static void ec_check(const char* prog, bg_ctx* ctx, const char* fn, const text_buf_t* t, int nfields,
+static inline void ec_check(const char* prog, bg_ctx* ctx, const char* fn, const text_buf_t* t, int nfields,
                      int has_rest) {
   bg_input in;
   in.data = t->data;

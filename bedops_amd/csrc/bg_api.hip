@@ -510,5 +510,6 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->right);
   bg_release(c, r->text);
   bg_release(c, r->toff);
+  if (r->own_set) bg_set_free(r->set);
   delete r;
 }

@@ -28,6 +28,7 @@ struct FmtArgs {
   const int64_t* e;
   const uint64_t* rows;
   const uint32_t* rlen;  // RES_MULTI: rows[k] = remainder address, rlen[k] its length
+  int rest_tab;          // RES_MULTI: '\t' before a non-empty remainder (sort-bed)
   const char* text;
   const uint64_t* rest_off;
   const uint32_t* rest_len;
@@ -787,6 +788,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
   } else if (KIND == RES_MULTI) {
     const uint32_t rl = A.rlen[k];
     const char* rp = (const char*)A.rows[k];
+    if (A.rest_tab && rl) o.put('\t');
     for (uint32_t q = 0; q < rl; ++q) o.put(rp[q]);
   }
   o.put('\n');
@@ -974,6 +976,7 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     A.e = r->e;
     A.rows = r->rows;
     A.rlen = r->rlen;
+    A.rest_tab = r->rest_tab ? 1 : 0;
   } else if (r->kind == RES_ROWS) {
     bg_table* T = s->t[r->tab];
     A.s = T->ks;

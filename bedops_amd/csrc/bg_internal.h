@@ -129,6 +129,8 @@ struct bg_result {
   // remainder, rlen = remainder length
   uint64_t* rows = nullptr;
   uint32_t* rlen = nullptr;
+  bool rest_tab = false;  // RES_MULTI: a non-empty remainder is printed after a tab (sort-bed)
+  bool own_set = false;   // the result owns its set (bg_sortbed)
   int tab = -1;
   // RES_MAP: per reference row columns
   int32_t* cnt = nullptr;    // rows in S(r) (Count, Indicator, --skip-unmapped)

@@ -251,6 +251,32 @@ void bg_device_free(bg_ctx* ctx, void* dptr);
 int bg_device_gather_host(bg_ctx* ctx, int n, const void* const* parts, const uint64_t* lens,
                           void** out, uint64_t* total);
 
+/* ---- sort-bed (applications/bed/sort-bed/src: Sort.cpp:41-234, SortDetails.cpp:536-1140) ----
+ * every line of the inputs checked with sort-bed's own grammar, sorted by chromosome
+ * (strcmp), start, end and the rest of the line (strcmp, none first), printed
+ * "%s\t%ld\t%ld[\t<rest>]\n" by the bg_result_* calls. On a bad line the call fails with
+ * BG_E_PARSE and *err names it (input index, 1-based line, BG_SB_* code). */
+typedef struct bg_sortbed_error {
+  int input;
+  uint64_t line;
+  int code;
+} bg_sortbed_error;
+#define BG_SB_LEADING_WS 1
+#define BG_SB_NO_TAB 2
+#define BG_SB_CHROM_LONG 3
+#define BG_SB_NO_START_SEP 4
+#define BG_SB_START_LONG 5
+#define BG_SB_START_EMPTY 6
+#define BG_SB_START_NONNUM 7
+#define BG_SB_NO_EOL 8
+#define BG_SB_END_LONG 9
+#define BG_SB_END_EMPTY 10
+#define BG_SB_END_NONNUM 11
+#define BG_SB_END_LE_START 12
+#define BG_SB_ID_LONG 13
+#define BG_SB_ROW_LONG 14
+int bg_sortbed(bg_ctx* ctx, int n, const bg_input* inputs, bg_result** out, bg_sortbed_error* err);
+
 /* per-stage device timings of the last call sequence (ms), for BEDGPU_STATS */
 int bg_stats(const bg_ctx* ctx, char* buf, uint64_t cap);
 

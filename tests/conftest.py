@@ -24,7 +24,8 @@ def oracle_bin():
     _make("oracle")
     return {"bedops": os.path.join(ROOT, "oracle", "build", "bedops_oracle"),
             "bedmap": os.path.join(ROOT, "oracle", "build", "bedmap_oracle"),
-            "closest": os.path.join(ROOT, "oracle", "build", "closest_oracle")}
+            "closest": os.path.join(ROOT, "oracle", "build", "closest_oracle"),
+            "sortbed": os.path.join(ROOT, "oracle", "build", "sortbed_oracle")}
 
 
 @pytest.fixture(scope="session")
@@ -33,7 +34,8 @@ def gpu_bin():
     _make("lib", "cli")
     return {"bedops": os.path.join(ROOT, "bedops_amd", "bin", "bedops"),
             "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap"),
-            "closest": os.path.join(ROOT, "bedops_amd", "bin", "closest-features")}
+            "closest": os.path.join(ROOT, "bedops_amd", "bin", "closest-features"),
+            "sortbed": os.path.join(ROOT, "bedops_amd", "bin", "sort-bed")}
 
 
 @pytest.fixture(scope="session")

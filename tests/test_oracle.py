@@ -154,3 +154,28 @@ def test_oracle_bedmap_drift_fixture(oracle_bin, tmp_path):
         got = subprocess.run([oracle_bin["bedmap"], *c["args"], str(pr), str(pm)],
                              stdout=subprocess.PIPE, check=True).stdout.decode()
         assert got == c["expect"], c["name"]
+
+
+def test_sortbed_oracle_matches_python_model(oracle_bin, tmp_path):
+    """oracle/sortbed_oracle.c against a few-line Python statement of sort-bed's order
+    (strcmp chromosome, start, end, rest; no rest first) and printBed's format"""
+    import random
+    rng = random.Random(4)
+    for trial in range(30):
+        rows, text = [], []
+        for _ in range(rng.choice([0, 3, 200])):
+            c = rng.choice(["chr1", "chr10", "chr2", "chrX", "1", "2"])
+            s = rng.randrange(1000)
+            e = s + rng.randint(1, 30)
+            rest = rng.choice([None, "a", "b\t1", "a b", "id3"])
+            sep = rng.choice(["\t", " "])
+            text.append(f"{c}{sep}{s}{sep}{e}" + ("" if rest is None else f"{sep}{rest}"))
+            rows.append((c.encode(), s, e, rest))
+        p = tmp_path / f"s{trial}.bed"
+        p.write_text("".join(ln + "\n" for ln in text))
+        rows.sort(key=lambda r: (r[0], r[1], r[2], (0, "") if r[3] is None else (1, r[3].encode())))
+        want = "".join(f"{c.decode()}\t{s}\t{e}" + ("" if r is None else f"\t{r}") + "\n"
+                       for c, s, e, r in rows)
+        got = subprocess.run([oracle_bin["sortbed"], str(p)], stdout=subprocess.PIPE,
+                             check=True).stdout.decode()
+        assert got == want, trial
