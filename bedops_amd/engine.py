@@ -46,7 +46,7 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message",
            "bg_write_device", "bg_bind", "bg_group_uid", "bg_group_open", "bg_group_open_rank",
            "bg_group_size", "bg_group_ctx", "bg_group_close", "bg_group_gather", "bg_device_free",
-           "bg_device_gather_host", "bg_read_file_device"]
+           "bg_device_gather_host", "bg_read_file_device", "bg_sortbed"]
 UID_BYTES = 128
 
 
