@@ -504,6 +504,9 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->rrank);
   bg_release(c, r->wlo);
   bg_release(c, r->whi);
+  bg_release(c, (void*)r->lrows.idx);
+  bg_release(c, (void*)r->lrows.ls);
+  bg_release(c, (void*)r->lrows.coff);
   bg_release(c, r->zin);
   bg_release(c, r->zout);
   bg_release(c, r->left);

@@ -54,6 +54,7 @@ struct FmtArgs {
   const double* score2;
   const uint64_t* wlo;
   const uint64_t* whi;
+  LongRows lrows;      // long map rows by length class (bg_map_cands)
   const int64_t* zin;  // zero-length rows: sweep-window membership (bg_map_live)
   const int64_t* zout;
   int crit, mapfields, mdlen;
@@ -521,27 +522,32 @@ __device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m
   return true;
 }
 
+// the sweep's padding of the criterion (RangedDist under --range)
+__device__ __forceinline__ int64_t fmt_pad(const FmtArgs& A) {
+  return A.crit == BG_OVR_RANGE ? A.range : 0;
+}
+
 // --echo-map* of reference row k: the window's rows in genomic order (EchoMapBed's set,
 // EchoMapBedVisitor.hpp:58-63) joined by --multidelim (PrintRangeDelim)
 template <typename Out>
 __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t k, int op) {
   const int64_t s = A.s[k], e = A.e[k];
-  bool first = true;
+  bool first = true, ok = true;
   int64_t rs = 0, re = 0;
-  for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
+  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
     const int64_t ms = A.s2[m], me = A.e2[m];
     if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me))
-      continue;
+      return true;
     if (op == BG_MAP_ECHO_MAP_RANGE) {  // PrintGenomicRange (ProcessBedVisitorRow.hpp:433-456)
       if (first) { rs = ms; re = me; }
       else { rs = min(rs, ms); re = max(re, me); }
       first = false;
-      continue;
+      return true;
     }
     if (!first) for (int d = 0; d < A.mdlen; ++d) o.put(A.mdelim[d]);
     first = false;
     if (op == BG_MAP_ECHO_MAP) {
-      if (!put_map_row(A, o, m)) return false;
+      if (!put_map_row(A, o, m)) { ok = false; return false; }
     } else if (op == BG_MAP_ECHO_MAP_ID) {
       const char* rp = A.text2 + A.rest_off2[m];
       const uint32_t rl = A.rest_len2[m];
@@ -549,7 +555,7 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
       while (i < rl && fmt_isws(rp[i])) ++i;
       for (; i < rl && !fmt_isws(rp[i]); ++i) o.put(rp[i]);
     } else if (op == BG_MAP_ECHO_MAP_SCORE) {
-      if (!put_real(o, A.score2[m], A.prec, A.sci)) return false;
+      if (!put_real(o, A.score2[m], A.prec, A.sci)) { ok = false; return false; }
     } else if (op == BG_MAP_ECHO_MAP_SIZE) {
       const uint64_t len = (uint64_t)(me - ms);
       put_u64(o, len, dec_len_u64(len));
@@ -558,7 +564,9 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
       const uint64_t len = ov > 0 ? (uint64_t)ov : 0;
       put_u64(o, len, dec_len_u64(len));
     }
-  }
+    return true;
+  });
+  if (!ok) return false;
   if (op == BG_MAP_ECHO_MAP_RANGE && !first) put_row(A, o, rs, re, nullptr, 0);
   return true;
 }
@@ -591,15 +599,16 @@ __device__ __forceinline__ void put_unique_ids(const FmtArgs& A, Out& o, uint64_
   for (;;) {
     const char* best = nullptr;
     uint32_t blen = 0;
-    for (uint64_t m = A.wlo[k]; m < A.whi[k]; ++m) {
+    bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
       if (!bg_map_live(A.zin, A.zout, k, m) ||
           !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]))
-        continue;
+        return true;
       uint32_t l;
       const char* id = map_id(A, m, l);
-      if (prev && id_cmp(id, l, prev, plen) <= 0) continue;
+      if (prev && id_cmp(id, l, prev, plen) <= 0) return true;
       if (!best || id_cmp(id, l, best, blen) < 0) { best = id; blen = l; }
-    }
+      return true;
+    });
     if (!best) return;
     if (prev) for (int d = 0; d < A.mdlen; ++d) o.put(A.mdelim[d]);
     for (uint32_t i = 0; i < blen; ++i) o.put(best[i]);
@@ -618,23 +627,26 @@ __device__ __forceinline__ double mad_dev(double x, double med) {
 __device__ __forceinline__ double window_rank(const FmtArgs& A, uint64_t k, uint32_t p,
                                               bool dev = false, double med = 0.0) {
   const int64_t s = A.s[k], e = A.e[k];
-  for (uint64_t i = A.wlo[k]; i < A.whi[k]; ++i) {
+  double out = 0.0;  // (every p < window size is found)
+  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t i) {
     if (!bg_map_live(A.zin, A.zout, k, i) ||
         !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[i], A.e2[i]))
-      continue;
+      return true;
     const double x = dev ? mad_dev(A.score2[i], med) : A.score2[i];
     uint32_t lt = 0, le = 0;
-    for (uint64_t j = A.wlo[k]; j < A.whi[k]; ++j) {
+    bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t j) {
       if (!bg_map_live(A.zin, A.zout, k, j) ||
           !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[j], A.e2[j]))
-        continue;
+        return true;
       const double y = dev ? mad_dev(A.score2[j], med) : A.score2[j];
       lt += y < x;
       le += y <= x;
-    }
-    if (lt <= p && p < le) return x;
-  }
-  return 0.0;  // not reached for p < window size
+      return true;
+    });
+    if (lt <= p && p < le) { out = x; return false; }
+    return true;
+  });
+  return out;
 }
 
 // RollingKthAverage::DoneReference (numerical/RollingKthAverageVisitor.hpp:61-92): with
@@ -1036,6 +1048,7 @@ static void fill_args(bg_result* r, FmtArgs& A) {
       A.whi = r->whi;
       A.zin = r->zin;
       A.zout = r->zout;
+      A.lrows = r->lrows;
       A.crit = r->mopts.criterion;
       A.ovr = (int64_t)r->mopts.overlap_bp;
       A.range = (int64_t)r->mopts.range_bp;

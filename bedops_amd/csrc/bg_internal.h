@@ -36,6 +36,16 @@ struct bg_dstatus {
   unsigned long long pad[3];
 };
 
+// bedmap: map rows longer than thr, by length class (see bg_map_cands below)
+#define BG_LONG_MAXC 30
+struct LongRows {
+  const uint64_t* idx;   // long rows' map indices, grouped by class, index order inside
+  const int64_t* ls;     // their starts
+  const uint64_t* coff;  // class c = [coff[c], coff[c + 1])
+  int ncls;              // 0: no long rows (one range is exact)
+  int64_t thr;
+};
+
 enum { ERR_PARSE = 1, ERR_CHROM = 2, ERR_RANGE = 3, ERR_UNSORTED = 4, ERR_BLANK = 5, ERR_SCORE = 6 };
 
 // ---------------------------------------------------------------------------------
@@ -145,6 +155,7 @@ struct bg_result {
   uint64_t* rrank = nullptr; // --echo-ref-row-id with --skip-unmapped: printed lines before row r
   uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
   uint64_t* whi = nullptr;
+  LongRows lrows = {nullptr, nullptr, nullptr, 0, 0};  // bedmap: long map rows by class (owned)
   // zero-length rows in a bedmap input: map row m is in the sweep window of reference rows
   // [zin[m], zout[m]) only (bg_map.hip, k_mz_member); null otherwise
   int64_t* zin = nullptr;
@@ -392,6 +403,51 @@ __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, 
 __device__ __forceinline__ bool bg_map_live(const int64_t* zin, const int64_t* zout, uint64_t r,
                                             uint64_t m) {
   return !zin || (zin[m] <= (int64_t)r && (int64_t)r < zout[m]);
+}
+
+// ---------------------------------------------------------------------------------
+// bedmap candidate windows by row-length class. Map rows of length <= thr are searched in
+// one start range [s - pad - thr + 1, e + pad); longer rows sit in per-class lists (class
+// c: lengths in (thr << c, thr << (c + 1)]), each searched with its own bound, so one
+// chromosome-length row no longer widens every reference row's window to its chromosome.
+// The candidates are visited in map-row (start) order: a merge of the short range and the
+// class ranges (the visitors that depend on order — bases-uniq, echo-map — see the same
+// sequence as from one range).
+__device__ __forceinline__ uint64_t bg_lb_range(const int64_t* A, uint64_t lo, uint64_t hi, int64_t v) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (A[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+template <typename F>
+__device__ __forceinline__ void bg_map_cands(const int64_t* MS, const int64_t* ME, uint64_t lo, uint64_t hi,
+                                             const LongRows& LR, int64_t s, int64_t e, int64_t pad, F f) {
+  if (LR.ncls == 0) {  // f returns false to stop
+    for (uint64_t m = lo; m < hi; ++m)
+      if (!f(m)) return;
+    return;
+  }
+  const int64_t g = s & ~BG_COORD_MASK;
+  const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad);
+  uint64_t q[BG_LONG_MAXC], qe[BG_LONG_MAXC];
+  for (int c = 0; c < LR.ncls; ++c) {
+    const int64_t klo = max(g, s - pad - (LR.thr << (c + 1)) + 1);
+    q[c] = bg_lb_range(LR.ls, LR.coff[c], LR.coff[c + 1], klo);
+    qe[c] = bg_lb_range(LR.ls, q[c], LR.coff[c + 1], khi);
+  }
+  uint64_t m = lo;
+  for (;;) {
+    while (m < hi && ME[m] - MS[m] > LR.thr) ++m;  // long rows come from their class
+    uint64_t best = m < hi ? m : ~0ULL;
+    int bc = -1;
+    for (int c = 0; c < LR.ncls; ++c)
+      if (q[c] < qe[c] && LR.idx[q[c]] < best) { best = LR.idx[q[c]]; bc = c; }
+    if (best == ~0ULL || !f(best)) break;
+    if (bc < 0) ++m;
+    else ++q[bc];
+  }
 }
 
 // first index k in [0,n) with A[k] >= v (A sorted ascending); n if none

@@ -65,6 +65,7 @@ struct MapArgs {
   int64_t* isq;
   uint64_t* wlo;
   uint64_t* whi;
+  LongRows lrows;      // rows longer than L by length class (bg_map_cands); L = its threshold
   const int64_t* zin;  // zero-length rows: window membership (bg_map_live), else null
   const int64_t* zout;
   bg_dstatus* st;
@@ -96,7 +97,7 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const int64_t* X, uint32_t l
 
 #define MAP_SLICE 3072  // map starts staged per workgroup (24 KiB of LDS)
 
-template <int CRIT, bool ZM>
+template <int CRIT, bool ZM, bool LONG>
 __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
@@ -148,6 +149,39 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   uint64_t bases = 0;
   uint32_t uniq = 0;                // unsigned int arithmetic, as OvrUnique's
   int64_t us = 0, ue = LLONG_MIN;  // current union piece
+  auto visit = [&](int64_t ms, int64_t me, double x) {  // one member of S(r), in start order
+    if (A.need & (NEED_SUM | NEED_EXT)) {
+      sum += (int64_t)x;
+      if (A.need & NEED_SQ) sq += (int64_t)x * (int64_t)x;
+      if (c == 0) vmin = vmax = x;
+      else {
+        if (x < vmin) vmin = x;
+        if (x > vmax) vmax = x;
+      }
+    }
+    ++c;
+    if (A.need & NEED_BASES) bases += (uint64_t)max(min(e, me) - max(s, ms), (int64_t)0);
+    if (A.need & NEED_UNIQ) {
+      // OvrUnique merges a row into the current piece only when they overlap by > 0 bp
+      // (BasicCoords::overlap, Bed.hpp:172-190): a zero-length row closes the piece
+      if (min(ue, me) > max(us, ms)) {
+        us = min(us, ms);
+        ue = max(ue, me);
+      } else {
+        if (ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
+        us = ms;
+        ue = me;
+      }
+    }
+  };
+  if (LONG) {  // short range + the long rows' class ranges, merged in index order
+    bg_map_cands(A.MS, A.ME, lo, hi, A.lrows, s, e, pad, [&](uint64_t m) {
+      const int64_t ms = A.MS[m], me = A.ME[m];
+      if ((!ZM || bg_map_live(A.zin, A.zout, r, m)) && map_in<CRIT>(s, e, ms, me, A))
+        visit(ms, me, (A.need & (NEED_SUM | NEED_EXT)) ? A.SC[m] : 0.0);
+      return true;
+    });
+  } else {
   // candidates in groups of MU: the group's loads are issued together (they are
   // independent; one at a time, every candidate paid a cache round trip)
   constexpr int MU = 4;
@@ -160,37 +194,15 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
       const uint64_t m = min(m0 + j, hi - 1);
       ms[j] = staged ? xs[m - blo] : A.MS[m];
       me[j] = A.ME[m];
-      if (A.need & (NEED_SUM | NEED_EXT)) sc[j] = A.SC[m];
+      sc[j] = (A.need & (NEED_SUM | NEED_EXT)) ? A.SC[m] : 0.0;
       live_m[j] = !ZM || bg_map_live(A.zin, A.zout, r, m);
     }
 #pragma unroll
     for (int j = 0; j < MU; ++j) {
       if (m0 + j >= hi || !live_m[j] || !map_in<CRIT>(s, e, ms[j], me[j], A)) continue;
-      if (A.need & (NEED_SUM | NEED_EXT)) {
-        const double x = sc[j];
-        sum += (int64_t)x;
-        if (A.need & NEED_SQ) sq += (int64_t)x * (int64_t)x;
-        if (c == 0) vmin = vmax = x;
-        else {
-          if (x < vmin) vmin = x;
-          if (x > vmax) vmax = x;
-        }
-      }
-      ++c;
-      if (A.need & NEED_BASES) bases += (uint64_t)max(min(e, me[j]) - max(s, ms[j]), (int64_t)0);
-      if (A.need & NEED_UNIQ) {
-        // OvrUnique merges a row into the current piece only when they overlap by > 0 bp
-        // (BasicCoords::overlap, Bed.hpp:172-190): a zero-length row closes the piece
-        if (min(ue, me[j]) > max(us, ms[j])) {
-          us = min(us, ms[j]);
-          ue = max(ue, me[j]);
-        } else {
-          if (ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
-          us = ms[j];
-          ue = me[j];
-        }
-      }
+      visit(ms[j], me[j], sc[j]);
     }
+  }
   }
   if ((A.need & NEED_UNIQ) && ue > us) uniq += (uint32_t)max(min(e, ue) - max(s, us), (int64_t)0);
   A.cnt[r] = c;
@@ -589,6 +601,74 @@ static int map_running_sums(bg_ctx* c, int crit, const EvArgs& A, bool need_sq, 
   }
 }
 
+// ------------------------------- long rows by length class --------------------------
+#define BG_LONG_THR 4096
+__global__ void k_len_class(const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
+                            int64_t thr, uint8_t* __restrict__ cls) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t len = E[i] - S[i];
+  uint8_t c = 0;
+  if (len > thr) {  // class k + 1: (thr << k, thr << (k + 1)]
+    int k = 0;
+    while ((thr << (k + 1)) < len) ++k;
+    c = (uint8_t)(k + 1);
+  }
+  cls[i] = c;
+}
+__global__ void k_is_class(const uint8_t* __restrict__ cls, uint64_t n, uint8_t want, uint8_t* __restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = cls[i] == want;
+}
+__global__ void k_gather_i64(const int64_t* __restrict__ src, const uint64_t* __restrict__ idx, uint64_t n,
+                             int64_t* __restrict__ dst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+
+// the map table's rows longer than BG_LONG_THR, grouped by length class (index order in
+// each class), with their starts: res->lrows
+static int map_long_rows(bg_ctx* c, const bg_table* M, bg_result* res) {
+  const uint64_t n = M->n;
+  uint8_t* cls = (uint8_t*)bg_alloc(c, n);
+  uint8_t* f = (uint8_t*)bg_alloc(c, n);
+  if (!cls || !f) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_len_class", k_len_class, dim3(bg_blocks(n, BG_NT)), dim3(BG_NT), M->ks, M->ke, n,
+            (int64_t)BG_LONG_THR, cls);
+  std::vector<uint64_t*> lists;
+  std::vector<uint64_t> counts;
+  int maxc = 0;
+  while (((int64_t)BG_LONG_THR << (maxc + 1)) < M->maxlen && maxc + 1 < BG_LONG_MAXC) ++maxc;
+  for (int k = 0; k <= maxc; ++k) {
+    BG_LAUNCH(c, "k_is_class", k_is_class, dim3(bg_blocks(n, BG_NT)), dim3(BG_NT), cls, n, (uint8_t)(k + 1), f);
+    uint64_t* idx = nullptr;
+    uint64_t cnt = 0;
+    int rc = bg_compact_flags(c, f, n, &idx, &cnt);
+    if (rc) return rc;
+    lists.push_back(idx);
+    counts.push_back(cnt);
+  }
+  uint64_t tot = 0;
+  std::vector<uint64_t> coff(lists.size() + 1, 0);
+  for (size_t k = 0; k < lists.size(); ++k) coff[k + 1] = coff[k] + counts[k];
+  tot = coff.back();
+  uint64_t* idx = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
+  int64_t* ls = (int64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
+  uint64_t* dco = (uint64_t*)bg_alloc(c, 8 * coff.size());
+  if (!idx || !ls || !dco) return BG_E_NOMEM;
+  for (size_t k = 0; k < lists.size(); ++k) {
+    if (counts[k]) BG_HIP(c, hipMemcpyAsync(idx + coff[k], lists[k], 8 * counts[k], hipMemcpyDeviceToDevice, c->stream));
+    bg_release(c, lists[k]);
+  }
+  if (tot) BG_LAUNCH(c, "k_gather_i64", k_gather_i64, dim3(bg_blocks(tot, BG_NT)), dim3(BG_NT), M->ks, idx, tot, ls);
+  BG_HIP(c, hipMemcpyAsync(dco, coff.data(), 8 * coff.size(), hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));  // coff is a host vector
+  bg_release(c, cls);
+  bg_release(c, f);
+  res->lrows = LongRows{idx, ls, dco, (int)lists.size(), (int64_t)BG_LONG_THR};
+  return 0;
+}
+
 // 1 per reference row that prints a line (MultiVisitor.hpp:83-84 skips rows without maps)
 __global__ void k_map_printed(const int32_t* __restrict__ cnt, uint64_t n, uint64_t* __restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -745,6 +825,19 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   A.SC = (need & (NEED_SUM | NEED_EXT)) ? M->score : nullptr;
   A.nm = M->n;
   A.L = M->maxlen > 0 ? M->maxlen : 1;  // longest map row (from the loader)
+  A.lrows = LongRows{nullptr, nullptr, nullptr, 0, 0};
+  // rows longer than BG_LONG_THR get per-length-class windows (bg_map_cands), so a few
+  // chromosome-length rows do not widen every reference row's window; the zero-length
+  // and running-double replays enumerate one contiguous window and keep the global bound
+  if (M->maxlen > BG_LONG_THR && !res->zin && !decimal) {
+    int rl = map_long_rows(c, M, res);
+    if (rl) {
+      bg_result_free(res);
+      return rl;
+    }
+    A.lrows = res->lrows;
+    if (A.lrows.ncls) A.L = BG_LONG_THR;
+  }
   A.ovr = (int64_t)opts->overlap_bp;
   A.range = (int64_t)opts->range_bp;
   A.perc = perc;
@@ -765,8 +858,13 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);
 #define BG_MAP_LAUNCH(K)                                                                   \
   do {                                                                                     \
-    if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true>), g, b, A);                   \
-    else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false>), g, b, A);                        \
+    if (A.lrows.ncls) {                                                                    \
+      if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, true>), g, b, A);           \
+      else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, true>), g, b, A);                \
+    } else {                                                                               \
+      if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, false>), g, b, A);          \
+      else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false>), g, b, A);               \
+    }                                                                                      \
   } while (0)
     switch (crit) {
       case BG_OVR_BP: BG_MAP_LAUNCH(BG_OVR_BP); break;

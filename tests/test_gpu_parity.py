@@ -497,3 +497,64 @@ def test_closest_large_vs_oracle(eng, oracle_bin, bedgen, tmp_path):
     want = subprocess.run([oracle_bin["closest"], "--closest", str(tmp_path / "q.bed"),
                            str(tmp_path / "c.bed")], stdout=subprocess.PIPE, check=True).stdout
     assert eng.closest(q, c, shortest=True) == want
+
+
+@pytest.mark.parametrize("crit,val", [("bp-ovr", 1), ("range", 500), ("fraction-ref", "0.2"), ("exact", None)])
+def test_bedmap_long_rows_by_class_vs_oracle(eng, oracle_bin, crit, val):
+    """map rows longer than 4 KiB are searched per length class (bg_map_cands): every
+    operation, in the same visiting order as one window, byte-equal to the oracle"""
+    rng = random.Random(zlib.crc32(repr(("long", crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(4):
+            ref = randbed.rows(rng, rng.choice([50, 800]), chroms=["chr1", "chr2"], span=400000, maxlen=2000)
+            mp = randbed.rows(rng, rng.choice([200, 3000]), chroms=["chr1", "chr2"], span=400000, maxlen=300)
+            for _ in range(rng.choice([1, 5, 40])):  # long rows of many length classes
+                c = rng.choice(["chr1", "chr2"])
+                s = rng.randrange(0, 300000)
+                mp.append((c, s, s + rng.choice([5000, 9000, 20000, 70000, 300000])))
+            mp.sort(key=lambda r: (r[0].encode(), r[1], r[2]))
+            rt = randbed.text(ref, rest="cols", rng=rng).encode()
+            mt = "".join(f"{c}\t{s}\t{e}\tid{i % 17}\t{rng.randint(0, 999)}\n"
+                         for i, (c, s, e) in enumerate(mp)).encode()
+            copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
+            kw = {"overlap_bp": val} if crit == "bp-ovr" else {"criterion": crit, "value": val}
+            for ops in (["count", "sum", "min", "max", "mean"], ["bases", "bases-uniq", "bases-uniq-f"],
+                        ["echo-map", "echo-map-id", "echo-overlap-size", "echo-map-range"],
+                        ["median", ("kth", 0.4), "echo-map-id-uniq"]):
+                args = [a for o in ops for a in ([f"--{o[0]}", str(o[1])] if isinstance(o, tuple)
+                                                 else [f"--{o}"])] + copt
+                want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                assert eng.bedmap(ops, rt, mt, **kw) == want, (crit, ops, trial)
+
+
+def test_bedmap_chromosome_length_row_stays_fast(eng, oracle_bin, bedgen):
+    """one chromosome-length map row in a 1M x 10M map: same answer as the oracle, and the
+    GPU time within 2x of the same input without that row (its own length class)"""
+    import time
+    from bedops_amd.engine import BED3, BED5
+    ref = subprocess.run([bedgen, "1000000", "7"], stdout=subprocess.PIPE, check=True).stdout
+    mp = subprocess.run([bedgen, "10000000", "8", "--bed5"], stdout=subprocess.PIPE, check=True).stdout
+    mp_long = b"chr1\t0\t248956422\tidLong\t7\n" + mp  # chr1's rows come first
+
+    def timed(m):
+        best = None
+        for _ in range(3):
+            s = eng.load([(ref, BED3), (m, BED5)])
+            eng.sync()
+            t0 = time.perf_counter()
+            r = eng.map_op(s, ["count", "mean"], 0, 1)
+            r.format()
+            eng.sync()
+            dt = time.perf_counter() - t0
+            txt = r.text()
+            r.free()
+            s.free()
+            best = dt if best is None else min(best, dt)
+        return best, txt
+
+    t_plain, _ = timed(mp)
+    t_long, got = timed(mp_long)
+    with tempfile.TemporaryDirectory() as td:
+        want = run_oracle(oracle_bin["bedmap"], ["--count", "--mean"], [ref, mp_long], td)
+    assert got == want
+    assert t_long < 2 * t_plain + 0.01, (t_long, t_plain)
