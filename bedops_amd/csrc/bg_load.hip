@@ -903,15 +903,8 @@ __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, 
   const RunInfo& I = R.info[run];
   uint64_t start, end;
   Fast F;
-#if defined(BG_EXP) && (BG_EXP == 1 || BG_EXP == 4)
-  if (true) { start = (uint64_t)ls; end = start + 10; } else
-#endif
-#if defined(BG_EXP) && BG_EXP == 2
-  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F)) {
-#else
   if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
       F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
-#endif
     start = F.start;
     end = F.end;
   } else {
@@ -1024,10 +1017,6 @@ __device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* ls
         E = (V)ke + 1;
       }
     }
-#if defined(BG_EXP) && (BG_EXP == 3 || BG_EXP == 4)
-    if (valid) carry_e ^= (V)(ks + ke);
-    continue;
-#endif
     const V ie = wave_incl_max_v(E);
     const V pk = wave_shr1_v(K);  // previous line's K (lane 0: from LDS below)
     const int p = j & 1;
@@ -1116,9 +1105,6 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
     set_rounds<uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
   }
   __syncthreads();  // klast complete (also when the tile has no lines)
-#if defined(BG_EXP) && (BG_EXP == 3 || BG_EXP == 4)
-  if (cmax == 12345) LCS[base] = 1;
-#endif
   if (threadIdx.x == 0) {
     if (nc > SCAP) {
       atomicOr(&st->flags, BG_SET_OVERFLOW);
