@@ -41,7 +41,8 @@ static void usage(FILE* f) {
           "      --echo-map --echo-map-id --echo-map-range --echo-map-score --echo-map-size\n"
           "      --echo-overlap-size --indicator --max --mean --min --sum\n"
           "      --cv --kth <val> --mad [mult] --median --stdev --variance --echo-map-id-uniq\n"
-          "      --echo-ref-row-id\n",
+          "      --echo-ref-row-id --min-element --max-element --min-element-rand\n"
+          "      --max-element-rand --tmean <low> <hi> --wmean\n",
           BEDOPS_AMD_VERSION);
 }
 
@@ -69,7 +70,10 @@ int main(int argc, char** argv) {
       {"echo-map-score", BG_MAP_ECHO_MAP_SCORE}, {"echo-map-size", BG_MAP_ECHO_MAP_SIZE},
       {"echo-overlap-size", BG_MAP_ECHO_OVERLAP_SIZE}, {"echo-map-range", BG_MAP_ECHO_MAP_RANGE},
       {"median", BG_MAP_MEDIAN}, {"variance", BG_MAP_VARIANCE}, {"stdev", BG_MAP_STDEV}, {"cv", BG_MAP_CV},
-      {"echo-map-id-uniq", BG_MAP_ECHO_MAP_ID_UNIQ}, {"echo-ref-row-id", BG_MAP_ECHO_REF_ROW_ID}};
+      {"echo-map-id-uniq", BG_MAP_ECHO_MAP_ID_UNIQ}, {"echo-ref-row-id", BG_MAP_ECHO_REF_ROW_ID},
+      {"min-element", BG_MAP_MIN_ELEMENT}, {"max-element", BG_MAP_MAX_ELEMENT},
+      {"min-element-rand", BG_MAP_MIN_ELEMENT_RAND}, {"max-element-rand", BG_MAP_MAX_ELEMENT_RAND},
+      {"wmean", BG_MAP_WMEAN}};
   const char* chrom = NULL;
   int a = 1;
   while (a < argc) {
@@ -188,6 +192,29 @@ int main(int argc, char** argv) {
       o.op_arg[o.n_ops] = kv;
       o.ops[o.n_ops++] = kv == 0 ? BG_MAP_MIN : (kv == 1 ? BG_MAP_MAX : BG_MAP_KTH);
       need5 = 1;
+    } else if (!strcmp(k, "tmean")) {  /* Input.hpp:303-325 */
+      char b[512];
+      if (a >= argc) arg_error("No <low> arg given for --tmean");
+      const char* lo = argv[a++];
+      if (strspn(lo, ".-0123456789") != strlen(lo)) {
+        snprintf(b, sizeof(b), "Non-numeric argument: %s for --tmean", lo);
+        arg_error(b);
+      }
+      if (a >= argc) arg_error("No <hi> arg given for --tmean");
+      const char* hi = argv[a++];
+      if (strspn(hi, ".-0123456789") != strlen(hi)) {
+        snprintf(b, sizeof(b), "Non-numeric argument: %s for --tmean", hi);
+        arg_error(b);
+      }
+      const double vl = strtod(lo, NULL), vh = strtod(hi, NULL);
+      if (!(vl >= 0 && vl <= 1) || !(vh >= 0 && vh <= 1)) arg_error("--tmean Expect 0 <= low < hi <= 1");
+      if (!(vl + vh <= 1)) arg_error("--tmean Expect (low + hi) <= 1.");
+      if (o.n_ops >= 16) arg_error("too many operations for this build");
+      o.op_arg[o.n_ops] = vl;
+      o.op_arg2[o.n_ops] = vh;
+      o.ops[o.n_ops++] = BG_MAP_TMEAN;
+      need5 = 1;
+      map_rest = 1;  /* equal scores are ordered by row (set order) in its replay */
     } else if (!strcmp(k, "exact")) {
       if (is_exact) arg_error("multiple --exact's detected - use one");
       is_exact = 1;
@@ -203,8 +230,11 @@ int main(int argc, char** argv) {
       if (o.n_ops >= 16) arg_error("too many operations for this build");
       o.ops[o.n_ops++] = op;
       if (op == BG_MAP_MEAN || op == BG_MAP_SUM || op == BG_MAP_MIN || op == BG_MAP_MAX ||
-          op == BG_MAP_ECHO_MAP_SCORE || (op >= BG_MAP_MEDIAN && op <= BG_MAP_CV))
+          op == BG_MAP_ECHO_MAP_SCORE || (op >= BG_MAP_MEDIAN && op <= BG_MAP_CV) ||
+          (op >= BG_MAP_MIN_ELEMENT && op <= BG_MAP_WMEAN))
         need5 = 1;
+      /* element operations print the whole map row and break ties by its remainder */
+      if (op >= BG_MAP_MIN_ELEMENT && op <= BG_MAP_MAX_ELEMENT_RAND) map_rest = 1;
       if (op == BG_MAP_ECHO) need_rest = 1;
       if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) map_rest = 1;
       // running-double operations order equal rows by their id and remainder
@@ -251,7 +281,29 @@ int main(int argc, char** argv) {
     in[0].nbytes = tr.n;
   }
   in[0].kind = need_rest ? BG_BED3_REST : BG_BED3;
-  if (nf == 2) {
+  const int mkind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
+  if (nf == 1) {
+    /* single-file mode (Bedmap.cpp:196-246, sweep overload 1): every row is a reference row
+     * and a map row, read as the map type (Bedmap.cpp:660-700) */
+    const int m4 = need4 && !need5;
+    in[0].kind = need5 ? ((map_rest || need_rest) ? BG_BED5_REST : BG_BED5)
+                       : ((map_rest || need_rest || m4) ? BG_BED3_REST : BG_BED3);
+    bg_set* set = NULL;
+    if ((rc = bg_load(ctx, 1, in, &set))) die_ctx(PROG, ctx, rc);
+    free_text(&tr);
+    if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
+    bg_result* res = NULL;
+    if ((rc = bg_map(ctx, set, 0, 0, &o, &res))) die_ctx(PROG, ctx, rc);
+    if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);
+    maybe_stats(ctx);
+    fast_exit();
+    bg_result_free(res);
+    bg_set_free(set);
+    free_input(ctx, &tr);
+    bg_close(ctx);
+    return EXIT_SUCCESS;
+  }
+  {
     if (read_input(ctx, argv[a + 1], check || ec, &tm, &in[1])) arg_error("Unable to read the map file");
     if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1);
     if (ec) {
@@ -259,10 +311,8 @@ int main(int argc, char** argv) {
       in[1].data = tm.data;
       in[1].nbytes = tm.n;
     }
-  } else { /* single-file mode: the reference file is also the map file */
-    in[1] = in[0];
   }
-  in[1].kind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
+  in[1].kind = mkind;
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
   free_text(&tr);

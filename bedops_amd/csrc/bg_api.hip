@@ -298,11 +298,11 @@ extern "C" int bg_result_text_device(const bg_result* r, const char** dptr, uint
 extern "C" int bg_result_copy_text(bg_ctx* c, bg_result* r, char* host, uint64_t cap) {
   uint64_t n = 0;
   int rc = bg_result_format(c, r, &n);
-  if (rc) return rc;
+  if (rc && rc != BG_E_VISITOR) return rc;  // BG_E_VISITOR: the text before the stop
   if (cap < n) return bg_fail(c, BG_E_ARG, "host buffer too small");
   if (n) BG_HIP(c, hipMemcpyAsync(host, r->text, n, hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
-  return 0;
+  return rc;
 }
 
 static int write_all(int fd, const char* p, uint64_t n) {
@@ -362,8 +362,9 @@ extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
 extern "C" int bg_result_write(bg_ctx* c, bg_result* r, int fd) {
   uint64_t n = 0;
   int rc = bg_result_format(c, r, &n);
-  if (rc) return rc;
-  return bg_write_device(c, r->text, n, fd);
+  if (rc && rc != BG_E_VISITOR) return rc;
+  const int wr = bg_write_device(c, r->text, n, fd);
+  return wr ? wr : rc;  // BG_E_VISITOR after the text before the stop is written
 }
 
 // host parts (pinned for async DMA) copied back to back into one new device buffer: a
@@ -501,6 +502,7 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->isq);
   bg_release(c, r->dsum);
   bg_release(c, r->dsq);
+  for (int q = 0; q < 16; ++q) bg_release(c, r->tmv[q]);
   bg_release(c, r->rrank);
   bg_release(c, r->wlo);
   bg_release(c, r->whi);

@@ -78,6 +78,12 @@ struct FmtArgs {
   const int64_t* left;
   const int64_t* right;
   int shortest, print_dist, no_ref;
+  // bedmap: --tmean values per operation; single-file mode; the row where the reference
+  // throws (an element operation with nothing mapped) and where its text ends
+  const double* tmv[16];
+  int single, has_elem;
+  uint64_t stop_row;
+  uint64_t* stop_out;
 };
 
 // decimal digits of v: compares only, 32-bit ones when v fits (the common case)
@@ -494,7 +500,7 @@ __device__ __forceinline__ bool fmt_isws(char ch) { return ch == ' ' || (ch >= '
 // B4Rest "%s\t%lu\t%lu\t%s%s" (id, then what follows it), B5Rest "...\t%s\t%lf%s"
 // (the score re-printed with "%lf", Formats.hpp:34)
 template <typename Out>
-__device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m) {
+__device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m, int sprec = -1) {
   const char* rp = A.text2 + A.rest_off2[m];
   const uint32_t rl = A.rest_len2[m];
   if (A.mapfields == 3) {
@@ -510,12 +516,16 @@ __device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m
     while (i < rl && fmt_isws(rp[i])) ++i;
     while (i < rl && !fmt_isws(rp[i])) ++i;  // the score's text, re-printed
     o.put('\t');
-    uint64_t N;
-    bool neg;
-    if (!fixed_digits(A.score2[m], 6, N, neg)) {
-      if (!put_fixed_big(o, A.score2[m], 6)) return false;
+    if (sprec >= 0) {  // PrintAllScorePrecision: "%.{p}lf" / "%.{p}e"
+      if (!put_real(o, A.score2[m], sprec, A.sci)) return false;
     } else {
-      put_fixed(o, N, neg, 6);
+      uint64_t N;
+      bool neg;
+      if (!fixed_digits(A.score2[m], 6, N, neg)) {
+        if (!put_fixed_big(o, A.score2[m], 6)) return false;
+      } else {
+        put_fixed(o, N, neg, 6);
+      }
     }
   }
   for (; i < rl; ++i) o.put(rp[i]);
@@ -664,6 +674,58 @@ __device__ __forceinline__ double window_kth(const FmtArgs& A, uint64_t k, uint3
   return window_rank(A, k, (uint32_t)up);
 }
 
+// --min-element / --max-element[-rand]: the window row Extreme<PrintAllScorePrecision>
+// prints (ExtremeVisitor.hpp:103-133). Stable: the set is ordered by
+// ScoreThenGenomicCompareLesser/Greater (score, then chrom/start/end; BedCompare.hpp:263-288)
+// and keeps the first of equivalent rows, which fixWindow adds in CoordRestAddressCompare
+// order (full_rest, then address). -rand: CompValueThenAddress order, then RandTie's
+// random pick among equal scores (the first of the set here: min lowest row, max highest).
+__device__ __forceinline__ bool elem_better(const FmtArgs& A, int op, uint64_t m, uint64_t b) {
+  const double x = A.score2[m], y = A.score2[b];
+  if (op == BG_MAP_MIN_ELEMENT_RAND) return x != y ? x < y : m < b;
+  if (op == BG_MAP_MAX_ELEMENT_RAND) return x != y ? x > y : m > b;
+  const bool mx = op == BG_MAP_MAX_ELEMENT;
+  if (x != y) return mx ? x > y : x < y;
+  if (A.s2[m] != A.s2[b]) return mx ? A.s2[m] > A.s2[b] : A.s2[m] < A.s2[b];
+  if (A.e2[m] != A.e2[b]) return mx ? A.e2[m] > A.e2[b] : A.e2[m] < A.e2[b];
+  const int c = bg_frest_cmp(A.text2, A.rest_off2, A.rest_len2, A.mapfields, m, b);
+  return c != 0 ? c < 0 : m < b;
+}
+template <typename Out>
+__device__ __forceinline__ bool put_element(const FmtArgs& A, Out& o, uint64_t k, int op) {
+  const int64_t s = A.s[k], e = A.e[k];
+  uint64_t best = ~0ULL;
+  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
+    if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]))
+      return true;
+    if (best == ~0ULL || elem_better(A, op, m, best)) best = m;
+    return true;
+  });
+  return put_map_row(A, o, best, A.prec);
+}
+// --wmean: WeightedAverage::DoneReference (bed/WeightedAverageVisitor.hpp:55-70) over its
+// std::set<MapType*> (address order = row order): sum of overlap/len(ref) * score, divided
+// by the sum of the weights
+__device__ __forceinline__ double window_wmean(const FmtArgs& A, uint64_t k) {
+  const int64_t s = A.s[k], e = A.e[k];
+  const double len = (double)(uint64_t)(e - s);
+  double value = 0, wsum = 0;
+  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
+    const int64_t ms = A.s2[m], me = A.e2[m];
+    if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me))
+      return true;
+    const int64_t ov = min(e, me) - max(s, ms);
+    const double w = (double)(uint64_t)(ov > 0 ? ov : 0) / len;
+    value += w * A.score2[m];
+    wsum += w;
+    return true;
+  });
+  return value / wsum;
+}
+__device__ __forceinline__ bool is_elem_op(int op) {
+  return op >= BG_MAP_MIN_ELEMENT && op <= BG_MAP_MAX_ELEMENT_RAND;
+}
+
 // renders (or measures) line k; returns false on a value outside the GPU range
 template <int KIND, typename Out>
 __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
@@ -697,7 +759,16 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         continue;
       }
       if (op == BG_MAP_ECHO) {
-        put_row(A, o, A.s[k], A.e[k], A.text + A.rest_off[k], A.rest_len[k]);
+        if (A.single) {  // the row as its own (map) type prints it
+          if (!put_map_row(A, o, k)) return false;
+        } else {
+          put_row(A, o, A.s[k], A.e[k], A.text + A.rest_off[k], A.rest_len[k]);
+        }
+        continue;
+      }
+      if (is_elem_op(op)) {
+        if (c <= 0) return true;  // the reference throws here: the line ends unfinished
+        if (!put_element(A, o, k, op)) return false;
         continue;
       }
       if (op == BG_MAP_ECHO_MAP_ID_UNIQ) {
@@ -774,6 +845,10 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         v = mad * (A.op_arg[q] > 0 ? A.op_arg[q] : 1.0);
       } else if (op == BG_MAP_MEDIAN || op == BG_MAP_KTH) {
         v = window_kth(A, k, (uint32_t)c, op == BG_MAP_MEDIAN ? 0.5 : A.op_arg[q]);
+      } else if (op == BG_MAP_TMEAN) {
+        v = A.tmv[q][k];
+      } else if (op == BG_MAP_WMEAN) {
+        v = window_wmean(A, k);
       } else {
         v = (op == BG_MAP_MIN) ? A.vmin[k] : A.vmax[k];
       }
@@ -823,6 +898,8 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __rest
     for (int k = 0; k < FT_TILE / 64; ++k) {
       const uint64_t row = base + (uint64_t)k * 64;
       if (row < A.n && !render<KIND>(A, row, co)) bg_report(st, row, ERR_RANGE);
+      if (KIND == RES_MAP && A.has_elem && row < A.n && A.cnt[row] <= 0)
+        atomicMin(&st->stop_row, (unsigned long long)row);
     }
     uint64_t v = co.n;
 #pragma unroll
@@ -848,6 +925,7 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
     uint64_t st;
     my[k] = tot + block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &st);
     tot += st;
+    if (KIND == RES_MAP && row == A.stop_row) *A.stop_out = toff[blockIdx.x] + my[k] + co.n;
   }
   const uint64_t dst0 = toff[blockIdx.x];
   if (tot > FT_LDS) {  // oversized tile (long names / rests): render straight to HBM
@@ -1059,6 +1137,21 @@ static void fill_args(bg_result* r, FmtArgs& A) {
     }
     A.nops = r->mopts.n_ops;
     for (int k = 0; k < A.nops; ++k) A.ops[k] = r->mopts.ops[k];
+    for (int k = 0; k < 16; ++k) A.tmv[k] = r->tmv[k];
+    A.single = r->single ? 1 : 0;
+    A.mapfields = r->mapfields;
+    if (r->single && !r->wlo) {  // --echo prints rows with the map table's printer
+      const bg_table* M = s->t[r->map_tab];
+      A.s2 = M->ks;
+      A.e2 = M->ke;
+      A.text2 = M->text;
+      A.rest_off2 = M->rest_off;
+      A.rest_len2 = M->rest_len;
+      A.score2 = M->score;
+    }
+    for (int k = 0; k < A.nops; ++k)
+      if (A.ops[k] >= BG_MAP_MIN_ELEMENT && A.ops[k] <= BG_MAP_MAX_ELEMENT_RAND && !r->mopts.skip_unmapped)
+        A.has_elem = 1;
     A.prec = r->mopts.precision;
     A.sci = r->mopts.scientific;
     A.skip_unmapped = r->mopts.skip_unmapped;
@@ -1069,20 +1162,22 @@ static void fill_args(bg_result* r, FmtArgs& A) {
 
 extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!c || !r) return BG_E_ARG;
-  if (r->formatted) {
-    if (nbytes) *nbytes = r->nbytes;
-    return 0;
-  }
   if (r->kind == RES_ROWS && !r->set->t[r->tab]->rest_off)
     return bg_fail(c, BG_E_ARG, "row result needs its table loaded as BG_BED3_REST");
+  if (r->formatted) {
+    if (nbytes) *nbytes = r->nbytes;
+    return r->stopped ? bg_fail(c, BG_E_VISITOR, "Unable to process a 'NAN' with PrintAllScorePrecision.") : 0;
+  }
   FmtArgs A;
   fill_args(r, A);
+  A.stop_row = ~0ULL;
   const unsigned nb = bg_blocks(r->n, FT_TILE);
   const unsigned nbc = bg_blocks(nb, FC_TILES);
   uint64_t* tb = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
   uint64_t* d_tot = (uint64_t*)bg_alloc(c, 8);
   if (!tb || !d_tot) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
+  BG_HIP(c, hipMemsetAsync(&c->dstat->stop_row, 0xff, 8, c->stream));
   if (nb) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_ivl_count, dim3(nb), dim3(BG_NT), A, tb); break;
@@ -1102,6 +1197,13 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
     return bg_fail(c, BG_E_UNSUPPORTED, "a value is outside the GPU formatter's range");
   r->text = (char*)bg_alloc(c, total + 16);
   if (!r->text) return BG_E_NOMEM;
+  uint64_t* d_stop = nullptr;
+  if (c->hstat->stop_row != ~0ULL) {  // the text ends inside this row (k_fmt_write finds where)
+    A.stop_row = c->hstat->stop_row;
+    d_stop = (uint64_t*)bg_alloc(c, 8);
+    if (!d_stop) return BG_E_NOMEM;
+    A.stop_out = d_stop;
+  }
   if (nb) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_write, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
@@ -1114,11 +1216,17 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   }
   r->toff = tb;
   bg_release(c, d_tot);
+  if (d_stop) {
+    rc = bg_fetch_u64(c, d_stop, &total);
+    bg_release(c, d_stop);
+    if (rc) return rc;
+    r->stopped = true;
+  }
   r->nbytes = total;
   r->formatted = true;
   if (nbytes) *nbytes = total;
   bg_mark(c, "format");
-  return 0;
+  return r->stopped ? bg_fail(c, BG_E_VISITOR, "Unable to process a 'NAN' with PrintAllScorePrecision.") : 0;
 }
 
 // Byte offset of the first output line of every chromosome g of the set's dictionary;
@@ -1185,9 +1293,9 @@ extern "C" const char* bg_set_chrom_name(const bg_set* s, uint32_t g) {
 extern "C" int bg_result_copy_text_device(bg_ctx* c, bg_result* r, void* dst, uint64_t cap) {
   uint64_t n = 0;
   int rc = bg_result_format(c, r, &n);
-  if (rc) return rc;
+  if (rc && rc != BG_E_VISITOR) return rc;
   if (cap < n) return bg_fail(c, BG_E_ARG, "device buffer too small");
   if (n) BG_HIP(c, hipMemcpyAsync(dst, r->text, n, hipMemcpyDeviceToDevice, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
-  return 0;
+  return rc;
 }

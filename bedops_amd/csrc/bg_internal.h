@@ -33,7 +33,8 @@ struct bg_dstatus {
   unsigned long long nblank;     // blank lines seen
   unsigned long long flags;      // bit0: non-integer score, bit1: zero-length row, bit2: |sum|>=2^53
   long long maxlen;              // max (end - start) seen (bedmap window)
-  unsigned long long pad[3];
+  unsigned long long stop_row;   // bedmap: first row where the reference throws (~0: none)
+  unsigned long long pad[2];
 };
 
 // bedmap: map rows longer than thr, by length class (see bg_map_cands below)
@@ -152,6 +153,8 @@ struct bg_result {
   int64_t* isq = nullptr;    // exact integer sum of squared scores (Variance, StdDev, CV)
   double* dsum = nullptr;    // decimal scores: the reference's running sum_ at each row
   double* dsq = nullptr;     //   and squareSum_ (bg_map.hip, k_mev_*), replacing isum / isq
+  double* tmv[16] = {};      // --tmean ops[q]: TrimmedMean's value at each row (k_tm_replay)
+  bool single = false;       // single-file mode (ref == map table)
   uint64_t* rrank = nullptr; // --echo-ref-row-id with --skip-unmapped: printed lines before row r
   uint64_t* wlo = nullptr;   // --echo-map*: candidate range [wlo, whi) of map rows per ref row
   uint64_t* whi = nullptr;
@@ -173,6 +176,7 @@ struct bg_result {
   char* text = nullptr;
   uint64_t nbytes = 0;
   bool formatted = false;
+  bool stopped = false;      // the text ends where the reference throws (BG_E_VISITOR)
   uint64_t* toff = nullptr;  // byte offset of each 1024-row format tile (kept for spans)
 };
 
@@ -489,6 +493,50 @@ __device__ __forceinline__ uint64_t upper_bound_i64(const int64_t* A, uint64_t n
     else hi = mid;
   }
   return lo;
+}
+
+// full_rest() of map row m (the third key of CoordRestAddressCompare, BedCompare.hpp:143-194)
+// as up to two byte ranges of the resident text: B3Rest the remainder after `end`, B4Rest
+// id + the remainder after it, B5Rest id + the remainder after the score (Bed.hpp:301, 537,
+// 788; the score itself is not part of it)
+__device__ __forceinline__ bool bg_frest_ws(char c) {
+  return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
+}
+__device__ __forceinline__ void bg_frest(const char* text, const uint64_t* rest_off, const uint32_t* rest_len,
+                                         int mapfields, uint64_t m, const char*& p1, uint32_t& l1,
+                                         const char*& p2, uint32_t& l2) {
+  const char* rp = text + rest_off[m];
+  const uint32_t rl = rest_len[m];
+  l2 = 0;
+  p2 = rp;
+  if (mapfields == 3) { p1 = rp; l1 = rl; return; }
+  uint32_t i = 0;
+  while (i < rl && bg_frest_ws(rp[i])) ++i;
+  p1 = rp + i;
+  if (mapfields == 4) { l1 = rl - i; return; }
+  uint32_t j = i;
+  while (j < rl && !bg_frest_ws(rp[j])) ++j;
+  l1 = j - i;
+  uint32_t k = j;
+  while (k < rl && bg_frest_ws(rp[k])) ++k;
+  while (k < rl && !bg_frest_ws(rp[k])) ++k;
+  p2 = rp + k;
+  l2 = rl - k;
+}
+// strcmp of the full_rest() strings of map rows a and b
+__device__ __forceinline__ int bg_frest_cmp(const char* text, const uint64_t* rest_off, const uint32_t* rest_len,
+                                            int mapfields, uint64_t a, uint64_t b) {
+  const char *a1, *a2, *b1, *b2;
+  uint32_t la1, la2, lb1, lb2;
+  bg_frest(text, rest_off, rest_len, mapfields, a, a1, la1, a2, la2);
+  bg_frest(text, rest_off, rest_len, mapfields, b, b1, lb1, b2, lb2);
+  const uint32_t la = la1 + la2, lb = lb1 + lb2;
+  for (uint32_t q = 0; q < la && q < lb; ++q) {
+    const uint8_t x = (uint8_t)(q < la1 ? a1[q] : a2[q - la1]);
+    const uint8_t y = (uint8_t)(q < lb1 ? b1[q] : b2[q - lb1]);
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return la == lb ? 0 : (la < lb ? -1 : 1);
 }
 
 __device__ __forceinline__ void bg_report(bg_dstatus* st, uint64_t row, int code) {

@@ -371,45 +371,8 @@ struct EvArgs {
   int mapfields;
 };
 
-__device__ __forceinline__ bool ev_ws(char c) {
-  return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f';
-}
-// full_rest() of map row m as up to two byte ranges: B3Rest the remainder after `end`,
-// B4Rest id + remainder after it, B5Rest id + remainder after the score (Bed.hpp:301,
-// 537, 788; the score itself is not part of it)
-__device__ __forceinline__ void ev_frest(const EvArgs& A, uint64_t m, const char*& p1, uint32_t& l1,
-                                         const char*& p2, uint32_t& l2) {
-  const char* rp = A.text + A.rest_off[m];
-  const uint32_t rl = A.rest_len[m];
-  l2 = 0;
-  p2 = rp;
-  if (A.mapfields == 3) { p1 = rp; l1 = rl; return; }
-  uint32_t i = 0;
-  while (i < rl && ev_ws(rp[i])) ++i;
-  p1 = rp + i;
-  if (A.mapfields == 4) { l1 = rl - i; return; }
-  uint32_t j = i;
-  while (j < rl && !ev_ws(rp[j])) ++j;
-  l1 = j - i;
-  uint32_t k = j;
-  while (k < rl && ev_ws(rp[k])) ++k;
-  while (k < rl && !ev_ws(rp[k])) ++k;
-  p2 = rp + k;
-  l2 = rl - k;
-}
-// strcmp of the two full_rest strings
 __device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
-  const char *a1, *a2, *b1, *b2;
-  uint32_t la1, la2, lb1, lb2;
-  ev_frest(A, a, a1, la1, a2, la2);
-  ev_frest(A, b, b1, lb1, b2, lb2);
-  const uint32_t la = la1 + la2, lb = lb1 + lb2;
-  for (uint32_t q = 0; q < la && q < lb; ++q) {
-    const uint8_t x = (uint8_t)(q < la1 ? a1[q] : a2[q - la1]);
-    const uint8_t y = (uint8_t)(q < lb1 ? b1[q] : b2[q - lb1]);
-    if (x != y) return x < y ? -1 : 1;
-  }
-  return la == lb ? 0 : (la < lb ? -1 : 1);
+  return bg_frest_cmp(A.text, A.rest_off, A.rest_len, A.mapfields, a, b);
 }
 // CoordRestAddressCompare for two rows of equal start
 __device__ __forceinline__ bool ev_less(const EvArgs& A, uint64_t a, uint64_t b) {
@@ -446,12 +409,11 @@ __device__ __forceinline__ void ev_walk(const EvArgs& A, uint64_t a, uint64_t b,
   }
 }
 
-template <int CRIT, bool WRITE>
-__global__ void __launch_bounds__(BG_NT) k_mev(EvArgs A, uint64_t* __restrict__ cnt,
-                                               const uint64_t* __restrict__ off,
-                                               double* __restrict__ X, double* __restrict__ X2) {
-  const uint64_t i = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (i >= A.nr) return;
+// the visitor events between reference rows i-1 and i, in the reference's order:
+// (a) sweep pops and (b) fixWindow Deletes of S(r_{i-1}) members (skipped when !dels),
+// then (c) the Adds of S(r_i) \ S(r_{i-1})
+template <int CRIT, typename Del, typename Add>
+__device__ __forceinline__ void ev_events(const EvArgs& A, uint64_t i, bool dels, Del emit_del, Add emit_add) {
   const int64_t s = A.RS[i], e = A.RE[i];
   const int64_t g = s & ~BG_COORD_MASK;
   const int64_t R = (CRIT == BG_OVR_RANGE) ? A.range : 0;
@@ -471,6 +433,20 @@ __global__ void __launch_bounds__(BG_NT) k_mev(EvArgs A, uint64_t* __restrict__ 
   auto popped = [&](uint64_t m) {
     return m < f && ((A.ME[m] & ~BG_COORD_MASK) != g || A.ME[m] + R <= s);
   };
+  if (hp && dels) {
+    for (uint64_t m = plo; m < phi; ++m)  // (a) in deque (file) order
+      if (in_prev(m) && popped(m)) emit_del(m);
+    ev_walk(A, plo, phi, [&](uint64_t m) { return in_prev(m) && !popped(m) && !in_cur(m); }, emit_del);
+  }
+  ev_walk(A, lo, hi, [&](uint64_t m) { return in_cur(m) && !in_prev(m); }, emit_add);  // (c)
+}
+
+template <int CRIT, bool WRITE>
+__global__ void __launch_bounds__(BG_NT) k_mev(EvArgs A, uint64_t* __restrict__ cnt,
+                                               const uint64_t* __restrict__ off,
+                                               double* __restrict__ X, double* __restrict__ X2) {
+  const uint64_t i = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (i >= A.nr) return;
   uint64_t k = 0;
   const uint64_t base = WRITE ? off[i] : 0;
   auto emit_del = [&](uint64_t m) {
@@ -489,12 +465,7 @@ __global__ void __launch_bounds__(BG_NT) k_mev(EvArgs A, uint64_t* __restrict__ 
     }
     ++k;
   };
-  if (hp) {
-    for (uint64_t m = plo; m < phi; ++m)  // (a) in deque (file) order
-      if (in_prev(m) && popped(m)) emit_del(m);
-    ev_walk(A, plo, phi, [&](uint64_t m) { return in_prev(m) && !popped(m) && !in_cur(m); }, emit_del);
-  }
-  ev_walk(A, lo, hi, [&](uint64_t m) { return in_cur(m) && !in_prev(m); }, emit_add);  // (c)
+  ev_events<CRIT>(A, i, true, emit_del, emit_add);
   if (!WRITE) cnt[i] = k;
 }
 
@@ -601,6 +572,213 @@ static int map_running_sums(bg_ctx* c, int crit, const EvArgs& A, bool need_sq, 
   }
 }
 
+// ------------------------------- --tmean: TrimmedMean replayed --------------------------
+// TrimmedMean (numerical/TrimmedMeanVisitor.hpp:40-220) keeps its window in a std::set
+// ordered by (score, address) (CompValueThenAddressLesser, OrderCompare.hpp:31-38) and two
+// markers, each an element with its position and a running double (lowerSum_/upperSum_)
+// moved by every Add/Delete (add :153-163, remove :165-184) and walked to the trim points
+// in DoneReference (doneRef :186-200). Positions equal the marker's rank, so the state is
+// the sorted window + two ranks + two doubles; the doubles carry rounding from row to row.
+// When S(r_{i-1}) and S(r_i) share no row, the Deletes empty the set, the last removal
+// sends both markers to end(), and the next Add restarts them (sum = score): nothing is
+// carried across such a row. The rows are cut there into independent segments (k_tm_seg),
+// and one thread per segment replays the visitor exactly, in the event order of ev_events,
+// on a sorted copy of the window in HBM scratch sized by the segment's largest window.
+// Addresses: row index (allocation order), as in ev_less.
+struct TmArgs {
+  double lo, hi;  // lowerKth_, upperKth_
+  int doKth, symmetric, lower;  // lower: the lower marker is maintained (lowerKth_ > 0 && !doKth_)
+};
+struct TmMark {
+  bool valid;  // not end()
+  uint64_t pos;
+  double sum;
+};
+__device__ __forceinline__ bool tm_less(double va, uint64_t ia, double vb, uint64_t ib) {
+  if (va != vb) return va < vb;
+  return ia < ib;
+}
+template <int CRIT>
+__global__ void k_tm_seg(EvArgs A, uint64_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.nr) return;
+  uint64_t st = 1;
+  if (i > 0) {
+    const int64_t s = A.RS[i], e = A.RE[i], ps = A.RS[i - 1], pe = A.RE[i - 1];
+    const int64_t g = s & ~BG_COORD_MASK;
+    const uint64_t lo = max(A.wlo[i], A.wlo[i - 1]), hi = min(A.whi[i], A.whi[i - 1]);
+    if ((ps & ~BG_COORD_MASK) == g)
+      for (uint64_t m = lo; m < hi; ++m)
+        if ((A.MS[m] & ~BG_COORD_MASK) == g && bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]) &&
+          bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m])) {
+        st = 0;
+        break;
+      }
+  }
+  flag[i] = st;
+}
+// segment starts (flag scanned to pos), then each segment's largest window (cnt)
+__global__ void k_tm_list(const uint64_t* __restrict__ flag, const uint64_t* __restrict__ pos, uint64_t n,
+                          uint64_t* __restrict__ seg) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) seg[pos[i]] = i;
+}
+__global__ void k_tm_cap(const uint64_t* __restrict__ seg, uint64_t nseg, uint64_t nr,
+                         const int32_t* __restrict__ cnt, uint64_t* __restrict__ cap) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nseg) return;
+  const uint64_t a = seg[q], b = q + 1 < nseg ? seg[q + 1] : nr;
+  int32_t mx = 0;
+  for (uint64_t i = a; i < b; ++i) mx = max(mx, cnt[i]);
+  cap[q] = (uint64_t)mx;
+}
+__device__ __forceinline__ double tm_iround(double d) {
+  const double d1 = ceil(d);
+  return (d >= 0) ? ((d1 - d > 0.5) ? floor(d) : d1) : ((d1 - d >= 0.5) ? floor(d) : d1);
+}
+template <int CRIT>
+__global__ void k_tm_replay(EvArgs A, TmArgs T, const uint64_t* __restrict__ seg, uint64_t nseg,
+                            const uint64_t* __restrict__ soff, double* __restrict__ SV,
+                            uint64_t* __restrict__ SI, double* __restrict__ out) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nseg) return;
+  const uint64_t a = seg[q], b = q + 1 < nseg ? seg[q + 1] : A.nr;
+  double* V = SV + soff[q];  // the set, ascending (score, row)
+  uint64_t* X = SI + soff[q];
+  uint64_t n = 0;
+  TmMark L = {false, 0, 0.0}, U = {false, 0, 0.0};
+  auto rank = [&](double v, uint64_t m) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (tm_less(V[mid], X[mid], v, m)) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  auto mark_add = [&](TmMark& k, uint64_t p, double v) {  // after the insert at p
+    if (!k.valid) { k.valid = true; k.pos = 0; k.sum = v; }
+    else if (p <= k.pos) { ++k.pos; k.sum += v; }  // ptr < *marker
+  };
+  auto mark_del = [&](TmMark& k, uint64_t p, double v) {  // before the erase of rank p
+    if (p < k.pos) { --k.pos; k.sum -= v; }
+    else if (p == k.pos) {
+      k.sum -= v;
+      if (k.pos != 0) --k.pos;
+      else if (n > 1) k.sum += V[1];  // ++marker: its successor (rank 0 after the erase)
+      else k.valid = false;
+    }
+  };
+  auto del = [&](uint64_t m) {
+    const double v = A.SC[m];
+    const uint64_t p = rank(v, m);
+    if (T.lower) mark_del(L, p, v);
+    mark_del(U, p, v);
+    for (uint64_t t = p; t + 1 < n; ++t) { V[t] = V[t + 1]; X[t] = X[t + 1]; }
+    --n;
+  };
+  auto add = [&](uint64_t m) {
+    const double v = A.SC[m];
+    const uint64_t p = rank(v, m);
+    for (uint64_t t = n; t > p; --t) { V[t] = V[t - 1]; X[t] = X[t - 1]; }
+    V[p] = v;
+    X[p] = m;
+    ++n;
+    if (T.lower) mark_add(L, p, v);
+    mark_add(U, p, v);
+  };
+  auto walk = [&](TmMark& k, uint64_t np) {
+    while (np > k.pos) { ++k.pos; k.sum += V[k.pos]; }
+    while (np < k.pos) { k.sum -= V[k.pos]; --k.pos; }
+  };
+  for (uint64_t i = a; i < b; ++i) {
+    // the first row of a segment starts from the emptied set (its Deletes reset everything)
+    ev_events<CRIT>(A, i, i > a, del, add);
+    if (n == 0) { out[i] = 0.0; continue; }  // NAN (the formatter prints it from cnt)
+    const uint64_t size = n;
+    uint64_t kl = (uint64_t)tm_iround(T.lo * (double)size);
+    uint64_t kh = (uint64_t)tm_iround(T.hi * (double)size);
+    kh = size - kh;
+    if (T.symmetric) {
+      kl = max(kl, size - kh);
+      kh = size - kl;
+    }
+    const bool doLow = kl > 0;
+    if (doLow) --kl;
+    if (kh > 0) --kh;
+    if (!T.doKth && doLow) walk(L, kl);
+    walk(U, kh);
+    double r;
+    if (T.doKth || U.pos == L.pos) r = V[U.pos];
+    else if (doLow) r = (U.sum - L.sum) / (double)(U.pos - L.pos);
+    else r = U.sum / (double)(U.pos + 1);
+    out[i] = r;
+  }
+}
+
+template <int CRIT>
+static int map_tmean_t(bg_ctx* c, const EvArgs& A, const int32_t* cnt, const bg_map_opts* o, bg_result* res) {
+  const uint64_t nr = A.nr;
+  const unsigned nb = bg_blocks(nr, BG_NT);
+  uint64_t* flag = (uint64_t*)bg_alloc(c, 8 * nr);
+  uint64_t* pos = (uint64_t*)bg_alloc(c, 8 * (nr + 1));
+  if (!flag || !pos) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_tm_seg", k_tm_seg<CRIT>, dim3(nb), dim3(BG_NT), A, flag);
+  BG_HIP(c, hipGetLastError());
+  int rc = bg_scan_sum_u64(c, flag, pos, nr, pos + nr);
+  uint64_t nseg = 0;
+  if (rc || (rc = bg_fetch_u64(c, pos + nr, &nseg))) return rc;
+  uint64_t* seg = (uint64_t*)bg_alloc(c, 8 * (nseg ? nseg : 1));
+  uint64_t* soff = (uint64_t*)bg_alloc(c, 8 * (nseg + 1));
+  if (!seg || !soff) return BG_E_NOMEM;
+  BG_LAUNCH(c, "k_tm_list", k_tm_list, dim3(nb), dim3(BG_NT), flag, pos, nr, seg);
+  const unsigned ns = bg_blocks(nseg ? nseg : 1, BG_NT);
+  BG_LAUNCH(c, "k_tm_cap", k_tm_cap, dim3(ns), dim3(BG_NT), seg, nseg, nr, cnt, soff);
+  BG_HIP(c, hipGetLastError());
+  uint64_t slots = 0;
+  if ((rc = bg_scan_sum_u64(c, soff, soff, nseg, soff + nseg)) || (rc = bg_fetch_u64(c, soff + nseg, &slots)))
+    return rc;
+  double* SV = (double*)bg_alloc(c, 8 * (slots ? slots : 1));
+  uint64_t* SI = (uint64_t*)bg_alloc(c, 8 * (slots ? slots : 1));
+  if (!SV || !SI) return BG_E_NOMEM;
+  for (int q = 0; q < o->n_ops && !rc; ++q) {
+    if (o->ops[q] != BG_MAP_TMEAN) continue;
+    TmArgs T;
+    T.lo = o->op_arg[q];
+    T.hi = o->op_arg2[q];
+    // the constructor's tests, in the same double arithmetic (TrimmedMeanVisitor.hpp:62-73)
+    T.doKth = fabs(1.0 - T.lo - T.hi) <= DBL_EPSILON;
+    T.symmetric = fabs(T.lo - T.hi) <= DBL_EPSILON;
+    T.lower = T.lo > 0 && !T.doKth;
+    res->tmv[q] = (double*)bg_alloc(c, 8 * nr);
+    if (!res->tmv[q]) return BG_E_NOMEM;
+    if (nseg) BG_LAUNCH(c, "k_tm_replay", k_tm_replay<CRIT>, dim3(ns), dim3(BG_NT), A, T, seg, nseg, soff, SV, SI,
+                        res->tmv[q]);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  bg_release(c, flag);
+  bg_release(c, pos);
+  bg_release(c, seg);
+  bg_release(c, soff);
+  bg_release(c, SV);
+  bg_release(c, SI);
+  return rc;
+}
+
+static int map_tmean(bg_ctx* c, int crit, const EvArgs& A, const int32_t* cnt, const bg_map_opts* o,
+                     bg_result* res) {
+  switch (crit) {
+    case BG_OVR_BP: return map_tmean_t<BG_OVR_BP>(c, A, cnt, o, res);
+    case BG_OVR_RANGE: return map_tmean_t<BG_OVR_RANGE>(c, A, cnt, o, res);
+    case BG_OVR_FRAC_REF: return map_tmean_t<BG_OVR_FRAC_REF>(c, A, cnt, o, res);
+    case BG_OVR_FRAC_MAP: return map_tmean_t<BG_OVR_FRAC_MAP>(c, A, cnt, o, res);
+    case BG_OVR_FRAC_EITHER: return map_tmean_t<BG_OVR_FRAC_EITHER>(c, A, cnt, o, res);
+    case BG_OVR_FRAC_BOTH: return map_tmean_t<BG_OVR_FRAC_BOTH>(c, A, cnt, o, res);
+    default: return map_tmean_t<BG_OVR_EXACT>(c, A, cnt, o, res);
+  }
+}
+
 // ------------------------------- long rows by length class --------------------------
 #define BG_LONG_THR 4096
 __global__ void k_len_class(const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
@@ -690,7 +868,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   uint32_t need = 0;
   bool need_sum = false, need_ext = false;
   int mapfields = 3;  // map row type (bedmap/src/Input.hpp:401-418 MapFields)
-  bool need_rrank = false;
+  bool need_rrank = false, tmean = false;
   for (int k = 0; k < opts->n_ops; ++k) {
     switch (opts->ops[k]) {
       case BG_MAP_COUNT: case BG_MAP_INDICATOR: case BG_MAP_ECHO_SIZE: case BG_MAP_ECHO_NAME: break;
@@ -727,6 +905,25 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
         need_sum = true;
         need |= NEED_SQ;
         break;
+      case BG_MAP_MIN_ELEMENT: case BG_MAP_MAX_ELEMENT: case BG_MAP_MIN_ELEMENT_RAND: case BG_MAP_MAX_ELEMENT_RAND:
+        // the whole row is printed, and rows equal in score and coordinates are told
+        // apart by their full_rest() (the set keeps the first added)
+        if (!M->rest_off) return bg_fail(c, BG_E_ARG, "--min-element/--max-element need the map file loaded as BG_BED5_REST");
+        [[fallthrough]];
+      case BG_MAP_WMEAN:
+        need_ext = true;
+        need |= NEED_WIN;
+        break;
+      case BG_MAP_TMEAN: {
+        const double lo = opts->op_arg[k], hi = opts->op_arg2[k];
+        // Input.hpp:303-325 and the constructor's assertions (TrimmedMeanVisitor.hpp:62-73)
+        if (!(lo >= 0 && lo <= 1 && hi >= 0 && hi <= 1 && lo + hi <= 1 + DBL_EPSILON))
+          return bg_fail(c, BG_E_ARG, "--tmean Expect 0 <= low < hi <= 1 and (low + hi) <= 1.");
+        need_ext = true;
+        need |= NEED_WIN;
+        tmean = true;
+        break;
+      }
       default: return bg_fail(c, BG_E_UNSUPPORTED, "bedmap operation not on the GPU path");
     }
   }
@@ -759,6 +956,12 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   // decimal scores: the running doubles are replayed in event order (map_running_sums)
   const bool decimal = need_sum && !M->score_int;
   const bool need_sq = (need & NEED_SQ) != 0;
+  if (ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
+    return bg_fail(c, BG_E_UNSUPPORTED, "single-file bedmap over zero-length rows is not on the GPU path");
+  if (tmean) {
+    if (R->has_zero_len || M->has_zero_len)
+      return bg_fail(c, BG_E_UNSUPPORTED, "--tmean with zero-length rows is not on the GPU path of bedmap");
+  }
   if (decimal) {
     if (R->has_zero_len || M->has_zero_len)
       return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores with zero-length rows are not on the GPU path of bedmap --mean/--sum/--variance/--stdev/--cv");
@@ -777,6 +980,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   res->mopts = *opts;
   if (!res->mopts.multidelim[0]) strcpy(res->mopts.multidelim, ";");  // unset: the default
   res->tab = ref;
+  res->single = ref == map;
   res->cnt = (int32_t*)bg_alloc(c, 4 * n1);
   if (need & NEED_SUM) res->isum = (int64_t*)bg_alloc(c, 8 * n1);
   if (need & NEED_EXT) {
@@ -829,7 +1033,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   // rows longer than BG_LONG_THR get per-length-class windows (bg_map_cands), so a few
   // chromosome-length rows do not widen every reference row's window; the zero-length
   // and running-double replays enumerate one contiguous window and keep the global bound
-  if (M->maxlen > BG_LONG_THR && !res->zin && !decimal) {
+  if (M->maxlen > BG_LONG_THR && !res->zin && !decimal && !tmean) {
     int rl = map_long_rows(c, M, res);
     if (rl) {
       bg_result_free(res);
@@ -878,7 +1082,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
 #undef BG_MAP_LAUNCH
   }
   int rc = bg_hip_ok(c, hipGetLastError());
-  if (!rc && decimal && R->n) {
+  if (!rc && (decimal || tmean) && R->n) {
     EvArgs E;
     E.RS = R->ks;
     E.RE = R->ke;
@@ -896,7 +1100,13 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     E.rest_off = M->rest_off;
     E.rest_len = M->rest_len;
     E.mapfields = mapfields;
-    rc = map_running_sums(c, crit, E, need_sq, res);
+    if (decimal) rc = map_running_sums(c, crit, E, need_sq, res);
+    if (!rc && tmean) {
+      if (!M->rest_off)
+        rc = bg_fail(c, BG_E_ARG, "--tmean needs the map file loaded as BG_BED5_REST (equal rows are ordered by id and remainder)");
+      else
+        rc = map_tmean(c, crit, E, res->cnt, opts, res);
+    }
   }
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));

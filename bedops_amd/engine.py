@@ -22,18 +22,21 @@ MAP_OPS = {"count": 1, "mean": 2, "sum": 3, "min": 4, "max": 5, "indicator": 6, 
            "echo-ref-name": 12, "echo-map": 13, "echo-map-id": 14, "echo-map-score": 15,
            "echo-map-size": 16, "echo-overlap-size": 17, "echo-map-range": 18, "median": 19,
            "kth": 20, "variance": 21, "stdev": 22, "cv": 23, "echo-map-id-uniq": 25, "mad": 24,
-           "echo-ref-row-id": 26}
+           "echo-ref-row-id": 26, "min-element": 27, "max-element": 28, "min-element-rand": 29,
+           "max-element-rand": 30, "tmean": 31, "wmean": 32}
 SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score", "median", "kth", "variance", "stdev",
-             "cv", "mad")
+             "cv", "mad", "min-element", "max-element", "min-element-rand", "max-element-rand",
+             "tmean", "wmean")
 # the map rows' remainders are printed, or order equal rows for the running-double
 # operations (CoordRestAddressCompare: id + remainder)
 MAP_REST_OPS = ("echo-map", "echo-map-id", "echo-map-id-uniq", "mean", "sum", "variance", "stdev",
-                "cv")
+                "cv", "min-element", "max-element", "min-element-rand", "max-element-rand", "tmean")
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}
 
 ERRORS = {-11: "INTERNAL", -1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", -5: "BLANK", -6: "ARG",
-          -7: "NOMEM", -8: "UNSUPPORTED", -9: "CHROM", -10: "IO"}
+          -7: "NOMEM", -8: "UNSUPPORTED", -9: "CHROM", -10: "IO", -12: "VISITOR"}
+BG_E_VISITOR = -12
 
 # exported symbols of include/bedgpu.h (checked by tests/test_abi.py)
 SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_load",
@@ -68,6 +71,14 @@ class BedgpuError(RuntimeError):
         self.msg = msg
 
 
+class BedgpuStop(BedgpuError):
+    """BG_E_VISITOR: the reference throws mid-output; `text` is what it printed before."""
+
+    def __init__(self, code, msg, text):
+        super().__init__(code, msg)
+        self.text = text
+
+
 class _Input(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("nbytes", ctypes.c_uint64),
                 ("on_device", ctypes.c_int), ("kind", ctypes.c_int)]
@@ -79,7 +90,8 @@ class _MapOpts(ctypes.Structure):
                 ("scientific", ctypes.c_int), ("skip_unmapped", ctypes.c_int),
                 ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
                 ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double),
-                ("multidelim", ctypes.c_char * 16), ("op_arg", ctypes.c_double * 16)]
+                ("multidelim", ctypes.c_char * 16), ("op_arg", ctypes.c_double * 16),
+                ("op_arg2", ctypes.c_double * 16)]
 
 
 class _ClosestOpts(ctypes.Structure):
@@ -212,9 +224,20 @@ class Result:
         return list(arr)
 
     def text(self):
-        n = self.format()
+        """the rendered text; raises BedgpuStop (carrying the text before the stop) where the
+        reference throws mid-output"""
+        n = ctypes.c_uint64()
+        rc = self.eng.L.bg_result_format(self.eng.ctx, self.h, ctypes.byref(n))
+        if rc and rc != BG_E_VISITOR:
+            self.eng._check(rc)
+        n = n.value
         buf = ctypes.create_string_buffer(max(n, 1))
-        self.eng._check(self.eng.L.bg_result_copy_text(self.eng.ctx, self.h, buf, n))
+        rc2 = self.eng.L.bg_result_copy_text(self.eng.ctx, self.h, buf, n)
+        if rc2 and rc2 != BG_E_VISITOR:
+            self.eng._check(rc2)
+        if rc == BG_E_VISITOR:
+            raise BedgpuStop(rc, self.eng.L.bg_last_error(self.eng.ctx).decode(errors="replace"),
+                             buf.raw[:n])
         return buf.raw[:n]
 
     def free(self):
@@ -406,10 +429,11 @@ class Engine:
         o = _MapOpts()
         o.overlap_bp = overlap_bp
         o.n_ops = len(ops)
-        for k, op in enumerate(ops):  # an op is a name, or (name, argument) for "kth"
-            name, arg = (op if isinstance(op, tuple) else (op, 0.0))
-            o.ops[k] = MAP_OPS[name]
-            o.op_arg[k] = float(arg)
+        for k, op in enumerate(ops):  # a name, (name, arg) for kth/mad, (name, lo, hi) for tmean
+            t = op if isinstance(op, tuple) else (op,)
+            o.ops[k] = MAP_OPS[t[0]]
+            o.op_arg[k] = float(t[1]) if len(t) > 1 else 0.0
+            o.op_arg2[k] = float(t[2]) if len(t) > 2 else 0.0
         o.precision = precision
         o.scientific = 1 if sci else 0
         o.skip_unmapped = 1 if skip_unmapped else 0
@@ -430,14 +454,19 @@ class Engine:
         names = [op[0] if isinstance(op, tuple) else op for op in ops]
         need5 = any(op in SCORE_OPS for op in names)
         mrest = any(op in MAP_REST_OPS for op in names)
+        single = map_text is None  # single-file mode: rows are their own map rows
+        if single:
+            mrest = mrest or "echo" in names or "echo-map-id" in names or "echo-map-id-uniq" in names
         mkind = (BED5_REST if mrest else BED5) if need5 else (BED3_REST if mrest else BED3)
-        s = self.load([(ref_text, BED3_REST if "echo" in names else BED3),
-                       (map_text if map_text is not None else ref_text, mkind)])
+        if single:
+            s = self.load([(ref_text, mkind)])
+        else:
+            s = self.load([(ref_text, BED3_REST if "echo" in names else BED3), (map_text, mkind)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)
-            r = self.map_op(s, ops, 0, 1, overlap_bp, precision, delim, skip_unmapped,
-                            criterion, value, multidelim, sci)
+            r = self.map_op(s, ops, 0, 0 if single else 1, overlap_bp, precision, delim,
+                            skip_unmapped, criterion, value, multidelim, sci)
             try:
                 return r.text()
             finally:

@@ -56,6 +56,9 @@ extern "C" {
 #define BG_E_CHROM (-9)       /* chromosome name longer than 127 bytes */
 #define BG_E_IO (-10)         /* read/write failure */
 #define BG_E_INTERNAL (-11)   /* a kernel-side consistency check failed (a bug: please report) */
+#define BG_E_VISITOR (-12)    /* the reference stops mid-output here (a visitor throws): the
+                                 formatted text up to that point is valid and is written /
+                                 copied; bg_last_error() has the reference's message */
 
 /* kinds of input, decided by the operation (Bedops.cpp:402-429, Bedmap.cpp:643-654) */
 #define BG_BED3 0      /* chrom start end; remainder ignored            (Bed::B3NoRest) */
@@ -94,7 +97,8 @@ typedef struct bg_map_opts {
   uint64_t range_bp;   /* --range <int> (> 0; --range 0 is --bp-ovr 1)          */
   double fraction;     /* --fraction-{ref,map,either,both} <val>, as given       */
   char multidelim[16]; /* --multidelim between --echo-map* items ("" = the default ";") */
-  double op_arg[16];   /* argument of ops[k] (--kth <val>)                         */
+  double op_arg[16];   /* argument of ops[k] (--kth <val>; --tmean <low>)           */
+  double op_arg2[16];  /* second argument of ops[k] (--tmean <hi>)                  */
 } bg_map_opts;
 /* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
  * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */
@@ -127,6 +131,16 @@ typedef struct bg_map_opts {
 #define BG_MAP_MAD 24          /* --mad [mult]     MedianAbsoluteDeviation (op_arg = mult, 0 = 1) */
 #define BG_MAP_ECHO_MAP_ID_UNIQ 25  /* --echo-map-id-uniq  the window's ids, sorted (strcmp) and unique */
 #define BG_MAP_ECHO_REF_ROW_ID 26   /* --echo-ref-row-id   "id-<n>", n = printed-line counter (PrintRowID) */
+/* one map row of the window, printed whole with its score at --prec
+ * (Extreme<PrintAllScorePrecision>, ExtremeVisitor.hpp:84-135; ProcessBedVisitorRow.hpp:181-207).
+ * A reference row with no mapped element makes the reference throw ("Unable to process a
+ * 'NAN' with PrintAllScorePrecision.") after the text before it: BG_E_VISITOR. */
+#define BG_MAP_MIN_ELEMENT 27       /* --min-element       lowest score, ties: lowest (start,end), then first added */
+#define BG_MAP_MAX_ELEMENT 28       /* --max-element       highest score, ties: highest (start,end), then first added */
+#define BG_MAP_MIN_ELEMENT_RAND 29  /* --min-element-rand  lowest score (the reference picks among ties at random; here the first row) */
+#define BG_MAP_MAX_ELEMENT_RAND 30  /* --max-element-rand  highest score (ties: here the last row) */
+#define BG_MAP_TMEAN 31             /* --tmean <low> <hi>  TrimmedMean (TrimmedMeanVisitor.hpp), its running sums replayed */
+#define BG_MAP_WMEAN 32             /* --wmean             WeightedAverage (bed/WeightedAverageVisitor.hpp) */
 /* overlap criteria (Bedmap.cpp:95-155 -> data/bed/BedDistances.hpp) */
 #define BG_OVR_BP 0            /* --bp-ovr N       Overlapping(N)            :80-118   */
 #define BG_OVR_RANGE 1         /* --range R        RangedDist(R)             :41-67    */
@@ -191,6 +205,8 @@ int bg_check(bg_ctx* ctx, const bg_input* in, int nfields, int has_rest, bg_chec
 /* the reference's message for `code` on `line` (host): the text after "in <file>\n" */
 int bg_check_message(const char* line, uint64_t len, int code, int nfields, int has_rest,
                      char* buf, uint64_t cap);
+/* ref == map: single-file mode (Bedmap.cpp:196-246, sweep overload 1): every row is a
+ * reference row and a map row, printed by --echo as the map type prints it */
 int bg_map(bg_ctx* ctx, bg_set* set, int ref, int map, const bg_map_opts* opts,
            bg_result** out);
 /* closest-features <input-file> <query-file>: `ref` = the <input-file> table, `query` =

@@ -23,7 +23,15 @@
  *                                     PrintSpanName (helpers/ProcessBedVisitorRow.hpp:309-342);
  *                                     VarianceVisitor.hpp / StdevVisitor.hpp / CoeffVariationVisitor.hpp
  *                                     (running double sums), Median / RollingKthAverageVisitor.hpp:61-92;
- *                                     option names: helpers/NamedVisitors.hpp:52-178
+ *                                     Extreme<PrintAllScorePrecision> for --min/max-element[-rand]
+ *                                     (ExtremeVisitor.hpp:84-135 with Bed::ScoreThenGenomicCompare*,
+ *                                     BedCompare.hpp:263-288, or CompValueThenAddress*,
+ *                                     OrderCompare.hpp:31-47; printer ProcessBedVisitorRow.hpp:181-207),
+ *                                     TrimmedMeanVisitor.hpp:40-220, bed/WeightedAverageVisitor.hpp:40-80;
+ *                                     option names: helpers/NamedVisitors.hpp:52-250
+ *   single-file mode ................ Bedmap.cpp:196-246 -> sweep overload 1,
+ *                                     WindowSweepImpl.cpp:66-162 (rows are their own map rows,
+ *                                     read as the map type, Bedmap.cpp:660-700)
  *   number formats .................. "%.{prec}lf"/"%.{prec}e" utility/Formats.hpp:42-50,
  *                                     "NAN" interfaces/src/data/measurement/NaN.cpp:26
  *   argv grammar (subset) ........... applications/bed/bedmap/src/Input.hpp:75-367
@@ -46,7 +54,8 @@ static uint64_t OVR = 1, RANGE = 0;
 static double PERC = 1.0; /* PercentOverlapMapping::perc_ after its constructor */
 
 typedef struct { int c; uint64_t s, e; int64_t id; } row_t;
-static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], -1 - r}; return x; }
+static int SINGLE; /* single-file mode: the reference rows are the map rows (same objects) */
+static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], SINGLE ? r : -1 - r}; return x; }
 static row_t M_(int64_t m) { row_t x = {MAP->chrom[m], MAP->start[m], MAP->end[m], m}; return x; }
 static int chrom_cmp(int a, int b) {
   if (a == b) return 0;
@@ -211,7 +220,8 @@ static void sort_rless(int64_t* v, int64_t n) { /* insertion sort: runs are shor
 enum { V_COUNT = 1, V_MEAN, V_SUM, V_MIN, V_MAX, V_INDICATOR, V_BASES, V_BASES_UNIQ,
        V_BASES_UNIQ_F, V_ECHO, V_ECHO_SIZE, V_ECHO_NAME, V_ECHO_MAP, V_ECHO_MAP_ID,
        V_ECHO_MAP_SCORE, V_ECHO_MAP_SIZE, V_ECHO_OVERLAP_SIZE, V_ECHO_MAP_RANGE, V_MEDIAN,
-       V_KTH, V_VARIANCE, V_STDEV, V_CV, V_ECHO_MAP_ID_UNIQ, V_ECHO_REF_ROW_ID, V_MAD };
+       V_KTH, V_VARIANCE, V_STDEV, V_CV, V_ECHO_MAP_ID_UNIQ, V_ECHO_REF_ROW_ID, V_MAD,
+       V_MIN_EL, V_MAX_EL, V_MIN_EL_RAND, V_MAX_EL_RAND, V_TMEAN, V_WMEAN };
 static double VARG[64];      /* --kth argument per visitor */
 static double sq_;           /* Variance-family running sum of squares */
 static int VIS[64], NVIS;
@@ -224,14 +234,142 @@ static const char* MULTIDELIM = ";";
 static int PREC = 6, SCI = 0, SKIP_UNMAPPED = 0;
 static oset_t VWIN;    /* the visitor window (BedBaseVisitor::win_) */
 
+/* Extreme<.., Bed::ScoreThenGenomicCompare{Lesser,Greater}> (--min-element/--max-element):
+ * a std::set keyed by (score, chrom, start, end) — an Add equivalent to a member is
+ * dropped, a Delete erases the equivalent member (ExtremeVisitor.hpp:92-98). Both orders
+ * share that equivalence, so one literal set serves both. */
+static oset_t EXT;
+static int ext_equiv(int64_t a, int64_t b) {
+  return MAP->score[a] == MAP->score[b] && MAP->chrom[a] == MAP->chrom[b] &&
+         MAP->start[a] == MAP->start[b] && MAP->end[a] == MAP->end[b];
+}
+static void ext_add(int64_t m) {
+  for (int64_t i = 0; i < EXT.n; ++i) if (ext_equiv(EXT.v[i], m)) return;
+  if (EXT.n == EXT.cap) { EXT.cap = EXT.cap ? 2 * EXT.cap : 64; EXT.v = (int64_t*)realloc(EXT.v, (size_t)EXT.cap * 8); }
+  EXT.v[EXT.n++] = m;
+}
+static void ext_del(int64_t m) {
+  for (int64_t i = 0; i < EXT.n; ++i)
+    if (ext_equiv(EXT.v[i], m)) { EXT.v[i] = EXT.v[--EXT.n]; return; }
+}
+/* ScoreThenGenomicCompareLesser(a, b) (BedCompare.hpp:263-278) */
+static int sg_less(int64_t a, int64_t b) {
+  if (MAP->score[a] != MAP->score[b]) return MAP->score[a] < MAP->score[b];
+  int v = chrom_cmp(MAP->chrom[a], MAP->chrom[b]);
+  if (v) return v < 0;
+  if (MAP->start[a] != MAP->start[b]) return MAP->start[a] < MAP->start[b];
+  return MAP->end[a] < MAP->end[b];
+}
+
+/* TrimmedMean (TrimmedMeanVisitor.hpp:40-220): scoresBuf_ is a std::set ordered by
+ * CompValueThenAddressLesser (score, then address = row index); each marker is an element
+ * (-1 = end()) with its position and running double sum. */
+typedef struct { int64_t el; size_t pos; double sum; } tm_mark_t;
+typedef struct {
+  double lo, hi;
+  int doKth, symmetric;
+  oset_t buf;
+  tm_mark_t L, U;
+} tmean_t;
+static tmean_t TM[64];
+static int vl_less(int64_t a, int64_t b) {
+  if (MAP->score[a] != MAP->score[b]) return MAP->score[a] < MAP->score[b];
+  return a < b;
+}
+static int64_t tm_rank(const oset_t* s, int64_t x) {
+  int64_t lo = 0, hi = s->n;
+  while (lo < hi) { int64_t mid = (lo + hi) / 2; if (vl_less(s->v[mid], x)) lo = mid + 1; else hi = mid; }
+  return lo;
+}
+static void tm_init(tmean_t* t, double lo, double hi) {
+  memset(t, 0, sizeof(*t));
+  t->lo = lo; t->hi = hi;
+  t->L.el = t->U.el = -1;
+  const double eps = DBL_EPSILON;
+  if (fabs(1.0 - lo - hi) <= eps) t->doKth = 1;
+  if (fabs(lo - hi) <= eps) t->symmetric = 1;
+}
+/* add(): after the insert */
+static void tm_mark_add(tmean_t* t, tm_mark_t* k, int64_t m) {
+  if (k->el < 0) { k->el = t->buf.v[0]; k->pos = 0; k->sum = MAP->score[m]; }
+  else if (vl_less(m, k->el)) { ++k->pos; k->sum += MAP->score[m]; }
+}
+/* remove(): before the erase */
+static void tm_mark_del(tmean_t* t, tm_mark_t* k, int64_t m) {
+  if (vl_less(m, k->el)) { --k->pos; k->sum -= MAP->score[m]; }
+  else if (m == k->el) {
+    k->sum -= MAP->score[m];
+    const int64_t r = tm_rank(&t->buf, k->el);
+    if (r != 0) { k->el = t->buf.v[r - 1]; --k->pos; }
+    else if (r + 1 < t->buf.n) { k->el = t->buf.v[r + 1]; k->sum += MAP->score[k->el]; }
+    else k->el = -1;
+  }
+}
+static void tm_add(tmean_t* t, int64_t m) {
+  int64_t p = tm_rank(&t->buf, m);
+  if (t->buf.n == t->buf.cap) { t->buf.cap = t->buf.cap ? 2 * t->buf.cap : 64; t->buf.v = (int64_t*)realloc(t->buf.v, (size_t)t->buf.cap * 8); }
+  memmove(t->buf.v + p + 1, t->buf.v + p, (size_t)(t->buf.n - p) * 8);
+  t->buf.v[p] = m;
+  t->buf.n++;
+  if (t->lo > 0 && !t->doKth) tm_mark_add(t, &t->L, m);
+  tm_mark_add(t, &t->U, m);
+}
+static void tm_del(tmean_t* t, int64_t m) {
+  if (t->lo > 0 && !t->doKth) tm_mark_del(t, &t->L, m);
+  tm_mark_del(t, &t->U, m);
+  int64_t p = tm_rank(&t->buf, m);
+  memmove(t->buf.v + p, t->buf.v + p + 1, (size_t)(t->buf.n - p - 1) * 8);
+  t->buf.n--;
+}
+static double tm_iround(double d) {
+  double d1 = ceil(d);
+  return (d >= 0) ? ((d1 - d > 0.5) ? floor(d) : d1) : ((d1 - d >= 0.5) ? floor(d) : d1);
+}
+/* doneRef(): walk the marker to newPos, summing what it passes */
+static void tm_walk(tmean_t* t, tm_mark_t* k, size_t np) {
+  int64_t r = tm_rank(&t->buf, k->el);
+  while (np > k->pos) { ++r; k->sum += MAP->score[t->buf.v[r]]; ++k->pos; }
+  while (np < k->pos) { k->sum -= MAP->score[t->buf.v[r]]; --r; --k->pos; }
+  k->el = t->buf.v[r];
+}
+/* DoneReference(): 1 = value in *out, 0 = NAN */
+static int tm_done(tmean_t* t, double* out) {
+  if (t->buf.n == 0) return 0;
+  const size_t size = (size_t)t->buf.n;
+  size_t kl = (size_t)tm_iround(t->lo * (double)size);
+  size_t kh = (size_t)tm_iround(t->hi * (double)size);
+  kh = size - kh;
+  if (t->symmetric) {
+    kl = kl > size - kh ? kl : size - kh;
+    kh = size - kl;
+  }
+  const int doLow = kl > 0;
+  if (doLow) --kl;
+  if (kh > 0) --kh;
+  if (!t->doKth && doLow) tm_walk(t, &t->L, kl);
+  tm_walk(t, &t->U, kh);
+  if (t->doKth || t->U.pos == t->L.pos) *out = MAP->score[t->U.el];
+  else if (doLow) *out = (t->U.sum - t->L.sum) / (double)(t->U.pos - t->L.pos);
+  else *out = t->U.sum / (double)(t->U.pos + 1);
+  return 1;
+}
+
 static void v_add(int64_t m) {
   ++count_;
-  if (MAP->score) { sum_ += MAP->score[m]; sq_ += MAP->score[m] * MAP->score[m]; ++counter_; }
+  if (MAP->score) {
+    sum_ += MAP->score[m]; sq_ += MAP->score[m] * MAP->score[m]; ++counter_;
+    ext_add(m);
+    for (int i = 0; i < NVIS; ++i) if (VIS[i] == V_TMEAN) tm_add(&TM[i], m);
+  }
   ++cnt_;
 }
 static void v_del(int64_t m) {
   --count_;
-  if (MAP->score) { sum_ -= MAP->score[m]; sq_ -= MAP->score[m] * MAP->score[m]; --counter_; }
+  if (MAP->score) {
+    sum_ -= MAP->score[m]; sq_ -= MAP->score[m] * MAP->score[m]; --counter_;
+    ext_del(m);
+    for (int i = 0; i < NVIS; ++i) if (VIS[i] == V_TMEAN) tm_del(&TM[i], m);
+  }
   --cnt_;
 }
 static void put_real(double v) {
@@ -276,12 +414,17 @@ static unsigned int ovr_uniq(int64_t r) {
 }
 /* one map row as its type prints it: B3Rest "%s\t%lu\t%lu%s", B4Rest "...\t%s%s",
  * B5Rest "...\t%s\t%lf%s" (Bed.hpp; Formats.hpp:34 "%lf") */
-static void print_map_row(int64_t m) {
+static void print_map_row_p(int64_t m, int prec_score) {
   printf("%s\t%" PRIu64 "\t%" PRIu64, POOL.names[MAP->chrom[m]], MAP->start[m], MAP->end[m]);
   if (MAPFIELDS >= 4) printf("\t%s", MAP->id[m]);
-  if (MAPFIELDS >= 5) printf("\t%lf", MAP->score[m]);
+  if (MAPFIELDS >= 5) {
+    fputc('\t', stdout);
+    if (prec_score) put_real(MAP->score[m]);
+    else printf("%lf", MAP->score[m]);
+  }
   fputs(MAP->rest ? MAP->rest[m] : "", stdout);
 }
+static void print_map_row(int64_t m) { print_map_row_p(m, 0); }
 static void echo_map(int how, int64_t r) {
   if (how == V_ECHO_MAP_RANGE) { /* PrintGenomicRange<PrintBED3>, ProcessBedVisitorRow.hpp:433-456 */
     if (VWIN.n == 0) return;
@@ -398,9 +541,61 @@ static void v_done(int64_t r) {
         put_real((double)ovr_uniq(r) / (double)(REF->end[r] - REF->start[r]));
         break;
       case V_ECHO:
+        if (SINGLE) { print_map_row(r); break; } /* the row as its (map) type prints it */
         printf("%s\t%" PRIu64 "\t%" PRIu64 "%s", POOL.names[REF->chrom[r]], REF->start[r], REF->end[r],
                REF->rest ? REF->rest[r] : "");
         break;
+      case V_MIN_EL: case V_MAX_EL: case V_MIN_EL_RAND: case V_MAX_EL_RAND: {
+        /* an empty set hands NaN to PrintAllScorePrecision, which throws
+         * (ProcessBedVisitorRow.hpp:206-208): bedmap stops with what it printed so far */
+        if (VWIN.n == 0) {
+          fflush(stdout);
+          fputs("May use bedmap --help for more help.\n\nError: Unable to process a 'NAN' with PrintAllScorePrecision.\n", stderr);
+          exit(EXIT_FAILURE);
+        }
+        int64_t b = -1;
+        if (VIS[i] == V_MIN_EL || VIS[i] == V_MAX_EL) { /* m_.begin() of the literal set */
+          for (int64_t k = 0; k < EXT.n; ++k) {
+            const int64_t x = EXT.v[k];
+            if (b < 0 || (VIS[i] == V_MIN_EL ? sg_less(x, b) : sg_less(b, x))) b = x;
+          }
+        } else { /* RandTie picks at random among equal scores: this restatement takes the
+                  * set's first (min: lowest address, max: highest) */
+          for (int64_t k = 0; k < VWIN.n; ++k) {
+            const int64_t x = VWIN.v[k];
+            if (b < 0 || (VIS[i] == V_MIN_EL_RAND ? vl_less(x, b) : vl_less(b, x))) b = x;
+          }
+        }
+        print_map_row_p(b, 1);
+        break;
+      }
+      case V_TMEAN: {
+        double v;
+        if (tm_done(&TM[i], &v)) put_real(v); else fputs("NAN", stdout);
+        break;
+      }
+      case V_WMEAN: { /* WeightedAverage::DoneReference over std::set<MapType*> (address order) */
+        if (VWIN.n == 0) { fputs("NAN", stdout); break; }
+        int64_t* v = (int64_t*)malloc((size_t)VWIN.n * 8);
+        memcpy(v, VWIN.v, (size_t)VWIN.n * 8);
+        for (int64_t p = 1; p < VWIN.n; ++p) { /* row order */
+          int64_t x = v[p], q = p;
+          while (q > 0 && v[q - 1] > x) { v[q] = v[q - 1]; --q; }
+          v[q] = x;
+        }
+        double value = 0, weightSum = 0;
+        const double len = (double)(REF->end[r] - REF->start[r]);
+        for (int64_t p = 0; p < VWIN.n; ++p) {
+          const int64_t m = v[p];
+          const double w = (double)ovr_len(REF->start[r], REF->end[r], MAP->start[m], MAP->end[m]) / len;
+          value += w * MAP->score[m];
+          weightSum += w;
+        }
+        free(v);
+        value /= weightSum;
+        put_real(value);
+        break;
+      }
       case V_ECHO_SIZE: printf("%" PRIu64, REF->end[r] - REF->start[r]); break;
       case V_ECHO_MAP_ID_UNIQ: put_unique_ids(); break;
       case V_ECHO_REF_ROW_ID: printf("id-%lu", ++ROWID); break;
@@ -441,6 +636,43 @@ static double parse_frac(const char* v) {
   return p;
 }
 
+static oset_t vcache, lst, ev;
+/* BedBaseVisitor::OnDelete (:145-154) */
+static void on_delete(int64_t m) {
+  if (os_erase(&VWIN, m)) v_del(m);
+  else os_erase(&vcache, m);
+}
+/* BedBaseVisitor::OnDone: fixWindow (deletions first, then insertions), then DoneReference */
+static void on_done(int64_t r) {
+  lst.n = 0;
+  ev.n = 0;
+  for (int64_t i = 0; i < VWIN.n;) {
+    int64_t m = VWIN.v[i];
+    if (crit_m2r(m, r) != 0) {
+      ev_push(&ev, m);
+      os_insert(&lst, m);
+      memmove(VWIN.v + i, VWIN.v + i + 1, (size_t)(VWIN.n - i - 1) * 8);
+      VWIN.n--;
+    } else ++i;
+  }
+  sort_rless(ev.v, ev.n);
+  for (int64_t i = 0; i < ev.n; ++i) v_del(ev.v[i]);
+  ev.n = 0;
+  for (int64_t i = 0; i < vcache.n;) {
+    int64_t m = vcache.v[i];
+    if (crit_m2r(m, r) == 0) {
+      ev_push(&ev, m);
+      os_insert(&VWIN, m);
+      memmove(vcache.v + i, vcache.v + i + 1, (size_t)(vcache.n - i - 1) * 8);
+      vcache.n--;
+    } else ++i;
+  }
+  sort_rless(ev.v, ev.n);
+  for (int64_t i = 0; i < ev.n; ++i) v_add(ev.v[i]);
+  for (int64_t i = 0; i < lst.n; ++i) os_insert(&vcache, lst.v[i]);
+  v_done(r);
+}
+
 int main(int argc, char** argv) {
   int a = 1, need5 = 0, need4 = 0, rest = 0;
   const char* only_chrom = NULL;
@@ -454,7 +686,10 @@ int main(int argc, char** argv) {
       {"--echo-map-size", V_ECHO_MAP_SIZE, 0}, {"--echo-overlap-size", V_ECHO_OVERLAP_SIZE, 0},
       {"--echo-map-range", V_ECHO_MAP_RANGE, 0}, {"--median", V_MEDIAN, 1},
       {"--variance", V_VARIANCE, 1},   {"--stdev", V_STDEV, 1},         {"--cv", V_CV, 1},
-      {"--echo-map-id-uniq", V_ECHO_MAP_ID_UNIQ, 0}, {"--echo-ref-row-id", V_ECHO_REF_ROW_ID, 0}};
+      {"--echo-map-id-uniq", V_ECHO_MAP_ID_UNIQ, 0}, {"--echo-ref-row-id", V_ECHO_REF_ROW_ID, 0},
+      {"--min-element", V_MIN_EL, 1}, {"--max-element", V_MAX_EL, 1},
+      {"--min-element-rand", V_MIN_EL_RAND, 1}, {"--max-element-rand", V_MAX_EL_RAND, 1},
+      {"--wmean", V_WMEAN, 1}};
   while (a < argc - 2 || (a < argc && strncmp(argv[a], "--", 2) == 0)) {
     const char* o = argv[a++];
     int found = 0;
@@ -471,6 +706,14 @@ int main(int argc, char** argv) {
       VARG[NVIS] = 1.0;
       if (a < argc && argv[a][0] && strspn(argv[a], ".-0123456789") == strlen(argv[a])) VARG[NVIS] = strtod(argv[a++], NULL);
       VIS[NVIS++] = V_MAD;
+      need5 = 1;
+      continue;
+    }
+    if (!strcmp(o, "--tmean") && a + 1 < argc) {
+      const double lo = strtod(argv[a], NULL), hi = strtod(argv[a + 1], NULL);
+      a += 2;
+      tm_init(&TM[NVIS], lo, hi);
+      VIS[NVIS++] = V_TMEAN;
       need5 = 1;
       continue;
     }
@@ -500,19 +743,24 @@ int main(int argc, char** argv) {
     else if (!strcmp(o, "--ec") || !strcmp(o, "--header") || !strcmp(o, "--sweep-all")) {}
     else { fprintf(stderr, "bedmap_oracle: unsupported option %s\n", o); return 2; }
   }
-  if (NVIS == 0 || argc - a != 2) { fprintf(stderr, "bedmap_oracle: bad usage\n"); return 2; }
+  const int nfiles = argc - a;
+  if (NVIS == 0 || nfiles < 1 || nfiles > 2) { fprintf(stderr, "bedmap_oracle: bad usage\n"); return 2; }
+  SINGLE = nfiles == 1;
   static bedfile_t ref, map;
   FILE* fr = open_input(argv[a]);
-  FILE* fm = open_input(argv[a + 1]);
-  if (!fr || !fm) { fprintf(stderr, "bedmap_oracle: cannot open input\n"); return 2; }
-  read_bed3(fr, &POOL, &ref, rest);
+  FILE* fm = SINGLE ? NULL : open_input(argv[a + 1]);
+  if (!fr || (!SINGLE && !fm)) { fprintf(stderr, "bedmap_oracle: cannot open input\n"); return 2; }
   MAPFIELDS = need5 ? 5 : (need4 ? 4 : 3);
-  if (need5) read_bed5(fm, &POOL, &map);
-  else if (need4) read_bed4(fm, &POOL, &map);
-  else read_bed3(fm, &POOL, &map, 1);
+  if (!SINGLE) {
+    read_bed3(fr, &POOL, &ref, rest);
+    fr = fm;
+  }
+  if (need5) read_bed5(fr, &POOL, &map);
+  else if (need4) read_bed4(fr, &POOL, &map);
+  else read_bed3(fr, &POOL, &map, 1);
   if (only_chrom) {
     bedfile_t* fs[2] = {&ref, &map};
-    for (int q = 0; q < 2; ++q) {
+    for (int q = SINGLE ? 1 : 0; q < 2; ++q) {
       bedfile_t* f = fs[q];
       int64_t k = 0;
       for (int64_t j = 0; j < f->n; ++j) {
@@ -526,58 +774,60 @@ int main(int argc, char** argv) {
       f->n = k;
     }
   }
-  REF = &ref;
+  REF = SINGLE ? &map : &ref;
   MAP = &map;
   static char obuf[1 << 20];
   setvbuf(stdout, obuf, _IOFBF, sizeof(obuf));
 
-  /* sweep() overload 2 with the sweep distance; fixWindow with the visitor distance */
   int64_t* win = (int64_t*)malloc(sizeof(int64_t) * (size_t)(map.n + 1));
-  int64_t wh = 0, wt = 0; /* deque [wh, wt) */
-  int64_t mi = 0, cache = -1;
-  oset_t vcache = {0}, lst = {0}, ev = {0};
-  for (int64_t r = 0; r < ref.n; ++r) {
-    while (wt > wh && sweep_m2r(win[wh], r) < 0) { /* OnDelete */
-      int64_t m = win[wh++];
-      if (os_erase(&VWIN, m)) v_del(m);
-      else os_erase(&vcache, m);
+  if (SINGLE) { /* sweep() overload 1, WindowSweepImpl.cpp:66-162 */
+    int64_t wh = 0, wt = 0, index = 0, next = 0, cache = -1, cur = -1;
+    int reset = 1;
+    for (;;) {
+      if (!(next < map.n || cache >= 0 || wt > wh)) break;
+      if (!reset) {
+        cur = win[wh + index]; /* OnStart */
+        while (wt > wh && sweep_m2r(win[wh], cur) < 0) { on_delete(win[wh++]); --index; }
+      } else if (next >= map.n && cache < 0) {
+        break; /* OnEnd; the rest of the window is deleted on behalf of no reference */
+      }
+      while (cache >= 0 || next < map.n) {
+        int64_t b;
+        if (cache >= 0) { b = cache; cache = -1; }
+        else b = next++;
+        if (wt == wh || reset || sweep_r2m(win[wh + index], b) == 0) {
+          if (reset) {
+            reset = 0;
+            index = 0;
+            cur = b; /* OnStart(bPtr) */
+            while (wt > wh) on_delete(win[wh++]);
+          }
+          win[wt++] = b;
+          os_insert(&vcache, b); /* OnAdd */
+        } else {
+          cache = b;
+          break;
+        }
+      }
+      on_done(cur);
+      reset = ++index >= wt - wh;
     }
-    while (cache >= 0 || mi < map.n) {
-      int64_t m;
-      if (cache >= 0) { m = cache; cache = -1; }
-      else m = mi++;
-      int v = sweep_r2m(r, m);
-      if (v == 0) { win[wt++] = m; os_insert(&vcache, m); } /* OnAdd -> cache_ */
-      else if (v < 0) { cache = m; break; }
+  } else {
+    /* sweep() overload 2 with the sweep distance; fixWindow with the visitor distance */
+    int64_t wh = 0, wt = 0; /* deque [wh, wt) */
+    int64_t mi = 0, cache = -1;
+    for (int64_t r = 0; r < ref.n; ++r) {
+      while (wt > wh && sweep_m2r(win[wh], r) < 0) on_delete(win[wh++]);
+      while (cache >= 0 || mi < map.n) {
+        int64_t m;
+        if (cache >= 0) { m = cache; cache = -1; }
+        else m = mi++;
+        int v = sweep_r2m(r, m);
+        if (v == 0) { win[wt++] = m; os_insert(&vcache, m); } /* OnAdd -> cache_ */
+        else if (v < 0) { cache = m; break; }
+      }
+      on_done(r);
     }
-    /* OnDone: fixWindow (deletions first, then insertions), then DoneReference */
-    lst.n = 0;
-    ev.n = 0;
-    for (int64_t i = 0; i < VWIN.n;) {
-      int64_t m = VWIN.v[i];
-      if (crit_m2r(m, r) != 0) {
-        ev_push(&ev, m);
-        os_insert(&lst, m);
-        memmove(VWIN.v + i, VWIN.v + i + 1, (size_t)(VWIN.n - i - 1) * 8);
-        VWIN.n--;
-      } else ++i;
-    }
-    sort_rless(ev.v, ev.n);
-    for (int64_t i = 0; i < ev.n; ++i) v_del(ev.v[i]);
-    ev.n = 0;
-    for (int64_t i = 0; i < vcache.n;) {
-      int64_t m = vcache.v[i];
-      if (crit_m2r(m, r) == 0) {
-        ev_push(&ev, m);
-        os_insert(&VWIN, m);
-        memmove(vcache.v + i, vcache.v + i + 1, (size_t)(vcache.n - i - 1) * 8);
-        vcache.n--;
-      } else ++i;
-    }
-    sort_rless(ev.v, ev.n);
-    for (int64_t i = 0; i < ev.n; ++i) v_add(ev.v[i]);
-    for (int64_t i = 0; i < lst.n; ++i) os_insert(&vcache, lst.v[i]);
-    v_done(r);
   }
   fflush(stdout);
   return 0;

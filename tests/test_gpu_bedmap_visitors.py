@@ -1,0 +1,198 @@
+"""GPU parity for the last bedmap operations of SURVEY.md §8 f2 and for single-file mode.
+
+--min-element / --max-element (Extreme<PrintAllScorePrecision> over
+Bed::ScoreThenGenomicCompare*: rows equal in score and coordinates keep the first added),
+--min-element-rand / --max-element-rand (the reference picks among equal scores with
+std::random_shuffle seeded by time(); the GPU and the oracle both take the set's first),
+--tmean (TrimmedMean with its running lower/upper doubles replayed exactly, k_tm_replay),
+--wmean (WeightedAverage in address = row order), and single-file mode (sweep overload 1,
+WindowSweepImpl.cpp:66-162). Every case is byte-compared with oracle/bedmap_oracle.c, which
+restates those visitors line by line (parity against the restatement: the reference ships no
+bedmap fixtures for them)."""
+import os
+import random
+import subprocess
+import tempfile
+import zlib
+
+import pytest
+
+import randbed
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from bedops_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _paths(texts, tmpdir):
+    paths = []
+    for i, t in enumerate(texts):
+        p = os.path.join(tmpdir, f"in{i}.bed")
+        with open(p, "wb") as f:
+            f.write(t)
+        paths.append(p)
+    return paths
+
+
+def oracle(binary, args, texts, tmpdir):
+    """(stdout, stderr, returncode) of the oracle"""
+    r = subprocess.run([binary] + args + _paths(texts, tmpdir), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE)
+    return r.stdout, r.stderr, r.returncode
+
+
+def gpu(eng, ops, rt, mt, **kw):
+    """(text, stopped) through the C ABI; stopped = the reference would throw there"""
+    from bedops_amd.engine import BedgpuStop
+    try:
+        return eng.bedmap(ops, rt, mt, **kw), False
+    except BedgpuStop as e:
+        return e.text, True
+
+
+def argv(ops):
+    out = []
+    for o in ops:
+        if isinstance(o, tuple):
+            out += [f"--{o[0]}"] + [str(v) for v in o[1:]]
+        else:
+            out.append(f"--{o}")
+    return out
+
+
+def scored_map(rng, rows, decimal):
+    """BED5 (+ sometimes more columns) with many equal scores and equal rows"""
+    out = []
+    for i, (c, s, e) in enumerate(rows):
+        if decimal:
+            sc = rng.choice(["0.5", "1.25", "-3.75", f"{rng.randint(0, 999) / 100}", f"{rng.randint(0, 99999) / 1000}",
+                             "1e-3", "7"])
+        else:
+            sc = str(rng.choice([1, 2, 3, rng.randint(0, 50), rng.randint(-20, 999)]))
+        out.append(f"{c}\t{s}\t{e}\tid{rng.randint(0, 6)}\t{sc}" + ("\tx\t+" if i % 3 == 0 else "") + "\n")
+    return "".join(out).encode()
+
+
+CRITS = [("bp-ovr", 1), ("bp-ovr", 6), ("range", 20), ("fraction-ref", "0.4"), ("fraction-map", "0.5"),
+         ("fraction-either", "0.6"), ("fraction-both", "0.2"), ("exact", None)]
+OPSETS = [["min-element", "max-element", "count"],
+          ["min-element-rand", "max-element-rand"],
+          ["wmean", "mean", ("tmean", 0.1, 0.1)],
+          [("tmean", 0.2, 0.3), ("tmean", 0, 0), ("tmean", 0.3, 0.7), ("tmean", 0.25, 0)],
+          [("tmean", 0, 0.5), ("tmean", 0.5, 0.5), ("tmean", 0.05, 0.4), "echo"]]
+
+
+def _kw(crit, val):
+    return {"overlap_bp": val} if crit == "bp-ovr" else {"criterion": crit, "value": val}
+
+
+def _copt(crit, val):
+    return [f"--{crit}"] + ([str(val)] if val is not None else [])
+
+
+@pytest.mark.parametrize("decimal", [False, True])
+@pytest.mark.parametrize("crit,val", CRITS)
+def test_new_visitors_vs_oracle(eng, oracle_bin, crit, val, decimal):
+    rng = random.Random(zlib.crc32(repr(("vis", crit, val, decimal)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(6):
+            ref = randbed.rows(rng, rng.choice([1, 30, 400, 1500]), span=rng.choice([300, 3000]),
+                               maxlen=rng.choice([10, 80]))
+            mp = randbed.rows(rng, rng.choice([1, 50, 700, 2500]), span=rng.choice([300, 3000]),
+                              maxlen=rng.choice([10, 80, 300]))
+            if trial % 2:  # equal coordinates (equal scores too, often), exact matches
+                mp = sorted(mp + mp[::3] + mp[::4] + ref[::5], key=lambda r: (r[0].encode(), r[1], r[2]))
+            rt = randbed.text(ref, rest="cols", rng=rng).encode()
+            mt = scored_map(rng, mp, decimal)
+            for ops in OPSETS:
+                for skip in (True, False):
+                    args = argv(ops) + _copt(crit, val) + (["--skip-unmapped"] if skip else [])
+                    want, err, rc = oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                    got, stopped = gpu(eng, ops, rt, mt, skip_unmapped=skip, **_kw(crit, val))
+                    assert got == want, (crit, val, ops, skip, trial)
+                    assert stopped == (rc != 0), (crit, val, ops, skip, trial, err)
+
+
+def test_element_stop_matches_reference_text(gpu_bin, oracle_bin, tmp_path):
+    """an unmapped reference row under --max-element: the reference prints what precedes the
+    throw (earlier rows, this row's earlier columns and delimiters) and exits with
+    "Unable to process a 'NAN' with PrintAllScorePrecision." (ProcessBedVisitorRow.hpp:206-208)"""
+    ref = b"chr1\t10\t50\nchr1\t100\t120\nchr1\t300\t400\nchr1\t500\t600\n"
+    mp = b"chr1\t5\t20\ta\t3\nchr1\t15\t30\tb\t7\nchr1\t105\t110\te\t2\n"
+    paths = _paths([ref, mp], str(tmp_path))
+    for ops in (["--echo", "--count", "--max-element"], ["--min-element"], ["--echo", "--max-element-rand", "--count"]):
+        o = subprocess.run([oracle_bin["bedmap"]] + ops + paths, capture_output=True)
+        g = subprocess.run([gpu_bin["bedmap"]] + ops + paths, capture_output=True)
+        assert o.returncode != 0 and g.returncode != 0
+        assert g.stdout == o.stdout, ops
+        assert g.stderr == o.stderr, ops
+        assert b"Unable to process a 'NAN' with PrintAllScorePrecision." in g.stderr
+
+
+SINGLE_OPSETS = [["echo", "count", "sum"], ["echo-map-id", "echo-ref-name", "bases-uniq"],
+                 ["echo", "mean", "median", "max-element"], ["variance", ("tmean", 0.1, 0.2), "wmean"],
+                 ["echo-map", "echo-ref-row-id", "indicator"]]
+
+
+@pytest.mark.parametrize("crit,val", [("bp-ovr", 1), ("bp-ovr", 10), ("range", 30), ("fraction-both", "0.5"),
+                                      ("exact", None)])
+def test_single_file_mode_vs_oracle(eng, oracle_bin, crit, val):
+    """bedmap <ops> <file>: every row is a reference row and a map row (sweep overload 1),
+    read as the map type, so --echo re-prints a BED5 score with "%lf" (Bedmap.cpp:660-700)"""
+    rng = random.Random(zlib.crc32(repr(("single", crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(6):
+            rows = randbed.rows(rng, rng.choice([1, 40, 600, 2500]), span=rng.choice([300, 3000]),
+                                maxlen=rng.choice([10, 80, 300]))
+            if trial % 2:
+                rows = sorted(rows + rows[::3], key=lambda r: (r[0].encode(), r[1], r[2]))
+            t = scored_map(rng, rows, decimal=trial % 3 == 0)
+            for ops in SINGLE_OPSETS:
+                args = argv(ops) + _copt(crit, val)
+                want, err, rc = oracle(oracle_bin["bedmap"], args, [t], td)
+                assert rc == 0, err
+                got, stopped = gpu(eng, ops, t, None, **_kw(crit, val))
+                assert not stopped
+                assert got == want, (crit, val, ops, trial)
+
+
+def test_single_file_cli_and_tmean_arguments(gpu_bin, oracle_bin, tmp_path):
+    rng = random.Random(3)
+    rows = randbed.rows(rng, 500, span=2000, maxlen=60)
+    t = scored_map(rng, rows, decimal=True)
+    p = _paths([t], str(tmp_path))[0]
+    for ops in (["--echo", "--count", "--mean"], ["--tmean", "0.1", "0.3", "--wmean", "--echo-ref-size"]):
+        o = subprocess.run([oracle_bin["bedmap"]] + ops + [p], capture_output=True, check=True)
+        g = subprocess.run([gpu_bin["bedmap"]] + ops + [p], capture_output=True)
+        assert g.returncode == 0, g.stderr
+        assert g.stdout == o.stdout, ops
+    # argument checks and messages of bedmap/src/Input.hpp:303-325
+    for bad, msg in ((["--tmean"], b"No <low> arg given for --tmean"),
+                     (["--tmean", "x", "0.1"], b"Non-numeric argument: x for --tmean"),
+                     (["--tmean", "0.1", "--count"], b"Non-numeric argument: --count for --tmean"),
+                     (["--tmean", "1.5", "0"], b"--tmean Expect 0 <= low < hi <= 1"),
+                     (["--tmean", "0.6", "0.6"], b"--tmean Expect (low + hi) <= 1.")):
+        g = subprocess.run([gpu_bin["bedmap"]] + bad + [p, p], capture_output=True)
+        assert g.returncode != 0 and msg in g.stderr, (bad, g.stderr)
+
+
+def test_tmean_long_segment(eng, oracle_bin):
+    """one chromosome-long row keeps every window overlapping the next: one segment, one
+    sequential replay over all rows, still exact"""
+    rng = random.Random(9)
+    ref = randbed.rows(rng, 3000, chroms=["chr1"], span=5000, maxlen=40)
+    mp = randbed.rows(rng, 4000, chroms=["chr1"], span=5000, maxlen=40) + [("chr1", 0, 6000)]
+    mp.sort(key=lambda r: (r[1], r[2]))
+    rt = randbed.text(ref).encode()
+    mt = scored_map(rng, mp, decimal=True)
+    with tempfile.TemporaryDirectory() as td:
+        for ops in ([("tmean", 0.1, 0.1), "count"], [("tmean", 0.2, 0.0), ("tmean", 0.3, 0.7)]):
+            want, err, rc = oracle(oracle_bin["bedmap"], argv(ops), [rt, mt], td)
+            got, _ = gpu(eng, ops, rt, mt)
+            assert got == want, ops

@@ -179,3 +179,35 @@ def test_sortbed_oracle_matches_python_model(oracle_bin, tmp_path):
         got = subprocess.run([oracle_bin["sortbed"], str(p)], stdout=subprocess.PIPE,
                              check=True).stdout.decode()
         assert got == want, trial
+
+
+# hand-worked answers for the visitors restated last (ExtremeVisitor with
+# ScoreThenGenomicCompare*, TrimmedMeanVisitor, WeightedAverageVisitor, sweep overload 1)
+VIS_REF = "chr1\t10\t50\nchr1\t100\t120\nchr1\t300\t400\n"
+VIS_MAP = ("chr1\t5\t20\ta\t3\nchr1\t15\t30\tb\t7\nchr1\t15\t30\tc\t7\n"
+           "chr1\t40\t60\td\t1.5\nchr1\t105\t110\te\t2\n")
+
+
+def test_bedmap_oracle_new_visitors_by_hand(oracle_bin, tmp_path):
+    r, m = tmp_path / "r.bed", tmp_path / "m.bed"
+    r.write_text(VIS_REF)
+    m.write_text(VIS_MAP)
+    run = lambda *a: subprocess.run([oracle_bin["bedmap"], *a], capture_output=True)
+    o = run("--echo", "--max-element", "--min-element", "--tmean", "0.1", "0.1", "--wmean",
+            "--max-element-rand", "--skip-unmapped", str(r), str(m))
+    # row 1: b and c tie on (7, chr1 15 30): the set keeps b, added first (its full_rest
+    # "b" < "c"); -rand: the last of the equal scores here; trimmed mean of 4 with nothing
+    # trimmed = 18.5/4; weights .25/.375/.375/.25 of scores 3/7/7/1.5 -> 6.375/1.25
+    assert o.stdout.decode() == (
+        "chr1\t10\t50|chr1\t15\t30\tb\t7.000000|chr1\t40\t60\td\t1.500000|4.625000|5.100000|chr1\t15\t30\tc\t7.000000\n"
+        "chr1\t100\t120|chr1\t105\t110\te\t2.000000|chr1\t105\t110\te\t2.000000|2.000000|2.000000|chr1\t105\t110\te\t2.000000\n")
+    # an unmapped row: PrintAllScorePrecision throws on NaN after what precedes it
+    o = run("--echo", "--min-element", str(r), str(m))
+    assert o.returncode != 0
+    assert o.stdout.decode().endswith("chr1\t300\t400|")
+    assert o.stderr.decode() == ("May use bedmap --help for more help.\n\n"
+                                 "Error: Unable to process a 'NAN' with PrintAllScorePrecision.\n")
+    # single-file mode: rows re-printed as B5Rest ("%lf" score); --tmean 0.2 0.3 of {3,7,7}
+    # trims one row at the bottom: (3 + 7 - 3) / 1
+    o = run("--echo", "--count", "--tmean", "0.2", "0.3", str(m))
+    assert o.stdout.decode().splitlines()[0] == "chr1\t5\t20\ta\t3.000000|3|7.000000"
