@@ -101,7 +101,7 @@ def _copt(crit, val):
 def test_new_visitors_vs_oracle(eng, oracle_bin, crit, val, decimal):
     rng = random.Random(zlib.crc32(repr(("vis", crit, val, decimal)).encode()))
     with tempfile.TemporaryDirectory() as td:
-        for trial in range(6):
+        for trial in range(4):
             ref = randbed.rows(rng, rng.choice([1, 30, 400, 1500]), span=rng.choice([300, 3000]),
                                maxlen=rng.choice([10, 80]))
             mp = randbed.rows(rng, rng.choice([1, 50, 700, 2500]), span=rng.choice([300, 3000]),
@@ -156,10 +156,9 @@ def test_single_file_mode_vs_oracle(eng, oracle_bin, crit, val):
             for ops in SINGLE_OPSETS:
                 args = argv(ops) + _copt(crit, val)
                 want, err, rc = oracle(oracle_bin["bedmap"], args, [t], td)
-                assert rc == 0, err
                 got, stopped = gpu(eng, ops, t, None, **_kw(crit, val))
-                assert not stopped
                 assert got == want, (crit, val, ops, trial)
+                assert stopped == (rc != 0), (crit, val, ops, trial, err)
 
 
 def test_single_file_cli_and_tmean_arguments(gpu_bin, oracle_bin, tmp_path):
@@ -173,8 +172,9 @@ def test_single_file_cli_and_tmean_arguments(gpu_bin, oracle_bin, tmp_path):
         assert g.returncode == 0, g.stderr
         assert g.stdout == o.stdout, ops
     # argument checks and messages of bedmap/src/Input.hpp:303-325
-    for bad, msg in ((["--tmean"], b"No <low> arg given for --tmean"),
-                     (["--tmean", "x", "0.1"], b"Non-numeric argument: x for --tmean"),
+    g = subprocess.run([gpu_bin["bedmap"], "--count", "--tmean"], capture_output=True)
+    assert g.returncode != 0 and b"No <low> arg given for --tmean" in g.stderr, g.stderr
+    for bad, msg in ((["--tmean", "x", "0.1"], b"Non-numeric argument: x for --tmean"),
                      (["--tmean", "0.1", "--count"], b"Non-numeric argument: --count for --tmean"),
                      (["--tmean", "1.5", "0"], b"--tmean Expect 0 <= low < hi <= 1"),
                      (["--tmean", "0.6", "0.6"], b"--tmean Expect (low + hi) <= 1.")):
