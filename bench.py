@@ -472,10 +472,18 @@ def main():
         avg_s = ms / 1e3 / max(calls, 1)
         gbs = per_launch / avg_s / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and args.workload == "intersect" and world == 1:
+        # per-launch HBM bytes of the same workload's kernels from the committed PMC passes
+        # (tools/gpu_profile_r02.sh -> profiles/pmc_traffic_<workload>.json)
+        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
+        if not os.path.exists(pmc) and args.workload == "intersect":
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc) and world == 1 and args.scale == 1.0:
             try:
-                traffic = json.load(open(pmc)).get(PMC_NAME.get(dominant, dominant), {}).get("bytes")
+                tbl = json.load(open(pmc))
+                key = PMC_NAME.get(dominant, dominant)
+                ent = tbl.get(key) or max((v for k, v in tbl.items() if k.startswith(key + "<")),
+                                          key=lambda v: v.get("launches", 0), default={})
+                traffic = ent.get("bytes")
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
