@@ -76,7 +76,34 @@ static int read_text(const char* path, text_buf_t* out) {
   out->data = buf;
   out->n = n;
   out->pinned = pinned;
+  /* a Starch archive from a file becomes the BED text its streams hold (the reference
+   * reads Starch only from files, not stdin: AllocateIterator_BED_starch.hpp:62) */
+  if (fd != 0 && bg_starch_is(buf, n)) {
+    char* txt = NULL;
+    uint64_t tn = 0;
+    char err[512];
+    int rc = bg_starch_decode(buf, n, NULL, &txt, &tn, err, sizeof(err));
+    if (pinned) bg_host_free(buf); else free(buf);
+    out->data = NULL;
+    if (rc) {
+      fprintf(stderr, "May use bedops --help for more help.\n\nError: %s: %s\n", path, err);
+      exit(EXIT_FAILURE);
+    }
+    out->data = txt;
+    out->n = tn;
+    out->pinned = 0;
+  }
   return 0;
+}
+
+/* the first bytes of a regular file mark a Starch archive */
+static inline int file_is_starch(const char* path) {
+  unsigned char b[4];
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return 0;
+  const ssize_t r = read(fd, b, 4);
+  close(fd);
+  return r == 4 && b[0] == 0xca && b[1] == 0x5c && b[2] == 0xad && b[3] == 0xe5;
 }
 
 /* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
@@ -86,7 +113,8 @@ static int read_text(const char* path, text_buf_t* out) {
 static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, text_buf_t* t, bg_input* in) {
   struct stat st;
   memset(t, 0, sizeof(*t));
-  if (!host_needed && strcmp(path, "-") != 0 && stat(path, &st) == 0 && S_ISREG(st.st_mode)) {
+  if (!host_needed && strcmp(path, "-") != 0 && stat(path, &st) == 0 && S_ISREG(st.st_mode) &&
+      !file_is_starch(path)) {
     void* d = NULL;
     uint64_t n = 0;
     const int rc = bg_read_file_device(ctx, path, &d, &n);

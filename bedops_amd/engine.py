@@ -49,7 +49,8 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message",
            "bg_write_device", "bg_bind", "bg_group_uid", "bg_group_open", "bg_group_open_rank",
            "bg_group_size", "bg_group_ctx", "bg_group_close", "bg_group_gather", "bg_device_free",
-           "bg_device_gather_host", "bg_read_file_device", "bg_sortbed"]
+           "bg_device_gather_host", "bg_read_file_device", "bg_sortbed", "bg_starch_is",
+           "bg_starch_decode"]
 UID_BYTES = 128
 
 
@@ -113,6 +114,9 @@ def load_library():
         raise BedgpuError(-6, f"{p} not built (run `make lib` or __graft_entry__.build())")
     L = ctypes.CDLL(p)
     vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    L.bg_starch_is.argtypes = [vp, u64]
+    L.bg_starch_decode.argtypes = [vp, u64, ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(u64),
+                                   ctypes.c_char_p, u64]
     L.bg_open.argtypes = [ctypes.POINTER(vp), i32]
     L.bg_close.argtypes = [vp]
     L.bg_close.restype = None
@@ -191,6 +195,24 @@ def parse_overlap_spec(spec):
             raise BedgpuError(-6, "Expect percentage less than or equal to 100%")
         return (1.0, 0) if d == 0 else (d, 1)
     return float(int(s.lstrip("-"))), 0
+
+
+def starch_to_bed(data, chrom=None):
+    """A Starch archive's bytes -> the BED text the reference's reader yields (host decode,
+    bg_starch_decode); bytes that are not a Starch archive are returned unchanged."""
+    L = load_library()
+    data = bytes(data)
+    if not L.bg_starch_is(data, len(data)):
+        return data
+    out, n, err = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.create_string_buffer(512)
+    rc = L.bg_starch_decode(data, len(data), chrom.encode() if chrom else None, ctypes.byref(out),
+                            ctypes.byref(n), err, 512)
+    if rc:
+        raise BedgpuError(rc, err.value.decode(errors="replace"))
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        ctypes.CDLL(None).free(out)
 
 
 class Result:

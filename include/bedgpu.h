@@ -238,6 +238,17 @@ int bg_read_file_device(bg_ctx* ctx, const char* path, void** dptr, uint64_t* nb
 /* make ctx's device current on the calling thread (a host thread per device in a group) */
 int bg_bind(bg_ctx* ctx);
 
+/* ---- Starch input (replaces the Starch branch of Bed::allocate_iterator_starch_bed,
+ * interfaces/general-headers/data/bed/AllocateIterator_BED_starch.hpp:62,100-112, and
+ * starch::Starch::extractLine, data/starch/starchApi.hpp:1490-1760) ------------------------
+ * bg_starch_is: the bytes start a Starch v2 archive (magic ca 5c ad e5, starchApi.hpp:645-676).
+ * bg_starch_decode: every stream (or only `chrom`; NULL = all) decompressed on the host
+ * (bzip2 / gzip) and reverse-transformed into the BED text the reference's reader yields
+ * (unstarchHelpers.c:884-1160); *out is malloc'd (free()), err gets a message. */
+int bg_starch_is(const void* data, uint64_t nbytes);
+int bg_starch_decode(const void* data, uint64_t nbytes, const char* chrom, char** out, uint64_t* outlen,
+                     char* err, uint64_t errcap);
+
 /* ---- multi-GPU: chromosome shards reassembled over RCCL ------------
  * Replaces the reference's per-chromosome process fan-out (`--chrom` per process,
  * docs/content/reference/set-operations/bedops.rst:721-726; comparators start with
