@@ -96,14 +96,15 @@ static int read_text(const char* path, text_buf_t* out) {
   return 0;
 }
 
-/* the first bytes of a regular file mark a Starch archive */
+/* the first bytes of a regular file mark a Starch archive (v2 magic or v1 JSON head) */
 static inline int file_is_starch(const char* path) {
-  unsigned char b[4];
+  unsigned char b[512];
   int fd = open(path, O_RDONLY);
   if (fd < 0) return 0;
-  const ssize_t r = read(fd, b, 4);
+  const ssize_t r = read(fd, b, sizeof(b));
   close(fd);
-  return r == 4 && b[0] == 0xca && b[1] == 0x5c && b[2] == 0xad && b[3] == 0xe5;
+  if (r >= 4 && b[0] == 0xca && b[1] == 0x5c && b[2] == 0xad && b[3] == 0xe5) return 1;
+  return r > 0 && bg_starch_is(b, (uint64_t)r);
 }
 
 /* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
