@@ -270,7 +270,7 @@ int main(int argc, char** argv) {
   text_buf_t tr = {0}, tm = {0};
   bg_input in[2];
   memset(in, 0, sizeof(in));
-  if (read_input(ctx, argv[a], check || ec, &tr, &in[0])) arg_error("Unable to read the reference file");
+  if (read_input_chrom(ctx, argv[a], chrom, check || ec, &tr, &in[0])) arg_error("Unable to read the reference file");
   /* --ec: the reference file is B3Rest, the map file B3Rest/B4Rest/B5Rest by the
    * operations' MapFields (Input.hpp:401-418, Bedmap.cpp:601-655) */
   const int mapfields = need5 ? 5 : (need4 ? 4 : 3);
@@ -304,7 +304,7 @@ int main(int argc, char** argv) {
     return EXIT_SUCCESS;
   }
   {
-    if (read_input(ctx, argv[a + 1], check || ec, &tm, &in[1])) arg_error("Unable to read the map file");
+    if (read_input_chrom(ctx, argv[a + 1], chrom, check || ec, &tm, &in[1])) arg_error("Unable to read the map file");
     if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1);
     if (ec) {
       apply_ec_header(&tm);

@@ -372,7 +372,7 @@ int main(int argc, char** argv) {
       in[i].data = tx[i].data;
       in[i].nbytes = tx[i].n;
       in[i].on_device = 0;
-    } else if (read_input(ctx, argv[a + i], check || ec, &tx[i], &in[i])) {
+    } else if (read_input_chrom(ctx, argv[a + i], chrom, check || ec, &tx[i], &in[i])) {
       char b[1024];
       snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
       die_msg(PROG, b);

@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -137,6 +138,91 @@ static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, tex
   in->nbytes = t->n;
   in->on_device = 0;
   return 0;
+}
+
+/* --chrom on a regular, sorted BED file: only that chromosome's lines are read. The
+ * reference seeks to them with find_bed_range and stops at the first row of another
+ * chromosome (AllocateIterator_BED_starch.hpp:113-160, operator++ :176-181), so rows of
+ * other chromosomes are never parsed (nor checked). Bisection over the mapped file on the
+ * first token of each line (strcmp order); -1 when a probed line has no usable token
+ * (headers, blank lines: the whole file is read instead). */
+static int ck_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+static uint64_t ck_line_start(const char* t, uint64_t p) {
+  while (p > 0 && t[p - 1] != '\n') --p;
+  return p;
+}
+static uint64_t ck_next_line(const char* t, uint64_t n, uint64_t p) {
+  const char* q = (const char*)memchr(t + p, '\n', (size_t)(n - p));
+  return q ? (uint64_t)(q - t) + 1 : n;
+}
+/* strcmp(token of the line at p, chrom), or 2 when the line has no token */
+static int ck_cmp(const char* t, uint64_t n, uint64_t p, const char* chrom) {
+  while (p < n && ck_ws(t[p])) ++p;
+  uint64_t q = p;
+  while (q < n && t[q] != '\n' && !ck_ws(t[q])) ++q;
+  if (q == p) return 2;
+  const size_t k = strlen(chrom), m = (size_t)(q - p);
+  const int v = memcmp(t + p, chrom, m < k ? m : k);
+  if (v) return v < 0 ? -1 : 1;
+  return m == k ? 0 : (m < k ? -1 : 1);
+}
+/* first line start whose token compares > `le ? 0 : -1` with chrom */
+static int ck_bound(const char* t, uint64_t n, const char* chrom, int le, uint64_t* out) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t ls = ck_line_start(t, lo + (hi - lo) / 2);
+    const int c = ck_cmp(t, n, ls, chrom);
+    if (c == 2) return -1;
+    if (le ? c <= 0 : c < 0) lo = ck_next_line(t, n, ls);
+    else hi = ls;
+  }
+  *out = lo;
+  return 0;
+}
+static int chrom_byte_range(const char* path, const char* chrom, uint64_t* a, uint64_t* b) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= 0) { close(fd); return -1; }
+  const uint64_t n = (uint64_t)st.st_size;
+  const char* t = (const char*)mmap(NULL, (size_t)n, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (t == MAP_FAILED) return -1;
+  int rc = ck_bound(t, n, chrom, 0, a);
+  if (!rc) rc = ck_bound(t, n, chrom, 1, b);
+  munmap((void*)t, (size_t)n);
+  return rc;
+}
+/* read_input for --chrom: the chromosome's byte range of a regular BED file into host
+ * memory (the loader copies it to the device); other inputs as read_input */
+static inline int read_input_chrom(bg_ctx* ctx, const char* path, const char* chrom, int host_needed,
+                                   text_buf_t* t, bg_input* in) {
+  uint64_t a = 0, b = 0;
+  struct stat st;
+  if (chrom && !host_needed && strcmp(path, "-") != 0 && stat(path, &st) == 0 && S_ISREG(st.st_mode) &&
+      !file_is_starch(path) && chrom_byte_range(path, chrom, &a, &b) == 0 && b >= a) {
+    memset(t, 0, sizeof(*t));
+    char* buf = (char*)malloc((size_t)(b - a) + 16);
+    int fd = open(path, O_RDONLY);
+    if (!buf || fd < 0) { free(buf); if (fd >= 0) close(fd); return -1; }
+    uint64_t got = 0;
+    while (got < b - a) {
+      const ssize_t r = pread(fd, buf + got, (size_t)(b - a - got), (off_t)(a + got));
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) break;
+      got += (uint64_t)r;
+    }
+    close(fd);
+    if (got != b - a) { free(buf); return -1; }
+    t->data = buf;
+    t->n = got;
+    t->pinned = 0;
+    in->data = buf;
+    in->nbytes = got;
+    in->on_device = 0;
+    return 0;
+  }
+  return read_input(ctx, path, host_needed, t, in);
 }
 
 static void free_text(text_buf_t* t) {

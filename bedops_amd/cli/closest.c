@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
   text_buf_t t[2] = {{0}, {0}};
   bg_input in[2];
   for (int k = 0; k < 2; ++k) {
-    if (read_input(ctx, argv[a + k], check || ec, &t[k], &in[k])) arg_error("Unable to read an input file");
+    if (read_input_chrom(ctx, argv[a + k], chrom, check || ec, &t[k], &in[k])) arg_error("Unable to read an input file");
     if (check) ec_check(PROG, ctx, argv[a + k], &t[k], 3, 1);
     if (ec) {
       apply_ec_header(&t[k]);
