@@ -110,32 +110,21 @@ __device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, i
 __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, uint32_t* kept,
                        bool emit) {
   const uint32_t cap = A.cap;
-  // The file candidates stream through registers in aligned groups of 4 (16-byte loads,
-  // 32 B of each of cs / ce: one sector apiece), the next group loaded while the current one
-  // is consumed. ~300K chunk threads walk disjoint regions at once, far more lines than L2
-  // holds: with one 8-byte load per candidate every load fetched a whole sector again
-  // (profiles/pmc_traffic_closest.json: 127 GB read for 16 GB of candidates).
-  const uint64_t nc = A.nc;
-  uint64_t gb = S.fp & ~3ull;  // index of g[0]: the group holding S.fp, then the next one
-  int64_t gs[8], ge[8];
-  auto load_group = [&](uint64_t base, int64_t* xs, int64_t* xe) {
-    if (base + 4 <= nc) {
-      const longlong2 a = reinterpret_cast<const longlong2*>(A.cs + base)[0];
-      const longlong2 b2 = reinterpret_cast<const longlong2*>(A.cs + base)[1];
-      const longlong2 c = reinterpret_cast<const longlong2*>(A.ce + base)[0];
-      const longlong2 d = reinterpret_cast<const longlong2*>(A.ce + base)[1];
-      xs[0] = a.x; xs[1] = a.y; xs[2] = b2.x; xs[3] = b2.y;
-      xe[0] = c.x; xe[1] = c.y; xe[2] = d.x; xe[3] = d.y;
-    } else {
+  // the next CPF file candidates, loaded ahead: the scan's loads are independent of its
+  // decisions, so the file stream is software-pipelined (one candidate at a time each
+  // lane waited an L2 round trip per candidate; lanes read disjoint regions)
+#ifndef BG_CPF
+#define BG_CPF 4
+#endif
+  constexpr int CPF = BG_CPF;
+  int64_t pcs[CPF], pce[CPF];
+  const uint64_t nc1 = A.nc ? A.nc - 1 : 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        xs[i] = base + i < nc ? A.cs[base + i] : 0;
-        xe[i] = base + i < nc ? A.ce[base + i] : 0;
-      }
-    }
-  };
-  load_group(gb, gs, ge);
-  load_group(gb + 4, gs + 4, ge + 4);
+  for (int i = 0; i < CPF; ++i) {
+    const uint64_t j = min(S.fp + i, nc1);
+    pcs[i] = A.nc ? A.cs[j] : 0;
+    pce[i] = A.nc ? A.ce[j] : 0;
+  }
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
     const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
@@ -157,18 +146,16 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
         ce = A.ce[c];
       } else if (S.fp < A.nc) {
         c = (int64_t)S.fp++;
-        const uint32_t o = (uint32_t)(c - (int64_t)gb);  // 0..3 (selects, no indexed registers)
-        cs = o == 0 ? gs[0] : (o == 1 ? gs[1] : (o == 2 ? gs[2] : gs[3]));
-        ce = o == 0 ? ge[0] : (o == 1 ? ge[1] : (o == 2 ? ge[2] : ge[3]));
-        if (o == 3) {  // the group is used up: the next one moves down, the one after loads
+        cs = pcs[0];
+        ce = pce[0];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            gs[i] = gs[i + 4];
-            ge[i] = ge[i + 4];
-          }
-          gb += 4;
-          load_group(gb + 4, gs + 4, ge + 4);
+        for (int i = 0; i + 1 < CPF; ++i) {
+          pcs[i] = pcs[i + 1];
+          pce[i] = pce[i + 1];
         }
+        const uint64_t j = min(S.fp + (CPF - 1), nc1);
+        pcs[CPF - 1] = A.cs[j];
+        pce[CPF - 1] = A.ce[j];
       } else {
         eof = true;
         break;
