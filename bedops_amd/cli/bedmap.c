@@ -13,6 +13,7 @@
  * available in this build.
  */
 #include "cli_common.h"
+#include "cli_shard.h"
 
 static const char* PROG = "bedmap";
 
@@ -47,6 +48,16 @@ static void usage(FILE* f) {
 }
 
 static void arg_error(const char* msg) { die_msg(PROG, msg); }
+
+typedef struct {
+  bg_map_opts o;
+  int single;
+} map_args_t;
+/* one chromosome shard: the same bg_map call on the member's set */
+static int run_map(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
+  const map_args_t* m = (const map_args_t*)arg;
+  return bg_map(ctx, set, 0, m->single ? 0 : 1, &m->o, res);
+}
 
 int main(int argc, char** argv) {
   if (argc <= 1) {
@@ -264,6 +275,41 @@ int main(int argc, char** argv) {
   }
   if (nf == 2 && !strcmp(argv[a], "-") && !strcmp(argv[a + 1], "-")) arg_error("Cannot have both input files set to '-'");
 
+  /* input kinds: the reference file B3Rest (--echo), the map file by the operations'
+   * MapFields (Input.hpp:401-418); single-file mode reads the one file as the map type */
+  const int mkind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
+  const int rkind = need_rest ? BG_BED3_REST : BG_BED3;
+  const int skind = need5 ? ((map_rest || need_rest) ? BG_BED5_REST : BG_BED5)
+                          : ((map_rest || need_rest || (need4 && !need5)) ? BG_BED3_REST : BG_BED3);
+  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h). Overlaps and
+   * visitors are chromosome-local except --echo-ref-row-id (one line counter for the file),
+   * an element operation's stop at the file's first unmapped row, and decimal running sums
+   * (one double across the file: bg_map refuses them on a shard and the run falls back to
+   * one device, as on any shard error) */
+  int shardable = !check && !ec && !chrom && getenv("BEDGPU_DEVICES") != NULL;
+  for (int k = 0; k < o.n_ops; ++k) {
+    if (o.ops[k] == BG_MAP_ECHO_REF_ROW_ID) shardable = 0;
+    if (o.ops[k] >= BG_MAP_MIN_ELEMENT && o.ops[k] <= BG_MAP_MAX_ELEMENT_RAND && !o.skip_unmapped) shardable = 0;
+  }
+  for (int i = a; i < argc; ++i)
+    if (!strcmp(argv[i], "-")) shardable = 0;
+  if (shardable) {
+    text_buf_t stx[2];
+    bg_input sin[2];
+    memset(stx, 0, sizeof(stx));
+    memset(sin, 0, sizeof(sin));
+    for (int k = 0; k < nf; ++k)
+      if (read_text(argv[a + k], &stx[k])) arg_error(k ? "Unable to read the map file" : "Unable to read the reference file");
+    sin[0].kind = nf == 1 ? skind : rkind;
+    sin[1].kind = mkind;
+    map_args_t ma;
+    ma.o = o;
+    ma.o.shard = 1;
+    ma.single = nf == 1;
+    if (shard_run(PROG, nf, sin, stx, run_map, &ma) == 0) return EXIT_SUCCESS;
+    for (int k = 0; k < nf; ++k) free_text(&stx[k]);  /* one device after all */
+  }
+
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
@@ -280,14 +326,11 @@ int main(int argc, char** argv) {
     in[0].data = tr.data;
     in[0].nbytes = tr.n;
   }
-  in[0].kind = need_rest ? BG_BED3_REST : BG_BED3;
-  const int mkind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
+  in[0].kind = rkind;
   if (nf == 1) {
     /* single-file mode (Bedmap.cpp:196-246, sweep overload 1): every row is a reference row
      * and a map row, read as the map type (Bedmap.cpp:660-700) */
-    const int m4 = need4 && !need5;
-    in[0].kind = need5 ? ((map_rest || need_rest) ? BG_BED5_REST : BG_BED5)
-                       : ((map_rest || need_rest || m4) ? BG_BED3_REST : BG_BED3);
+    in[0].kind = skind;
     bg_set* set = NULL;
     if ((rc = bg_load(ctx, 1, in, &set))) die_ctx(PROG, ctx, rc);
     free_text(&tr);

@@ -12,6 +12,7 @@
  * <msg>" (ClosestFeature.cpp:93-95).
  */
 #include "cli_common.h"
+#include "cli_shard.h"
 
 static const char* PROG = "closest-features";
 
@@ -39,6 +40,13 @@ static void usage(FILE* f) {
 }
 
 static void arg_error(const char* msg) { die_msg(PROG, msg); }
+
+/* one chromosome shard: findDistances never looks across chromosomes (rows of earlier
+ * chromosomes are dropped, ClosestFeature.cpp:289-291; a later chromosome ends the scan,
+ * :292-298), so the same call on a member's set gives that member's lines */
+static int run_closest(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
+  return bg_closest(ctx, set, 0, 1, (const bg_closest_opts*)arg, res);
+}
 
 int main(int argc, char** argv) {
   if (argc <= 1) {
@@ -95,6 +103,20 @@ int main(int argc, char** argv) {
     }
   }
   if (!strcmp(argv[a], "-") && !strcmp(argv[a + 1], "-")) arg_error("Cannot have both input files set to '-'");
+
+  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h) */
+  if (!check && !ec && !chrom && getenv("BEDGPU_DEVICES") && strcmp(argv[a], "-") && strcmp(argv[a + 1], "-")) {
+    text_buf_t stx[2];
+    bg_input sin[2];
+    memset(stx, 0, sizeof(stx));
+    memset(sin, 0, sizeof(sin));
+    for (int k = 0; k < 2; ++k) {
+      if (read_text(argv[a + k], &stx[k])) arg_error("Unable to read an input file");
+      sin[k].kind = BG_BED3_REST;
+    }
+    if (shard_run(PROG, 2, sin, stx, run_closest, &o) == 0) return EXIT_SUCCESS;
+    for (int k = 0; k < 2; ++k) free_text(&stx[k]);  /* one device after all */
+  }
 
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());

@@ -958,6 +958,8 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   const bool need_sq = (need & NEED_SQ) != 0;
   if (ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
     return bg_fail(c, BG_E_UNSUPPORTED, "single-file bedmap over zero-length rows is not on the GPU path");
+  if (decimal && opts->shard)
+    return bg_fail(c, BG_E_UNSUPPORTED, "decimal-score running sums span every chromosome: not on a chromosome shard");
   if (tmean) {
     if (R->has_zero_len || M->has_zero_len)
       return bg_fail(c, BG_E_UNSUPPORTED, "--tmean with zero-length rows is not on the GPU path of bedmap");

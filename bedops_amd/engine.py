@@ -92,7 +92,7 @@ class _MapOpts(ctypes.Structure):
                 ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
                 ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double),
                 ("multidelim", ctypes.c_char * 16), ("op_arg", ctypes.c_double * 16),
-                ("op_arg2", ctypes.c_double * 16)]
+                ("op_arg2", ctypes.c_double * 16), ("shard", ctypes.c_int)]
 
 
 class _ClosestOpts(ctypes.Structure):

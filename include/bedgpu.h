@@ -99,6 +99,9 @@ typedef struct bg_map_opts {
   char multidelim[16]; /* --multidelim between --echo-map* items ("" = the default ";") */
   double op_arg[16];   /* argument of ops[k] (--kth <val>; --tmean <low>)           */
   double op_arg2[16];  /* second argument of ops[k] (--tmean <hi>)                  */
+  int shard;           /* 1: the set holds some chromosomes of the inputs (multi-GPU shard):
+                          results that depend on other chromosomes (decimal-score running
+                          sums, one double across the file) are refused, BG_E_UNSUPPORTED */
 } bg_map_opts;
 /* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
  * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */

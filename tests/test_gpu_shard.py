@@ -122,3 +122,72 @@ def test_engine_group_gather_equals_single_run(oracle_bin):
             want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE,
                                   check=True).stdout
         assert got == want, world
+
+
+MAP_CASES = [
+    ["--count", "--mean", "--sum", "--max"],
+    ["--echo", "--echo-map-id", "--bases", "--median"],
+    ["--bp-ovr", "5", "--echo-map-score", "--indicator"],
+    ["--fraction-both", "0.3", "--stdev", "--echo-map-range"],
+    ["--range", "20", "--kth", "0.25", "--tmean", "0.1", "0.2"],
+    ["--skip-unmapped", "--min-element", "--max-element"],
+    ["--exact", "--count", "--echo-map"],
+]
+
+
+@pytest.mark.parametrize("case", MAP_CASES, ids=lambda c: "_".join(x.strip("-") for x in c))
+@pytest.mark.parametrize("decimal", [False, True], ids=["int", "decimal"])
+def test_bedmap_sharded_equals_single_device(gpu_bin, oracle_bin, case, decimal):
+    """bedmap windows never cross chromosomes; decimal running sums span the whole file
+    (the reference's double accumulators), so such a request falls back to one device"""
+    rng = random.Random(zlib.crc32(repr((case, decimal)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(3):
+            ref = randbed.rows(rng, rng.choice([1, 300, 2000]),
+                               chroms=rng.sample(CHROMS, rng.choice([1, 4, 9])), span=4000,
+                               maxlen=rng.choice([10, 120]))
+            mp = randbed.rows(rng, rng.choice([1, 500, 3000]),
+                              chroms=rng.sample(CHROMS, rng.choice([1, 4, 9])), span=4000,
+                              maxlen=rng.choice([10, 120]))
+            pr = randbed.write(os.path.join(td, f"r{trial}.bed"),
+                               randbed.text(ref, rest="cols", rng=rng))
+            mtext = randbed.text(mp, rest="bed5", rng=rng)
+            if decimal:
+                mtext = "".join(ln.rsplit("\t", 1)[0] + f"\t{rng.randint(-999, 999) / 8}\n"
+                                for ln in mtext.splitlines())
+            pm = randbed.write(os.path.join(td, f"m{trial}.bed"), mtext)
+            for files in ([pr, pm], [pm]):   # two files, and single-file mode
+                want = subprocess.run([oracle_bin["bedmap"], *case, *files],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+                for devs in (None, "0,0", "0,0,0"):
+                    got = _cli(gpu_bin["bedmap"], case + files, devs)
+                    assert (got.returncode == 0) == (want.returncode == 0), (got.stderr, devs)
+                    assert got.stdout == want.stdout, (case, trial, files, devs)
+
+
+CLOSEST_CASES = [[], ["--closest"], ["--dist"], ["--closest", "--dist", "--no-overlaps"],
+                 ["--no-ref", "--dist"], ["--delim", "|", "--closest", "--no-overlaps"]]
+
+
+@pytest.mark.parametrize("case", CLOSEST_CASES, ids=lambda c: "_".join(x.strip("-|") for x in c) or "plain")
+def test_closest_sharded_equals_single_device(gpu_bin, oracle_bin, case):
+    """findDistances drops earlier-chromosome candidates and stops at a later chromosome,
+    so each chromosome's lines depend on that chromosome alone"""
+    rng = random.Random(zlib.crc32(repr(case).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(4):
+            files = []
+            for f in range(2):
+                rows = randbed.rows(rng, rng.choice([1, 200, 2500]),
+                                    chroms=rng.sample(CHROMS, rng.choice([1, 4, 9])),
+                                    span=rng.choice([3000, 30000]), maxlen=rng.choice([10, 120]),
+                                    zero_frac=0.03)
+                p = os.path.join(td, f"c{trial}_{f}.bed")
+                randbed.write(p, randbed.text(rows, rest="cols" if f == 0 else "bed5", rng=rng))
+                files.append(p)
+            want = subprocess.run([oracle_bin["closest"], *case, *files], stdout=subprocess.PIPE,
+                                  check=True).stdout
+            for devs in (None, "0,0", "0,0,0"):
+                got = _cli(gpu_bin["closest"], case + files, devs)
+                assert got.returncode == 0, got.stderr
+                assert got.stdout == want, (case, trial, devs)
