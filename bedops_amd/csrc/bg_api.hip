@@ -318,41 +318,62 @@ static int write_all(int fd, const char* p, uint64_t n) {
   return 0;
 }
 
-// streams n bytes of device memory to fd through two pinned buffers, so the D2H copy of
-// chunk k+1 overlaps write(2) of chunk k; every exit path frees the buffers and events
+// BEDGPU_RD_THREADS (1..32, default 8) and BEDGPU_RD_CHUNK_MB (1..64, default 16) size the
+// ring; read once per process (the slots are allocated at a context's first read)
+static int rd_env(const char* name, int dflt, int lo, int hi) {
+  const char* s = getenv(name);
+  if (!s || !*s) return dflt;
+  const int v = atoi(s);
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+static const int RD_THREADS = rd_env("BEDGPU_RD_THREADS", 8, 1, 32);
+static const uint64_t RD_CHUNK = (uint64_t)rd_env("BEDGPU_RD_CHUNK_MB", 16, 1, 64) << 20;
+
+// streams n bytes of device memory to fd through pinned buffers, so the D2H copies of the
+// next chunks overlap write(2) of this one: the context's reader ring when it exists (its
+// slots are free once the loader's stream has waited for the input copies, and the copies
+// below are on that stream), else two 64 MiB buffers of its own; every exit path frees
+// what it allocated
 extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
   if (!c || (!d && n)) return BG_E_ARG;
   if (n == 0) return 0;
   bg_bind(c);
-  const uint64_t CH = 64ull << 20;
-  char* hb[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  const bool ring = !c->rd_slot.empty();
+  const uint64_t CH = ring ? RD_CHUNK : (64ull << 20);
+  const uint64_t ns = ring ? c->rd_slot.size() : 2;
+  char* own[2] = {nullptr, nullptr};
+  hipEvent_t own_ev[2] = {nullptr, nullptr};
   int rc = 0;
-  for (int k = 0; k < 2 && !rc; ++k) {
-    hipError_t e = hipHostMalloc((void**)&hb[k], CH, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+  for (int k = 0; k < 2 && !ring && !rc; ++k) {
+    hipError_t e = hipHostMalloc((void**)&own[k], CH, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&own_ev[k], hipEventDisableTiming);
     if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device buffers");
   }
+  char* const* hb = ring ? c->rd_slot.data() : own;
+  hipEvent_t* ev = ring ? c->rd_ev.data() : own_ev;
   const char* src = (const char*)d;
   const uint64_t nch = (n + CH - 1) / CH;
   auto issue = [&](uint64_t k) -> int {
     const uint64_t off = k * CH, len = std::min(CH, n - off);
-    hipError_t e = hipMemcpyAsync(hb[k & 1], src + off, len, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipEventRecord(ev[k & 1], c->stream);
+    hipError_t e = hipMemcpyAsync(hb[k % ns], src + off, len, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(ev[k % ns], c->stream);
     return e == hipSuccess ? 0 : bg_hip_fail(c, e, "bg_write_device copy");
   };
-  if (!rc) rc = issue(0);
+  for (uint64_t k = 0; k < std::min(ns, nch) && !rc; ++k) rc = issue(k);
   for (uint64_t k = 0; k < nch && !rc; ++k) {
-    hipError_t e = hipEventSynchronize(ev[k & 1]);
+    hipError_t e = hipEventSynchronize(ev[k % ns]);
     if (e != hipSuccess) { rc = bg_hip_fail(c, e, "bg_write_device sync"); break; }
-    if (k + 1 < nch && (rc = issue(k + 1))) break;
     const uint64_t off = k * CH, len = std::min(CH, n - off);
-    if (write_all(fd, hb[k & 1], len)) rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
+    if (write_all(fd, hb[k % ns], len)) {
+      rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
+      break;
+    }
+    if (k + ns < nch) rc = issue(k + ns);  // the slot just written out takes chunk k + ns
   }
   hipStreamSynchronize(c->stream);
   for (int k = 0; k < 2; ++k) {
-    if (hb[k]) hipHostFree(hb[k]);
-    if (ev[k]) hipEventDestroy(ev[k]);
+    if (own[k]) hipHostFree(own[k]);
+    if (own_ev[k]) hipEventDestroy(own_ev[k]);
   }
   bg_mark(c, "write");
   return rc;
@@ -391,8 +412,6 @@ extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts,
 // while reading the next, so the page-cache reads run in parallel and overlap the H2D
 // copies; only 2 x RD_THREADS x 16 MiB of host memory is ever pinned (pinning the whole
 // file costs more than reading it). The context's stream waits for every copy.
-#define RD_THREADS 8
-#define RD_CHUNK (16ull << 20)
 extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint64_t* nbytes) {
   if (!c || !path || !out || !nbytes) return BG_E_ARG;
   *out = nullptr;
@@ -425,6 +444,7 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
       BG_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       c->rd_stream.push_back(s);
     }
+    bg_mark(c, "ring");
   }
   const uint64_t nch = (n + RD_CHUNK - 1) / RD_CHUNK;
   std::atomic<int> bad{0};
@@ -450,7 +470,7 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
     }
   };
   std::vector<std::thread> th;
-  const int nt = (int)std::min<uint64_t>(RD_THREADS, nch);
+  const int nt = (int)std::min<uint64_t>((uint64_t)RD_THREADS, nch);
   for (int t = 0; t < nt; ++t) th.emplace_back(reader, t);
   for (auto& x : th) x.join();
   close(fd);

@@ -8,9 +8,9 @@ out=build/ab/$name; mkdir -p $out
 objs=()
 for f in bedops_amd/csrc/*.hip; do
   o=$out/$(basename $f .hip).o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $* -c $f -o $o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-value -Wno-unused-result $* -c $f -o $o &
   objs+=($o)
 done
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libbedgpu.so ${objs[@]} -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libbedgpu.so ${objs[@]} -L/opt/rocm/lib -lrccl -lz -ldl -Wl,-rpath,/opt/rocm/lib
 echo built $out/libbedgpu.so
