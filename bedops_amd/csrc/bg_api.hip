@@ -181,9 +181,12 @@ extern "C" void bg_close(bg_ctx* c) {
   hipFree(c->dstat);
   hipHostFree(c->hstat);
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
-  for (auto s : c->rd_stream) { hipStreamSynchronize(s); hipStreamDestroy(s); }
-  for (auto e : c->rd_ev) hipEventDestroy(e);
-  for (auto p : c->rd_slot) hipHostFree(p);
+  for (auto s : c->rd_stream)
+    if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
+  for (auto e : c->rd_ev)
+    if (e) hipEventDestroy(e);
+  for (auto p : c->rd_slot)
+    if (p) hipHostFree(p);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -318,7 +321,7 @@ static int write_all(int fd, const char* p, uint64_t n) {
   return 0;
 }
 
-// BEDGPU_RD_THREADS (1..32, default 8) and BEDGPU_RD_CHUNK_MB (1..64, default 16) size the
+// BEDGPU_RD_THREADS (1..32, default 8) and BEDGPU_RD_CHUNK_MB (1..64, default 2) size the
 // ring; read once per process (the slots are allocated at a context's first read)
 static int rd_env(const char* name, int dflt, int lo, int hi) {
   const char* s = getenv(name);
@@ -327,7 +330,7 @@ static int rd_env(const char* name, int dflt, int lo, int hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 static const int RD_THREADS = rd_env("BEDGPU_RD_THREADS", 8, 1, 32);
-static const uint64_t RD_CHUNK = (uint64_t)rd_env("BEDGPU_RD_CHUNK_MB", 16, 1, 64) << 20;
+static const uint64_t RD_CHUNK = (uint64_t)rd_env("BEDGPU_RD_CHUNK_MB", 2, 1, 64) << 20;
 
 // streams n bytes of device memory to fd through pinned buffers, so the D2H copies of the
 // next chunks overlap write(2) of this one: the context's reader ring when it exists (its
@@ -430,26 +433,25 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
     close(fd);
     return BG_E_NOMEM;
   }
-  if (c->rd_slot.empty()) {
-    for (int k = 0; k < 2 * RD_THREADS; ++k) {
-      char* p = nullptr;
-      hipEvent_t e = nullptr;
-      BG_HIP(c, hipHostMalloc((void**)&p, RD_CHUNK, hipHostMallocDefault));
-      BG_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->rd_slot.push_back(p);
-      c->rd_ev.push_back(e);
-    }
-    for (int t = 0; t < RD_THREADS; ++t) {
-      hipStream_t s = nullptr;
-      BG_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      c->rd_stream.push_back(s);
-    }
-    bg_mark(c, "ring");
+  bg_mark(c, "dalloc");
+  // the ring is allocated by the reader threads themselves at the context's first read
+  // (two slots, their events and a copy stream each, in parallel: pinning is slow)
+  const bool fresh = c->rd_slot.empty();
+  if (fresh) {
+    c->rd_slot.assign(2 * RD_THREADS, nullptr);
+    c->rd_ev.assign(2 * RD_THREADS, nullptr);
+    c->rd_stream.assign(RD_THREADS, nullptr);
   }
   const uint64_t nch = (n + RD_CHUNK - 1) / RD_CHUNK;
   std::atomic<int> bad{0};
   auto reader = [&](int t) {
     if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
+    if (fresh) {
+      for (int k = 2 * t; k < 2 * t + 2; ++k)
+        if (hipHostMalloc((void**)&c->rd_slot[k], RD_CHUNK, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&c->rd_ev[k], hipEventDisableTiming) != hipSuccess) { bad = 1; return; }
+      if (hipStreamCreateWithFlags(&c->rd_stream[t], hipStreamNonBlocking) != hipSuccess) { bad = 1; return; }
+    }
     uint64_t j = 0;
     for (uint64_t k = (uint64_t)t; k < nch && !bad; k += RD_THREADS, ++j) {
       const int slot = 2 * t + (int)(j & 1);
@@ -470,19 +472,32 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
     }
   };
   std::vector<std::thread> th;
-  const int nt = (int)std::min<uint64_t>((uint64_t)RD_THREADS, nch);
+  const int nt = fresh ? RD_THREADS : (int)std::min<uint64_t>((uint64_t)RD_THREADS, nch);
   for (int t = 0; t < nt; ++t) th.emplace_back(reader, t);
   for (auto& x : th) x.join();
   close(fd);
-  for (int t = 0; t < nt; ++t) {  // the context's stream (the loader) waits for the copies
-    BG_HIP(c, hipEventRecord(c->rd_ev[2 * t], c->rd_stream[t]));
-    BG_HIP(c, hipStreamWaitEvent(c->stream, c->rd_ev[2 * t], 0));
-  }
-  if (bad) {
-    hipStreamSynchronize(c->stream);
+  bg_mark(c, "preads");
+  if (bad) {  // copies already issued still target d: drain them before releasing it
+    for (auto s : c->rd_stream)
+      if (s) hipStreamSynchronize(s);
+    if (fresh) {  // a ring that failed to build is dropped whole (the next read rebuilds it)
+      for (auto s : c->rd_stream)
+        if (s) hipStreamDestroy(s);
+      for (auto e : c->rd_ev)
+        if (e) hipEventDestroy(e);
+      for (auto p : c->rd_slot)
+        if (p) hipHostFree(p);
+      c->rd_stream.clear();
+      c->rd_ev.clear();
+      c->rd_slot.clear();
+    }
     bg_release(c, d);
     return bad == 2 ? bg_fail(c, BG_E_IO, std::string("read failed: ") + path)
                     : bg_fail(c, BG_E_HIP, std::string("copy failed: ") + path);
+  }
+  for (int t = 0; t < nt; ++t) {  // the context's stream (the loader) waits for the copies
+    BG_HIP(c, hipEventRecord(c->rd_ev[2 * t], c->rd_stream[t]));
+    BG_HIP(c, hipStreamWaitEvent(c->stream, c->rd_ev[2 * t], 0));
   }
   *out = d;
   *nbytes = n;
