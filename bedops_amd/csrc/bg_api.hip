@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <thread>
 #include <unordered_map>
 
@@ -331,6 +332,10 @@ static int rd_env(const char* name, int dflt, int lo, int hi) {
 }
 static const int RD_THREADS = rd_env("BEDGPU_RD_THREADS", 8, 1, 32);
 static const uint64_t RD_CHUNK = (uint64_t)rd_env("BEDGPU_RD_CHUNK_MB", 2, 1, 64) << 20;
+// copy streams of the ring (BEDGPU_RD_STREAMS, 0..32, default 2): reader t issues on stream
+// t % RD_STREAMS; 0 issues every copy on the context's own stream. Creating a stream costs
+// several ms on first use, and the H2D copies share one link either way.
+static const int RD_STREAMS = rd_env("BEDGPU_RD_STREAMS", 2, 0, 32);
 
 // streams n bytes of device memory to fd through pinned buffers, so the D2H copies of the
 // next chunks overlap write(2) of this one: the context's reader ring when it exists (its
@@ -440,17 +445,33 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
   if (fresh) {
     c->rd_slot.assign(2 * RD_THREADS, nullptr);
     c->rd_ev.assign(2 * RD_THREADS, nullptr);
-    c->rd_stream.assign(RD_THREADS, nullptr);
+    c->rd_stream.assign(std::min(RD_STREAMS, RD_THREADS), nullptr);
+    for (auto& x : c->rd_stream)
+      if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) {
+        for (auto& y : c->rd_stream)
+          if (y) hipStreamDestroy(y);
+        c->rd_stream.clear();
+        c->rd_slot.clear();
+        c->rd_ev.clear();
+        bg_release(c, d);
+        close(fd);
+        return bg_fail(c, BG_E_HIP, "reader ring streams");
+      }
   }
+  auto rd_strm = [&](int t) { return c->rd_stream.empty() ? c->stream : c->rd_stream[t % c->rd_stream.size()]; };
   const uint64_t nch = (n + RD_CHUNK - 1) / RD_CHUNK;
   std::atomic<int> bad{0};
   auto reader = [&](int t) {
     if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
     if (fresh) {
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
       for (int k = 2 * t; k < 2 * t + 2; ++k)
         if (hipHostMalloc((void**)&c->rd_slot[k], RD_CHUNK, hipHostMallocDefault) != hipSuccess ||
             hipEventCreateWithFlags(&c->rd_ev[k], hipEventDisableTiming) != hipSuccess) { bad = 1; return; }
-      if (hipStreamCreateWithFlags(&c->rd_stream[t], hipStreamNonBlocking) != hipSuccess) { bad = 1; return; }
+      if (c->stats && t == 0)  // first-use cost of the ring (stderr, BEDGPU_STATS only)
+        fprintf(stderr, "bedgpu ring   pin+events %.3f ms\n",
+                std::chrono::duration<double, std::milli>(clk::now() - t0).count());
     }
     uint64_t j = 0;
     for (uint64_t k = (uint64_t)t; k < nch && !bad; k += RD_THREADS, ++j) {
@@ -464,11 +485,15 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
         if (r <= 0) { bad = 2; return; }
         got += (uint64_t)r;
       }
-      if (hipMemcpyAsync(d + off, c->rd_slot[slot], len, hipMemcpyHostToDevice, c->rd_stream[t]) != hipSuccess ||
-          hipEventRecord(c->rd_ev[slot], c->rd_stream[t]) != hipSuccess) {
+      const auto q0 = std::chrono::steady_clock::now();
+      if (hipMemcpyAsync(d + off, c->rd_slot[slot], len, hipMemcpyHostToDevice, rd_strm(t)) != hipSuccess ||
+          hipEventRecord(c->rd_ev[slot], rd_strm(t)) != hipSuccess) {
         bad = 1;
         return;
       }
+      if (c->stats && t == 0 && j == 0)
+        fprintf(stderr, "bedgpu ring   first copy issue %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
     }
   };
   std::vector<std::thread> th;
@@ -478,6 +503,7 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
   close(fd);
   bg_mark(c, "preads");
   if (bad) {  // copies already issued still target d: drain them before releasing it
+    hipStreamSynchronize(c->stream);
     for (auto s : c->rd_stream)
       if (s) hipStreamSynchronize(s);
     if (fresh) {  // a ring that failed to build is dropped whole (the next read rebuilds it)
@@ -495,7 +521,7 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
     return bad == 2 ? bg_fail(c, BG_E_IO, std::string("read failed: ") + path)
                     : bg_fail(c, BG_E_HIP, std::string("copy failed: ") + path);
   }
-  for (int t = 0; t < nt; ++t) {  // the context's stream (the loader) waits for the copies
+  for (size_t t = 0; t < c->rd_stream.size(); ++t) {  // the loader's stream waits for the copies
     BG_HIP(c, hipEventRecord(c->rd_ev[2 * t], c->rd_stream[t]));
     BG_HIP(c, hipStreamWaitEvent(c->stream, c->rd_ev[2 * t], 0));
   }

@@ -328,6 +328,31 @@ def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
     assert bad.returncode != 0 and b"More than one overlap specification used." in bad.stderr
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,chunk_mb,streams", [(1, 1, 0), (3, 1, 1), (32, 1, 2), (8, 64, 8),
+                                                     (2, 1, 9)])
+def test_cli_reader_ring_settings(gpu_bin, oracle_bin, tmp_path, threads, chunk_mb, streams):
+    """file -> HBM reader ring (bg_read_file_device) at odd sizes: inputs of several 1 MiB
+    chunks plus a ragged tail, more readers than chunks, one reader, copies on the context's
+    own stream (0 streams) and more streams than readers; the output written back
+    through the same ring must equal the oracle's"""
+    rng = random.Random(11 + threads)
+    a = randbed.rows(rng, 120000, span=40_000_000, maxlen=500)
+    b = randbed.rows(rng, 90000, span=40_000_000, maxlen=500)
+    pa = randbed.write(str(tmp_path / "a.bed"), randbed.text(a))
+    pb = randbed.write(str(tmp_path / "b.bed"), randbed.text(b))
+    assert os.path.getsize(pa) > 2 << 20 and os.path.getsize(pa) % (1 << 20)
+    env = dict(os.environ, BEDGPU_RD_THREADS=str(threads), BEDGPU_RD_CHUNK_MB=str(chunk_mb),
+               BEDGPU_RD_STREAMS=str(streams))
+    env.pop("BEDGPU_DEVICES", None)
+    for mode in (["--intersect"], ["--everything"], ["--element-of", "1"]):
+        want = subprocess.run([oracle_bin["bedops"]] + mode + [pa, pb], stdout=subprocess.PIPE,
+                              check=True).stdout
+        got = subprocess.run([gpu_bin["bedops"]] + mode + [pa, pb], stdout=subprocess.PIPE,
+                             check=True, env=env).stdout
+        assert got == want, (mode, threads, chunk_mb, streams)
+
+
 # ---------------------------------------------------------------------------------
 # I/O edge cases (Appendix B of SURVEY.md)
 # ---------------------------------------------------------------------------------
