@@ -12,8 +12,10 @@
  *                                     PercentOverlapMapping/Reference/Either/Both :123-288,
  *                                     Exact :293-317
  *   window repair (fixWindow) ....... algorithm/visitors/bed/BedBaseVisitor.hpp:131-215
- *   set order (start,end,rest,addr) . data/bed/BedCompare.hpp:143-194 (row index stands in
- *                                     for the heap address: allocation order)
+ *   set order (start,end,rest,addr) . data/bed/BedCompare.hpp:143-194; the address of a map
+ *                                     row comes from oracle/heapsim.h (the reference's glibc
+ *                                     allocator replayed over the sweep's new/delete calls;
+ *                                     row index in single-file mode)
  *   fan-out / row printing .......... algorithm/visitors/other/MultiVisitor.hpp:71-98
  *   visitors ........................ numerical/CountVisitor.hpp ("%d"), AverageVisitor.hpp and
  *                                     SumVisitor.hpp (running double), ExtremeVisitor.hpp (min/max),
@@ -44,6 +46,7 @@
 #include <math.h>
 
 #include "bedio.h"
+#include "heapsim.h"
 
 static chrom_pool_t POOL;
 static const bedfile_t *REF, *MAP;
@@ -54,6 +57,8 @@ static uint64_t OVR = 1, RANGE = 0;
 static double PERC = 1.0; /* PercentOverlapMapping::perc_ after its constructor */
 
 typedef struct { int c; uint64_t s, e; int64_t id; } row_t;
+static int64_t* ADDR; /* simulated heap address of each map row (NULL: row index) */
+#define A_(m) (ADDR ? ADDR[m] : (m))
 static int SINGLE; /* single-file mode: the reference rows are the map rows (same objects) */
 static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], SINGLE ? r : -1 - r}; return x; }
 static row_t M_(int64_t m) { row_t x = {MAP->chrom[m], MAP->start[m], MAP->end[m], m}; return x; }
@@ -146,7 +151,7 @@ typedef struct { int64_t* v; int64_t n, cap; } oset_t;
 static int mless(int64_t a, int64_t b) {
   if (MAP->start[a] != MAP->start[b]) return MAP->start[a] < MAP->start[b];
   if (MAP->end[a] != MAP->end[b]) return MAP->end[a] < MAP->end[b];
-  return a < b;
+  return A_(a) < A_(b);
 }
 static int64_t os_lb(const oset_t* s, int64_t x) {
   int64_t lo = 0, hi = s->n;
@@ -202,7 +207,7 @@ static int rless(int64_t a, int64_t b) {
   if (MAP->end[a] != MAP->end[b]) return MAP->end[a] < MAP->end[b];
   int v = frest_cmp(a, b);
   if (v) return v < 0;
-  return a < b;
+  return A_(a) < A_(b);
 }
 static void ev_push(oset_t* s, int64_t x) {
   if (s->n == s->cap) { s->cap = s->cap ? 2 * s->cap : 64; s->v = (int64_t*)realloc(s->v, (size_t)s->cap * 8); }
@@ -274,7 +279,7 @@ typedef struct {
 static tmean_t TM[64];
 static int vl_less(int64_t a, int64_t b) {
   if (MAP->score[a] != MAP->score[b]) return MAP->score[a] < MAP->score[b];
-  return a < b;
+  return A_(a) < A_(b);
 }
 static int64_t tm_rank(const oset_t* s, int64_t x) {
   int64_t lo = 0, hi = s->n;
@@ -578,9 +583,9 @@ static void v_done(int64_t r) {
         if (VWIN.n == 0) { fputs("NAN", stdout); break; }
         int64_t* v = (int64_t*)malloc((size_t)VWIN.n * 8);
         memcpy(v, VWIN.v, (size_t)VWIN.n * 8);
-        for (int64_t p = 1; p < VWIN.n; ++p) { /* row order */
+        for (int64_t p = 1; p < VWIN.n; ++p) { /* address order */
           int64_t x = v[p], q = p;
-          while (q > 0 && v[q - 1] > x) { v[q] = v[q - 1]; --q; }
+          while (q > 0 && A_(v[q - 1]) > A_(x)) { v[q] = v[q - 1]; --q; }
           v[q] = x;
         }
         double value = 0, weightSum = 0;
@@ -634,6 +639,46 @@ static double parse_frac(const char* v) {
   p -= DBL_EPSILON;
   if (p <= 0.0) p = DBL_EPSILON;
   return p;
+}
+
+/* the reference's heap traffic for one row object (Bed.hpp constructors / readline /
+ * destructors): object; ChromInfo() new char[1]; Bed4() new char[1] (B4/B5); readline
+ * re-allocates chrom_ and id_, then rest_ and fullrest_ (B4/B5: id + rest); the destructor
+ * frees rest_, fullrest_, id_, chrom_, then the object */
+typedef struct { int64_t o, c, i, r, f; size_t lc, li, lr; } rowmem_t;
+static heapsim_t HS;
+static void row_new(rowmem_t* x, int fields, size_t lc, size_t li, size_t lr) {
+  x->lc = lc; x->li = li; x->lr = lr;
+  x->o = hs_malloc(&HS, fields == 3 ? 32 : (fields == 4 ? 48 : 56));
+  const int64_t c1 = hs_malloc(&HS, 1);
+  const int64_t i1 = fields >= 4 ? hs_malloc(&HS, 1) : 0;
+  hs_free(&HS, 1, c1);
+  x->c = hs_malloc(&HS, lc + 1);
+  if (fields >= 4) { hs_free(&HS, 1, i1); x->i = hs_malloc(&HS, li + 1); }
+  x->r = hs_malloc(&HS, lr + 1);
+  if (fields >= 4) x->f = hs_malloc(&HS, lr + 1 + li + 1);
+}
+static void row_del(const rowmem_t* x, int fields) {
+  hs_free(&HS, x->lr + 1, x->r);
+  if (fields >= 4) { hs_free(&HS, x->lr + 1 + x->li + 1, x->f); hs_free(&HS, x->li + 1, x->i); }
+  hs_free(&HS, x->lc + 1, x->c);
+  hs_free(&HS, fields == 3 ? 32 : (fields == 4 ? 48 : 56), x->o);
+}
+static rowmem_t* MMEM;
+static rowmem_t RMEM[2];
+static void map_new(int64_t m) { /* m == MAP->n: the row read at end of file (never freed) */
+  if (m < MAP->n)
+    row_new(&MMEM[m], MAPFIELDS, strlen(POOL.names[MAP->chrom[m]]), MAPFIELDS >= 4 ? strlen(MAP->id[m]) : 0,
+            MAP->rest ? strlen(MAP->rest[m]) : 0);
+  else
+    row_new(&MMEM[m], MAPFIELDS, 0, 0, 0);
+  ADDR[m] = MMEM[m].o;
+}
+static void ref_new(int64_t r) {
+  if (r < REF->n)
+    row_new(&RMEM[r & 1], 3, strlen(POOL.names[REF->chrom[r]]), 0, REF->rest ? strlen(REF->rest[r]) : 0);
+  else
+    row_new(&RMEM[r & 1], 3, 0, 0, 0);
 }
 
 static oset_t vcache, lst, ev;
@@ -816,17 +861,25 @@ int main(int argc, char** argv) {
     /* sweep() overload 2 with the sweep distance; fixWindow with the visitor distance */
     int64_t wh = 0, wt = 0; /* deque [wh, wt) */
     int64_t mi = 0, cache = -1;
+    /* heap addresses: the iterators read one row ahead (ref first, Bedmap.cpp:282-284) */
+    ADDR = (int64_t*)calloc((size_t)map.n + 1, sizeof(int64_t));
+    MMEM = (rowmem_t*)calloc((size_t)map.n + 1, sizeof(rowmem_t));
+    ref_new(0);
+    map_new(0);
     for (int64_t r = 0; r < ref.n; ++r) {
-      while (wt > wh && sweep_m2r(win[wh], r) < 0) on_delete(win[wh++]);
+      ref_new(r + 1); /* ++refStart */
+      while (wt > wh && sweep_m2r(win[wh], r) < 0) { on_delete(win[wh]); row_del(&MMEM[win[wh]], MAPFIELDS); ++wh; }
       while (cache >= 0 || mi < map.n) {
         int64_t m;
         if (cache >= 0) { m = cache; cache = -1; }
-        else m = mi++;
+        else { m = mi++; map_new(mi); } /* ++mapFromStart */
         int v = sweep_r2m(r, m);
         if (v == 0) { win[wt++] = m; os_insert(&vcache, m); } /* OnAdd -> cache_ */
         else if (v < 0) { cache = m; break; }
+        else row_del(&MMEM[m], MAPFIELDS);
       }
       on_done(r);
+      row_del(&RMEM[r & 1], 3); /* delete rPtr */
     }
   }
   fflush(stdout);
