@@ -16,15 +16,18 @@ Strong scaling by default: the dataset is the fixed 100M x 100M at every N (`--w
 100M rows per file). After the timed steps rank 0 hashes the reassembled output against the
 reference binary's hash at every N.
 
-Rank 0, N = 1, also times:
-  e2e_intervals_per_s  the drop-in CLI `bedops_amd/bin/bedops --intersect A B > out`, input
-                       files in page cache -> output file (process start and HIP init
-                       included), best of two runs;
-  cpu_baseline         the oracle (plain-C restatement of the reference) on the same full
-                       inputs, fanned out per chromosome over the host cores — the
-                       reference's own documented scale-out (`--chrom` per process,
-                       bedops.rst:721-726) — file -> file, outputs concatenated in order;
-  gpu_vs_cpu           e2e_intervals_per_s / cpu_baseline (both file -> file).
+Rank 0, N = 1, also times, all file -> file with the inputs
+in the page cache and the output written to a file:
+  e2e           the drop-in CLI `bedops_amd/bin/bedops --intersect A B > out` (process start,
+                HIP init, reads, device work, output write), median of 3, with the
+                BEDGPU_STATS phase marks of the median run; `--e2e-devices 0,1,..` also times
+                the sharded drop-in (BEDGPU_DEVICES);
+  cpu_baseline  the genuine reference (oracle/_ref, built from /root/reference by
+                oracle/build_ref.sh): run (ii) one `--chrom` process per chromosome over the
+                full files, min(nproc, 25) at a time, outputs concatenated in strcmp order
+                (the reference's documented scale-out, bedops.rst:721-726), median of 3; run
+                (i) one process on the full inputs; CPU model and core counts;
+  gpu_vs_cpu    e2e / run (ii); gpu_vs_cpu_single: e2e / run (i).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -211,84 +214,164 @@ def write_inputs(L, W, td):
     return paths, rows
 
 
-def e2e_cli(W, paths, rows, td):
-    """drop-in CLI, file -> file (BEDGPU_DEVICES unset: one GPU), best of two runs"""
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
+def _sha16_file(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 26), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def _phases(stderr):
+    """BEDGPU_STATS=1 marks (bedops_amd/cli/cli_common.h cli_mark, bg_stats): host phase
+    deltas and per-stage times, in ms"""
+    host, stage = {}, {}
+    for ln in stderr.splitlines():
+        f = ln.split()
+        if len(f) >= 5 and f[0] == "bedgpu" and f[1] == "host" and f[-1].startswith("(+"):
+            host[f[2]] = round(float(f[-1][2:-1]), 3)
+        elif len(f) >= 5 and f[0] == "bedgpu" and f[1] == "stage":
+            stage[f[2]] = round(stage.get(f[2], 0.0) + float(f[3]), 3)
+    return {"host_ms": host, "stage_ms": stage}
+
+
+def e2e_cli(W, paths, rows, td, runs=3, devices=None):
+    """the drop-in CLI, file -> file: `bedops_amd/bin/<tool> <args> <files> > out`, input files
+    in the page cache, process start + HIP init + reads + device work + output write all
+    inside the wall clock. Median of `runs`, with the BEDGPU_STATS phase
+    marks of the median run. devices: BEDGPU_DEVICES for the sharded drop-in (None: 1 GPU)."""
     exe = os.path.join(ROOT, "bedops_amd", "bin", W["cli"])
     out = os.path.join(td, "cli_out.bed")
     args = W["args"] if W["cli"] != "closest-features" else ["--closest"]
     env = {k: v for k, v in os.environ.items() if k != "BEDGPU_DEVICES"}
-    best = None
-    for _ in range(2):
+    env["BEDGPU_STATS"] = "1"
+    if devices:
+        env["BEDGPU_DEVICES"] = devices
+    times, logs = [], []
+    for i in range(runs):
         with open(out, "wb") as fo:
             t0 = time.perf_counter()
-            subprocess.run([exe, *args, *paths], stdout=fo, check=True, env=env)
+            r = subprocess.run([exe, *args, *paths], stdout=fo, stderr=subprocess.PIPE, env=env)
             dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-    h = hashlib.sha256()
-    with open(out, "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 26), b""):
-            h.update(chunk)
-    nbytes = os.path.getsize(out)
+        if r.returncode != 0:
+            raise RuntimeError(f"CLI failed: {r.stderr.decode(errors='replace')[-2000:]}")
+        times.append(dt)
+        logs.append(r.stderr.decode(errors="replace"))
+        log(f"e2e run {i}: {dt:.3f} s")
+    med = _median(times)
+    sha, nbytes = _sha16_file(out), os.path.getsize(out)
     os.unlink(out)
-    return {"value": rows / best, "unit": "intervals/s", "seconds": round(best, 3),
-            "command": f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> > out",
-            "output_sha16": h.hexdigest()[:16], "output_bytes": nbytes}
+    rec = {"value": rows / med, "unit": "intervals/s", "median_s": round(med, 4),
+           "runs_s": [round(t, 4) for t in times],
+           "command": f"{'BEDGPU_DEVICES=' + devices + ' ' if devices else ''}"
+                      f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> > out",
+           "output_sha16": sha, "output_bytes": nbytes,
+           "phases": _phases(logs[times.index(med)])}
+    return rec
 
 
-def cpu_fanout(L, W, td, workers):
-    """The oracle (test infrastructure: plain-C restatement of the reference; the reference
-    is not buildable in this image) on the full inputs, one process per
-    chromosome, `workers` at a time (the reference's documented `--chrom` fan-out). Each
-    chromosome's inputs are written as their own files first (untimed: what the reference's
-    --chrom seek reads); the timed region runs the processes and concatenates their outputs
-    in strcmp chromosome order, file -> file."""
-    exe = os.path.join(ROOT, "oracle", "build", W["oracle"])
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-s", "oracle"], cwd=ROOT, check=True)
-    cs = contigs(L)
-    jobs, rows = [], 0
-    for c, (name, ln) in enumerate(cs):
-        files = []
-        for i, (seed, mode) in enumerate(W["gen"]):
-            p, nb, r = gen(L, W["rows"][i], seed, 1 << c, mode)
-            path = os.path.join(td, f"c{c}_in{i}.bed")
-            with open(path, "wb") as f:
-                f.write(host_bytes(p, nb))
-            L.bedgen_free(p)
-            files.append(path)
-            rows += r
-        jobs.append((ln, c, files))
-    jobs.sort(key=lambda j: -j[0])  # longest first
-    outs = {c: os.path.join(td, f"c{c}_out.bed") for _, c, _ in jobs}
-    t0 = time.perf_counter()
-    running, pending = [], list(jobs)
-    while pending or running:
-        while pending and len(running) < workers:
-            _, c, files = pending.pop(0)
-            fo = open(outs[c], "wb")
-            running.append((subprocess.Popen([exe, *W["args"], *files], stdout=fo), fo))
-        p, fo = running.pop(0)
-        if p.wait() != 0:
-            raise RuntimeError("oracle failed in the CPU baseline")
-        fo.close()
-    final = os.path.join(td, "cpu_out.bed")
-    with open(final, "wb") as fo:
-        for c in range(len(cs)):
-            with open(outs[c], "rb") as fi:
-                while True:
-                    b = fi.read(1 << 26)
-                    if not b:
-                        break
-                    fo.write(b)
-    dt = time.perf_counter() - t0
-    for _, c, files in jobs:
-        for f in files + [outs[c]]:
-            os.unlink(f)
-    os.unlink(final)
-    return {"value": rows / dt, "unit": "intervals/s", "cores": workers, "kind": "port",
-            "sample": f"full inputs ({rows} rows): {W['oracle']} {' '.join(W['args'])} per "
-                      f"chromosome ({len(cs)} contigs, {workers} processes at a time), outputs "
-                      f"concatenated in strcmp order, file->file, {dt:.2f} s"}
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
+
+
+def _ref_exe(W):
+    """the genuine reference binary built by oracle/build_ref.sh (None: not built)"""
+    exe = os.path.join(ROOT, "oracle", "_ref", "bin", {"bedops": "bedops", "bedmap": "bedmap",
+                                                        "closest-features": "closest-features"}[W["cli"]])
+    return exe if os.access(exe, os.X_OK) else None
+
+
+def cpu_single(W, paths, rows, td, runs):
+    """BASELINE.md run (i): one reference process on the full inputs, file -> file"""
+    exe = _ref_exe(W)
+    kind = "reference"
+    if exe is None:
+        exe, kind = os.path.join(ROOT, "oracle", "build", W["oracle"]), "port"
+    out = os.path.join(td, "cpu1_out.bed")
+    times = []
+    for i in range(runs):
+        with open(out, "wb") as fo:
+            t0 = time.perf_counter()
+            subprocess.run([exe, *W["args"], *paths], stdout=fo, check=True)
+            times.append(time.perf_counter() - t0)
+        log(f"cpu run (i) {i}: {times[-1]:.2f} s")
+    sha = _sha16_file(out)
+    os.unlink(out)
+    med = _median(times)
+    return {"value": rows / med, "unit": "intervals/s", "cores": 1, "kind": kind,
+            "median_s": round(med, 3), "runs_s": [round(t, 2) for t in times],
+            "output_sha16": sha,
+            "sample": f"full inputs ({rows} rows), one process: "
+                      f"{os.path.relpath(exe, ROOT)} {' '.join(W['args'])} <files> > out, "
+                      f"median of {runs}"}
+
+
+def cpu_fanout_ref(L, W, paths, rows, td, workers, runs):
+    """BASELINE.md run (ii), the reference's documented scale-out (bedops.rst:721-726): one
+    `--chrom <c>` process per chromosome over the FULL input files (the reference's own
+    --chrom seek), `workers` at a time (xargs -P), outputs concatenated in strcmp order,
+    file -> file, median of `runs`"""
+    exe = _ref_exe(W)
+    names = sorted((nm for nm, _ in contigs(L)), key=lambda n: n.encode())
+    lens = dict(contigs(L))
+    order = sorted(names, key=lambda n: -lens[n])  # longest first, as a scheduler would
+    times, sha = [], None
+    for i in range(runs):
+        outs = {n: os.path.join(td, f"fan_{n}.bed") for n in names}
+        t0 = time.perf_counter()
+        running, pending = [], list(order)
+        while pending or running:
+            while pending and len(running) < workers:
+                n = pending.pop(0)
+                fo = open(outs[n], "wb")
+                running.append((subprocess.Popen([exe, "--chrom", n, *W["args"], *paths], stdout=fo), fo))
+            p, fo = running.pop(0)
+            if p.wait() != 0:
+                raise RuntimeError("reference failed in the CPU fan-out")
+            fo.close()
+        final = os.path.join(td, "fan_out.bed")
+        with open(final, "wb") as fo:
+            for n in names:
+                with open(outs[n], "rb") as fi:
+                    while True:
+                        b = fi.read(1 << 26)
+                        if not b:
+                            break
+                        fo.write(b)
+        times.append(time.perf_counter() - t0)
+        log(f"cpu run (ii) {i}: {times[-1]:.2f} s")
+        sha = _sha16_file(final)
+        for n in names:
+            os.unlink(outs[n])
+        os.unlink(final)
+    med = _median(times)
+    return {"value": rows / med, "unit": "intervals/s", "cores": workers, "kind": "reference",
+            "median_s": round(med, 3), "runs_s": [round(t, 2) for t in times], "output_sha16": sha,
+            "sample": f"full inputs ({rows} rows): {os.path.relpath(exe, ROOT)} --chrom <c> "
+                      f"{' '.join(W['args'])} <files>, one process per chromosome ({len(names)}), "
+                      f"{workers} at a time, outputs concatenated in strcmp order, file->file, "
+                      f"median of {runs}"}
 
 
 # ----------------------------------------------------------------------------- main
@@ -305,8 +388,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=16,
-                    help="host processes of the CPU fan-out (capped at os.cpu_count())")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="processes of the CPU fan-out, run (ii) (default: min(nproc, 25))")
+    ap.add_argument("--cpu-single-runs", type=int, default=1,
+                    help="runs of the one-process reference, run (i) (median; ~60 s each)")
+    ap.add_argument("--cpu-fanout-runs", type=int, default=3)
+    ap.add_argument("--e2e-runs", type=int, default=3)
+    ap.add_argument("--e2e-devices", default=None,
+                    help="also time the drop-in CLI sharded over BEDGPU_DEVICES (e.g. 0,1)")
     ap.add_argument("--load-only", action="store_true",
                     help="time the loader stage alone (text in HBM -> keyed columns)")
     ap.add_argument("--profile-all", action="store_true",
@@ -491,19 +580,31 @@ def main():
                 "avg_ms": round(avg_s * 1e3, 4), "launches": calls,
                 "bytes_per_launch": int(per_launch), "rank": 0}
 
-    e2e = cpu = None
+    e2e = cpu = e2e_sh = None
     if world == 1 and args.scale == 1.0 and not args.load_only and (
             not args.no_e2e or not args.no_cpu_baseline):
         with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as td:
+            paths, nrows = write_inputs(L, W, td)
             if not args.no_e2e:
-                paths, nrows = write_inputs(L, W, td)
-                e2e = e2e_cli(W, paths, nrows, td)
+                e2e = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs)
                 if W["ref"]:
                     e2e["matches_reference"] = e2e["output_sha16"] == W["ref"]["sha16"]
-                for p in paths:
-                    os.unlink(p)
+                if args.e2e_devices:
+                    e2e_sh = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs, devices=args.e2e_devices)
+                    if W["ref"]:
+                        e2e_sh["matches_reference"] = e2e_sh["output_sha16"] == W["ref"]["sha16"]
             if not args.no_cpu_baseline:
-                cpu = cpu_fanout(L, W, td, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
+                info = cpu_info()
+                workers = args.cpu_workers or max(1, min(info["affinity_cpus"], 25))
+                fan = cpu_fanout_ref(L, W, paths, nrows, td, workers, args.cpu_fanout_runs) \
+                    if _ref_exe(W) else None
+                single = cpu_single(W, paths, nrows, td, args.cpu_single_runs)
+                top = fan or single
+                cpu = {"value": top["value"], "unit": "intervals/s", "cores": top["cores"],
+                       "kind": top["kind"], "sample": top["sample"], **info,
+                       "single": single, "fanout": fan}
+            for p in paths:
+                os.unlink(p)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = total_rows * args.steps / elapsed
@@ -526,8 +627,12 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "e2e_intervals_per_s": round(e2e["value"], 1) if e2e else None,
         "e2e": e2e,
+        "e2e_sharded": e2e_sh,
         "gpu_vs_cpu": round(e2e["value"] / cpu["value"], 2) if (cpu and e2e) else None,
-        "gpu_vs_cpu_scope": "file->file CLI vs file->file CPU fan-out" if (cpu and e2e) else None,
+        "gpu_vs_cpu_single": round(e2e["value"] / cpu["single"]["value"], 2) if (cpu and e2e) else None,
+        "gpu_vs_cpu_scope": ("file->file CLI (median) vs the reference file->file: gpu_vs_cpu "
+                             "against run (ii) (--chrom fan-out), gpu_vs_cpu_single against run (i) "
+                             "(one process)") if (cpu and e2e) else None,
         "parity": verify,
         "kernels_first_step_ms": {k: round(v[1], 4) for k, v in
                                   sorted(first.items(), key=lambda kv: -kv[1][1])},
