@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
   o.precision = 6;
   strcpy(o.delim, "|");
   strcpy(o.multidelim, ";");
-  int ec = 0, check = 0, need4 = 0, need5 = 0, need_rest = 0, map_rest = 0, set_prec = 0, set_delim = 0;
+  int ec = 0, check = 0, need4 = 0, need5 = 0, need_rest = 0, map_rest = 0, addr_ops = 0, set_prec = 0, set_delim = 0;
   int is_bp = 0, is_range = 0, range_alias = 0, is_exact = 0, is_frac[4] = {0, 0, 0, 0};
   static const struct { const char* name; int op; } OPS[] = {
       {"count", BG_MAP_COUNT}, {"mean", BG_MAP_MEAN}, {"sum", BG_MAP_SUM}, {"min", BG_MAP_MIN},
@@ -254,6 +254,12 @@ int main(int argc, char** argv) {
           op == BG_MAP_CV)
         map_rest = 1;
       if (op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_ID_UNIQ) need4 = 1;
+      /* operations that can see the reference's heap-address order of equal rows: the
+       * replay (bg_heap.hip) sizes each row's strings from both files' remainders */
+      if (op == BG_MAP_WMEAN || op == BG_MAP_TMEAN || op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID ||
+          op == BG_MAP_ECHO_MAP_SCORE || op == BG_MAP_ECHO_MAP_SIZE || op == BG_MAP_ECHO_OVERLAP_SIZE ||
+          (op >= BG_MAP_MIN_ELEMENT && op <= BG_MAP_MAX_ELEMENT_RAND))
+        map_rest = addr_ops = 1;
     }
   }
   {  /* one overlap specification (Input.hpp:330-343) */
@@ -278,7 +284,7 @@ int main(int argc, char** argv) {
   /* input kinds: the reference file B3Rest (--echo), the map file by the operations'
    * MapFields (Input.hpp:401-418); single-file mode reads the one file as the map type */
   const int mkind = need5 ? (map_rest ? BG_BED5_REST : BG_BED5) : (map_rest ? BG_BED3_REST : BG_BED3);
-  const int rkind = need_rest ? BG_BED3_REST : BG_BED3;
+  const int rkind = (need_rest || addr_ops) ? BG_BED3_REST : BG_BED3;
   const int skind = need5 ? ((map_rest || need_rest) ? BG_BED5_REST : BG_BED5)
                           : ((map_rest || need_rest || (need4 && !need5)) ? BG_BED3_REST : BG_BED3);
   /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h). Overlaps and

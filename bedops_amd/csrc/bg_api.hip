@@ -572,6 +572,7 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, (void*)r->lrows.coff);
   bg_release(c, r->zin);
   bg_release(c, r->zout);
+  bg_release(c, r->maddr);
   bg_release(c, r->left);
   bg_release(c, r->right);
   bg_release(c, r->text);

@@ -57,6 +57,8 @@ struct FmtArgs {
   LongRows lrows;      // long map rows by length class (bg_map_cands)
   const int64_t* zin;  // zero-length rows: sweep-window membership (bg_map_live)
   const int64_t* zout;
+  const int64_t* maddr;  // map rows' heap addresses (bg_heap.hip), null: row order
+  uint64_t n2;           // map rows
   int crit, mapfields, mdlen;
   int64_t ovr, range;
   double perc;
@@ -537,6 +539,41 @@ __device__ __forceinline__ int64_t fmt_pad(const FmtArgs& A) {
   return A.crit == BG_OVR_RANGE ? A.range : 0;
 }
 
+// the window's rows of reference row k in GenomicAddressCompare order (BedCompare.hpp:51-63):
+// row order, except that a run of rows equal in (start, end) comes in heap-address order
+// (A.maddr, bg_heap.hip); f returns false to stop
+template <typename F>
+__device__ __forceinline__ void map_window_genomic(const FmtArgs& A, uint64_t k, F f) {
+  const int64_t s = A.s[k], e = A.e[k];
+  auto member = [&](uint64_t m) {
+    return bg_map_live(A.zin, A.zout, k, m) && bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]);
+  };
+  uint64_t skip = 0;  // rows below this went out with their tie run
+  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
+    if (m < skip) return true;
+    if (A.maddr && m + 1 < A.n2 && A.s2[m + 1] == A.s2[m] && A.e2[m + 1] == A.e2[m]) {
+      uint64_t t = m + 1;
+      while (t < A.n2 && A.s2[t] == A.s2[m] && A.e2[t] == A.e2[m]) ++t;
+      skip = t;
+      bool has = false;
+      int64_t last = 0;
+      for (;;) {  // the run's members by increasing address
+        uint64_t best = ~0ULL;
+        for (uint64_t u = m; u < t; ++u) {
+          if (!member(u) || (has && A.maddr[u] <= last)) continue;
+          if (best == ~0ULL || A.maddr[u] < A.maddr[best]) best = u;
+        }
+        if (best == ~0ULL) return true;
+        if (!f(best)) return false;
+        has = true;
+        last = A.maddr[best];
+      }
+    }
+    if (!member(m)) return true;
+    return f(m);
+  });
+}
+
 // --echo-map* of reference row k: the window's rows in genomic order (EchoMapBed's set,
 // EchoMapBedVisitor.hpp:58-63) joined by --multidelim (PrintRangeDelim)
 template <typename Out>
@@ -544,10 +581,8 @@ __device__ __forceinline__ bool put_echo_map(const FmtArgs& A, Out& o, uint64_t 
   const int64_t s = A.s[k], e = A.e[k];
   bool first = true, ok = true;
   int64_t rs = 0, re = 0;
-  bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
+  map_window_genomic(A, k, [&](uint64_t m) {
     const int64_t ms = A.s2[m], me = A.e2[m];
-    if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me))
-      return true;
     if (op == BG_MAP_ECHO_MAP_RANGE) {  // PrintGenomicRange (ProcessBedVisitorRow.hpp:433-456)
       if (first) { rs = ms; re = me; }
       else { rs = min(rs, ms); re = max(re, me); }
@@ -682,14 +717,15 @@ __device__ __forceinline__ double window_kth(const FmtArgs& A, uint64_t k, uint3
 // random pick among equal scores (the first of the set here: min lowest row, max highest).
 __device__ __forceinline__ bool elem_better(const FmtArgs& A, int op, uint64_t m, uint64_t b) {
   const double x = A.score2[m], y = A.score2[b];
-  if (op == BG_MAP_MIN_ELEMENT_RAND) return x != y ? x < y : m < b;
-  if (op == BG_MAP_MAX_ELEMENT_RAND) return x != y ? x > y : m > b;
+  const int64_t am = bg_maddr(A.maddr, m), ab = bg_maddr(A.maddr, b);
+  if (op == BG_MAP_MIN_ELEMENT_RAND) return x != y ? x < y : am < ab;
+  if (op == BG_MAP_MAX_ELEMENT_RAND) return x != y ? x > y : am > ab;
   const bool mx = op == BG_MAP_MAX_ELEMENT;
   if (x != y) return mx ? x > y : x < y;
   if (A.s2[m] != A.s2[b]) return mx ? A.s2[m] > A.s2[b] : A.s2[m] < A.s2[b];
   if (A.e2[m] != A.e2[b]) return mx ? A.e2[m] > A.e2[b] : A.e2[m] < A.e2[b];
   const int c = bg_frest_cmp(A.text2, A.rest_off2, A.rest_len2, A.mapfields, m, b);
-  return c != 0 ? c < 0 : m < b;
+  return c != 0 ? c < 0 : am < ab;
 }
 template <typename Out>
 __device__ __forceinline__ bool put_element(const FmtArgs& A, Out& o, uint64_t k, int op) {
@@ -704,12 +740,34 @@ __device__ __forceinline__ bool put_element(const FmtArgs& A, Out& o, uint64_t k
   return put_map_row(A, o, best, A.prec);
 }
 // --wmean: WeightedAverage::DoneReference (bed/WeightedAverageVisitor.hpp:55-70) over its
-// std::set<MapType*> (address order = row order): sum of overlap/len(ref) * score, divided
-// by the sum of the weights
+// std::set<MapType*> (heap-address order, A.maddr; row order without a replay): sum of
+// overlap/len(ref) * score, divided by the sum of the weights
 __device__ __forceinline__ double window_wmean(const FmtArgs& A, uint64_t k) {
   const int64_t s = A.s[k], e = A.e[k];
   const double len = (double)(uint64_t)(e - s);
   double value = 0, wsum = 0;
+  if (A.maddr) {  // by repeated selection of the next larger address
+    bool has = false;
+    int64_t last = 0;
+    for (;;) {
+      uint64_t best = ~0ULL;
+      bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
+        if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]))
+          return true;
+        if (has && A.maddr[m] <= last) return true;
+        if (best == ~0ULL || A.maddr[m] < A.maddr[best]) best = m;
+        return true;
+      });
+      if (best == ~0ULL) break;
+      const int64_t ov = min(e, A.e2[best]) - max(s, A.s2[best]);
+      const double w = (double)(uint64_t)(ov > 0 ? ov : 0) / len;
+      value += w * A.score2[best];
+      wsum += w;
+      has = true;
+      last = A.maddr[best];
+    }
+    return value / wsum;
+  }
   bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
     const int64_t ms = A.s2[m], me = A.e2[m];
     if (!bg_map_live(A.zin, A.zout, k, m) || !bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, ms, me))
@@ -1126,6 +1184,8 @@ static void fill_args(bg_result* r, FmtArgs& A) {
       A.whi = r->whi;
       A.zin = r->zin;
       A.zout = r->zout;
+      A.maddr = r->maddr;
+      A.n2 = M->n;
       A.lrows = r->lrows;
       A.crit = r->mopts.criterion;
       A.ovr = (int64_t)r->mopts.overlap_bp;

@@ -163,6 +163,9 @@ struct bg_result {
   // [zin[m], zout[m]) only (bg_map.hip, k_mz_member); null otherwise
   int64_t* zin = nullptr;
   int64_t* zout = nullptr;
+  // map row -> simulated heap address of the reference's row object, the tie-break of its
+  // address-ordered sets (bg_heap.hip); null: row order (no tie an operation can see)
+  int64_t* maddr = nullptr;
   int map_tab = -1;          // the map table
   int mapfields = 3;         // map row type printed by --echo-map (B3Rest / B4Rest / B5Rest)
   double perc = 1.0;         // PercentOverlapMapping::perc_ of the criterion
@@ -541,6 +544,16 @@ __device__ __forceinline__ int bg_frest_cmp(const char* text, const uint64_t* re
 
 __device__ __forceinline__ void bg_report(bg_dstatus* st, uint64_t row, int code) {
   atomicMin(&st->first_bad, (unsigned long long)((row << 8) | (uint64_t)code));
+}
+
+// bg_heap.hip: the reference's heap address of every map row (device array), and whether
+// adjacent map rows tie on (start, end) [+ full_rest()]
+int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, int fields, bool ranged,
+                 int64_t range, int64_t** out);
+int bg_heap_ties(bg_ctx* c, const bg_table* M, int fields, bool rest, bool* any);
+// the address of map row m (row order without a replay)
+__device__ __forceinline__ int64_t bg_maddr(const int64_t* addr, uint64_t m) {
+  return addr ? addr[m] : (int64_t)m;
 }
 
 static inline unsigned bg_blocks(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }

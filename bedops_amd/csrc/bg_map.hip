@@ -369,6 +369,7 @@ struct EvArgs {
   const uint64_t* rest_off;
   const uint32_t* rest_len;
   int mapfields;
+  const int64_t* addr;  // simulated heap addresses (bg_heap.hip), null: row order
 };
 
 __device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
@@ -379,7 +380,7 @@ __device__ __forceinline__ bool ev_less(const EvArgs& A, uint64_t a, uint64_t b)
   if (A.ME[a] != A.ME[b]) return A.ME[a] < A.ME[b];
   const int c = ev_rest_cmp(A, a, b);
   if (c != 0) return c < 0;
-  return a < b;
+  return bg_maddr(A.addr, a) < bg_maddr(A.addr, b);
 }
 // the rows of [a, b) that satisfy `pred`, in set order (rows are start-sorted: only runs of
 // equal starts need ordering, by selection)
@@ -584,7 +585,7 @@ static int map_running_sums(bg_ctx* c, int crit, const EvArgs& A, bool need_sq, 
 // carried across such a row. The rows are cut there into independent segments (k_tm_seg),
 // and one thread per segment replays the visitor exactly, in the event order of ev_events,
 // on a sorted copy of the window in HBM scratch sized by the segment's largest window.
-// Addresses: row index (allocation order), as in ev_less.
+// Addresses: the replayed heap addresses (bg_heap.hip) when a tie is possible, as in ev_less.
 struct TmArgs {
   double lo, hi;  // lowerKth_, upperKth_
   int doKth, symmetric, lower;  // lower: the lower marker is maintained (lowerKth_ > 0 && !doKth_)
@@ -671,7 +672,7 @@ __global__ void k_tm_replay(EvArgs A, TmArgs T, const uint64_t* __restrict__ seg
   };
   auto del = [&](uint64_t m) {
     const double v = A.SC[m];
-    const uint64_t p = rank(v, m);
+    const uint64_t p = rank(v, (uint64_t)bg_maddr(A.addr, m));
     if (T.lower) mark_del(L, p, v);
     mark_del(U, p, v);
     for (uint64_t t = p; t + 1 < n; ++t) { V[t] = V[t + 1]; X[t] = X[t + 1]; }
@@ -679,10 +680,11 @@ __global__ void k_tm_replay(EvArgs A, TmArgs T, const uint64_t* __restrict__ seg
   };
   auto add = [&](uint64_t m) {
     const double v = A.SC[m];
-    const uint64_t p = rank(v, m);
+    const uint64_t am = (uint64_t)bg_maddr(A.addr, m);
+    const uint64_t p = rank(v, am);
     for (uint64_t t = n; t > p; --t) { V[t] = V[t - 1]; X[t] = X[t - 1]; }
     V[p] = v;
-    X[p] = m;
+    X[p] = am;
     ++n;
     if (T.lower) mark_add(L, p, v);
     mark_add(U, p, v);
@@ -1084,6 +1086,30 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
 #undef BG_MAP_LAUNCH
   }
   int rc = bg_hip_ok(c, hipGetLastError());
+  // equal map rows are ordered by the reference's heap addresses (bg_heap.hip): replay them
+  // when an operation can see such a tie (two-file mode; single-file mode keeps row order)
+  if (!rc && ref != map && R->n && M->n) {
+    bool want = false, all = false, echo = false, rest_ties = false;
+    for (int k = 0; k < opts->n_ops; ++k) {
+      const int op = opts->ops[k];
+      if (op == BG_MAP_WMEAN || op == BG_MAP_TMEAN) all = true;  // every window's address order
+      if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_SCORE ||
+          op == BG_MAP_ECHO_MAP_SIZE || op == BG_MAP_ECHO_OVERLAP_SIZE)
+        echo = true;  // GenomicAddressCompare: ties of (chrom, start, end)
+      if (op >= BG_MAP_MIN_ELEMENT && op <= BG_MAP_MAX_ELEMENT_RAND) rest_ties = true;
+    }
+    if (decimal) rest_ties = true;  // CoordRestAddressCompare: ties of (start, end, full_rest)
+    if (all) want = true;
+    else if (echo || rest_ties) {
+      bool any = false;
+      rc = bg_heap_ties(c, M, mapfields, !echo, &any);
+      want = any;
+    }
+    if (!rc && want) {
+      if (opts->shard) rc = bg_fail(c, BG_E_UNSUPPORTED, "address-ordered ties span every chromosome: not on a chromosome shard");
+      else rc = bg_heap_addr(c, set, R, M, mapfields, crit == BG_OVR_RANGE, (int64_t)opts->range_bp, &res->maddr);
+    }
+  }
   if (!rc && (decimal || tmean) && R->n) {
     EvArgs E;
     E.RS = R->ks;
@@ -1102,6 +1128,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     E.rest_off = M->rest_off;
     E.rest_len = M->rest_len;
     E.mapfields = mapfields;
+    E.addr = res->maddr;
     if (decimal) rc = map_running_sums(c, crit, E, need_sq, res);
     if (!rc && tmean) {
       if (!M->rest_off)
