@@ -26,7 +26,7 @@ $(OBJ)/%.o: $(SRC)/%.hip $(SRC)/bg_internal.h include/bedgpu.h
 
 $(LIB): $(HIPOBJS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -lz -ldl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lz -ldl -Wl,-rpath,/opt/rocm/lib
 
 $(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)

@@ -60,6 +60,7 @@ static int run_map(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
 }
 
 int main(int argc, char** argv) {
+  CLI_PROG = PROG;
   if (argc <= 1) {
     usage(stderr);
     return EXIT_FAILURE;
@@ -300,25 +301,24 @@ int main(int argc, char** argv) {
   for (int i = a; i < argc; ++i)
     if (!strcmp(argv[i], "-")) shardable = 0;
   if (shardable) {
-    text_buf_t stx[2];
     bg_input sin[2];
-    memset(stx, 0, sizeof(stx));
     memset(sin, 0, sizeof(sin));
-    for (int k = 0; k < nf; ++k)
-      if (read_text(argv[a + k], &stx[k])) arg_error(k ? "Unable to read the map file" : "Unable to read the reference file");
     sin[0].kind = nf == 1 ? skind : rkind;
     sin[1].kind = mkind;
     map_args_t ma;
     ma.o = o;
     ma.o.shard = 1;
     ma.single = nf == 1;
-    if (shard_run(PROG, nf, sin, stx, run_map, &ma) == 0) return EXIT_SUCCESS;
-    for (int k = 0; k < nf; ++k) free_text(&stx[k]);  /* one device after all */
+    if (shard_run(PROG, nf, sin, (const char* const*)(argv + a), run_map, &ma) == 0) return EXIT_SUCCESS;
   }
 
+  cli_mark("start");
+  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+    for (int i = 0; i < nf; ++i) cli_prefetch(argv[a + i]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
+  cli_mark("open");
   text_buf_t tr = {0}, tm = {0};
   bg_input in[2];
   memset(in, 0, sizeof(in));
@@ -339,6 +339,7 @@ int main(int argc, char** argv) {
     in[0].kind = skind;
     bg_set* set = NULL;
     if ((rc = bg_load(ctx, 1, in, &set))) die_ctx(PROG, ctx, rc);
+    cli_prefetch_release(ctx);
     free_text(&tr);
     if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);
     bg_result* res = NULL;
@@ -364,6 +365,8 @@ int main(int argc, char** argv) {
   in[1].kind = mkind;
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
+  cli_prefetch_release(ctx);
+  cli_mark("load");
   free_text(&tr);
   free_text(&tm);
   if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);

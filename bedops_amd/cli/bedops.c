@@ -189,6 +189,7 @@ static int run_op(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
 }
 
 int main(int argc, char** argv) {
+  CLI_PROG = PROG;
   if (argc <= 1) {
     usage(stderr);
     return EXIT_FAILURE;
@@ -351,28 +352,19 @@ int main(int argc, char** argv) {
   /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h); every mode is
    * chromosome-local except --range padding, which looks across the whole file */
   if (!check && !ec && !chrom && !has_range && getenv("BEDGPU_DEVICES")) {
-    for (int i = 0; i < nf; ++i) {
-      if (read_text(argv[a + i], &tx[i])) {
-        char b[1024];
-        snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
-        die_msg(PROG, b);
-      }
-      in[i].kind = input_kind(mode, i, chrom, has_range);
-    }
+    for (int i = 0; i < nf; ++i) in[i].kind = input_kind(mode, i, chrom, has_range);
     op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
-    if (shard_run(PROG, nf, in, tx, run_op, &oa) == 0) return EXIT_SUCCESS;
+    if (shard_run(PROG, nf, in, (const char* const*)(argv + a), run_op, &oa) == 0) return EXIT_SUCCESS;
   }
   cli_mark("start");
+  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+    for (int i = 0; i < nf; ++i) cli_prefetch(argv[a + i]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   cli_mark("open");
   for (int i = 0; i < nf; ++i) {
-    if (tx[i].data) { /* read for the sharded attempt */
-      in[i].data = tx[i].data;
-      in[i].nbytes = tx[i].n;
-      in[i].on_device = 0;
-    } else if (read_input_chrom(ctx, argv[a + i], chrom, check || ec, &tx[i], &in[i])) {
+    if (read_input_chrom(ctx, argv[a + i], chrom, check || ec, &tx[i], &in[i])) {
       char b[1024];
       snprintf(b, sizeof(b), "Unable to read %s", argv[a + i]);
       die_msg(PROG, b);
@@ -393,6 +385,7 @@ int main(int argc, char** argv) {
   cli_mark("read");
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, nf, in, &set))) die_ctx(PROG, ctx, rc);
+  cli_prefetch_release(ctx);
   cli_mark("load");
   for (int i = 0; i < nf; ++i) free_text(&tx[i]);
   if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);

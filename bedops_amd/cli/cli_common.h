@@ -30,6 +30,11 @@ typedef struct {
   void* ddata;    /* the text on the device instead (read_input), freed by free_input */
 } text_buf_t;
 
+/* the running front-end (messages of shared helpers), and whether Starch archives are
+ * decoded (sort-bed reads every input as BED text, as the reference's sort-bed does) */
+static const char* CLI_PROG = "bedops";
+static int CLI_NO_STARCH = 0;
+
 static void die_msg(const char* prog, const char* msg) {
   fprintf(stderr, "May use %s --help for more help.\n\nError: %s\n", prog, msg);
   exit(EXIT_FAILURE);
@@ -79,7 +84,7 @@ static int read_text(const char* path, text_buf_t* out) {
   out->pinned = pinned;
   /* a Starch archive from a file becomes the BED text its streams hold (the reference
    * reads Starch only from files, not stdin: AllocateIterator_BED_starch.hpp:62) */
-  if (fd != 0 && bg_starch_is(buf, n)) {
+  if (fd != 0 && !CLI_NO_STARCH && bg_starch_is(buf, n)) {
     char* txt = NULL;
     uint64_t tn = 0;
     char err[512];
@@ -87,7 +92,7 @@ static int read_text(const char* path, text_buf_t* out) {
     if (pinned) bg_host_free(buf); else free(buf);
     out->data = NULL;
     if (rc) {
-      fprintf(stderr, "May use bedops --help for more help.\n\nError: %s: %s\n", path, err);
+      fprintf(stderr, "May use %s --help for more help.\n\nError: %s: %s\n", CLI_PROG, path, err);
       exit(EXIT_FAILURE);
     }
     out->data = txt;
@@ -108,15 +113,92 @@ static inline int file_is_starch(const char* path) {
   return r > 0 && bg_starch_is(b, (uint64_t)r);
 }
 
+/* Input files that go straight to device memory are mapped (bg_file_map_open: page-cache
+ * pages faulted in, no GPU call) by one thread each, started before bg_open so the mapping
+ * overlaps HIP's initialisation; read_input then registers the mapping and DMAs it to HBM,
+ * and cli_prefetch_release drops the mappings once the loads have copied them. */
+#include <pthread.h>
+#define CLI_MAX_PF 16
+typedef struct {
+  const char* path;
+  bg_file_map m;
+  int ok, started;
+  pthread_t th;
+} cli_pf_t;
+static cli_pf_t CLI_PF[CLI_MAX_PF];
+static int CLI_NPF;
+static inline void* cli_pf_run(void* a) {
+  cli_pf_t* p = (cli_pf_t*)a;
+  p->ok = bg_file_map_open(p->path, &p->m) == 0;
+  if (p->ok && p->m.n >= 4 && !CLI_NO_STARCH) { /* Starch archives: decoded on the host (read_text) */
+    const unsigned char* b = (const unsigned char*)p->m.data;
+    if ((b[0] == 0xca && b[1] == 0x5c && b[2] == 0xad && b[3] == 0xe5) ||
+        bg_starch_is(p->m.data, p->m.n < 512 ? p->m.n : 512)) {
+      bg_file_map_close(&p->m);
+      p->ok = 0;
+    }
+  }
+  return NULL;
+}
+static inline void cli_prefetch(const char* path) {
+  struct stat st;
+  if (CLI_NPF >= CLI_MAX_PF || !strcmp(path, "-") || stat(path, &st) != 0 || !S_ISREG(st.st_mode)) return;
+  cli_pf_t* p = &CLI_PF[CLI_NPF];
+  memset(p, 0, sizeof(*p));
+  p->path = path;
+  if (pthread_create(&p->th, NULL, cli_pf_run, p) == 0) {
+    p->started = 1;
+    ++CLI_NPF;
+  }
+}
+static inline cli_pf_t* cli_pf_take(const char* path) {
+  for (int k = 0; k < CLI_NPF; ++k) {
+    cli_pf_t* p = &CLI_PF[k];
+    if (p->path != path && strcmp(p->path, path) != 0) continue;
+    if (p->started) {
+      pthread_join(p->th, NULL);
+      p->started = 0;
+    }
+    if (p->ok) return p;
+  }
+  return NULL;
+}
+static inline void cli_prefetch_release(bg_ctx* ctx) {
+  if (ctx) bg_sync(ctx); /* every copy from the mappings has completed */
+  for (int k = 0; k < CLI_NPF; ++k) {
+    cli_pf_t* p = &CLI_PF[k];
+    if (p->started) {
+      pthread_join(p->th, NULL);
+      p->started = 0;
+    }
+    if (p->ok) bg_file_map_close(&p->m);
+    p->ok = 0;
+  }
+  CLI_NPF = 0;
+}
+
 /* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
- * go straight to device memory (bg_read_file_device: parallel page-cache reads through a
- * small pinned ring, no whole-file pinning); stdin, pipes and checked inputs are read
- * into host memory. Returns 0 or -1 (unreadable). */
+ * go straight to device memory (their mapping DMA'd from the page cache: cli_prefetch /
+ * bg_read_file_device); stdin, pipes and checked inputs are read into host memory.
+ * Returns 0 or -1 (unreadable). */
 static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, text_buf_t* t, bg_input* in) {
   struct stat st;
   memset(t, 0, sizeof(*t));
+  cli_pf_t* pf = host_needed ? NULL : cli_pf_take(path);
+  if (pf) {
+    void* d = NULL;
+    (void)bg_file_map_register(&pf->m);
+    if (bg_file_map_to_device(ctx, &pf->m, 0, pf->m.n, &d) == 0) {
+      t->ddata = d;
+      t->n = pf->m.n;
+      in->data = d;
+      in->nbytes = pf->m.n;
+      in->on_device = 1;
+      return 0;
+    }
+  }
   if (!host_needed && strcmp(path, "-") != 0 && stat(path, &st) == 0 && S_ISREG(st.st_mode) &&
-      !file_is_starch(path)) {
+      (CLI_NO_STARCH || !file_is_starch(path))) {
     void* d = NULL;
     uint64_t n = 0;
     const int rc = bg_read_file_device(ctx, path, &d, &n);
@@ -322,6 +404,10 @@ static void maybe_stats(bg_ctx* ctx) {
 static inline void fast_exit(void) {
   fflush(stdout);
   fflush(stderr);
+  cli_mark("exit");
+  /* BEDGPU_FULL_EXIT=1: tear down normally (profilers write their traces at exit) */
+  const char* f = getenv("BEDGPU_FULL_EXIT");
+  if (f && *f && strcmp(f, "0") != 0) return;
   _exit(EXIT_SUCCESS);
 }
 

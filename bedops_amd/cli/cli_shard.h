@@ -8,13 +8,16 @@
  *      text — the idea of find_bed_range (interfaces/general-headers/algorithm/bed/
  *      FindBedRange.hpp:67-188): O(chromosomes x log(bytes)) line probes, no full scan;
  *   2. chromosomes go to devices by longest-processing-time on their bytes in all inputs;
- *   3. each device receives only its chromosomes' bytes (one H2D copy per run, over its
- *      own link) and runs load -> operation -> format on its own host thread;
+ *   3. each device receives only its chromosomes' bytes, DMA'd straight from the input
+ *      file's page cache (the files are mapped and registered once, bg_file_map; nothing is
+ *      read into or pinned in host memory), over its own link, and runs load -> operation
+ *      -> format on its own host thread;
  *   4. bg_group_gather reassembles the texts on device 0 in strcmp chromosome order over
  *      RCCL, and device 0 streams them to stdout.
- * Inputs the host checks cannot split cleanly (blank or out-of-order chromosome lines) and
- * any error inside a shard fall back to the one-device path, so error messages and their
- * line numbers are the single-device ones.
+ * Inputs that are not regular files (stdin, pipes), inputs the host checks cannot split
+ * cleanly (blank or out-of-order chromosome lines), a group that cannot be opened (fewer
+ * GPUs than listed, RCCL unavailable) and any error inside a shard fall back to the
+ * one-device path, so error messages and their line numbers are the single-device ones.
  */
 #ifndef BEDOPS_AMD_CLI_SHARD_H
 #define BEDOPS_AMD_CLI_SHARD_H
@@ -118,7 +121,7 @@ typedef struct {
   bg_ctx* ctx;
   int nf;
   const bg_input* proto; /* kinds */
-  const text_buf_t* tx;
+  const bg_file_map* fm; /* the mapped input files */
   const cruns_t* runs;   /* per file */
   const int* owner;      /* global chromosome -> device */
   char (*gnames)[BG_CHR_NAME_CAP];
@@ -160,7 +163,7 @@ static void* shard_worker(void* p) {
     for (int k = 0; k < R->n; ++k) {
       const int g = sh_gindex(J->gnames, J->ngc, R->r[k].name);
       if (g < 0 || J->owner[g] != J->dev) continue;
-      parts[np] = J->tx[f].data + R->r[k].a;
+      parts[np] = J->fm[f].data + R->r[k].a;
       lens[np++] = R->r[k].b - R->r[k].a;
     }
     uint64_t tot = 0;
@@ -189,22 +192,30 @@ static void* shard_worker(void* p) {
     }
     free(o);
   }
+  bg_sync(J->ctx); /* the copies out of the mapped files have completed */
   free(in);
   return NULL;
 }
 
 /* Runs the operation on every device of BEDGPU_DEVICES (>= 2 entries) and writes the
  * reassembled output to fd 1. Returns 0 when done, 1 when the caller should take the
- * one-device path instead (nothing written). */
-static int shard_run(const char* prog, int nf, const bg_input* proto, const text_buf_t* tx,
+ * one-device path instead (nothing written, no input consumed). */
+static int shard_run(const char* prog, int nf, const bg_input* proto, const char* const* paths,
                      shard_op_fn op, void* oparg) {
   int dev[SHARD_MAX_DEV];
   const int nd = env_devices(dev, SHARD_MAX_DEV);
   if (nd < 2) return 1;
-  cruns_t* runs = (cruns_t*)calloc((size_t)nf, sizeof(cruns_t));
-  int ok = 1, total_runs = 0;
+  bg_file_map* fm = (bg_file_map*)calloc((size_t)nf, sizeof(bg_file_map));
+  int ok = 1;
   for (int f = 0; f < nf && ok; ++f) {
-    if (sh_find_runs(tx[f].data, tx[f].n, &runs[f])) ok = 0;
+    struct stat st;
+    ok = strcmp(paths[f], "-") != 0 && stat(paths[f], &st) == 0 && S_ISREG(st.st_mode) &&
+         !file_is_starch(paths[f]) && bg_file_map_open(paths[f], &fm[f]) == 0;
+  }
+  cruns_t* runs = (cruns_t*)calloc((size_t)nf, sizeof(cruns_t));
+  int total_runs = 0;
+  for (int f = 0; f < nf && ok; ++f) {
+    if (sh_find_runs(fm[f].data, fm[f].n, &runs[f])) ok = 0;
     total_runs += runs[f].n;
   }
   /* the global chromosome list (strcmp order) and bytes per chromosome */
@@ -220,9 +231,13 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const text
     ngc = u;
   }
   if (!ok || ngc < 2) { /* nothing to split */
-    for (int f = 0; f < nf; ++f) free(runs[f].r);
+    for (int f = 0; f < nf; ++f) {
+      free(runs[f].r);
+      bg_file_map_close(&fm[f]);
+    }
     free(runs);
     free(gn);
+    free(fm);
     return 1;
   }
   uint64_t* bytes = (uint64_t*)calloc((size_t)ngc, sizeof(uint64_t));
@@ -252,14 +267,31 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const text
   }
   bg_group* grp = NULL;
   int rc = bg_group_open(&grp, dev, nd);
-  if (rc) die_msg(prog, "cannot open the GPU devices of BEDGPU_DEVICES (libbedgpu/HIP/RCCL)");
+  if (rc) { /* fewer GPUs than listed, RCCL unavailable, ...: one device instead */
+    const char* st = getenv("BEDGPU_STATS");
+    if (st && *st && strcmp(st, "0") != 0)
+      fprintf(stderr, "bedgpu: BEDGPU_DEVICES group not available (%d); one device\n", rc);
+    for (int f = 0; f < nf; ++f) {
+      free(runs[f].r);
+      bg_file_map_close(&fm[f]);
+    }
+    free(runs);
+    free(gn);
+    free(bytes);
+    free(order);
+    free(owner);
+    free(fm);
+    return 1;
+  }
+  cli_mark("open");
+  for (int f = 0; f < nf; ++f) (void)bg_file_map_register(&fm[f]); /* DMA source for every device */
   shard_job_t* J = (shard_job_t*)calloc((size_t)nd, sizeof(shard_job_t));
   pthread_t* th = (pthread_t*)calloc((size_t)nd, sizeof(pthread_t));
   for (int d = 0; d < nd; ++d) {
     J[d].ctx = bg_group_ctx(grp, d);
     J[d].nf = nf;
     J[d].proto = proto;
-    J[d].tx = tx;
+    J[d].fm = fm;
     J[d].runs = runs;
     J[d].owner = owner;
     J[d].gnames = gn;
@@ -277,6 +309,8 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const text
     pthread_join(th[d], NULL);
     failed = failed || J[d].rc;
   }
+  cli_mark("shards");
+  for (int f = 0; f < nf; ++f) bg_file_map_close(&fm[f]); /* the loads have synchronised */
   int done = 0;
   if (!failed) {
     const char** texts = (const char**)calloc((size_t)nd, sizeof(char*));
@@ -319,6 +353,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const text
   free(owner);
   free(J);
   free(th);
+  free(fm);
   return done ? 0 : 1;
 }
 

@@ -49,6 +49,7 @@ static int run_closest(void* arg, bg_ctx* ctx, bg_set* set, bg_result** res) {
 }
 
 int main(int argc, char** argv) {
+  CLI_PROG = PROG;
   if (argc <= 1) {
     usage(stderr);
     return EXIT_FAILURE;
@@ -106,21 +107,19 @@ int main(int argc, char** argv) {
 
   /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h) */
   if (!check && !ec && !chrom && getenv("BEDGPU_DEVICES") && strcmp(argv[a], "-") && strcmp(argv[a + 1], "-")) {
-    text_buf_t stx[2];
     bg_input sin[2];
-    memset(stx, 0, sizeof(stx));
     memset(sin, 0, sizeof(sin));
-    for (int k = 0; k < 2; ++k) {
-      if (read_text(argv[a + k], &stx[k])) arg_error("Unable to read an input file");
-      sin[k].kind = BG_BED3_REST;
-    }
-    if (shard_run(PROG, 2, sin, stx, run_closest, &o) == 0) return EXIT_SUCCESS;
-    for (int k = 0; k < 2; ++k) free_text(&stx[k]);  /* one device after all */
+    for (int k = 0; k < 2; ++k) sin[k].kind = BG_BED3_REST;
+    if (shard_run(PROG, 2, sin, (const char* const*)(argv + a), run_closest, &o) == 0) return EXIT_SUCCESS;
   }
 
+  cli_mark("start");
+  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+    for (int k = 0; k < 2; ++k) cli_prefetch(argv[a + k]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
+  cli_mark("open");
   text_buf_t t[2] = {{0}, {0}};
   bg_input in[2];
   for (int k = 0; k < 2; ++k) {
@@ -135,6 +134,8 @@ int main(int argc, char** argv) {
   }
   bg_set* set = NULL;
   if ((rc = bg_load(ctx, 2, in, &set))) die_ctx(PROG, ctx, rc);
+  cli_prefetch_release(ctx);
+  cli_mark("load");
   free_text(&t[0]);
   free_text(&t[1]);
   if (chrom && (rc = bg_set_restrict_chrom(ctx, set, chrom))) die_ctx(PROG, ctx, rc);

@@ -87,6 +87,8 @@ static void line_error(const bg_sortbed_error* e, const char* fn) {
 }
 
 int main(int argc, char** argv) {
+  CLI_PROG = PROG;
+  CLI_NO_STARCH = 1; /* the reference's sort-bed reads Starch archives as BED text */
   if (argc < 2) {
     banner(stderr, 1);
     return EXIT_FAILURE;

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -182,12 +183,6 @@ extern "C" void bg_close(bg_ctx* c) {
   hipFree(c->dstat);
   hipHostFree(c->hstat);
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
-  for (auto s : c->rd_stream)
-    if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
-  for (auto e : c->rd_ev)
-    if (e) hipEventDestroy(e);
-  for (auto p : c->rd_slot)
-    if (p) hipHostFree(p);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -322,67 +317,217 @@ static int write_all(int fd, const char* p, uint64_t n) {
   return 0;
 }
 
-// BEDGPU_RD_THREADS (1..32, default 8) and BEDGPU_RD_CHUNK_MB (1..64, default 2) size the
-// ring; read once per process (the slots are allocated at a context's first read)
-static int rd_env(const char* name, int dflt, int lo, int hi) {
-  const char* s = getenv(name);
-  if (!s || !*s) return dflt;
-  const int v = atoi(s);
-  return v < lo ? lo : (v > hi ? hi : v);
+// ---------------------------------------------------------------------------------------
+// Files <-> HBM without host copies. Inputs: the file is mapped (MAP_POPULATE: page-table
+// entries for its page-cache pages, no GPU call, so it can run while bg_open initialises
+// HIP), the mapping is registered for DMA (hipHostRegister, portable: every device of a group
+// can read it) and copied to HBM by the DMA engines straight from the page cache. Measured on
+// the box (tools/e2e_probe.cpp, 2.38 GB): populate ~20 ms, register 10-19 ms, copy ~45 ms
+// (50-57 GB/s), against a pinned ring filled by pread threads (~70 ms incl. pinning) that
+// also needed extra copy streams (8-40 ms each to create, and more to tear down at exit).
+// ---------------------------------------------------------------------------------------
+extern "C" int bg_file_map_open(const char* path, bg_file_map* m) {
+  if (!path || !m) return BG_E_ARG;
+  memset(m, 0, sizeof(*m));
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return BG_E_IO;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+    close(fd);
+    return BG_E_ARG;
+  }
+  m->n = (uint64_t)st.st_size;
+  if (m->n) {
+    void* p = mmap(nullptr, (size_t)m->n, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+    if (p == MAP_FAILED) {
+      close(fd);
+      m->n = 0;
+      return BG_E_IO;
+    }
+    m->data = (const char*)p;
+  }
+  close(fd);
+  return 0;
 }
-static const int RD_THREADS = rd_env("BEDGPU_RD_THREADS", 8, 1, 32);
-static const uint64_t RD_CHUNK = (uint64_t)rd_env("BEDGPU_RD_CHUNK_MB", 2, 1, 64) << 20;
-// copy streams of the ring (BEDGPU_RD_STREAMS, 0..32, default 2): reader t issues on stream
-// t % RD_STREAMS; 0 issues every copy on the context's own stream. Creating a stream costs
-// several ms on first use, and the H2D copies share one link either way.
-static const int RD_STREAMS = rd_env("BEDGPU_RD_STREAMS", 2, 0, 32);
 
-// streams n bytes of device memory to fd through pinned buffers, so the D2H copies of the
-// next chunks overlap write(2) of this one: the context's reader ring when it exists (its
-// slots are free once the loader's stream has waited for the input copies, and the copies
-// below are on that stream), else two 64 MiB buffers of its own; every exit path frees
-// what it allocated
+extern "C" int bg_file_map_register(bg_file_map* m) {
+  if (!m) return BG_E_ARG;
+  if (m->registered || !m->n) return 0;
+  if (hipHostRegister((void*)m->data, (size_t)m->n, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return BG_E_HIP;  // the copies still work (pageable source), staged by the runtime
+  }
+  m->registered = 1;
+  return 0;
+}
+
+extern "C" int bg_file_map_to_device(bg_ctx* c, const bg_file_map* m, uint64_t off, uint64_t len, void** out) {
+  if (!c || !m || !out || off > m->n || len > m->n - off) return BG_E_ARG;
+  *out = nullptr;
+  bg_bind(c);
+  char* d = (char*)bg_alloc(c, len + 64);
+  if (!d) return BG_E_NOMEM;
+  if (len) {
+    const hipError_t e = hipMemcpyAsync(d, m->data + off, (size_t)len, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+      bg_release(c, d);
+      return bg_hip_fail(c, e, "file map copy");
+    }
+  }
+  *out = d;
+  return 0;
+}
+
+extern "C" void bg_file_map_close(bg_file_map* m) {
+  if (!m) return;
+  if (m->registered) (void)hipHostUnregister((void*)m->data);
+  if (m->data && m->n) munmap((void*)m->data, (size_t)m->n);
+  memset(m, 0, sizeof(*m));
+}
+
+// a regular file straight into a new device buffer (the four calls above, in order); the
+// mapping is released once the copy completed
+extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint64_t* nbytes) {
+  if (!c || !path || !out || !nbytes) return BG_E_ARG;
+  *out = nullptr;
+  *nbytes = 0;
+  bg_file_map m;
+  int rc = bg_file_map_open(path, &m);
+  if (rc) return bg_fail(c, rc, std::string("cannot map ") + path);
+  const uint64_t n = m.n;
+  bg_bind(c);
+  (void)bg_file_map_register(&m);
+  void* d = nullptr;
+  rc = bg_file_map_to_device(c, &m, 0, n, &d);
+  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  bg_file_map_close(&m);
+  if (rc) {
+    bg_release(c, d);
+    return rc;
+  }
+  bg_mark(c, "read");
+  *out = d;
+  *nbytes = n;
+  return 0;
+}
+
+// Output to a regular file: the byte range [off, off + n) of the file is mapped shared, its
+// pages are allocated by a few threads at once (MADV_POPULATE_WRITE; buffered write(2) to
+// one file serialises on its inode lock: ~90 ms for 0.92 GB measured), the mapping is
+// registered and the text is DMA'd from HBM into the page cache. -1: not possible here (the
+// caller streams through write(2) instead; nothing reached the file).
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+static int write_device_mapped(bg_ctx* c, const void* d, uint64_t n, int fd) {
+  struct stat st;
+  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return -1;
+  const int fl = fcntl(fd, F_GETFL);
+  if (fl < 0 || (fl & O_APPEND) || (fl & O_ACCMODE) == O_RDONLY) return -1;
+  const off_t off = lseek(fd, 0, SEEK_CUR);
+  if (off < 0) return -1;
+  // a MAP_SHARED writable mapping needs the descriptor open for reading too: map through
+  // /proc/self/fd (the same file, opened O_RDWR) when fd is write-only
+  int mfd = fd;
+  if ((fl & O_ACCMODE) != O_RDWR) {
+    char p[64];
+    snprintf(p, sizeof(p), "/proc/self/fd/%d", fd);
+    mfd = open(p, O_RDWR);
+    if (mfd < 0) return -1;
+  }
+  const uint64_t end = (uint64_t)off + n;
+  const bool grow = (uint64_t)st.st_size < end;
+  if (grow && ftruncate(mfd, (off_t)end) != 0) {
+    if (mfd != fd) close(mfd);
+    return -1;
+  }
+  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uint64_t pa = (uint64_t)off & ~(pg - 1), len = end - pa;
+  char* map = (char*)mmap(nullptr, (size_t)len, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, (off_t)pa);
+  if (mfd != fd) close(mfd);
+  if (map == MAP_FAILED) {
+    if (grow) (void)ftruncate(fd, st.st_size);
+    return -1;
+  }
+  // page allocation in parallel slices (without MADV_POPULATE_WRITE the registration below
+  // faults the pages in itself)
+  const int T = (int)std::min<uint64_t>(8, (len + (64ull << 20) - 1) / (64ull << 20));
+  if (T > 1) {
+    std::vector<std::thread> th;
+    const uint64_t per = ((len / T) + pg - 1) & ~(pg - 1);
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([=]() {
+        const uint64_t a = (uint64_t)t * per;
+        if (a < len) (void)madvise(map + a, (size_t)std::min(per, len - a), MADV_POPULATE_WRITE);
+      });
+    for (auto& x : th) x.join();
+  }
+  int rc = 0;
+  if (hipHostRegister(map, (size_t)len, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    rc = -1;
+  } else {
+    hipError_t e = hipMemcpyAsync(map + ((uint64_t)off - pa), d, (size_t)n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipHostUnregister(map);
+    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device copy");
+  }
+  munmap(map, (size_t)len);
+  if (rc == -1 && grow) (void)ftruncate(fd, st.st_size);
+  if (rc == 0 && lseek(fd, (off_t)end, SEEK_SET) < 0)
+    rc = bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
+  return rc;
+}
+
+// streams n bytes of device memory to fd: a regular file by DMA into its mapped pages
+// (write_device_mapped), anything else (pipes, terminals, appends) through two registered
+// 64 MiB host buffers, the D2H copy of the next chunk overlapping write(2) of this one
 extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
   if (!c || (!d && n)) return BG_E_ARG;
   if (n == 0) return 0;
   bg_bind(c);
-  const bool ring = !c->rd_slot.empty();
-  const uint64_t CH = ring ? RD_CHUNK : (64ull << 20);
-  const uint64_t ns = ring ? c->rd_slot.size() : 2;
-  char* own[2] = {nullptr, nullptr};
-  hipEvent_t own_ev[2] = {nullptr, nullptr};
-  int rc = 0;
-  for (int k = 0; k < 2 && !ring && !rc; ++k) {
-    hipError_t e = hipHostMalloc((void**)&own[k], CH, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&own_ev[k], hipEventDisableTiming);
-    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device buffers");
+  const char* nm = getenv("BEDGPU_WRITE_MAP");  // 0: always stream through write(2)
+  const int mr = (nm && strcmp(nm, "0") == 0) ? -1 : write_device_mapped(c, d, n, fd);
+  if (mr != -1) {
+    bg_mark(c, "write");
+    return mr;
   }
-  char* const* hb = ring ? c->rd_slot.data() : own;
-  hipEvent_t* ev = ring ? c->rd_ev.data() : own_ev;
+  const uint64_t CH = std::min<uint64_t>(64ull << 20, (n + 4095) & ~4095ull);
+  char* buf = (char*)malloc(2 * CH);
+  if (!buf) return BG_E_NOMEM;
+  const bool reg = hipHostRegister(buf, 2 * CH, hipHostRegisterDefault) == hipSuccess;
+  if (!reg) (void)hipGetLastError();
+  char* hb[2] = {buf, buf + CH};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = 0;
+  for (int k = 0; k < 2 && !rc; ++k) {
+    const hipError_t e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device events");
+  }
   const char* src = (const char*)d;
   const uint64_t nch = (n + CH - 1) / CH;
   auto issue = [&](uint64_t k) -> int {
     const uint64_t off = k * CH, len = std::min(CH, n - off);
-    hipError_t e = hipMemcpyAsync(hb[k % ns], src + off, len, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipEventRecord(ev[k % ns], c->stream);
+    hipError_t e = hipMemcpyAsync(hb[k % 2], src + off, len, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(ev[k % 2], c->stream);
     return e == hipSuccess ? 0 : bg_hip_fail(c, e, "bg_write_device copy");
   };
-  for (uint64_t k = 0; k < std::min(ns, nch) && !rc; ++k) rc = issue(k);
+  for (uint64_t k = 0; k < std::min<uint64_t>(2, nch) && !rc; ++k) rc = issue(k);
   for (uint64_t k = 0; k < nch && !rc; ++k) {
-    hipError_t e = hipEventSynchronize(ev[k % ns]);
+    hipError_t e = hipEventSynchronize(ev[k % 2]);
     if (e != hipSuccess) { rc = bg_hip_fail(c, e, "bg_write_device sync"); break; }
     const uint64_t off = k * CH, len = std::min(CH, n - off);
-    if (write_all(fd, hb[k % ns], len)) {
+    if (write_all(fd, hb[k % 2], len)) {
       rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
       break;
     }
-    if (k + ns < nch) rc = issue(k + ns);  // the slot just written out takes chunk k + ns
+    if (k + 2 < nch) rc = issue(k + 2);  // the buffer just written out takes chunk k + 2
   }
   hipStreamSynchronize(c->stream);
-  for (int k = 0; k < 2; ++k) {
-    if (own[k]) hipHostFree(own[k]);
-    if (own_ev[k]) hipEventDestroy(own_ev[k]);
-  }
+  for (int k = 0; k < 2; ++k)
+    if (ev[k]) hipEventDestroy(ev[k]);
+  if (reg) (void)hipHostUnregister(buf);
+  free(buf);
   bg_mark(c, "write");
   return rc;
 }
@@ -396,11 +541,12 @@ extern "C" int bg_result_write(bg_ctx* c, bg_result* r, int fd) {
   return wr ? wr : rc;  // BG_E_VISITOR after the text before the stop is written
 }
 
-// host parts (pinned for async DMA) copied back to back into one new device buffer: a
-// chromosome shard of a file assembled on the GPU that will parse it (bg_input.on_device)
+// host parts (pinned, registered or pageable) copied back to back into one new device
+// buffer: a chromosome shard of a file assembled on the GPU that will parse it
 extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts, const uint64_t* lens,
                                      void** out, uint64_t* total) {
   if (!c || n < 0 || !out || !total || (n && (!parts || !lens))) return BG_E_ARG;
+  bg_bind(c);
   uint64_t t = 0;
   for (int k = 0; k < n; ++k) t += lens[k];
   char* d = (char*)bg_alloc(c, t + 64);
@@ -412,121 +558,6 @@ extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts,
   }
   *out = d;
   *total = t;
-  return 0;
-}
-
-// A regular file straight into a new device buffer: RD_THREADS readers pread interleaved
-// 16 MiB chunks into their own two pinned slots and copy each to HBM on their own stream
-// while reading the next, so the page-cache reads run in parallel and overlap the H2D
-// copies; only 2 x RD_THREADS x 16 MiB of host memory is ever pinned (pinning the whole
-// file costs more than reading it). The context's stream waits for every copy.
-extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint64_t* nbytes) {
-  if (!c || !path || !out || !nbytes) return BG_E_ARG;
-  *out = nullptr;
-  *nbytes = 0;
-  const int fd = open(path, O_RDONLY);
-  if (fd < 0) return bg_fail(c, BG_E_IO, std::string("cannot open ") + path);
-  struct stat st;
-  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
-    close(fd);
-    return bg_fail(c, BG_E_ARG, std::string(path) + " is not a regular file");
-  }
-  const uint64_t n = (uint64_t)st.st_size;
-  bg_bind(c);
-  char* d = (char*)bg_alloc(c, n + 64);
-  if (!d) {
-    close(fd);
-    return BG_E_NOMEM;
-  }
-  bg_mark(c, "dalloc");
-  // the ring is allocated by the reader threads themselves at the context's first read
-  // (two slots, their events and a copy stream each, in parallel: pinning is slow)
-  const bool fresh = c->rd_slot.empty();
-  if (fresh) {
-    c->rd_slot.assign(2 * RD_THREADS, nullptr);
-    c->rd_ev.assign(2 * RD_THREADS, nullptr);
-    c->rd_stream.assign(std::min(RD_STREAMS, RD_THREADS), nullptr);
-    for (auto& x : c->rd_stream)
-      if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) {
-        for (auto& y : c->rd_stream)
-          if (y) hipStreamDestroy(y);
-        c->rd_stream.clear();
-        c->rd_slot.clear();
-        c->rd_ev.clear();
-        bg_release(c, d);
-        close(fd);
-        return bg_fail(c, BG_E_HIP, "reader ring streams");
-      }
-  }
-  auto rd_strm = [&](int t) { return c->rd_stream.empty() ? c->stream : c->rd_stream[t % c->rd_stream.size()]; };
-  const uint64_t nch = (n + RD_CHUNK - 1) / RD_CHUNK;
-  std::atomic<int> bad{0};
-  auto reader = [&](int t) {
-    if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
-    if (fresh) {
-      using clk = std::chrono::steady_clock;
-      const auto t0 = clk::now();
-      for (int k = 2 * t; k < 2 * t + 2; ++k)
-        if (hipHostMalloc((void**)&c->rd_slot[k], RD_CHUNK, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&c->rd_ev[k], hipEventDisableTiming) != hipSuccess) { bad = 1; return; }
-      if (c->stats && t == 0)  // first-use cost of the ring (stderr, BEDGPU_STATS only)
-        fprintf(stderr, "bedgpu ring   pin+events %.3f ms\n",
-                std::chrono::duration<double, std::milli>(clk::now() - t0).count());
-    }
-    uint64_t j = 0;
-    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += RD_THREADS, ++j) {
-      const int slot = 2 * t + (int)(j & 1);
-      if (hipEventSynchronize(c->rd_ev[slot]) != hipSuccess) { bad = 1; return; }
-      const uint64_t off = k * RD_CHUNK, len = std::min<uint64_t>(RD_CHUNK, n - off);
-      uint64_t got = 0;
-      while (got < len) {
-        const ssize_t r = pread(fd, c->rd_slot[slot] + got, len - got, (off_t)(off + got));
-        if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) { bad = 2; return; }
-        got += (uint64_t)r;
-      }
-      const auto q0 = std::chrono::steady_clock::now();
-      if (hipMemcpyAsync(d + off, c->rd_slot[slot], len, hipMemcpyHostToDevice, rd_strm(t)) != hipSuccess ||
-          hipEventRecord(c->rd_ev[slot], rd_strm(t)) != hipSuccess) {
-        bad = 1;
-        return;
-      }
-      if (c->stats && t == 0 && j == 0)
-        fprintf(stderr, "bedgpu ring   first copy issue %.3f ms\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
-    }
-  };
-  std::vector<std::thread> th;
-  const int nt = fresh ? RD_THREADS : (int)std::min<uint64_t>((uint64_t)RD_THREADS, nch);
-  for (int t = 0; t < nt; ++t) th.emplace_back(reader, t);
-  for (auto& x : th) x.join();
-  close(fd);
-  bg_mark(c, "preads");
-  if (bad) {  // copies already issued still target d: drain them before releasing it
-    hipStreamSynchronize(c->stream);
-    for (auto s : c->rd_stream)
-      if (s) hipStreamSynchronize(s);
-    if (fresh) {  // a ring that failed to build is dropped whole (the next read rebuilds it)
-      for (auto s : c->rd_stream)
-        if (s) hipStreamDestroy(s);
-      for (auto e : c->rd_ev)
-        if (e) hipEventDestroy(e);
-      for (auto p : c->rd_slot)
-        if (p) hipHostFree(p);
-      c->rd_stream.clear();
-      c->rd_ev.clear();
-      c->rd_slot.clear();
-    }
-    bg_release(c, d);
-    return bad == 2 ? bg_fail(c, BG_E_IO, std::string("read failed: ") + path)
-                    : bg_fail(c, BG_E_HIP, std::string("copy failed: ") + path);
-  }
-  for (size_t t = 0; t < c->rd_stream.size(); ++t) {  // the loader's stream waits for the copies
-    BG_HIP(c, hipEventRecord(c->rd_ev[2 * t], c->rd_stream[t]));
-    BG_HIP(c, hipStreamWaitEvent(c->stream, c->rd_ev[2 * t], 0));
-  }
-  *out = d;
-  *nbytes = n;
   return 0;
 }
 

@@ -14,13 +14,68 @@
 //                       caller distributes): bench.py under torch.distributed.run
 // A device listed twice (tests on a one-GPU machine) gets no communicator; transfers then
 // are device-local copies and the sizes are exchanged on the host.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
-
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "bg_internal.h"
+
+// RCCL is loaded on first use (dlopen), not linked: librccl is a 570 MB library whose load
+// and fat-binary registration would otherwise be paid by every single-GPU run of the CLIs at
+// process start. The header gives the types; these pointers are the entry points.
+namespace {
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclAllReduce) AllReduce = nullptr;
+  decltype(&ncclSend) Send = nullptr;
+  decltype(&ncclRecv) Recv = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+Rccl& rccl() {
+  static Rccl R;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      R.err = e ? e : "dlopen librccl.so.1 failed";
+      return;
+    }
+#define BG_SYM(f)                                                         \
+  R.f = reinterpret_cast<decltype(R.f)>(dlsym(h, "nccl" #f));             \
+  if (!R.f) {                                                             \
+    R.err = "librccl.so.1 lacks nccl" #f;                                 \
+    return;                                                               \
+  }
+    BG_SYM(GetUniqueId) BG_SYM(CommInitAll) BG_SYM(CommInitRank) BG_SYM(CommDestroy) BG_SYM(AllReduce)
+    BG_SYM(Send) BG_SYM(Recv) BG_SYM(GroupStart) BG_SYM(GroupEnd) BG_SYM(GetErrorString)
+#undef BG_SYM
+    R.ok = true;
+  });
+  return R;
+}
+}  // namespace
+#define ncclGetUniqueId rccl().GetUniqueId
+#define ncclCommInitAll rccl().CommInitAll
+#define ncclCommInitRank rccl().CommInitRank
+#define ncclCommDestroy rccl().CommDestroy
+#define ncclAllReduce rccl().AllReduce
+#define ncclSend rccl().Send
+#define ncclRecv rccl().Recv
+#define ncclGroupStart rccl().GroupStart
+#define ncclGroupEnd rccl().GroupEnd
+#define ncclGetErrorString rccl().GetErrorString
 
 struct bg_group {
   std::vector<bg_ctx*> ctx;      // local members
@@ -40,6 +95,7 @@ static int nccl_fail(bg_ctx* c, ncclResult_t r, const char* what) {
 
 extern "C" int bg_group_uid(void* uid) {
   if (!uid) return BG_E_ARG;
+  if (!rccl().ok) return BG_E_HIP;
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) return BG_E_HIP;
   static_assert(sizeof(ncclUniqueId) <= BG_UID_BYTES, "unique id size");
@@ -65,6 +121,11 @@ extern "C" int bg_group_open(bg_group** out, const int* devices, int n) {
   }
   g->nranks = n;
   if (distinct && n > 1) {
+    if (!rccl().ok) {
+      bg_fail(g->ctx[0], BG_E_HIP, "RCCL unavailable: " + rccl().err);
+      bg_group_close(g);
+      return BG_E_HIP;
+    }
     g->comm.resize(n);
     if (ncclCommInitAll(g->comm.data(), n, devices) != ncclSuccess) {
       g->comm.clear();
@@ -90,6 +151,10 @@ extern "C" int bg_group_open_rank(bg_group** out, int device, const void* uid, i
   g->nranks = nranks;
   g->rank0 = rank;
   if (nranks > 1) {
+    if (!rccl().ok) {
+      bg_group_close(g);
+      return BG_E_HIP;
+    }
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
     g->comm.resize(1);
@@ -150,7 +215,18 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
   } else {
     std::vector<uint64_t*> dbuf(nl, nullptr);
     std::vector<uint64_t> h(2 * nc);
-    for (int k = 0; k < nl; ++k) {
+    // every exit below releases the size buffers, and a group that was started is ended
+    auto release = [&]() {
+      for (int k = 0; k < nl; ++k)
+        if (dbuf[k]) {
+          bg_bind(g->ctx[k]);
+          hipStreamSynchronize(g->ctx[k]->stream);
+          bg_release(g->ctx[k], dbuf[k]);
+          dbuf[k] = nullptr;
+        }
+    };
+    int rc = 0;
+    for (int k = 0; k < nl && !rc; ++k) {
       bg_ctx* c = g->ctx[k];
       bg_bind(c);
       for (uint64_t q = 0; q < nc; ++q) {
@@ -158,25 +234,29 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
         h[nc + q] = len[k][q] ? (uint64_t)(g->rank0 + k) + 1 : 0;
       }
       dbuf[k] = (uint64_t*)bg_alloc(c, 16 * (nc ? nc : 1));
-      if (!dbuf[k]) return BG_E_NOMEM;
-      if (nc) BG_HIP(c, hipMemcpyAsync(dbuf[k], h.data(), 16 * nc, hipMemcpyHostToDevice, c->stream));
-      BG_HIP(c, hipStreamSynchronize(c->stream));  // h is reused for the next member
+      if (!dbuf[k]) { rc = BG_E_NOMEM; break; }
+      if (nc) rc = bg_hip_ok(c, hipMemcpyAsync(dbuf[k], h.data(), 16 * nc, hipMemcpyHostToDevice, c->stream));
+      if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));  // h is reused for the next member
     }
-    if (nc) {
-      BG_NCCL(c0, ncclGroupStart());
-      for (int k = 0; k < nl; ++k)
-        BG_NCCL(g->ctx[k], ncclAllReduce(dbuf[k], dbuf[k], 2 * nc, ncclUint64, ncclSum, g->comm[k],
-                                         g->ctx[k]->stream));
-      BG_NCCL(c0, ncclGroupEnd());
+    if (!rc && nc) {
+      ncclResult_t r = ncclGroupStart();
+      const bool started = r == ncclSuccess;
+      if (!started) rc = nccl_fail(c0, r, "ncclGroupStart");
+      for (int k = 0; k < nl && !rc; ++k) {
+        r = ncclAllReduce(dbuf[k], dbuf[k], 2 * nc, ncclUint64, ncclSum, g->comm[k], g->ctx[k]->stream);
+        if (r != ncclSuccess) rc = nccl_fail(g->ctx[k], r, "ncclAllReduce");
+      }
+      if (started) {  // a started group is always ended
+        const ncclResult_t e = ncclGroupEnd();
+        if (!rc && e != ncclSuccess) rc = nccl_fail(c0, e, "ncclGroupEnd");
+      }
     }
-    for (int k = 0; k < nl; ++k) {
-      bg_ctx* c = g->ctx[k];
-      bg_bind(c);
-      if (k == 0 && nc)
-        BG_HIP(c, hipMemcpyAsync(tot.data(), dbuf[k], 16 * nc, hipMemcpyDeviceToHost, c->stream));
-      BG_HIP(c, hipStreamSynchronize(c->stream));
-      bg_release(c, dbuf[k]);
+    if (!rc && nc) {
+      bg_bind(c0);
+      rc = bg_hip_ok(c0, hipMemcpyAsync(tot.data(), dbuf[0], 16 * nc, hipMemcpyDeviceToHost, c0->stream));
     }
+    release();
+    if (rc) return rc;
   }
   std::vector<uint64_t> G(nc + 1, 0);
   for (uint64_t q = 0; q < nc; ++q) G[q + 1] = G[q] + tot[q];
@@ -215,17 +295,35 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
     bool any = false;
     for (const Run& r : runs) any = any || r.owner != 0;
     if (any) {
-      BG_NCCL(c0, ncclGroupStart());
-      for (const Run& r : runs) {
+      int rc = 0;
+      ncclResult_t e = ncclGroupStart();
+      const bool started = e == ncclSuccess;
+      if (!started) rc = nccl_fail(c0, e, "ncclGroupStart");
+      for (size_t i = 0; i < runs.size() && !rc; ++i) {
+        const Run& r = runs[i];
         if (r.owner == 0) continue;
         const int ks = r.owner - g->rank0;
-        if (ks >= 0 && ks < nl)
-          BG_NCCL(g->ctx[ks], ncclSend(text[ks] + off[ks][r.first], r.bytes, ncclChar, 0, g->comm[ks],
-                                       g->ctx[ks]->stream));
-        if (root)
-          BG_NCCL(c0, ncclRecv(dst + G[r.first], r.bytes, ncclChar, r.owner, g->comm[0], c0->stream));
+        if (ks >= 0 && ks < nl) {
+          e = ncclSend(text[ks] + off[ks][r.first], r.bytes, ncclChar, 0, g->comm[ks], g->ctx[ks]->stream);
+          if (e != ncclSuccess) rc = nccl_fail(g->ctx[ks], e, "ncclSend");
+        }
+        if (!rc && root) {
+          e = ncclRecv(dst + G[r.first], r.bytes, ncclChar, r.owner, g->comm[0], c0->stream);
+          if (e != ncclSuccess) rc = nccl_fail(c0, e, "ncclRecv");
+        }
       }
-      BG_NCCL(c0, ncclGroupEnd());
+      if (started) {  // a started group is always ended
+        const ncclResult_t z = ncclGroupEnd();
+        if (!rc && z != ncclSuccess) rc = nccl_fail(c0, z, "ncclGroupEnd");
+      }
+      if (rc) {
+        for (int k = 0; k < nl; ++k) {
+          bg_bind(g->ctx[k]);
+          hipStreamSynchronize(g->ctx[k]->stream);
+        }
+        if (dst) bg_release(c0, dst);
+        return rc;
+      }
     }
   }
   for (int k = 0; k < nl; ++k) {

@@ -66,10 +66,6 @@ struct bg_ctx {
   std::vector<std::pair<char*, size_t>> pin_chunks;
   size_t pin_chunk = 0, pin_used = 0;
   hipStream_t stream = nullptr;
-  // bg_read_file_device: pinned staging slots, their events and one copy stream per reader
-  std::vector<char*> rd_slot;
-  std::vector<hipEvent_t> rd_ev;
-  std::vector<hipStream_t> rd_stream;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
   bg_dstatus* hstat = nullptr;  // pinned host mirror

@@ -22,8 +22,9 @@
 //                             to the host, ranked by strcmp, ranks looked up per line and
 //                             every line's name compared with its representative's
 //   sort                      stable LSD radix: by end, then by (rank << 40 | start)
-//   k_sb_ties                 runs of equal (chromosome, start, end): ordered by the rest
-//                             (strcmp; no rest first) by insertion inside the run
+//   sb_order_ties             runs of equal (chromosome, start, end): ordered by the rest
+//                             (strcmp; no rest first) by rounds of radix refinement on
+//                             8-byte rest chunks (k_sb_tflag/tgather/trid/tpick/tput)
 // The output is a RES_MULTI result (chrom/start/end keys + the rest's address and length)
 // whose rest is printed after a tab.
 #include <string.h>
@@ -313,27 +314,122 @@ __device__ __forceinline__ bool sb_rest_less(const uint64_t* R, const uint32_t* 
   return la < lb;
 }
 
-// runs of equal (chromosome, start, end) ordered by their rests (insertion inside the run)
-__global__ void k_sb_ties(const uint64_t* __restrict__ k1, const uint64_t* __restrict__ idx,
-                          const int64_t* __restrict__ endv, const uint64_t* __restrict__ R,
-                          const uint32_t* __restrict__ RL, uint64_t nd, uint32_t* __restrict__ ord) {
+// Runs of equal (chromosome, start, end) are ordered by their rests (bcd_cmp: no rest first,
+// else strcmp) in rounds of radix refinement, so a run of any length costs O(run) per round:
+// round q sorts the rows still tied on (key, end, rest bytes [0, 8q)) by rest bytes
+// [8q, 8q + 8) inside their run (stable radix by that chunk, then by run id), until no row is
+// tied or every tied rest is exhausted (then the rows are identical).
+// rest bytes [8q, 8q + 8) of row i, big-endian, zero-padded (no rest: 0, first)
+__device__ __forceinline__ uint64_t sb_chunk(const uint64_t* R, const uint32_t* RL, uint64_t i, uint32_t q) {
+  const uint32_t l = RL[i];
+  const uint8_t* p = (const uint8_t*)R[i];
+  uint64_t v = 0;
+  for (uint32_t b = 0; b < 8; ++b) {
+    const uint32_t o = 8 * q + b;
+    v = (v << 8) | (o < l ? p[o] : 0u);
+  }
+  return v;
+}
+__device__ __forceinline__ bool sb_same(const uint64_t* k1, const uint64_t* idx, const int64_t* endv,
+                                        const uint64_t* R, const uint32_t* RL, const uint32_t* ord, uint64_t a,
+                                        uint64_t b, uint32_t q) {
+  if (k1[a] != k1[b]) return false;
+  const uint64_t ia = idx[ord[a]], ib = idx[ord[b]];
+  if (endv[ia] != endv[ib]) return false;
+  for (uint32_t z = 0; z < q; ++z)
+    if (sb_chunk(R, RL, ia, z) != sb_chunk(R, RL, ib, z)) return false;
+  return true;
+}
+// tied[j]: row j shares its run with a neighbour; start[j]: it opens a run; more[j]: a tied
+// row whose rest goes past byte 8q (another round can still split the run)
+__global__ void k_sb_tflag(const uint64_t* __restrict__ k1, const uint64_t* __restrict__ idx,
+                           const int64_t* __restrict__ endv, const uint64_t* __restrict__ R,
+                           const uint32_t* __restrict__ RL, const uint32_t* __restrict__ ord, uint64_t nd,
+                           uint32_t q, uint64_t* __restrict__ tied, uint64_t* __restrict__ start,
+                           unsigned long long* __restrict__ more) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nd) return;
-  auto same = [&](uint64_t a, uint64_t b) {
-    return k1[a] == k1[b] && endv[idx[ord[a]]] == endv[idx[ord[b]]];
-  };
-  if (j > 0 && same(j, j - 1)) return;
-  uint64_t g1 = j + 1;
-  while (g1 < nd && same(g1, j)) ++g1;
-  for (uint64_t a = j + 1; a < g1; ++a) {
-    const uint32_t x = ord[a];
-    uint64_t b = a;
-    while (b > j && sb_rest_less(R, RL, idx[x], idx[ord[b - 1]])) {
-      ord[b] = ord[b - 1];
-      --b;
+  const bool prev = j > 0 && sb_same(k1, idx, endv, R, RL, ord, j, j - 1, q);
+  const bool next = j + 1 < nd && sb_same(k1, idx, endv, R, RL, ord, j, j + 1, q);
+  const bool t = prev || next;
+  tied[j] = t;
+  start[j] = t && !prev;
+  if (t && RL[idx[ord[j]]] > 8 * q) atomicOr(more, 1ULL);
+}
+__global__ void k_sb_tgather(const uint64_t* __restrict__ tied, const uint64_t* __restrict__ pos,
+                             const uint64_t* __restrict__ start, const uint64_t* __restrict__ rid,
+                             const uint64_t* __restrict__ idx,
+                             const uint64_t* __restrict__ R, const uint32_t* __restrict__ RL,
+                             const uint32_t* __restrict__ ord, uint64_t nd, uint32_t q, uint64_t* __restrict__ P,
+                             uint64_t* __restrict__ K, uint32_t* __restrict__ V, uint64_t* __restrict__ RID) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nd || !tied[j]) return;
+  const uint64_t k = pos[j];
+  P[k] = j;
+  K[k] = sb_chunk(R, RL, idx[ord[j]], q);
+  V[k] = (uint32_t)k;
+  RID[k] = rid[j] + start[j];  // run starts up to and including j: one id per run
+}
+__global__ void k_sb_trid(const uint64_t* __restrict__ RID, const uint32_t* __restrict__ V, uint64_t m,
+                          uint64_t* __restrict__ K) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < m) K[t] = RID[V[t]];
+}
+// the t-th row in (run, chunk) order takes the t-th tied position
+__global__ void k_sb_tpick(const uint64_t* __restrict__ P, const uint32_t* __restrict__ V, uint64_t m,
+                           const uint32_t* __restrict__ ord, uint32_t* __restrict__ tmp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < m) tmp[t] = ord[P[V[t]]];
+}
+__global__ void k_sb_tput(const uint64_t* __restrict__ P, uint64_t m, const uint32_t* __restrict__ tmp,
+                          uint32_t* __restrict__ ord) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < m) ord[P[t]] = tmp[t];
+}
+static int sb_order_ties(bg_ctx* c, const uint64_t* key, const uint64_t* idx, const int64_t* endv, const uint64_t* R,
+                         const uint32_t* RL, uint64_t nd, uint32_t* ord) {
+  uint64_t* tied = (uint64_t*)bg_alloc(c, 8 * (nd + 1));
+  uint64_t* start = (uint64_t*)bg_alloc(c, 8 * (nd + 1));
+  uint64_t* pos = (uint64_t*)bg_alloc(c, 8 * (nd + 1));
+  uint64_t* rid = (uint64_t*)bg_alloc(c, 8 * (nd + 1));
+  unsigned long long* more = (unsigned long long*)bg_alloc(c, 8);
+  if (!tied || !start || !pos || !rid || !more) return BG_E_NOMEM;
+  int rc = 0;
+  for (uint32_t q = 0; !rc; ++q) {
+    BG_HIP(c, hipMemsetAsync(more, 0, 8, c->stream));
+    BG_LAUNCH(c, "k_sb_tflag", k_sb_tflag, dim3(bg_blocks(nd, BG_NT)), dim3(BG_NT), key, idx, endv, R, RL, ord, nd, q,
+              tied, start, more);
+    BG_HIP(c, hipGetLastError());
+    uint64_t m = 0, hm = 0;
+    if ((rc = bg_scan_sum_u64(c, tied, pos, nd, pos + nd)) || (rc = bg_fetch_u64(c, pos + nd, &m))) break;
+    if ((rc = bg_fetch_u64(c, (const uint64_t*)more, &hm))) break;
+    if (m == 0 || !hm) break;  // nothing tied, or every tied rest already compared in full
+    if ((rc = bg_scan_sum_u64(c, start, rid, nd, nullptr))) break;  // run starts before each row
+    uint64_t* P = (uint64_t*)bg_alloc(c, 8 * m);
+    uint64_t* K = (uint64_t*)bg_alloc(c, 8 * m);
+    uint32_t* V = (uint32_t*)bg_alloc(c, 4 * m);
+    uint64_t* RID = (uint64_t*)bg_alloc(c, 8 * m);
+    uint32_t* tmp = (uint32_t*)bg_alloc(c, 4 * m);
+    if (!P || !K || !V || !RID || !tmp) rc = BG_E_NOMEM;
+    const dim3 gm(bg_blocks(m, BG_NT));
+    if (!rc) {
+      BG_LAUNCH(c, "k_sb_tgather", k_sb_tgather, dim3(bg_blocks(nd, BG_NT)), dim3(BG_NT), tied, pos, start, rid,
+                idx, R, RL, ord, nd, q, P, K, V, RID);
+      rc = bg_sort_u64(c, K, V, m);  // stable: by this chunk
     }
-    ord[b] = x;
+    if (!rc) {
+      BG_LAUNCH(c, "k_sb_trid", k_sb_trid, gm, dim3(BG_NT), RID, V, m, K);
+      rc = bg_sort_u64(c, K, V, m);  // stable: by run, keeping the chunk order inside it
+    }
+    if (!rc) {
+      BG_LAUNCH(c, "k_sb_tpick", k_sb_tpick, gm, dim3(BG_NT), P, V, m, ord, tmp);
+      BG_LAUNCH(c, "k_sb_tput", k_sb_tput, gm, dim3(BG_NT), P, m, tmp, ord);
+      rc = bg_hip_ok(c, hipGetLastError());
+    }
+    for (void* x : {(void*)P, (void*)K, (void*)V, (void*)RID, (void*)tmp}) bg_release(c, x);
   }
+  for (void* x : {(void*)tied, (void*)start, (void*)pos, (void*)rid, (void*)more}) bg_release(c, x);
+  return rc;
 }
 
 __global__ void k_sb_emit(const uint32_t* __restrict__ ord, const uint64_t* __restrict__ idx,
@@ -480,6 +576,9 @@ extern "C" int bg_sortbed(bg_ctx* c, int nin, const bg_input* in, bg_result** ou
     uint64_t* upos = nullptr;
     uint64_t nu = 0;
     if ((rc = bg_compact_flags(c, uf, nd, &upos, &nu))) return fail(rc);
+    // ranks go into the key above bit 40 (rank << BG_KEY_SHIFT | start): as the loader
+    // (bg_load.hip), at most 2^22 - 1 names keep the keys positive and distinct
+    if (nu >= (1ull << 22)) return fail(bg_fail(c, BG_E_UNSUPPORTED, "too many chromosomes"));
     // representatives: hash, data-line ordinal, token address / length, then the names
     uint64_t* rinfo = (uint64_t*)bg_alloc(c, 8 * 4 * nu);
     if (!rinfo) return fail(BG_E_NOMEM);
@@ -574,8 +673,7 @@ extern "C" int bg_sortbed(bg_ctx* c, int nin, const bg_input* in, bg_result** ou
     BG_LAUNCH(c, "k_sb_key", k_sb_key, dim3(bg_blocks(nd, BG_NT)), dim3(BG_NT), idx, ord, nd, O.start, rank,
               true, key);
     if ((rc = bg_sort_u64(c, key, ord, nd))) return fail(rc);
-    BG_LAUNCH(c, "k_sb_ties", k_sb_ties, dim3(bg_blocks(nd, BG_NT)), dim3(BG_NT), key, idx, O.end, O.rest,
-              O.restlen, nd, ord);
+    if ((rc = sb_order_ties(c, key, idx, O.end, O.rest, O.restlen, nd, ord))) return fail(rc);
   }
   bg_result* r = new bg_result();
   r->ctx = c;

@@ -232,12 +232,31 @@ int bg_set_chroms(const bg_set* set, uint32_t* n);
 const char* bg_set_chrom_name(const bg_set* set, uint32_t g);
 void bg_result_free(bg_result* res);
 
-/* stream n bytes of device memory (on ctx's device) to fd: double-buffered D2H + write */
+/* stream n bytes of device memory (on ctx's device) to fd: a regular file by DMA into its
+ * mapped pages (BEDGPU_WRITE_MAP=0: not), anything else by double-buffered D2H + write(2) */
 int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
-/* read a regular file into a new device buffer of ctx's device (parallel page-cache reads
- * through a small pinned ring, overlapped with the H2D copies; ordered before later work on
- * ctx's stream); load it with bg_input.on_device = 1, free with bg_device_free */
+/* read a regular file into a new device buffer of ctx's device (its mapping DMA'd straight
+ * from the page cache, see bg_file_map below); load it with bg_input.on_device = 1, free
+ * with bg_device_free. Replaces the reader side of allocate_iterator_starch_bed for plain
+ * BED files (AllocateIterator_BED_starch.hpp:205-215). */
 int bg_read_file_device(bg_ctx* ctx, const char* path, void** dptr, uint64_t* nbytes);
+/* File mappings (inputs without host copies):
+ *   bg_file_map_open      mmap a regular file read-only and fault its page-cache pages in;
+ *                         no GPU call, so it may run on any thread while bg_open initialises
+ *   bg_file_map_register  pin the mapping for DMA from every device (portable); a failure
+ *                         (BG_E_HIP) leaves the mapping usable as a pageable source
+ *   bg_file_map_to_device copy bytes [off, off + len) into a new device buffer of ctx, on
+ *                         ctx's stream (free with bg_device_free)
+ *   bg_file_map_close     unpin and unmap, once every copy from it has completed (bg_sync) */
+typedef struct {
+  const char* data; /* the mapped file (NULL when empty) */
+  uint64_t n;       /* its size */
+  int registered;
+} bg_file_map;
+int bg_file_map_open(const char* path, bg_file_map* m);
+int bg_file_map_register(bg_file_map* m);
+int bg_file_map_to_device(bg_ctx* ctx, const bg_file_map* m, uint64_t off, uint64_t len, void** dptr);
+void bg_file_map_close(bg_file_map* m);
 /* make ctx's device current on the calling thread (a host thread per device in a group) */
 int bg_bind(bg_ctx* ctx);
 

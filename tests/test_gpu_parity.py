@@ -329,28 +329,52 @@ def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads,chunk_mb,streams", [(1, 1, 0), (3, 1, 1), (32, 1, 2), (8, 64, 8),
-                                                     (2, 1, 9)])
-def test_cli_reader_ring_settings(gpu_bin, oracle_bin, tmp_path, threads, chunk_mb, streams):
-    """file -> HBM reader ring (bg_read_file_device) at odd sizes: inputs of several 1 MiB
-    chunks plus a ragged tail, more readers than chunks, one reader, copies on the context's
-    own stream (0 streams) and more streams than readers; the output written back
-    through the same ring must equal the oracle's"""
-    rng = random.Random(11 + threads)
+@pytest.mark.parametrize("how", ["file_wb", "file_rw_offset", "append", "pipe", "stream_env", "stdin"])
+def test_cli_io_paths(gpu_bin, oracle_bin, tmp_path, how):
+    """inputs mapped and DMA'd from the page cache (or read from stdin), output DMA'd into the
+    mapped pages of a regular file (write-only and read-write descriptors, at an unaligned
+    offset), or streamed through write(2) (pipes, appends, BEDGPU_WRITE_MAP=0): every path
+    gives the oracle's bytes, around whatever the file held before"""
+    rng = random.Random(hash(how) & 0xffff)
     a = randbed.rows(rng, 120000, span=40_000_000, maxlen=500)
     b = randbed.rows(rng, 90000, span=40_000_000, maxlen=500)
     pa = randbed.write(str(tmp_path / "a.bed"), randbed.text(a))
     pb = randbed.write(str(tmp_path / "b.bed"), randbed.text(b))
-    assert os.path.getsize(pa) > 2 << 20 and os.path.getsize(pa) % (1 << 20)
-    env = dict(os.environ, BEDGPU_RD_THREADS=str(threads), BEDGPU_RD_CHUNK_MB=str(chunk_mb),
-               BEDGPU_RD_STREAMS=str(streams))
+    env = dict(os.environ)
     env.pop("BEDGPU_DEVICES", None)
+    if how == "stream_env":
+        env["BEDGPU_WRITE_MAP"] = "0"
+    out = tmp_path / "out.bed"
     for mode in (["--intersect"], ["--everything"], ["--element-of", "1"]):
         want = subprocess.run([oracle_bin["bedops"]] + mode + [pa, pb], stdout=subprocess.PIPE,
                               check=True).stdout
-        got = subprocess.run([gpu_bin["bedops"]] + mode + [pa, pb], stdout=subprocess.PIPE,
-                             check=True, env=env).stdout
-        assert got == want, (mode, threads, chunk_mb, streams)
+        files = [pa, pb]
+        stdin = None
+        if how == "stdin":
+            files = ["-", pb]
+            stdin = open(pa, "rb")
+        if how == "pipe":
+            got = subprocess.run([gpu_bin["bedops"]] + mode + files, stdout=subprocess.PIPE, check=True,
+                                 env=env).stdout
+            assert got == want, (mode, how)
+            continue
+        prefix = b""
+        if how == "file_wb" or how == "stream_env" or how == "stdin":
+            fo = open(out, "wb")
+        elif how == "file_rw_offset":
+            fo = open(out, "w+b")
+            prefix = b"#" * 12345  # not page aligned
+            fo.write(prefix)
+            fo.flush()
+        else:  # append: O_APPEND
+            prefix = b"previous line\n"
+            out.write_bytes(prefix)
+            fo = open(out, "ab")
+        with fo:
+            subprocess.run([gpu_bin["bedops"]] + mode + files, stdout=fo, check=True, env=env, stdin=stdin)
+        if stdin:
+            stdin.close()
+        assert out.read_bytes() == prefix + want, (mode, how)
 
 
 # ---------------------------------------------------------------------------------

@@ -71,6 +71,30 @@ def test_cli_sharded_errors_match_single_device(gpu_bin, tmp_path):
     assert (two.returncode, two.stderr, two.stdout) == (one.returncode, one.stderr, one.stdout)
 
 
+def test_cli_sharded_stdin_and_missing_devices_fall_back(gpu_bin, oracle_bin, tmp_path):
+    """BEDGPU_DEVICES naming more GPUs than exist (the group cannot open), or a stdin input
+    (not a mappable file), take the one-device path with the same output; stdin is not
+    consumed by the declined shard attempt"""
+    import torch
+    rng = random.Random(9)
+    a = randbed.write(str(tmp_path / "a.bed"), randbed.text(randbed.rows(rng, 4000, chroms=CHROMS)))
+    b = randbed.write(str(tmp_path / "b.bed"), randbed.text(randbed.rows(rng, 3000, chroms=CHROMS)))
+    want = subprocess.run([oracle_bin["bedops"], "-i", a, b], stdout=subprocess.PIPE, check=True).stdout
+    n = torch.cuda.device_count()
+    got = _cli(gpu_bin["bedops"], ["-i", a, b], ",".join(str(d) for d in range(n + 1)))
+    assert got.returncode == 0 and got.stdout == want, got.stderr
+    env = dict(os.environ, BEDGPU_DEVICES="0,0")
+    with open(a, "rb") as fi:
+        got = subprocess.run([gpu_bin["bedops"], "-i", "-", b], stdin=fi, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, env=env, timeout=120)
+    assert got.returncode == 0 and got.stdout == want, got.stderr
+    wantm = subprocess.run([oracle_bin["bedmap"], "--count", a, b], stdout=subprocess.PIPE, check=True).stdout
+    with open(a, "rb") as fi:
+        got = subprocess.run([gpu_bin["bedmap"], "--count", "-", b], stdin=fi, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, env=env, timeout=120)
+    assert got.returncode == 0 and got.stdout == wantm, got.stderr
+
+
 def test_engine_group_gather_equals_single_run(oracle_bin):
     """bench.py's multi-rank step on one GPU: each member loads only its chromosomes,
     intersects, formats; Group.gather reassembles on member 0"""
