@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 
@@ -411,83 +412,86 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
   return 0;
 }
 
-// Output to a regular file: the byte range [off, off + n) of the file is mapped shared, its
-// pages are allocated by a few threads at once (MADV_POPULATE_WRITE; buffered write(2) to
-// one file serialises on its inode lock: ~90 ms for 0.92 GB measured), the mapping is
-// registered and the text is DMA'd from HBM into the page cache. -1: not possible here (the
-// caller streams through write(2) instead; nothing reached the file).
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-static int write_device_mapped(bg_ctx* c, const void* d, uint64_t n, int fd) {
+// Output to a regular file: BG_WR_THREADS threads each stage 16 MiB chunks through two
+// registered buffers of their own (D2H by DMA on ctx's stream) and pwrite(2) them at their
+// offsets, so the page-cache copies of several chunks run at once. Measured on the box
+// (tools/out_probe.cpp, 0.92 GB): one write(2) stream 88-165 ms, pwrite from 4 threads
+// ~105 ms, a shared mapping of the file filled by DMA 128 ms (page allocation through faults
+// does not scale with threads: 285 ms with 4). -1: not a regular file or an append
+// descriptor (the caller streams through write(2); nothing reached the file).
+#define BG_WR_THREADS 4
+static int write_device_pwrite(bg_ctx* c, const void* d, uint64_t n, int fd) {
   struct stat st;
   if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return -1;
   const int fl = fcntl(fd, F_GETFL);
-  if (fl < 0 || (fl & O_APPEND) || (fl & O_ACCMODE) == O_RDONLY) return -1;
-  const off_t off = lseek(fd, 0, SEEK_CUR);
-  if (off < 0) return -1;
-  // a MAP_SHARED writable mapping needs the descriptor open for reading too: map through
-  // /proc/self/fd (the same file, opened O_RDWR) when fd is write-only
-  int mfd = fd;
-  if ((fl & O_ACCMODE) != O_RDWR) {
-    char p[64];
-    snprintf(p, sizeof(p), "/proc/self/fd/%d", fd);
-    mfd = open(p, O_RDWR);
-    if (mfd < 0) return -1;
-  }
-  const uint64_t end = (uint64_t)off + n;
-  const bool grow = (uint64_t)st.st_size < end;
-  if (grow && ftruncate(mfd, (off_t)end) != 0) {
-    if (mfd != fd) close(mfd);
-    return -1;
-  }
-  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
-  const uint64_t pa = (uint64_t)off & ~(pg - 1), len = end - pa;
-  char* map = (char*)mmap(nullptr, (size_t)len, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, (off_t)pa);
-  if (mfd != fd) close(mfd);
-  if (map == MAP_FAILED) {
-    if (grow) (void)ftruncate(fd, st.st_size);
-    return -1;
-  }
-  // page allocation in parallel slices (without MADV_POPULATE_WRITE the registration below
-  // faults the pages in itself)
-  const int T = (int)std::min<uint64_t>(8, (len + (64ull << 20) - 1) / (64ull << 20));
-  if (T > 1) {
+  if (fl < 0 || (fl & O_APPEND)) return -1;
+  const off_t off0 = lseek(fd, 0, SEEK_CUR);
+  if (off0 < 0) return -1;
+  const uint64_t CH = 16ull << 20;
+  const uint64_t nch = (n + CH - 1) / CH;
+  const int T = (int)std::min<uint64_t>(BG_WR_THREADS, nch);
+  const uint64_t slot = std::min<uint64_t>(CH, (n + 4095) & ~4095ull);
+  char* buf = (char*)malloc(2 * (size_t)T * slot);
+  if (!buf) return BG_E_NOMEM;
+  const bool reg = hipHostRegister(buf, 2 * (size_t)T * slot, hipHostRegisterDefault) == hipSuccess;
+  if (!reg) (void)hipGetLastError();
+  std::mutex mu;  // one stream: copies issued in any order, each waited on by its thread
+  std::atomic<int> bad{0};
+  std::vector<hipEvent_t> ev(2 * T, nullptr);
+  for (auto& e : ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) bad = 1;
+  auto worker = [&](int t) {
+    (void)hipSetDevice(c->device);
+    uint64_t j = 0;
+    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T, ++j) {
+      const int sl = 2 * t + (int)(j & 1);
+      char* hb = buf + (size_t)sl * slot;
+      const uint64_t o = k * CH, len = std::min(CH, n - o);
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (hipMemcpyAsync(hb, (const char*)d + o, len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipEventRecord(ev[sl], c->stream) != hipSuccess) {
+          bad = 1;
+          return;
+        }
+      }
+      if (hipEventSynchronize(ev[sl]) != hipSuccess) { bad = 1; return; }
+      uint64_t w = 0;
+      while (w < len) {
+        const ssize_t r = pwrite(fd, hb + w, len - w, off0 + (off_t)(o + w));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) { bad = 2; return; }
+        w += (uint64_t)r;
+      }
+    }
+  };
+  if (!bad) {
     std::vector<std::thread> th;
-    const uint64_t per = ((len / T) + pg - 1) & ~(pg - 1);
-    for (int t = 0; t < T; ++t)
-      th.emplace_back([=]() {
-        const uint64_t a = (uint64_t)t * per;
-        if (a < len) (void)madvise(map + a, (size_t)std::min(per, len - a), MADV_POPULATE_WRITE);
-      });
+    for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
+    worker(0);
     for (auto& x : th) x.join();
   }
-  int rc = 0;
-  if (hipHostRegister(map, (size_t)len, hipHostRegisterDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    rc = -1;
-  } else {
-    hipError_t e = hipMemcpyAsync(map + ((uint64_t)off - pa), d, (size_t)n, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipHostUnregister(map);
-    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device copy");
-  }
-  munmap(map, (size_t)len);
-  if (rc == -1 && grow) (void)ftruncate(fd, st.st_size);
-  if (rc == 0 && lseek(fd, (off_t)end, SEEK_SET) < 0)
-    rc = bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
-  return rc;
+  hipStreamSynchronize(c->stream);
+  for (auto e : ev)
+    if (e) hipEventDestroy(e);
+  if (reg) (void)hipHostUnregister(buf);
+  free(buf);
+  if (bad == 2) return bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
+  if (bad) return bg_fail(c, BG_E_HIP, "bg_write_device copy");
+  if (lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
+    return bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
+  return 0;
 }
 
-// streams n bytes of device memory to fd: a regular file by DMA into its mapped pages
-// (write_device_mapped), anything else (pipes, terminals, appends) through two registered
+// streams n bytes of device memory to fd: a regular file by parallel pwrite(2)
+// (write_device_pwrite), anything else (pipes, terminals, appends) through two registered
 // 64 MiB host buffers, the D2H copy of the next chunk overlapping write(2) of this one
 extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
   if (!c || (!d && n)) return BG_E_ARG;
   if (n == 0) return 0;
   bg_bind(c);
-  const char* nm = getenv("BEDGPU_WRITE_MAP");  // 0: always stream through write(2)
-  const int mr = (nm && strcmp(nm, "0") == 0) ? -1 : write_device_mapped(c, d, n, fd);
+  const char* nm = getenv("BEDGPU_WRITE_PAR");  // 0: always stream through write(2)
+  const int mr = (nm && strcmp(nm, "0") == 0) ? -1 : write_device_pwrite(c, d, n, fd);
   if (mr != -1) {
     bg_mark(c, "write");
     return mr;

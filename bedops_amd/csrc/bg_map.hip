@@ -1092,7 +1092,10 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     bool want = false, all = false, echo = false, rest_ties = false;
     for (int k = 0; k < opts->n_ops; ++k) {
       const int op = opts->ops[k];
-      if (op == BG_MAP_WMEAN || op == BG_MAP_TMEAN) all = true;  // every window's address order
+      // every window's address order: WeightedAverage sums in it; TrimmedMean and the *-rand
+      // element operations order equal SCORES by address
+      if (op == BG_MAP_WMEAN || op == BG_MAP_TMEAN || op == BG_MAP_MIN_ELEMENT_RAND || op == BG_MAP_MAX_ELEMENT_RAND)
+        all = true;
       if (op == BG_MAP_ECHO_MAP || op == BG_MAP_ECHO_MAP_ID || op == BG_MAP_ECHO_MAP_SCORE ||
           op == BG_MAP_ECHO_MAP_SIZE || op == BG_MAP_ECHO_OVERLAP_SIZE)
         echo = true;  // GenomicAddressCompare: ties of (chrom, start, end)

@@ -232,8 +232,9 @@ int bg_set_chroms(const bg_set* set, uint32_t* n);
 const char* bg_set_chrom_name(const bg_set* set, uint32_t g);
 void bg_result_free(bg_result* res);
 
-/* stream n bytes of device memory (on ctx's device) to fd: a regular file by DMA into its
- * mapped pages (BEDGPU_WRITE_MAP=0: not), anything else by double-buffered D2H + write(2) */
+/* stream n bytes of device memory (on ctx's device) to fd: a regular file by parallel
+ * pwrite(2) of DMA'd chunks (BEDGPU_WRITE_PAR=0: not), anything else by double-buffered D2H
+ * + write(2) */
 int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
 /* read a regular file into a new device buffer of ctx's device (its mapping DMA'd straight
  * from the page cache, see bg_file_map below); load it with bg_input.on_device = 1, free

@@ -331,9 +331,9 @@ def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("how", ["file_wb", "file_rw_offset", "append", "pipe", "stream_env", "stdin"])
 def test_cli_io_paths(gpu_bin, oracle_bin, tmp_path, how):
-    """inputs mapped and DMA'd from the page cache (or read from stdin), output DMA'd into the
-    mapped pages of a regular file (write-only and read-write descriptors, at an unaligned
-    offset), or streamed through write(2) (pipes, appends, BEDGPU_WRITE_MAP=0): every path
+    """inputs mapped and DMA'd from the page cache (or read from stdin), output by parallel
+    pwrite(2) into a regular file (write-only and read-write descriptors, at an unaligned
+    offset), or streamed through write(2) (pipes, appends, BEDGPU_WRITE_PAR=0): every path
     gives the oracle's bytes, around whatever the file held before"""
     rng = random.Random(hash(how) & 0xffff)
     a = randbed.rows(rng, 120000, span=40_000_000, maxlen=500)
@@ -343,7 +343,7 @@ def test_cli_io_paths(gpu_bin, oracle_bin, tmp_path, how):
     env = dict(os.environ)
     env.pop("BEDGPU_DEVICES", None)
     if how == "stream_env":
-        env["BEDGPU_WRITE_MAP"] = "0"
+        env["BEDGPU_WRITE_PAR"] = "0"
     out = tmp_path / "out.bed"
     for mode in (["--intersect"], ["--everything"], ["--element-of", "1"]):
         want = subprocess.run([oracle_bin["bedops"]] + mode + [pa, pb], stdout=subprocess.PIPE,

@@ -91,3 +91,26 @@ def test_sortbed_large_vs_oracle(gpu_bin, oracle_bin, bedgen, tmp_path):
     got = _run(gpu_bin["sortbed"], files)
     assert want.returncode == 0
     assert got.returncode == 0 and got.stdout == want.stdout
+
+
+def test_sortbed_long_tie_runs_vs_oracle(gpu_bin, oracle_bin, tmp_path):
+    """1e5 rows at one coordinate with random rests (amplicon / duplicate-heavy data), rests
+    that share long prefixes (several 8-byte refinement rounds) and rows without a rest:
+    ordered like the oracle, in seconds (the tie order is radix refinement, not per-run
+    insertion)"""
+    import time
+    rng = random.Random(123)
+    lines = [f"chr2\t700\t900\tread{rng.randint(0, 10 ** 9)}\t{rng.randint(0, 60)}" for _ in range(100000)]
+    lines += [f"chr2\t700\t900\tshared_prefix_0123456789_{rng.randint(0, 999):03d}" for _ in range(3000)]
+    lines += ["chr2\t700\t900"] * 50 + [f"chr1\t5\t9\tx{k % 7}" for k in range(20000)]
+    rng.shuffle(lines)
+    p = tmp_path / "ties.bed"
+    p.write_text("\n".join(lines) + "\n")
+    want = subprocess.run([oracle_bin["sortbed"], str(p)], stdout=subprocess.PIPE, check=True).stdout
+    t0 = time.time()
+    got = subprocess.run([gpu_bin["sortbed"], str(p)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         timeout=120)
+    dt = time.time() - t0
+    assert got.returncode == 0, got.stderr
+    assert got.stdout == want
+    assert dt < 30, dt
