@@ -113,15 +113,15 @@ static inline int file_is_starch(const char* path) {
   return r > 0 && bg_starch_is(b, (uint64_t)r);
 }
 
-/* Input files that go straight to device memory are mapped (bg_file_map_open: page-cache
- * pages faulted in, no GPU call) by one thread each, started before bg_open so the mapping
- * overlaps HIP's initialisation; read_input then registers the mapping and DMAs it to HBM,
- * and cli_prefetch_release drops the mappings once the loads have copied them. */
+/* Input files that go straight to device memory are read into host images
+ * (bg_file_image_open: parallel preads, no GPU call) by one thread each, started before
+ * bg_open so the reads overlap HIP's initialisation; read_input then registers the image and
+ * DMAs it to HBM, and cli_prefetch_release frees the images once the loads have copied them. */
 #include <pthread.h>
 #define CLI_MAX_PF 16
 typedef struct {
   const char* path;
-  bg_file_map m;
+  bg_file_image m;
   int ok, started;
   pthread_t th;
 } cli_pf_t;
@@ -129,12 +129,12 @@ static cli_pf_t CLI_PF[CLI_MAX_PF];
 static int CLI_NPF;
 static inline void* cli_pf_run(void* a) {
   cli_pf_t* p = (cli_pf_t*)a;
-  p->ok = bg_file_map_open(p->path, &p->m) == 0;
+  p->ok = bg_file_image_open(p->path, &p->m) == 0;
   if (p->ok && p->m.n >= 4 && !CLI_NO_STARCH) { /* Starch archives: decoded on the host (read_text) */
     const unsigned char* b = (const unsigned char*)p->m.data;
     if ((b[0] == 0xca && b[1] == 0x5c && b[2] == 0xad && b[3] == 0xe5) ||
         bg_starch_is(p->m.data, p->m.n < 512 ? p->m.n : 512)) {
-      bg_file_map_close(&p->m);
+      bg_file_image_close(&p->m);
       p->ok = 0;
     }
   }
@@ -171,14 +171,14 @@ static inline void cli_prefetch_release(bg_ctx* ctx) {
       pthread_join(p->th, NULL);
       p->started = 0;
     }
-    if (p->ok) bg_file_map_close(&p->m);
+    if (p->ok) bg_file_image_close(&p->m);
     p->ok = 0;
   }
   CLI_NPF = 0;
 }
 
 /* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
- * go straight to device memory (their mapping DMA'd from the page cache: cli_prefetch /
+ * go straight to device memory (their host image DMA'd to HBM: cli_prefetch /
  * bg_read_file_device); stdin, pipes and checked inputs are read into host memory.
  * Returns 0 or -1 (unreadable). */
 static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, text_buf_t* t, bg_input* in) {
@@ -187,8 +187,8 @@ static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, tex
   cli_pf_t* pf = host_needed ? NULL : cli_pf_take(path);
   if (pf) {
     void* d = NULL;
-    (void)bg_file_map_register(&pf->m);
-    if (bg_file_map_to_device(ctx, &pf->m, 0, pf->m.n, &d) == 0) {
+    (void)bg_file_image_register(&pf->m);
+    if (bg_file_image_to_device(ctx, &pf->m, 0, pf->m.n, &d) == 0) {
       t->ddata = d;
       t->n = pf->m.n;
       in->data = d;

@@ -8,10 +8,10 @@
  *      text — the idea of find_bed_range (interfaces/general-headers/algorithm/bed/
  *      FindBedRange.hpp:67-188): O(chromosomes x log(bytes)) line probes, no full scan;
  *   2. chromosomes go to devices by longest-processing-time on their bytes in all inputs;
- *   3. each device receives only its chromosomes' bytes, DMA'd straight from the input
- *      file's page cache (the files are mapped and registered once, bg_file_map; nothing is
- *      read into or pinned in host memory), over its own link, and runs load -> operation
- *      -> format on its own host thread;
+ *   3. each device receives only its chromosomes' bytes, DMA'd from the input files' host
+ *      images (read once by parallel preads and registered once, bg_file_image: portable, so
+ *      every device copies its byte ranges from them over its own link), and runs load ->
+ *      operation -> format on its own host thread;
  *   4. bg_group_gather reassembles the texts on device 0 in strcmp chromosome order over
  *      RCCL, and device 0 streams them to stdout.
  * Inputs that are not regular files (stdin, pipes), inputs the host checks cannot split
@@ -121,7 +121,7 @@ typedef struct {
   bg_ctx* ctx;
   int nf;
   const bg_input* proto; /* kinds */
-  const bg_file_map* fm; /* the mapped input files */
+  const bg_file_image* fm; /* the input files' host images */
   const cruns_t* runs;   /* per file */
   const int* owner;      /* global chromosome -> device */
   char (*gnames)[BG_CHR_NAME_CAP];
@@ -205,12 +205,12 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
   int dev[SHARD_MAX_DEV];
   const int nd = env_devices(dev, SHARD_MAX_DEV);
   if (nd < 2) return 1;
-  bg_file_map* fm = (bg_file_map*)calloc((size_t)nf, sizeof(bg_file_map));
+  bg_file_image* fm = (bg_file_image*)calloc((size_t)nf, sizeof(bg_file_image));
   int ok = 1;
   for (int f = 0; f < nf && ok; ++f) {
     struct stat st;
     ok = strcmp(paths[f], "-") != 0 && stat(paths[f], &st) == 0 && S_ISREG(st.st_mode) &&
-         !file_is_starch(paths[f]) && bg_file_map_open(paths[f], &fm[f]) == 0;
+         !file_is_starch(paths[f]) && bg_file_image_open(paths[f], &fm[f]) == 0;
   }
   cruns_t* runs = (cruns_t*)calloc((size_t)nf, sizeof(cruns_t));
   int total_runs = 0;
@@ -233,7 +233,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
   if (!ok || ngc < 2) { /* nothing to split */
     for (int f = 0; f < nf; ++f) {
       free(runs[f].r);
-      bg_file_map_close(&fm[f]);
+      bg_file_image_close(&fm[f]);
     }
     free(runs);
     free(gn);
@@ -273,7 +273,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
       fprintf(stderr, "bedgpu: BEDGPU_DEVICES group not available (%d); one device\n", rc);
     for (int f = 0; f < nf; ++f) {
       free(runs[f].r);
-      bg_file_map_close(&fm[f]);
+      bg_file_image_close(&fm[f]);
     }
     free(runs);
     free(gn);
@@ -284,7 +284,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
     return 1;
   }
   cli_mark("open");
-  for (int f = 0; f < nf; ++f) (void)bg_file_map_register(&fm[f]); /* DMA source for every device */
+  for (int f = 0; f < nf; ++f) (void)bg_file_image_register(&fm[f]); /* DMA source for every device */
   shard_job_t* J = (shard_job_t*)calloc((size_t)nd, sizeof(shard_job_t));
   pthread_t* th = (pthread_t*)calloc((size_t)nd, sizeof(pthread_t));
   for (int d = 0; d < nd; ++d) {
@@ -310,7 +310,7 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
     failed = failed || J[d].rc;
   }
   cli_mark("shards");
-  for (int f = 0; f < nf; ++f) bg_file_map_close(&fm[f]); /* the loads have synchronised */
+  for (int f = 0; f < nf; ++f) bg_file_image_close(&fm[f]); /* the loads have synchronised */
   int done = 0;
   if (!failed) {
     const char** texts = (const char**)calloc((size_t)nd, sizeof(char*));

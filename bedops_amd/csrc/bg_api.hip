@@ -155,12 +155,14 @@ extern "C" int bg_open(bg_ctx** out, int device) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
+    (void)hipGetLastError();  // not sticky: a later context's checks must not see it
     delete c;
     return BG_E_HIP;
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess ||
       hipHostMalloc(&c->hstat, sizeof(bg_dstatus), hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
     delete c;
     return BG_E_HIP;
   }
@@ -319,15 +321,19 @@ static int write_all(int fd, const char* p, uint64_t n) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Files <-> HBM without host copies. Inputs: the file is mapped (MAP_POPULATE: page-table
-// entries for its page-cache pages, no GPU call, so it can run while bg_open initialises
-// HIP), the mapping is registered for DMA (hipHostRegister, portable: every device of a group
-// can read it) and copied to HBM by the DMA engines straight from the page cache. Measured on
-// the box (tools/e2e_probe.cpp, 2.38 GB): populate ~20 ms, register 10-19 ms, copy ~45 ms
-// (50-57 GB/s), against a pinned ring filled by pread threads (~70 ms incl. pinning) that
-// also needed extra copy streams (8-40 ms each to create, and more to tear down at exit).
+// Input files -> HBM. A file is read into anonymous host memory (transparent huge pages) by
+// BG_IMG_THREADS parallel preads — no GPU call, so the front-ends run it while bg_open
+// initialises HIP — then that image is registered for DMA (hipHostRegister, portable: every
+// device of a group can read it) and copied to HBM by the DMA engines. Measured on the box
+// (tools/e2e_probe.cpp, 2.38 GB): 16 threads read the page cache into fresh anonymous
+// memory at ~120 GB/s (20 ms), registering it takes ~5 ms, the copy ~45 ms (50-57 GB/s).
+// Registering the file's own page-cache mapping instead saves the host copy in isolation,
+// but inside the CLI it stalled the first kernels by 250-450 ms (the driver's user-pointer
+// pages of a file mapping get invalidated and restored), and the pinned pread ring it
+// replaced needed extra copy streams (8-40 ms each to create, more to tear down at exit).
 // ---------------------------------------------------------------------------------------
-extern "C" int bg_file_map_open(const char* path, bg_file_map* m) {
+#define BG_IMG_THREADS 8
+extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
   if (!path || !m) return BG_E_ARG;
   memset(m, 0, sizeof(*m));
   const int fd = open(path, O_RDONLY);
@@ -337,21 +343,46 @@ extern "C" int bg_file_map_open(const char* path, bg_file_map* m) {
     close(fd);
     return BG_E_ARG;
   }
-  m->n = (uint64_t)st.st_size;
-  if (m->n) {
-    void* p = mmap(nullptr, (size_t)m->n, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+  const uint64_t n = (uint64_t)st.st_size;
+  if (n) {
+    void* p = mmap(nullptr, (size_t)n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) {
       close(fd);
-      m->n = 0;
+      return BG_E_NOMEM;
+    }
+    (void)madvise(p, (size_t)n, MADV_HUGEPAGE);
+    const uint64_t CH = 8ull << 20, nch = (n + CH - 1) / CH;
+    const int T = (int)std::min<uint64_t>(BG_IMG_THREADS, nch);
+    std::atomic<int> bad{0};
+    auto reader = [&](int t) {
+      for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T) {
+        const uint64_t off = k * CH, len = std::min(CH, n - off);
+        uint64_t got = 0;
+        while (got < len) {
+          const ssize_t r = pread(fd, (char*)p + off + got, len - got, (off_t)(off + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) { bad = 1; return; }
+          got += (uint64_t)r;
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(reader, t);
+    reader(0);
+    for (auto& x : th) x.join();
+    if (bad) {
+      munmap(p, (size_t)n);
+      close(fd);
       return BG_E_IO;
     }
     m->data = (const char*)p;
   }
+  m->n = n;
   close(fd);
   return 0;
 }
 
-extern "C" int bg_file_map_register(bg_file_map* m) {
+extern "C" int bg_file_image_register(bg_file_image* m) {
   if (!m) return BG_E_ARG;
   if (m->registered || !m->n) return 0;
   if (hipHostRegister((void*)m->data, (size_t)m->n, hipHostRegisterPortable) != hipSuccess) {
@@ -362,7 +393,7 @@ extern "C" int bg_file_map_register(bg_file_map* m) {
   return 0;
 }
 
-extern "C" int bg_file_map_to_device(bg_ctx* c, const bg_file_map* m, uint64_t off, uint64_t len, void** out) {
+extern "C" int bg_file_image_to_device(bg_ctx* c, const bg_file_image* m, uint64_t off, uint64_t len, void** out) {
   if (!c || !m || !out || off > m->n || len > m->n - off) return BG_E_ARG;
   *out = nullptr;
   bg_bind(c);
@@ -379,7 +410,7 @@ extern "C" int bg_file_map_to_device(bg_ctx* c, const bg_file_map* m, uint64_t o
   return 0;
 }
 
-extern "C" void bg_file_map_close(bg_file_map* m) {
+extern "C" void bg_file_image_close(bg_file_image* m) {
   if (!m) return;
   if (m->registered) (void)hipHostUnregister((void*)m->data);
   if (m->data && m->n) munmap((void*)m->data, (size_t)m->n);
@@ -387,21 +418,21 @@ extern "C" void bg_file_map_close(bg_file_map* m) {
 }
 
 // a regular file straight into a new device buffer (the four calls above, in order); the
-// mapping is released once the copy completed
+// host image is released once the copy completed
 extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint64_t* nbytes) {
   if (!c || !path || !out || !nbytes) return BG_E_ARG;
   *out = nullptr;
   *nbytes = 0;
-  bg_file_map m;
-  int rc = bg_file_map_open(path, &m);
-  if (rc) return bg_fail(c, rc, std::string("cannot map ") + path);
+  bg_file_image m;
+  int rc = bg_file_image_open(path, &m);
+  if (rc) return bg_fail(c, rc, std::string("cannot read ") + path);
   const uint64_t n = m.n;
   bg_bind(c);
-  (void)bg_file_map_register(&m);
+  (void)bg_file_image_register(&m);
   void* d = nullptr;
-  rc = bg_file_map_to_device(c, &m, 0, n, &d);
+  rc = bg_file_image_to_device(c, &m, 0, n, &d);
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
-  bg_file_map_close(&m);
+  bg_file_image_close(&m);
   if (rc) {
     bg_release(c, d);
     return rc;

@@ -66,10 +66,51 @@ struct ClArgs {
   uint32_t* overflow;
 };
 
+// The cache stack and the kept list of a chunk live in LDS, CL_D entries per thread (one
+// column per thread: [entry][thread], so a wave's accesses stay in distinct banks), and
+// spill to the chunk's global slot only when deeper: the stack keeps its top CL_D entries
+// in a ring in LDS and moves the oldest to global memory on overflow; the kept list keeps
+// its first CL_D entries in LDS. Global memory sees the state only at the two snapshots
+// (after the warm-up, at the chunk's end) and on deep stacks (nested inputs).
+#define CL_D 16
 struct ClState {
   uint64_t fp;
-  uint32_t n;
-  uint32_t* c;  // stack storage (global, `cap` entries)
+  uint32_t n;   // stack depth
+  uint32_t m;   // top entries resident in the LDS ring (entries [n - m, n))
+  uint32_t* c;  // stack storage (global, `cap` entries): entries [0, n - m)
+  uint32_t* l;  // this thread's LDS ring column (entry i at l[(i % CL_D) * BG_NT])
+};
+__device__ __forceinline__ void cl_push(ClState& S, uint32_t x) {
+  if (S.m == CL_D) {  // spill the oldest ring entry
+    const uint32_t i = S.n - S.m;
+    S.c[i] = S.l[(i & (CL_D - 1)) * BG_NT];
+    --S.m;
+  }
+  S.l[(S.n & (CL_D - 1)) * BG_NT] = x;
+  ++S.n;
+  ++S.m;
+}
+__device__ __forceinline__ uint32_t cl_pop(ClState& S) {
+  --S.n;
+  if (S.m) {
+    --S.m;
+    return S.l[(S.n & (CL_D - 1)) * BG_NT];
+  }
+  return S.c[S.n];
+}
+// the whole stack in global memory (snapshots, comparisons)
+__device__ __forceinline__ void cl_flush(ClState& S) {
+  for (uint32_t i = S.n - S.m; i < S.n; ++i) S.c[i] = S.l[(i & (CL_D - 1)) * BG_NT];
+  S.m = 0;
+}
+struct ClKept {  // the per-row kept list: entries [0, CL_D) in LDS, the rest in global
+  uint32_t* l;   // LDS column
+  uint32_t* g;   // global overflow (`cap` entries)
+  __device__ __forceinline__ void put(uint32_t i, uint32_t x) const {
+    if (i < CL_D) l[i * BG_NT] = x;
+    else g[i] = x;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t i) const { return i < CL_D ? l[i * BG_NT] : g[i]; }
 };
 
 #define D_MINUS LLONG_MIN
@@ -107,7 +148,7 @@ __device__ __forceinline__ int64_t cl_dist(int64_t cs, int64_t ce, int64_t bs, i
 //   d = 0, overlaps, be <= ce (hangR)      keepL; keepR; right = c, rdist = 0
 //   d = 0, overlaps, inside: by the centroid proportion (:227-239, :355-388)
 //   d = 0, no-overlaps (noov)              keepL (lc = 1); keepC          :389-397
-__device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, uint32_t* kept,
+__device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, const ClKept& kept,
                        bool emit) {
   const uint32_t cap = A.cap;
   // the next CPF file candidates, loaded ahead: the scan's loads are independent of its
@@ -133,15 +174,15 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
     bool lc = false;  // leftCached
     uint32_t nk = 0;  // the std::list "read" of findDistances
     bool ovf = false, eof = false;
-#define KEEP(x)                      \
-  do {                               \
-    if (nk == cap) ovf = true;       \
-    else kept[nk++] = (uint32_t)(x); \
+#define KEEP(x)                         \
+  do {                                  \
+    if (nk == cap) ovf = true;          \
+    else kept.put(nk++, (uint32_t)(x)); \
   } while (0)
     for (;;) {
       int64_t c, cs, ce;
       if (S.n) {
-        c = S.c[--S.n];
+        c = cl_pop(S);
         cs = A.cs[c];
         ce = A.ce[c];
       } else if (S.fp < A.nc) {
@@ -220,7 +261,7 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, ui
 #undef KEEP
     // BedReader::PushBack(list): the list comes back out in list order
     if (ovf || S.n + nk > cap) return false;
-    for (uint32_t i = nk; i-- > 0;) S.c[S.n++] = kept[i];
+    for (uint32_t i = nk; i-- > 0;) cl_push(S, kept.get(i));
     if (emit) {
       A.left[b] = left;
       A.right[b] = right;
@@ -249,16 +290,21 @@ __device__ __forceinline__ bool cl_same(const ClArgs& A, uint64_t x, uint64_t y)
   return true;
 }
 
-// run chunk k's own rows from the state held in its working slot
-__device__ __forceinline__ void cl_own(const ClArgs& A, uint32_t k) {
+__device__ __forceinline__ ClKept cl_kept(const ClArgs& A, uint32_t k, uint32_t* lk) {
+  return ClKept{lk + threadIdx.x, A.kl + (uint64_t)k * A.cap};
+}
+
+// run chunk k's own rows from the state held in its working slot (global)
+__device__ __forceinline__ void cl_own(const ClArgs& A, uint32_t k, uint32_t* ls, uint32_t* lk) {
   const uint64_t q0 = (uint64_t)k * A.cq, q1 = min(q0 + A.cq, A.nq);
   const uint64_t w = 2ull * k + 1;
-  ClState S{A.st_fp[w], A.st_n[w], cl_slot(A, w)};
-  if (!cl_run(A, q0, q1, S, A.kl + (uint64_t)k * A.cap, true)) {
+  ClState S{A.st_fp[w], A.st_n[w], 0, cl_slot(A, w), ls + threadIdx.x};
+  if (!cl_run(A, q0, q1, S, cl_kept(A, k, lk), true)) {
     atomicOr(A.overflow, 1u);
     S.fp = ~0ull - 1;  // a final state no successor starts from
-    S.n = 0;
+    S.n = S.m = 0;
   }
+  cl_flush(S);
   A.st_fp[w] = S.fp;
   A.st_n[w] = S.n;
 }
@@ -267,11 +313,12 @@ __device__ __forceinline__ void cl_own(const ClArgs& A, uint32_t k) {
 #define BG_CL_WAVES
 #endif
 __global__ void __launch_bounds__(BG_NT) BG_CL_WAVES k_closest_chunks(ClArgs A) {
+  __shared__ uint32_t ls[CL_D * BG_NT], lk[CL_D * BG_NT];
   const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
   if (k >= A.nchunks) return;
   const uint64_t q0 = (uint64_t)k * A.cq;
   const uint64_t w = 2ull * k + 1;
-  ClState S{0, 0, cl_slot(A, w)};
+  ClState S{0, 0, 0, cl_slot(A, w), ls + threadIdx.x};
   if (k > 0) {
     const uint64_t qw = q0 - A.cw;
     // speculative start: every candidate that can still overlap row qw or anything
@@ -280,7 +327,7 @@ __global__ void __launch_bounds__(BG_NT) BG_CL_WAVES k_closest_chunks(ClArgs A) 
     const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
     const uint64_t f = lower_bound_i64(A.cs, A.nc, A.qs[qw] - A.lmax - 1);
     S.fp = (p - f > CBACK) ? p - CBACK : f;
-    if (!cl_run(A, qw, q0, S, A.kl + (uint64_t)k * A.cap, false)) {
+    if (!cl_run(A, qw, q0, S, cl_kept(A, k, lk), false)) {
       // speculation overflowed: leave this chunk to the fix-up
       A.st_fp[2ull * k] = ~0ull;  // a start state no predecessor ends in
       A.st_n[2ull * k] = 0;
@@ -289,10 +336,11 @@ __global__ void __launch_bounds__(BG_NT) BG_CL_WAVES k_closest_chunks(ClArgs A) 
       return;
     }
   }
+  cl_flush(S);
   A.st_fp[w] = S.fp;
   A.st_n[w] = S.n;
   cl_copy(A, w, 2ull * k);  // snapshot of the start state
-  cl_own(A, k);
+  cl_own(A, k, ls, lk);
 }
 
 __global__ void k_closest_check(ClArgs A) {
@@ -305,21 +353,23 @@ __global__ void k_closest_check(ClArgs A) {
 
 // re-run chunks whose predecessor is consistent (its final state is stable this round)
 __global__ void __launch_bounds__(BG_NT) k_closest_fix(ClArgs A) {
+  __shared__ uint32_t ls[CL_D * BG_NT], lk[CL_D * BG_NT];
   const uint32_t k = blockIdx.x * BG_NT + threadIdx.x;
   if (k == 0 || k >= A.nchunks || !A.flag[k] || A.flag[k - 1]) return;
   cl_copy(A, 2ull * (k - 1) + 1, 2ull * k);
   cl_copy(A, 2ull * k, 2ull * k + 1);
-  cl_own(A, k);
+  cl_own(A, k, ls, lk);
 }
 
 // last resort: one in-order pass (exact for any input)
-__global__ void k_closest_serial(ClArgs A) {
+__global__ void __launch_bounds__(BG_NT) k_closest_serial(ClArgs A) {
+  __shared__ uint32_t ls[CL_D * BG_NT], lk[CL_D * BG_NT];
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (uint32_t k = 1; k < A.nchunks; ++k) {
     if (cl_same(A, 2ull * k, 2ull * (k - 1) + 1)) continue;
     cl_copy(A, 2ull * (k - 1) + 1, 2ull * k);
     cl_copy(A, 2ull * k, 2ull * k + 1);
-    cl_own(A, k);
+    cl_own(A, k, ls, lk);
   }
 }
 
@@ -351,7 +401,7 @@ static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf) {
     if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
     if (rc || h[0] == 0 || h[1]) break;
     if (round == FIX_ROUNDS) {
-      BG_LAUNCH(c, "k_closest_serial", k_closest_serial, dim3(1), dim3(64), A);
+      BG_LAUNCH(c, "k_closest_serial", k_closest_serial, dim3(1), dim3(BG_NT), A);
       rc = bg_hip_ok(c, hipGetLastError());
       if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(h, A.nflag, 8, hipMemcpyDeviceToHost, c->stream));
       if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));

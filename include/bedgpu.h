@@ -236,28 +236,29 @@ void bg_result_free(bg_result* res);
  * pwrite(2) of DMA'd chunks (BEDGPU_WRITE_PAR=0: not), anything else by double-buffered D2H
  * + write(2) */
 int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
-/* read a regular file into a new device buffer of ctx's device (its mapping DMA'd straight
- * from the page cache, see bg_file_map below); load it with bg_input.on_device = 1, free
- * with bg_device_free. Replaces the reader side of allocate_iterator_starch_bed for plain
- * BED files (AllocateIterator_BED_starch.hpp:205-215). */
+/* read a regular file into a new device buffer of ctx's device (its host image DMA'd to HBM,
+ * see bg_file_image below); load it with bg_input.on_device = 1, free with bg_device_free.
+ * Replaces the reader side of allocate_iterator_starch_bed for plain BED files
+ * (AllocateIterator_BED_starch.hpp:205-215). */
 int bg_read_file_device(bg_ctx* ctx, const char* path, void** dptr, uint64_t* nbytes);
-/* File mappings (inputs without host copies):
- *   bg_file_map_open      mmap a regular file read-only and fault its page-cache pages in;
- *                         no GPU call, so it may run on any thread while bg_open initialises
- *   bg_file_map_register  pin the mapping for DMA from every device (portable); a failure
- *                         (BG_E_HIP) leaves the mapping usable as a pageable source
- *   bg_file_map_to_device copy bytes [off, off + len) into a new device buffer of ctx, on
- *                         ctx's stream (free with bg_device_free)
- *   bg_file_map_close     unpin and unmap, once every copy from it has completed (bg_sync) */
+/* File images (inputs read once, by parallel preads, into host memory that the DMA engines
+ * copy to HBM):
+ *   bg_file_image_open      read a regular file into anonymous (huge-page) host memory; no
+ *                           GPU call, so it may run on any thread while bg_open initialises
+ *   bg_file_image_register  pin the image for DMA from every device (portable); a failure
+ *                           (BG_E_HIP) leaves it usable as a pageable source
+ *   bg_file_image_to_device copy bytes [off, off + len) into a new device buffer of ctx, on
+ *                           ctx's stream (free with bg_device_free)
+ *   bg_file_image_close     unpin and free, once every copy from it has completed (bg_sync) */
 typedef struct {
-  const char* data; /* the mapped file (NULL when empty) */
+  const char* data; /* the file's bytes (NULL when empty) */
   uint64_t n;       /* its size */
   int registered;
-} bg_file_map;
-int bg_file_map_open(const char* path, bg_file_map* m);
-int bg_file_map_register(bg_file_map* m);
-int bg_file_map_to_device(bg_ctx* ctx, const bg_file_map* m, uint64_t off, uint64_t len, void** dptr);
-void bg_file_map_close(bg_file_map* m);
+} bg_file_image;
+int bg_file_image_open(const char* path, bg_file_image* m);
+int bg_file_image_register(bg_file_image* m);
+int bg_file_image_to_device(bg_ctx* ctx, const bg_file_image* m, uint64_t off, uint64_t len, void** dptr);
+void bg_file_image_close(bg_file_image* m);
 /* make ctx's device current on the calling thread (a host thread per device in a group) */
 int bg_bind(bg_ctx* ctx);
 
