@@ -186,6 +186,10 @@ extern "C" void bg_close(bg_ctx* c) {
   hipFree(c->dstat);
   hipHostFree(c->hstat);
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
+  for (auto e : c->ring_ev)
+    if (e) hipEventDestroy(e);
+  for (auto p : c->ring)
+    if (p) hipHostFree(p);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -307,18 +311,6 @@ extern "C" int bg_result_copy_text(bg_ctx* c, bg_result* r, char* host, uint64_t
   return rc;
 }
 
-static int write_all(int fd, const char* p, uint64_t n) {
-  while (n) {
-    ssize_t w = write(fd, p, n > (1u << 30) ? (1u << 30) : n);
-    if (w < 0) {
-      if (errno == EINTR) continue;
-      return -1;
-    }
-    p += w;
-    n -= (uint64_t)w;
-  }
-  return 0;
-}
 
 // ---------------------------------------------------------------------------------------
 // Input files -> HBM. A file is read into anonymous host memory (transparent huge pages) by
@@ -382,9 +374,93 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
   return 0;
 }
 
+// The staging ring: BG_RING_SLOTS driver-pinned slots of BG_RING_CH bytes with one event
+// each, allocated on first use by as many threads (hipHostMalloc of a few MiB costs 5-25 ms
+// per call on the box). Host memory registered with hipHostRegister is avoided for bulk
+// copies: in the CLI, kernels running while registered (user-pointer) pages of the input
+// images or of output bounce buffers were in use stalled by 250-450 ms per run (the driver
+// evicts and restores the queues when such pages are invalidated); the ring's pages are the
+// driver's own.
+#define BG_RING_SLOTS 16
+#define BG_RING_CH (8ull << 20)
+static int ring_get(bg_ctx* c) {
+  if (!c->ring.empty()) return 0;
+  c->ring.assign(BG_RING_SLOTS, nullptr);
+  c->ring_ev.assign(BG_RING_SLOTS, nullptr);
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int k = 0; k < BG_RING_SLOTS; ++k)
+    th.emplace_back([&, k]() {
+      if (hipSetDevice(c->device) != hipSuccess ||
+          hipHostMalloc((void**)&c->ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming) != hipSuccess)
+        bad = 1;
+    });
+  for (auto& x : th) x.join();
+  if (bad) {
+    (void)hipGetLastError();
+    for (auto e : c->ring_ev)
+      if (e) hipEventDestroy(e);
+    for (auto p : c->ring)
+      if (p) hipHostFree(p);
+    c->ring.clear();
+    c->ring_ev.clear();
+    return bg_fail(c, BG_E_HIP, "staging ring");
+  }
+  return 0;
+}
+
+// host -> device through the ring: T threads copy chunks of `src` into their slots (CPU
+// memcpy from cached pages) and queue the slot's DMA on ctx's stream, reusing a slot once its
+// event says the previous DMA out of it has completed
+#define BG_RING_THREADS 8
+static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
+  if (!n) return 0;
+  int rc = ring_get(c);
+  if (rc) return rc;
+  const uint64_t nch = (n + BG_RING_CH - 1) / BG_RING_CH;
+  const int T = (int)std::min<uint64_t>(BG_RING_THREADS, nch);
+  const int per = BG_RING_SLOTS / BG_RING_THREADS;  // slots per thread
+  std::mutex mu;
+  std::atomic<int> bad{0};
+  auto worker = [&](int t) {
+    if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
+    uint64_t j = 0;
+    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T, ++j) {
+      const int sl = t * per + (int)(j % per);
+      if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = 1; return; }
+      const uint64_t off = k * BG_RING_CH, len = std::min<uint64_t>(BG_RING_CH, n - off);
+      memcpy(c->ring[sl], src + off, len);
+      std::lock_guard<std::mutex> g(mu);
+      if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+          hipEventRecord(c->ring_ev[sl], c->stream) != hipSuccess) {
+        bad = 1;
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  return bad ? bg_fail(c, BG_E_HIP, "staging ring copy") : 0;
+}
+
+// BEDGPU_IMG_COPY=reg: register the image and DMA from it; =pageable: the runtime's own
+// staging; default: through the ring (above)
+static int img_copy_mode() {
+  static const int m = [] {
+    const char* s = getenv("BEDGPU_IMG_COPY");
+    if (s && !strcmp(s, "reg")) return 1;
+    if (s && !strcmp(s, "pageable")) return 2;
+    return 0;
+  }();
+  return m;
+}
+
 extern "C" int bg_file_image_register(bg_file_image* m) {
   if (!m) return BG_E_ARG;
-  if (m->registered || !m->n) return 0;
+  if (m->registered || !m->n || img_copy_mode() != 1) return 0;
   if (hipHostRegister((void*)m->data, (size_t)m->n, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
     return BG_E_HIP;  // the copies still work (pageable source), staged by the runtime
@@ -399,12 +475,19 @@ extern "C" int bg_file_image_to_device(bg_ctx* c, const bg_file_image* m, uint64
   bg_bind(c);
   char* d = (char*)bg_alloc(c, len + 64);
   if (!d) return BG_E_NOMEM;
+  int rc = 0;
   if (len) {
-    const hipError_t e = hipMemcpyAsync(d, m->data + off, (size_t)len, hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) {
-      bg_release(c, d);
-      return bg_hip_fail(c, e, "file map copy");
+    if (m->registered || img_copy_mode() == 2) {
+      const hipError_t e = hipMemcpyAsync(d, m->data + off, (size_t)len, hipMemcpyHostToDevice, c->stream);
+      if (e != hipSuccess) rc = bg_hip_fail(c, e, "file image copy");
+    } else {
+      rc = ring_h2d(c, d, m->data + off, len);
     }
+  }
+  if (rc) {
+    hipStreamSynchronize(c->stream);
+    bg_release(c, d);
+    return rc;
   }
   *out = d;
   return 0;
@@ -443,126 +526,74 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
   return 0;
 }
 
-// Output to a regular file: BG_WR_THREADS threads each stage 16 MiB chunks through two
-// registered buffers of their own (D2H by DMA on ctx's stream) and pwrite(2) them at their
-// offsets, so the page-cache copies of several chunks run at once. Measured on the box
-// (tools/out_probe.cpp, 0.92 GB): one write(2) stream 88-165 ms, pwrite from 4 threads
-// ~105 ms, a shared mapping of the file filled by DMA 128 ms (page allocation through faults
-// does not scale with threads: 285 ms with 4). -1: not a regular file or an append
-// descriptor (the caller streams through write(2); nothing reached the file).
+// Output to a regular file: BG_WR_THREADS threads each stage ring-slot chunks (D2H by DMA on
+// ctx's stream) and pwrite(2) them at their offsets, so the page-cache copies of several
+// chunks run at once. Measured on the box (tools/out_probe.cpp, 0.92 GB): one write(2)
+// stream 88-165 ms, pwrite from 4 threads ~105 ms, a shared mapping of the file filled by DMA
+// 128 ms (page allocation through faults does not scale with threads: 285 ms with 4).
+// Anything else (pipes, terminals, appends): the same chunks written in order by one thread.
 #define BG_WR_THREADS 4
-static int write_device_pwrite(bg_ctx* c, const void* d, uint64_t n, int fd) {
+static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd) {
+  int rc = ring_get(c);
+  if (rc) return rc;
   struct stat st;
-  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) return -1;
   const int fl = fcntl(fd, F_GETFL);
-  if (fl < 0 || (fl & O_APPEND)) return -1;
   const off_t off0 = lseek(fd, 0, SEEK_CUR);
-  if (off0 < 0) return -1;
-  const uint64_t CH = 16ull << 20;
-  const uint64_t nch = (n + CH - 1) / CH;
-  const int T = (int)std::min<uint64_t>(BG_WR_THREADS, nch);
-  const uint64_t slot = std::min<uint64_t>(CH, (n + 4095) & ~4095ull);
-  char* buf = (char*)malloc(2 * (size_t)T * slot);
-  if (!buf) return BG_E_NOMEM;
-  const bool reg = hipHostRegister(buf, 2 * (size_t)T * slot, hipHostRegisterDefault) == hipSuccess;
-  if (!reg) (void)hipGetLastError();
-  std::mutex mu;  // one stream: copies issued in any order, each waited on by its thread
+  const char* par = getenv("BEDGPU_WRITE_PAR");  // 0: one thread, write(2)
+  const bool pw = fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && fl >= 0 && !(fl & O_APPEND) && off0 >= 0 &&
+                  !(par && strcmp(par, "0") == 0);
+  const uint64_t CH = BG_RING_CH, nch = (n + CH - 1) / CH;
+  const int T = pw ? (int)std::min<uint64_t>(BG_WR_THREADS, nch) : 1;
+  const int per = BG_RING_SLOTS / BG_WR_THREADS;
+  std::mutex mu;
   std::atomic<int> bad{0};
-  std::vector<hipEvent_t> ev(2 * T, nullptr);
-  for (auto& e : ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) bad = 1;
+  // one writer: chunks in order, the DMA of the next `per` chunks queued ahead of write(2)
+  auto issue = [&](uint64_t k, int sl) -> bool {
+    const uint64_t o = k * CH, len = std::min(CH, n - o);
+    std::lock_guard<std::mutex> g(mu);
+    return hipMemcpyAsync(c->ring[sl], (const char*)d + o, len, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+           hipEventRecord(c->ring_ev[sl], c->stream) == hipSuccess;
+  };
   auto worker = [&](int t) {
-    (void)hipSetDevice(c->device);
-    uint64_t j = 0;
-    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T, ++j) {
-      const int sl = 2 * t + (int)(j & 1);
-      char* hb = buf + (size_t)sl * slot;
-      const uint64_t o = k * CH, len = std::min(CH, n - o);
-      {
-        std::lock_guard<std::mutex> g(mu);
-        if (hipMemcpyAsync(hb, (const char*)d + o, len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipEventRecord(ev[sl], c->stream) != hipSuccess) {
-          bad = 1;
-          return;
-        }
-      }
-      if (hipEventSynchronize(ev[sl]) != hipSuccess) { bad = 1; return; }
+    if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
+    std::vector<uint64_t> mine;
+    for (uint64_t k = (uint64_t)t; k < nch; k += (uint64_t)T) mine.push_back(k);
+    const size_t depth = std::min<size_t>(per, mine.size());
+    for (size_t q = 0; q < depth; ++q)
+      if (!issue(mine[q], t * per + (int)(q % per))) { bad = 1; return; }
+    for (size_t q = 0; q < mine.size() && !bad; ++q) {
+      const int sl = t * per + (int)(q % per);
+      const uint64_t k = mine[q], o = k * CH, len = std::min(CH, n - o);
+      if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = 1; return; }
       uint64_t w = 0;
       while (w < len) {
-        const ssize_t r = pwrite(fd, hb + w, len - w, off0 + (off_t)(o + w));
+        const ssize_t r = pw ? pwrite(fd, c->ring[sl] + w, len - w, off0 + (off_t)(o + w))
+                             : write(fd, c->ring[sl] + w, len - w);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) { bad = 2; return; }
         w += (uint64_t)r;
       }
+      if (q + depth < mine.size() && !issue(mine[q + depth], sl)) { bad = 1; return; }
     }
   };
-  if (!bad) {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
-    worker(0);
-    for (auto& x : th) x.join();
-  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
   hipStreamSynchronize(c->stream);
-  for (auto e : ev)
-    if (e) hipEventDestroy(e);
-  if (reg) (void)hipHostUnregister(buf);
-  free(buf);
   if (bad == 2) return bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
   if (bad) return bg_fail(c, BG_E_HIP, "bg_write_device copy");
-  if (lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
+  if (pw && lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
     return bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
   return 0;
 }
 
-// streams n bytes of device memory to fd: a regular file by parallel pwrite(2)
-// (write_device_pwrite), anything else (pipes, terminals, appends) through two registered
-// 64 MiB host buffers, the D2H copy of the next chunk overlapping write(2) of this one
+// streams n bytes of device memory to fd (write_device_ring)
 extern "C" int bg_write_device(bg_ctx* c, const void* d, uint64_t n, int fd) {
   if (!c || (!d && n)) return BG_E_ARG;
   if (n == 0) return 0;
   bg_bind(c);
-  const char* nm = getenv("BEDGPU_WRITE_PAR");  // 0: always stream through write(2)
-  const int mr = (nm && strcmp(nm, "0") == 0) ? -1 : write_device_pwrite(c, d, n, fd);
-  if (mr != -1) {
-    bg_mark(c, "write");
-    return mr;
-  }
-  const uint64_t CH = std::min<uint64_t>(64ull << 20, (n + 4095) & ~4095ull);
-  char* buf = (char*)malloc(2 * CH);
-  if (!buf) return BG_E_NOMEM;
-  const bool reg = hipHostRegister(buf, 2 * CH, hipHostRegisterDefault) == hipSuccess;
-  if (!reg) (void)hipGetLastError();
-  char* hb[2] = {buf, buf + CH};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  int rc = 0;
-  for (int k = 0; k < 2 && !rc; ++k) {
-    const hipError_t e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
-    if (e != hipSuccess) rc = bg_hip_fail(c, e, "bg_write_device events");
-  }
-  const char* src = (const char*)d;
-  const uint64_t nch = (n + CH - 1) / CH;
-  auto issue = [&](uint64_t k) -> int {
-    const uint64_t off = k * CH, len = std::min(CH, n - off);
-    hipError_t e = hipMemcpyAsync(hb[k % 2], src + off, len, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipEventRecord(ev[k % 2], c->stream);
-    return e == hipSuccess ? 0 : bg_hip_fail(c, e, "bg_write_device copy");
-  };
-  for (uint64_t k = 0; k < std::min<uint64_t>(2, nch) && !rc; ++k) rc = issue(k);
-  for (uint64_t k = 0; k < nch && !rc; ++k) {
-    hipError_t e = hipEventSynchronize(ev[k % 2]);
-    if (e != hipSuccess) { rc = bg_hip_fail(c, e, "bg_write_device sync"); break; }
-    const uint64_t off = k * CH, len = std::min(CH, n - off);
-    if (write_all(fd, hb[k % 2], len)) {
-      rc = bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
-      break;
-    }
-    if (k + 2 < nch) rc = issue(k + 2);  // the buffer just written out takes chunk k + 2
-  }
-  hipStreamSynchronize(c->stream);
-  for (int k = 0; k < 2; ++k)
-    if (ev[k]) hipEventDestroy(ev[k]);
-  if (reg) (void)hipHostUnregister(buf);
-  free(buf);
+  const int rc = write_device_ring(c, d, n, fd);
   bg_mark(c, "write");
   return rc;
 }
@@ -587,8 +618,13 @@ extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts,
   char* d = (char*)bg_alloc(c, t + 64);
   if (!d) return BG_E_NOMEM;
   uint64_t o = 0;
-  for (int k = 0; k < n; ++k) {
-    if (lens[k]) BG_HIP(c, hipMemcpyAsync(d + o, parts[k], lens[k], hipMemcpyHostToDevice, c->stream));
+  for (int k = 0; k < n; ++k) {  // through the staging ring (pageable or registered parts alike)
+    const int rc = ring_h2d(c, d + o, (const char*)parts[k], lens[k]);
+    if (rc) {
+      hipStreamSynchronize(c->stream);
+      bg_release(c, d);
+      return rc;
+    }
     o += lens[k];
   }
   *out = d;

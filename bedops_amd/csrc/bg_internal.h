@@ -65,6 +65,10 @@ struct bg_ctx {
   // chunks are kept for the context's lifetime, handed out by a bump pointer reset per call
   std::vector<std::pair<char*, size_t>> pin_chunks;
   size_t pin_chunk = 0, pin_used = 0;
+  // staging ring for bulk host<->device copies (bg_ring_get): driver-allocated pinned slots,
+  // so no user-pointer pages the kernel driver could invalidate under running kernels
+  std::vector<char*> ring;
+  std::vector<hipEvent_t> ring_ev;
   hipStream_t stream = nullptr;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
