@@ -113,10 +113,11 @@ static inline int file_is_starch(const char* path) {
   return r > 0 && bg_starch_is(b, (uint64_t)r);
 }
 
-/* Input files that go straight to device memory are read into host images
- * (bg_file_image_open: parallel preads, no GPU call) by one thread each, started before
- * bg_open so the reads overlap HIP's initialisation; read_input then registers the image and
- * DMAs it to HBM, and cli_prefetch_release frees the images once the loads have copied them. */
+/* Input files that go straight to device memory are mapped with their pages faulted in
+ * (bg_file_image_open, no GPU call) by one thread each, started before bg_open so this
+ * overlaps HIP's initialisation; read_input then copies the image to HBM through the
+ * context's pinned ring, and cli_prefetch_release unmaps the images once the loads have
+ * copied them. */
 #include <pthread.h>
 #define CLI_MAX_PF 16
 typedef struct {
@@ -178,8 +179,9 @@ static inline void cli_prefetch_release(bg_ctx* ctx) {
 }
 
 /* one input into `in`: regular files whose bytes no host code needs (no --ec/--header)
- * go straight to device memory (their host image DMA'd to HBM: cli_prefetch /
- * bg_read_file_device); stdin, pipes and checked inputs are read into host memory.
+ * go straight to device memory (their mapped pages copied to HBM through the pinned ring:
+ * cli_prefetch / bg_read_file_device); stdin, pipes and checked inputs are read into host
+ * memory.
  * Returns 0 or -1 (unreadable). */
 static inline int read_input(bg_ctx* ctx, const char* path, int host_needed, text_buf_t* t, bg_input* in) {
   struct stat st;

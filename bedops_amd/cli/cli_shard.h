@@ -8,9 +8,9 @@
  *      text — the idea of find_bed_range (interfaces/general-headers/algorithm/bed/
  *      FindBedRange.hpp:67-188): O(chromosomes x log(bytes)) line probes, no full scan;
  *   2. chromosomes go to devices by longest-processing-time on their bytes in all inputs;
- *   3. each device receives only its chromosomes' bytes, DMA'd from the input files' host
- *      images (read once by parallel preads and registered once, bg_file_image: portable, so
- *      every device copies its byte ranges from them over its own link), and runs load ->
+ *   3. each device receives only its chromosomes' bytes, copied from the input files'
+ *      mappings (bg_file_image: page-cache pages, nothing read whole into or pinned in host
+ *      memory) through its context's pinned ring over its own link, and runs load ->
  *      operation -> format on its own host thread;
  *   4. bg_group_gather reassembles the texts on device 0 in strcmp chromosome order over
  *      RCCL, and device 0 streams them to stdout.
@@ -121,7 +121,7 @@ typedef struct {
   bg_ctx* ctx;
   int nf;
   const bg_input* proto; /* kinds */
-  const bg_file_image* fm; /* the input files' host images */
+  const bg_file_image* fm; /* the input files' mappings */
   const cruns_t* runs;   /* per file */
   const int* owner;      /* global chromosome -> device */
   char (*gnames)[BG_CHR_NAME_CAP];

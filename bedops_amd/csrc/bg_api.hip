@@ -313,18 +313,19 @@ extern "C" int bg_result_copy_text(bg_ctx* c, bg_result* r, char* host, uint64_t
 
 
 // ---------------------------------------------------------------------------------------
-// Input files -> HBM. A file is read into anonymous host memory (transparent huge pages) by
-// BG_IMG_THREADS parallel preads — no GPU call, so the front-ends run it while bg_open
-// initialises HIP — then that image is registered for DMA (hipHostRegister, portable: every
-// device of a group can read it) and copied to HBM by the DMA engines. Measured on the box
-// (tools/e2e_probe.cpp, 2.38 GB): 16 threads read the page cache into fresh anonymous
-// memory at ~120 GB/s (20 ms), registering it takes ~5 ms, the copy ~45 ms (50-57 GB/s).
-// Registering the file's own page-cache mapping instead saves the host copy in isolation,
-// but inside the CLI it stalled the first kernels by 250-450 ms (the driver's user-pointer
-// pages of a file mapping get invalidated and restored), and the pinned pread ring it
-// replaced needed extra copy streams (8-40 ms each to create, more to tear down at exit).
+// Input files -> HBM. A file is mapped read-only with its page-cache pages faulted in
+// (MAP_POPULATE: page-table entries only, no copy, no GPU call, so the front-ends run it
+// while bg_open initialises HIP); after that, threads copy it from the page cache into a
+// driver-pinned staging ring whose slots the DMA engines stream to HBM (ring_h2d below).
+// What was measured on the box and dropped (tools/e2e_probe.cpp, tools/gpu_e2e_r03.sh):
+//   - registering the mapping (or an anonymous copy of it) with hipHostRegister and DMA-ing
+//     straight from it: fast in isolation (register 5-19 ms, copy ~45 ms per 2.38 GB) but
+//     inside the CLI the first kernels stalled by 250-450 ms;
+//   - reading the file into anonymous memory during HIP init: freeing 2.38 GB of 4 KiB
+//     pages afterwards costs ~240 ms (munmap, or the same at process exit);
+//   - the round-2 pread ring: needed extra copy streams (8-40 ms each to create, more to
+//     tear down at exit) and could not start before HIP was up.
 // ---------------------------------------------------------------------------------------
-#define BG_IMG_THREADS 8
 extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
   if (!path || !m) return BG_E_ARG;
   memset(m, 0, sizeof(*m));
@@ -335,41 +336,16 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
     close(fd);
     return BG_E_ARG;
   }
-  const uint64_t n = (uint64_t)st.st_size;
-  if (n) {
-    void* p = mmap(nullptr, (size_t)n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  m->n = (uint64_t)st.st_size;
+  if (m->n) {
+    void* p = mmap(nullptr, (size_t)m->n, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
     if (p == MAP_FAILED) {
       close(fd);
-      return BG_E_NOMEM;
-    }
-    (void)madvise(p, (size_t)n, MADV_HUGEPAGE);
-    const uint64_t CH = 8ull << 20, nch = (n + CH - 1) / CH;
-    const int T = (int)std::min<uint64_t>(BG_IMG_THREADS, nch);
-    std::atomic<int> bad{0};
-    auto reader = [&](int t) {
-      for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T) {
-        const uint64_t off = k * CH, len = std::min(CH, n - off);
-        uint64_t got = 0;
-        while (got < len) {
-          const ssize_t r = pread(fd, (char*)p + off + got, len - got, (off_t)(off + got));
-          if (r < 0 && errno == EINTR) continue;
-          if (r <= 0) { bad = 1; return; }
-          got += (uint64_t)r;
-        }
-      }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(reader, t);
-    reader(0);
-    for (auto& x : th) x.join();
-    if (bad) {
-      munmap(p, (size_t)n);
-      close(fd);
+      m->n = 0;
       return BG_E_IO;
     }
     m->data = (const char*)p;
   }
-  m->n = n;
   close(fd);
   return 0;
 }

@@ -241,15 +241,13 @@ int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
  * Replaces the reader side of allocate_iterator_starch_bed for plain BED files
  * (AllocateIterator_BED_starch.hpp:205-215). */
 int bg_read_file_device(bg_ctx* ctx, const char* path, void** dptr, uint64_t* nbytes);
-/* File images (inputs read once, by parallel preads, into host memory that the DMA engines
- * copy to HBM):
- *   bg_file_image_open      read a regular file into anonymous (huge-page) host memory; no
- *                           GPU call, so it may run on any thread while bg_open initialises
- *   bg_file_image_register  pin the image for DMA from every device (portable); a failure
- *                           (BG_E_HIP) leaves it usable as a pageable source
+/* File images (inputs as the host reads them, copied to HBM through a pinned ring):
+ *   bg_file_image_open      map a regular file read-only with its pages faulted in; no GPU
+ *                           call, so it may run on any thread while bg_open initialises
+ *   bg_file_image_register  optional (BEDGPU_IMG_COPY=reg: DMA straight from the mapping)
  *   bg_file_image_to_device copy bytes [off, off + len) into a new device buffer of ctx, on
  *                           ctx's stream (free with bg_device_free)
- *   bg_file_image_close     unpin and free, once every copy from it has completed (bg_sync) */
+ *   bg_file_image_close     unmap, once every copy from it has completed (bg_sync) */
 typedef struct {
   const char* data; /* the file's bytes (NULL when empty) */
   uint64_t n;       /* its size */
