@@ -390,6 +390,8 @@ static inline void cli_mark(const char* what) {
   const double t = cli_now();
   if (t0 == 0) t0 = last = t;
   fprintf(stderr, "bedgpu host  %-12s %10.3f ms (+%.3f)\n", what, 1e3 * (t - t0), 1e3 * (t - last));
+  if (!strcmp(what, "start") || !strcmp(what, "exit")) /* CLOCK_MONOTONIC, for the caller's clock */
+    fprintf(stderr, "bedgpu mono  %-12s %.6f\n", what, t);
   last = t;
 }
 

@@ -148,6 +148,7 @@ extern "C" int bg_prof_read(bg_ctx* c, char* buf, uint64_t cap) {
   return 0;
 }
 
+void bg_ring_start(bg_ctx* c);
 extern "C" int bg_open(bg_ctx** out, int device) {
   if (!out) return BG_E_ARG;
   *out = nullptr;
@@ -170,6 +171,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
     c->ncu = 256;
   const char* st = getenv("BEDGPU_STATS");
   c->stats = st && *st && strcmp(st, "0") != 0;
+  bg_ring_start(c);
   bg_mark(c, "open");
   *out = c;
   return 0;
@@ -177,6 +179,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
 
 extern "C" void bg_close(bg_ctx* c) {
   if (!c) return;
+  if (c->ring_th.joinable()) c->ring_th.join();
   hipStreamSynchronize(c->stream);
   for (auto& b : c->free_list) hipFree(b.p);
   for (auto& kv : c->live) hipFree(kv.first);
@@ -358,29 +361,50 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
 // evicts and restores the queues when such pages are invalidated); the ring's pages are the
 // driver's own.
 #define BG_RING_SLOTS 16
-#define BG_RING_CH (8ull << 20)
-static int ring_get(bg_ctx* c) {
-  if (!c->ring.empty()) return 0;
-  c->ring.assign(BG_RING_SLOTS, nullptr);
-  c->ring_ev.assign(BG_RING_SLOTS, nullptr);
+#define BG_RING_CH (4ull << 20)
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// pins the ring's slots, one thread each (bg_open runs this on a thread of its own, so the
+// pinning overlaps whatever the caller does next)
+static int ring_alloc(bg_ctx* c) {
+  const double t0 = now_ms();
+  std::vector<char*> ring(BG_RING_SLOTS, nullptr);
+  std::vector<hipEvent_t> ev(BG_RING_SLOTS, nullptr);
   std::atomic<int> bad{0};
   std::vector<std::thread> th;
   for (int k = 0; k < BG_RING_SLOTS; ++k)
     th.emplace_back([&, k]() {
       if (hipSetDevice(c->device) != hipSuccess ||
-          hipHostMalloc((void**)&c->ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
-          hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming) != hipSuccess)
+          hipHostMalloc((void**)&ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess)
         bad = 1;
     });
   for (auto& x : th) x.join();
   if (bad) {
     (void)hipGetLastError();
-    for (auto e : c->ring_ev)
+    for (auto e : ev)
       if (e) hipEventDestroy(e);
-    for (auto p : c->ring)
+    for (auto p : ring)
       if (p) hipHostFree(p);
-    c->ring.clear();
-    c->ring_ev.clear();
+    return BG_E_HIP;
+  }
+  c->ring = ring;
+  c->ring_ev = ev;
+  if (c->stats)
+    fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", BG_RING_SLOTS,
+            (unsigned long long)(BG_RING_CH >> 20), now_ms() - t0);
+  return 0;
+}
+void bg_ring_start(bg_ctx* c) {
+  c->ring_th = std::thread([c]() { c->ring_rc = ring_alloc(c); });
+}
+static int ring_get(bg_ctx* c) {
+  if (c->ring_th.joinable()) c->ring_th.join();
+  if (!c->ring.empty()) return 0;
+  if (c->ring_rc == 0) c->ring_rc = ring_alloc(c);  // not started, or an earlier attempt failed
+  if (c->ring_rc) {
+    c->ring_rc = 0;  // a later call may retry
     return bg_fail(c, BG_E_HIP, "staging ring");
   }
   return 0;
@@ -389,14 +413,23 @@ static int ring_get(bg_ctx* c) {
 // host -> device through the ring: T threads copy chunks of `src` into their slots (CPU
 // memcpy from cached pages) and queue the slot's DMA on ctx's stream, reusing a slot once its
 // event says the previous DMA out of it has completed
-#define BG_RING_THREADS 8
+// (BEDGPU_RING_THREADS: 1..32, default 16)
+static int ring_threads() {
+  static const int t = [] {
+    const char* s = getenv("BEDGPU_RING_THREADS");
+    const int v = s ? atoi(s) : 16;
+    return v < 1 ? 1 : (v > BG_RING_SLOTS ? BG_RING_SLOTS : v);
+  }();
+  return t;
+}
 static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   if (!n) return 0;
   int rc = ring_get(c);
   if (rc) return rc;
   const uint64_t nch = (n + BG_RING_CH - 1) / BG_RING_CH;
-  const int T = (int)std::min<uint64_t>(BG_RING_THREADS, nch);
-  const int per = BG_RING_SLOTS / BG_RING_THREADS;  // slots per thread
+  const int TT_ = ring_threads();
+  const int T = (int)std::min<uint64_t>(TT_, nch);
+  const int per = BG_RING_SLOTS / TT_;  // slots per thread
   std::mutex mu;
   std::atomic<int> bad{0};
   auto worker = [&](int t) {
@@ -415,10 +448,17 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
       }
     }
   };
+  const double t0 = now_ms();
   std::vector<std::thread> th;
   for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
   worker(0);
   for (auto& x : th) x.join();
+  if (c->stats) {  // the last copies drained (stats runs only: this waits)
+    const double t1 = now_ms();
+    hipStreamSynchronize(c->stream);
+    fprintf(stderr, "bedgpu ring   %.1f MB: copies issued %.3f ms, drained %.3f ms\n", n / 1e6, t1 - t0,
+            now_ms() - t0);
+  }
   return bad ? bg_fail(c, BG_E_HIP, "staging ring copy") : 0;
 }
 

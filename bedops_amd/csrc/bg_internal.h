@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../../include/bedgpu.h"
@@ -69,6 +70,8 @@ struct bg_ctx {
   // so no user-pointer pages the kernel driver could invalidate under running kernels
   std::vector<char*> ring;
   std::vector<hipEvent_t> ring_ev;
+  std::thread ring_th;  // bg_open starts pinning the ring; its first use joins
+  int ring_rc = 0;
   hipStream_t stream = nullptr;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device

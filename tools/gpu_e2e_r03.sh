@@ -12,7 +12,7 @@ D=/tmp/e2e; mkdir -p $D
 [ -f $D/B.bed ] || ./tools/build/bedgen 100000000 43 > $D/B.bed || exit 1
 ( time cat $D/A.bed $D/B.bed > /dev/null ) 2> "$O/cat.txt"
 for k in $(seq 1 "$RUNS"); do
-  ( time env BEDGPU_STATS=1 "$@" timeout -k 10 120 ./bedops_amd/bin/bedops --intersect $D/A.bed $D/B.bed > $D/out.bed ) 2> "$O/run_$k.txt" || exit 1
+  ( time env BEDGPU_STATS=1 "$@" timeout -k 10 120 python3 tools/e2e_time.py $D/out.bed ./bedops_amd/bin/bedops --intersect $D/A.bed $D/B.bed ) 2> "$O/run_$k.txt" || exit 1
 done
 sha256sum $D/out.bed | cut -c1-16 > "$O/sha.txt"
 grep -h real "$O"/run_*.txt > "$O/real.txt"
