@@ -28,7 +28,7 @@ $(LIB): $(HIPOBJS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lz -ldl -Wl,-rpath,/opt/rocm/lib
 
-$(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h include/bedgpu.h $(LIB)
+$(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h bedops_amd/cli/cli_stream.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
 
@@ -36,7 +36,7 @@ $(BIN)/sort-bed: bedops_amd/cli/sortbed.c bedops_amd/cli/cli_common.h include/be
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
 
-$(BIN)/closest-features: bedops_amd/cli/closest.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h include/bedgpu.h $(LIB)
+$(BIN)/closest-features: bedops_amd/cli/closest.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h bedops_amd/cli/cli_stream.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) -o $@ $< -Lbedops_amd/lib -lbedgpu -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,/opt/rocm/lib
 

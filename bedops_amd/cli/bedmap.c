@@ -13,7 +13,7 @@
  * available in this build.
  */
 #include "cli_common.h"
-#include "cli_shard.h"
+#include "cli_stream.h"
 
 static const char* PROG = "bedmap";
 
@@ -293,32 +293,41 @@ int main(int argc, char** argv) {
    * an element operation's stop at the file's first unmapped row, and decimal running sums
    * (one double across the file: bg_map refuses them on a shard and the run falls back to
    * one device, as on any shard error) */
-  int shardable = !check && !ec && !chrom && getenv("BEDGPU_DEVICES") != NULL;
+  int shardable = !check && !ec && !chrom;
   for (int k = 0; k < o.n_ops; ++k) {
     if (o.ops[k] == BG_MAP_ECHO_REF_ROW_ID) shardable = 0;
     if (o.ops[k] >= BG_MAP_MIN_ELEMENT && o.ops[k] <= BG_MAP_MAX_ELEMENT_RAND && !o.skip_unmapped) shardable = 0;
   }
   for (int i = a; i < argc; ++i)
     if (!strcmp(argv[i], "-")) shardable = 0;
-  if (shardable) {
-    bg_input sin[2];
-    memset(sin, 0, sizeof(sin));
-    sin[0].kind = nf == 1 ? skind : rkind;
-    sin[1].kind = mkind;
-    map_args_t ma;
-    ma.o = o;
-    ma.o.shard = 1;
-    ma.single = nf == 1;
-    if (shard_run(PROG, nf, sin, (const char* const*)(argv + a), run_map, &ma) == 0) return EXIT_SUCCESS;
-  }
+  bg_input sin[2];
+  memset(sin, 0, sizeof(sin));
+  sin[0].kind = nf == 1 ? skind : rkind;
+  sin[1].kind = mkind;
+  map_args_t ma;
+  ma.o = o;
+  ma.o.shard = 1;
+  ma.single = nf == 1;
+  if (shardable && getenv("BEDGPU_DEVICES") &&
+      shard_run(PROG, nf, sin, (const char* const*)(argv + a), run_map, &ma) == 0)
+    return EXIT_SUCCESS;
 
   cli_mark("start");
-  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+  /* one GPU: chromosome groups in a pipeline (cli_stream.h), same conditions as the shards */
+  const int streamed = shardable && stream_prepare(nf, (const char* const*)(argv + a));
+  if (!chrom && !check && !ec && !streamed) /* map the inputs while HIP initialises */
     for (int i = 0; i < nf; ++i) cli_prefetch(argv[a + i]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   cli_mark("open");
+  if (streamed && stream_run(ctx, sin, run_map, &ma) == 0) {
+    cli_mark("write");
+    maybe_stats(ctx);
+    fast_exit();
+    bg_close(ctx);
+    return EXIT_SUCCESS;
+  }
   text_buf_t tr = {0}, tm = {0};
   bg_input in[2];
   memset(in, 0, sizeof(in));

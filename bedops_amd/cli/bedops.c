@@ -13,7 +13,7 @@
 #include <ctype.h>
 
 #include "cli_common.h"
-#include "cli_shard.h"
+#include "cli_stream.h"
 
 static const char* PROG = "bedops";
 
@@ -349,20 +349,33 @@ int main(int argc, char** argv) {
 
   text_buf_t* tx = (text_buf_t*)calloc((size_t)nf, sizeof(text_buf_t));
   bg_input* in = (bg_input*)calloc((size_t)nf, sizeof(bg_input));
-  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h); every mode is
-   * chromosome-local except --range padding, which looks across the whole file */
-  if (!check && !ec && !chrom && !has_range && getenv("BEDGPU_DEVICES")) {
+  /* every mode is chromosome-local except --range padding, which looks across the whole
+   * file: BEDGPU_DEVICES=0,1,... runs chromosome shards on several GPUs (cli_shard.h), and a
+   * single GPU runs chromosome groups in a pipeline (cli_stream.h) */
+  const int chrom_local = !check && !ec && !chrom && !has_range;
+  op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
+  if (chrom_local)
     for (int i = 0; i < nf; ++i) in[i].kind = input_kind(mode, i, chrom, has_range);
-    op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
-    if (shard_run(PROG, nf, in, (const char* const*)(argv + a), run_op, &oa) == 0) return EXIT_SUCCESS;
-  }
+  if (chrom_local && getenv("BEDGPU_DEVICES") &&
+      shard_run(PROG, nf, in, (const char* const*)(argv + a), run_op, &oa) == 0)
+    return EXIT_SUCCESS;
   cli_mark("start");
-  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+  const int streamed = chrom_local && stream_prepare(nf, (const char* const*)(argv + a));
+  if (!chrom && !check && !ec && !streamed) /* map the inputs while HIP initialises */
     for (int i = 0; i < nf; ++i) cli_prefetch(argv[a + i]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   cli_mark("open");
+  if (streamed && stream_run(ctx, in, run_op, &oa) == 0) {
+    cli_mark("write");
+    maybe_stats(ctx);
+    fast_exit();
+    bg_close(ctx);
+    free(in);
+    free(tx);
+    return EXIT_SUCCESS;
+  }
   for (int i = 0; i < nf; ++i) {
     if (read_input_chrom(ctx, argv[a + i], chrom, check || ec, &tx[i], &in[i])) {
       char b[1024];
@@ -394,7 +407,6 @@ int main(int argc, char** argv) {
     if (!((mode == 'e' || mode == 'n') && i == 0) && (rc = bg_set_pad(ctx, set, i, lpad, rpad)))
       die_ctx(PROG, ctx, rc);
   bg_result* res = NULL;
-  op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
   if ((rc = run_op(&oa, ctx, set, &res))) die_ctx(PROG, ctx, rc);
   cli_mark("operation");
   if ((rc = bg_result_write(ctx, res, 1))) die_ctx(PROG, ctx, rc);

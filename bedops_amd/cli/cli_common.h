@@ -143,6 +143,8 @@ static inline void* cli_pf_run(void* a) {
 }
 static inline void cli_prefetch(const char* path) {
   struct stat st;
+  const char* e = getenv("BEDGPU_PF"); /* BEDGPU_PF=0: no mapping before bg_open */
+  if (e && !strcmp(e, "0")) return;
   if (CLI_NPF >= CLI_MAX_PF || !strcmp(path, "-") || stat(path, &st) != 0 || !S_ISREG(st.st_mode)) return;
   cli_pf_t* p = &CLI_PF[CLI_NPF];
   memset(p, 0, sizeof(*p));

@@ -12,7 +12,7 @@
  * <msg>" (ClosestFeature.cpp:93-95).
  */
 #include "cli_common.h"
-#include "cli_shard.h"
+#include "cli_stream.h"
 
 static const char* PROG = "closest-features";
 
@@ -105,21 +105,31 @@ int main(int argc, char** argv) {
   }
   if (!strcmp(argv[a], "-") && !strcmp(argv[a + 1], "-")) arg_error("Cannot have both input files set to '-'");
 
-  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h) */
-  if (!check && !ec && !chrom && getenv("BEDGPU_DEVICES") && strcmp(argv[a], "-") && strcmp(argv[a + 1], "-")) {
-    bg_input sin[2];
-    memset(sin, 0, sizeof(sin));
-    for (int k = 0; k < 2; ++k) sin[k].kind = BG_BED3_REST;
-    if (shard_run(PROG, 2, sin, (const char* const*)(argv + a), run_closest, &o) == 0) return EXIT_SUCCESS;
-  }
+  /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h); one GPU:
+   * chromosome groups in a pipeline (cli_stream.h) */
+  const int chrom_local = !check && !ec && !chrom && strcmp(argv[a], "-") && strcmp(argv[a + 1], "-");
+  bg_input sin[2];
+  memset(sin, 0, sizeof(sin));
+  for (int k = 0; k < 2; ++k) sin[k].kind = BG_BED3_REST;
+  if (chrom_local && getenv("BEDGPU_DEVICES") &&
+      shard_run(PROG, 2, sin, (const char* const*)(argv + a), run_closest, &o) == 0)
+    return EXIT_SUCCESS;
 
   cli_mark("start");
-  if (!chrom && !check && !ec) /* map the inputs while HIP initialises */
+  const int streamed = chrom_local && stream_prepare(2, (const char* const*)(argv + a));
+  if (!chrom && !check && !ec && !streamed) /* map the inputs while HIP initialises */
     for (int k = 0; k < 2; ++k) cli_prefetch(argv[a + k]);
   bg_ctx* ctx = NULL;
   int rc = bg_open(&ctx, env_device());
   if (rc) die_msg(PROG, "cannot open the GPU device (libbedgpu/HIP)");
   cli_mark("open");
+  if (streamed && stream_run(ctx, sin, run_closest, &o) == 0) {
+    cli_mark("write");
+    maybe_stats(ctx);
+    fast_exit();
+    bg_close(ctx);
+    return EXIT_SUCCESS;
+  }
   text_buf_t t[2] = {{0}, {0}};
   bg_input in[2];
   for (int k = 0; k < 2; ++k) {

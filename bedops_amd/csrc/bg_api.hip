@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -341,7 +343,15 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
   }
   m->n = (uint64_t)st.st_size;
   if (m->n) {
-    void* p = mmap(nullptr, (size_t)m->n, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+    // BEDGPU_POPULATE=1: fault the page-table entries in here (MAP_POPULATE). Off by default:
+    // populating holds the mm's lock for the whole file and HIP's initialisation (its own
+    // mappings) waited on it — bg_open 135-155 ms instead of ~80 ms on the box, with the
+    // copies no faster (gpurun_out/e2e_var, profiles/r03_e2e_var.txt)
+    static const bool populate = [] {
+      const char* s = getenv("BEDGPU_POPULATE");
+      return s && strcmp(s, "1") == 0;
+    }();
+    void* p = mmap(nullptr, (size_t)m->n, PROT_READ, MAP_SHARED | (populate ? MAP_POPULATE : 0), fd, 0);
     if (p == MAP_FAILED) {
       close(fd);
       m->n = 0;
@@ -361,6 +371,7 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
 // evicts and restores the queues when such pages are invalidated); the ring's pages are the
 // driver's own.
 #define BG_RING_SLOTS 16
+#define BG_WR_SLOTS 8  // after the ring's slots: the output queue's (bg_writer)
 #define BG_RING_CH (4ull << 20)
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -369,11 +380,11 @@ static double now_ms() {
 // pinning overlaps whatever the caller does next)
 static int ring_alloc(bg_ctx* c) {
   const double t0 = now_ms();
-  std::vector<char*> ring(BG_RING_SLOTS, nullptr);
-  std::vector<hipEvent_t> ev(BG_RING_SLOTS, nullptr);
+  std::vector<char*> ring(BG_RING_SLOTS + BG_WR_SLOTS, nullptr);
+  std::vector<hipEvent_t> ev(BG_RING_SLOTS + BG_WR_SLOTS, nullptr);
   std::atomic<int> bad{0};
   std::vector<std::thread> th;
-  for (int k = 0; k < BG_RING_SLOTS; ++k)
+  for (int k = 0; k < BG_RING_SLOTS + BG_WR_SLOTS; ++k)
     th.emplace_back([&, k]() {
       if (hipSetDevice(c->device) != hipSuccess ||
           hipHostMalloc((void**)&ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
@@ -392,7 +403,7 @@ static int ring_alloc(bg_ctx* c) {
   c->ring = ring;
   c->ring_ev = ev;
   if (c->stats)
-    fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", BG_RING_SLOTS,
+    fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", BG_RING_SLOTS + BG_WR_SLOTS,
             (unsigned long long)(BG_RING_CH >> 20), now_ms() - t0);
   return 0;
 }
@@ -646,6 +657,147 @@ extern "C" int bg_device_gather_host(bg_ctx* c, int n, const void* const* parts,
   *out = d;
   *total = t;
   return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Output queue (bg_writer): device texts handed over in order are copied D2H on a stream of
+// the queue's own into the ring's writer slots and written with write(2) by one host thread,
+// so the output of one chromosome group goes out while the next group is read (H2D on ctx's
+// stream, the other direction of the link) and computed. One writer thread: buffered writes
+// to one file serialise on its inode lock anyway (tools/out_probe.cpp measurements above).
+// ---------------------------------------------------------------------------------------
+struct bg_writer {
+  bg_ctx* c = nullptr;
+  int fd = -1;
+  hipStream_t st = nullptr;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  struct Job {
+    const char* d;
+    uint64_t n;
+    hipEvent_t ready;
+  };
+  std::deque<Job> q;
+  std::vector<hipEvent_t> spare;  // ready events the writer has finished with
+  uint64_t done = 0;
+  bool closing = false;
+  int err = 0;  // BG_E_IO / BG_E_HIP
+  int eno = 0;
+};
+
+static void writer_loop(bg_writer* w) {
+  bg_ctx* c = w->c;
+  if (hipSetDevice(c->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking) != hipSuccess) {
+    std::lock_guard<std::mutex> g(w->mu);
+    w->err = BG_E_HIP;
+  }
+  const uint64_t CH = BG_RING_CH;
+  for (;;) {
+    bg_writer::Job J;
+    {
+      std::unique_lock<std::mutex> g(w->mu);
+      w->cv.wait(g, [&] { return w->closing || !w->q.empty(); });
+      if (w->q.empty()) return;  // closing, everything written
+      J = w->q.front();
+    }
+    int bad = 0, eno = 0;
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      bad = w->err;
+    }
+    if (!bad && J.n) {
+      const uint64_t nch = (J.n + CH - 1) / CH;
+      auto slot = [&](uint64_t k) { return BG_RING_SLOTS + (int)(k % BG_WR_SLOTS); };
+      auto issue = [&](uint64_t k) -> bool {
+        const uint64_t o = k * CH, len = std::min(CH, J.n - o);
+        const int sl = slot(k);
+        return hipMemcpyAsync(c->ring[sl], J.d + o, len, hipMemcpyDeviceToHost, w->st) == hipSuccess &&
+               hipEventRecord(c->ring_ev[sl], w->st) == hipSuccess;
+      };
+      if (hipStreamWaitEvent(w->st, J.ready, 0) != hipSuccess) bad = BG_E_HIP;
+      const uint64_t depth = std::min<uint64_t>(BG_WR_SLOTS, nch);
+      for (uint64_t k = 0; k < depth && !bad; ++k)
+        if (!issue(k)) bad = BG_E_HIP;
+      for (uint64_t k = 0; k < nch && !bad; ++k) {
+        const int sl = slot(k);
+        if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = BG_E_HIP; break; }
+        const uint64_t o = k * CH, len = std::min(CH, J.n - o);
+        uint64_t x = 0;
+        while (x < len) {
+          const ssize_t r = write(w->fd, c->ring[sl] + x, len - x);
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) { bad = BG_E_IO; eno = r < 0 ? errno : EIO; break; }
+          x += (uint64_t)r;
+        }
+        if (!bad && k + depth < nch && !issue(k + depth)) bad = BG_E_HIP;
+      }
+      if (bad) (void)hipStreamSynchronize(w->st);  // no copy into a slot stays in flight
+    }
+    std::lock_guard<std::mutex> g(w->mu);
+    if (bad && !w->err) { w->err = bad; w->eno = eno; }
+    w->spare.push_back(J.ready);
+    w->q.pop_front();
+    ++w->done;
+    w->cv.notify_all();
+  }
+}
+
+extern "C" int bg_writer_open(bg_ctx* c, int fd, bg_writer** out) {
+  if (!c || !out || fd < 0) return BG_E_ARG;
+  *out = nullptr;
+  bg_bind(c);
+  int rc = ring_get(c);  // the writer slots are pinned with the ring
+  if (rc) return rc;
+  bg_writer* w = new bg_writer();
+  w->c = c;
+  w->fd = fd;
+  w->th = std::thread(writer_loop, w);
+  *out = w;
+  return 0;
+}
+
+extern "C" int bg_writer_push(bg_writer* w, const void* d, uint64_t n) {
+  if (!w || (!d && n)) return BG_E_ARG;
+  bg_ctx* c = w->c;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(w->mu);
+    if (w->err) return bg_fail(c, w->err, "output queue failed");
+    if (!w->spare.empty()) { ev = w->spare.back(); w->spare.pop_back(); }
+  }
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+    return bg_fail(c, BG_E_HIP, "output queue event");
+  BG_HIP(c, hipEventRecord(ev, c->stream));  // the text is complete once ctx's stream gets here
+  std::lock_guard<std::mutex> g(w->mu);
+  w->q.push_back({(const char*)d, n, ev});
+  w->cv.notify_all();
+  return 0;
+}
+
+extern "C" uint64_t bg_writer_done(bg_writer* w) {
+  if (!w) return 0;
+  std::lock_guard<std::mutex> g(w->mu);
+  return w->done;
+}
+
+extern "C" int bg_writer_close(bg_writer* w) {
+  if (!w) return BG_E_ARG;
+  {
+    std::lock_guard<std::mutex> g(w->mu);
+    w->closing = true;
+    w->cv.notify_all();
+  }
+  w->th.join();
+  bg_ctx* c = w->c;
+  int rc = w->err;
+  if (rc == BG_E_IO) bg_fail(c, rc, std::string("write failed: ") + strerror(w->eno));
+  else if (rc) bg_fail(c, rc, "output queue copy failed");
+  for (auto e : w->spare) hipEventDestroy(e);
+  if (w->st) hipStreamDestroy(w->st);
+  delete w;
+  return rc;
 }
 
 extern "C" int bg_bind(bg_ctx* c) {

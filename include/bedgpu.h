@@ -257,6 +257,17 @@ int bg_file_image_open(const char* path, bg_file_image* m);
 int bg_file_image_register(bg_file_image* m);
 int bg_file_image_to_device(bg_ctx* ctx, const bg_file_image* m, uint64_t off, uint64_t len, void** dptr);
 void bg_file_image_close(bg_file_image* m);
+/* Output queue: texts (device pointers of ctx, e.g. bg_result_text_device) written to fd in
+ * the order they are pushed, by a host thread of the queue's own (D2H on its own stream into
+ * pinned slots, then write(2)), so output can go out while the caller reads and computes the
+ * next chromosome group. A pushed text must stay allocated until bg_writer_done() counts it.
+ * Replaces the reference's record/Println streaming to stdout (Bedops.cpp:148-152) for the
+ * chromosome-group pipeline of the front-ends (bedops_amd/cli/cli_stream.h). */
+typedef struct bg_writer bg_writer;
+int bg_writer_open(bg_ctx* ctx, int fd, bg_writer** w);
+int bg_writer_push(bg_writer* w, const void* dptr, uint64_t n); /* after ctx's queued work */
+uint64_t bg_writer_done(bg_writer* w);                         /* pushes fully written */
+int bg_writer_close(bg_writer* w); /* waits for every push; first error (message on ctx) */
 /* make ctx's device current on the calling thread (a host thread per device in a group) */
 int bg_bind(bg_ctx* ctx);
 
