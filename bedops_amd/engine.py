@@ -47,7 +47,7 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_result_copy_text_device", "bg_result_chrom_spans", "bg_set_chroms",
            "bg_set_chrom_name", "bg_closest", "bg_complement", "bg_chop", "bg_partition",
            "bg_symmdiff", "bg_everything", "bg_set_pad", "bg_check", "bg_check_message",
-           "bg_write_device", "bg_bind", "bg_group_uid", "bg_group_open", "bg_group_open_rank",
+           "bg_write_device", "bg_writer_open", "bg_writer_push", "bg_writer_done", "bg_writer_close", "bg_bind", "bg_group_uid", "bg_group_open", "bg_group_open_rank",
            "bg_group_size", "bg_group_ctx", "bg_group_close", "bg_group_gather", "bg_device_free",
            "bg_device_gather_host", "bg_read_file_device", "bg_sortbed", "bg_starch_is",
            "bg_starch_decode", "bg_file_image_open", "bg_file_image_register", "bg_file_image_to_device",
