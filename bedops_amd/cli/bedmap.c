@@ -293,6 +293,7 @@ int main(int argc, char** argv) {
    * an element operation's stop at the file's first unmapped row, and decimal running sums
    * (one double across the file: bg_map refuses them on a shard and the run falls back to
    * one device, as on any shard error) */
+  cli_detach(); /* the GPU work runs in a worker whose teardown the caller does not wait for */
   int shardable = !check && !ec && !chrom;
   for (int k = 0; k < o.n_ops; ++k) {
     if (o.ops[k] == BG_MAP_ECHO_REF_ROW_ID) shardable = 0;

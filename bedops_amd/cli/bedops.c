@@ -352,6 +352,7 @@ int main(int argc, char** argv) {
   /* every mode is chromosome-local except --range padding, which looks across the whole
    * file: BEDGPU_DEVICES=0,1,... runs chromosome shards on several GPUs (cli_shard.h), and a
    * single GPU runs chromosome groups in a pipeline (cli_stream.h) */
+  cli_detach(); /* the GPU work runs in a worker whose teardown the caller does not wait for */
   const int chrom_local = !check && !ec && !chrom && !has_range;
   op_args_t oa = {mode, full_left, thres, use_pct, (uint64_t)chop_bp, (uint64_t)chop_stagger, chop_x};
   if (chrom_local)

@@ -404,6 +404,57 @@ static void maybe_stats(bg_ctx* ctx) {
   if (bg_stats(ctx, buf, sizeof(buf)) == 0) fputs(buf, stderr);
 }
 
+/* Detached teardown. Even a process that only initialised HIP spends 60-100 ms in the
+ * kernel driver after exit(2) (KFD queues and the GPU VM torn down; measured on the box,
+ * tools/gpu_exit_r03b.sh, profiles/r03_exit_teardown.txt) before its parent sees it end. So
+ * the front-end forks before touching the GPU: the worker (child) does everything and, once
+ * its output is complete (written to fd 1, i.e. in the page cache or the pipe), closes its
+ * stdout/stderr and reports its status over a pipe; the front process, which never touched
+ * the GPU, exits with that status at once while the worker's teardown finishes detached.
+ * A worker that fails (die_msg, a crash) is waited for and its status mirrored.
+ * BEDGPU_DETACH=0, or BEDGPU_FULL_EXIT=1 (profilers), keep everything in one process. */
+#include <signal.h>
+#include <sys/wait.h>
+static int CLI_DETACH_FD = -1;
+static inline int cli_env_on(const char* name) {
+  const char* s = getenv(name);
+  return s && *s && strcmp(s, "0") != 0;
+}
+static inline void cli_detach(void) {
+  const char* d = getenv("BEDGPU_DETACH");
+  if ((d && !strcmp(d, "0")) || cli_env_on("BEDGPU_FULL_EXIT")) return;
+  int p[2];
+  if (pipe(p) != 0) return;
+  fflush(stdout);
+  fflush(stderr);
+  const pid_t pid = fork();
+  if (pid < 0) {
+    close(p[0]);
+    close(p[1]);
+    return;
+  }
+  if (pid == 0) { /* the worker */
+    close(p[0]);
+    CLI_DETACH_FD = p[1];
+    return;
+  }
+  close(p[1]);
+  close(0); /* stdin belongs to the worker ('-' inputs) */
+  unsigned char st = 0;
+  ssize_t r;
+  do r = read(p[0], &st, 1); while (r < 0 && errno == EINTR);
+  if (r == 1) _exit(st);
+  int ws = 0;
+  while (waitpid(pid, &ws, 0) < 0)
+    if (errno != EINTR) _exit(EXIT_FAILURE);
+  if (WIFEXITED(ws)) _exit(WEXITSTATUS(ws));
+  if (WIFSIGNALED(ws)) {
+    signal(WTERMSIG(ws), SIG_DFL);
+    raise(WTERMSIG(ws));
+  }
+  _exit(EXIT_FAILURE);
+}
+
 /* after the output is written: leave without tearing down the device state (freeing
  * every HBM block, the pinned ring and the HIP runtime costs ~0.3 s; the kernel driver
  * reclaims a process's GPU resources at exit). Output went through write(2) only. */
@@ -412,8 +463,14 @@ static inline void fast_exit(void) {
   fflush(stderr);
   cli_mark("exit");
   /* BEDGPU_FULL_EXIT=1: tear down normally (profilers write their traces at exit) */
-  const char* f = getenv("BEDGPU_FULL_EXIT");
-  if (f && *f && strcmp(f, "0") != 0) return;
+  if (cli_env_on("BEDGPU_FULL_EXIT")) return;
+  if (CLI_DETACH_FD >= 0) { /* output complete: release the front process (cli_detach) */
+    close(1);
+    close(2);
+    const unsigned char ok = EXIT_SUCCESS;
+    ssize_t r;
+    do r = write(CLI_DETACH_FD, &ok, 1); while (r < 0 && errno == EINTR);
+  }
   _exit(EXIT_SUCCESS);
 }
 

@@ -107,6 +107,7 @@ int main(int argc, char** argv) {
 
   /* BEDGPU_DEVICES=0,1,...: chromosome shards on several GPUs (cli_shard.h); one GPU:
    * chromosome groups in a pipeline (cli_stream.h) */
+  cli_detach(); /* the GPU work runs in a worker whose teardown the caller does not wait for */
   const int chrom_local = !check && !ec && !chrom && strcmp(argv[a], "-") && strcmp(argv[a + 1], "-");
   bg_input sin[2];
   memset(sin, 0, sizeof(sin));

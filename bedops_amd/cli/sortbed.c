@@ -144,6 +144,7 @@ int main(int argc, char** argv) {
       return EXIT_FAILURE;
     }
   bg_ctx* ctx = NULL;
+  cli_detach(); /* the GPU work runs in a worker whose teardown the caller does not wait for */
   if (bg_open(&ctx, env_device())) {
     fprintf(stderr, "cannot open the GPU device (libbedgpu/HIP)\n");
     return EXIT_FAILURE;

@@ -158,3 +158,25 @@ def test_closest_groups_equal_oracle(gpu_bin, oracle_bin, tmp_path, opts):
         assert rc == 0, err
         assert got == want, (opts, groups)
         assert _streamed(err), err
+
+
+def test_detached_teardown_status_and_output(gpu_bin, oracle_bin, tmp_path):
+    """cli_detach: the front process returns once the worker's output is complete, with the
+    worker's status; stdout/stderr pipes see EOF; failures are mirrored"""
+    rng = random.Random(8)
+    a = randbed.write(str(tmp_path / "a.bed"), randbed.text(randbed.rows(rng, 5000, chroms=CHROMS)))
+    b = randbed.write(str(tmp_path / "b.bed"), randbed.text(randbed.rows(rng, 5000, chroms=CHROMS)))
+    want = subprocess.run([oracle_bin["bedops"], "-u", a, b], stdout=subprocess.PIPE, check=True).stdout
+    for det in ("1", "0"):
+        env = dict(os.environ, BEDGPU_DETACH=det)
+        r = subprocess.run([gpu_bin["bedops"], "-u", a, b], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           env=env, timeout=120)
+        assert r.returncode == 0 and r.stdout == want, r.stderr
+        with open(a, "rb") as fi:  # stdin read by the worker
+            r = subprocess.run([gpu_bin["bedops"], "-u", "-", b], stdin=fi, stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE, env=env, timeout=120)
+        assert r.returncode == 0 and r.stdout == want, r.stderr
+        bad = randbed.write(str(tmp_path / "bad.bed"), "chr1\t5\t1\n")
+        r = subprocess.run([gpu_bin["bedops"], "-u", bad, b], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           env=env, timeout=120)
+        assert r.returncode == 1 and b"Error" in r.stderr and r.stdout == b""
