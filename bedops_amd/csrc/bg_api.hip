@@ -195,6 +195,8 @@ extern "C" void bg_close(bg_ctx* c) {
     if (e) hipEventDestroy(e);
   for (auto p : c->ring)
     if (p) hipHostFree(p);
+  if (c->cjoin) hipEventDestroy(c->cjoin);
+  if (c->cstream) hipStreamDestroy(c->cstream);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -378,6 +380,7 @@ static double now_ms() {
 }
 // pins the ring's slots, one thread each (bg_open runs this on a thread of its own, so the
 // pinning overlaps whatever the caller does next)
+static int copy_streams();
 static int ring_alloc(bg_ctx* c) {
   const double t0 = now_ms();
   std::vector<char*> ring(BG_RING_SLOTS + BG_WR_SLOTS, nullptr);
@@ -402,6 +405,11 @@ static int ring_alloc(bg_ctx* c) {
   }
   c->ring = ring;
   c->ring_ev = ev;
+  if (copy_streams() == 2 && (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
+                              hipEventCreateWithFlags(&c->cjoin, hipEventDisableTiming) != hipSuccess)) {
+    (void)hipGetLastError();
+    c->cstream = nullptr;  // one copy stream
+  }
   if (c->stats)
     fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", BG_RING_SLOTS + BG_WR_SLOTS,
             (unsigned long long)(BG_RING_CH >> 20), now_ms() - t0);
@@ -433,6 +441,15 @@ static int ring_threads() {
   }();
   return t;
 }
+// BEDGPU_COPY_STREAMS: 1 or 2 streams carry the ring's H2D copies (2: chunks alternate
+// between ctx's stream and a second one, so two DMA engines pull from the slots)
+static int copy_streams() {
+  static const int v = [] {
+    const char* s = getenv("BEDGPU_COPY_STREAMS");
+    return (s && atoi(s) == 2) ? 2 : 1;
+  }();
+  return v;
+}
 static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   if (!n) return 0;
   int rc = ring_get(c);
@@ -451,9 +468,10 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
       if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = 1; return; }
       const uint64_t off = k * BG_RING_CH, len = std::min<uint64_t>(BG_RING_CH, n - off);
       memcpy(c->ring[sl], src + off, len);
+      hipStream_t cs = (c->cstream && (k & 1)) ? c->cstream : c->stream;
       std::lock_guard<std::mutex> g(mu);
-      if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-          hipEventRecord(c->ring_ev[sl], c->stream) != hipSuccess) {
+      if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipEventRecord(c->ring_ev[sl], cs) != hipSuccess) {
         bad = 1;
         return;
       }
@@ -464,6 +482,9 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
   worker(0);
   for (auto& x : th) x.join();
+  if (c->cstream && nch > 1 &&  // later work on ctx's stream waits for the second stream's copies
+      (hipEventRecord(c->cjoin, c->cstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->cjoin, 0) != hipSuccess))
+    bad = 1;
   if (c->stats) {  // the last copies drained (stats runs only: this waits)
     const double t1 = now_ms();
     hipStreamSynchronize(c->stream);
