@@ -1120,6 +1120,248 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
   }
 }
 
+// ---- k_parse_set with NT-thread workgroups --------------------------------------------
+// The same tile (8 KiB), staging and outputs as k_parse_set, run by NT = 128 threads: each
+// thread stages and classifies 64 tile bytes, and the ~340 lines of a tile (24-byte rows)
+// go in rounds of 128 (3 rounds, 89% of the lanes busy) instead of 256 (2 rounds, 67%).
+// The kernel is VALU-issue bound, so lanes idle in a partial round are time lost.
+template <int NT>
+struct TileRegsN {
+  uint4 v[TT / NT / 16];  // this thread's TT / NT tile bytes
+  uint4 vh;               // halo piece (as TileRegs)
+};
+template <int NT>
+__device__ __forceinline__ void load_tile_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
+                                            TileRegsN<NT>& R) {
+  constexpr int BPT = TT / NT;
+  const int64_t b = t0 + (int64_t)threadIdx.x * BPT;
+#pragma unroll
+  for (int i = 0; i < BPT / 16; ++i) R.v[i] = load16(txt, b + 16 * i, nb);
+  if (threadIdx.x < (HA + 32) / 16) R.vh = load16(txt, t0 + TT + (int64_t)threadIdx.x * 16, nb);
+  else if (threadIdx.x == NT - 1) R.vh = load16(txt, t0 - HB, nb);
+}
+template <int NT>
+__device__ __forceinline__ void store_tile_n(uint8_t* buf, const TileRegsN<NT>& R) {
+  constexpr int BPT = TT / NT;
+#pragma unroll
+  for (int i = 0; i < BPT / 16; ++i) *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * BPT + 16 * i]) = R.v[i];
+  if (threadIdx.x < (HA + 32) / 16) *reinterpret_cast<uint4*>(&buf[HB + TT + threadIdx.x * 16]) = R.vh;
+  else if (threadIdx.x == NT - 1) *reinterpret_cast<uint4*>(&buf[0]) = R.vh;
+}
+// tile_line_starts for TT / NT bytes per thread (G 32-byte groups, lines in byte order)
+template <int NT>
+__device__ __forceinline__ uint32_t tile_line_starts_n(const TileRegsN<NT>& R, const uint8_t* buf, int64_t t0,
+                                                       uint16_t* ls, uint32_t cap, uint32_t* shs, bool& has0) {
+  constexpr int G = TT / NT / 32;
+  has0 = (t0 == 0) || buf[HB - 1] == '\n';
+  uint32_t nlg[G];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= bgp_group4(nl_mask4(w[k])) << (4 * k);
+    if (g == G - 1 && threadIdx.x == NT - 1) m &= 0x7FFFFFFFu;  // starts a line in the next tile
+    nlg[g] = m;
+    cnt += (uint32_t)__popc(m);
+  }
+  const uint32_t inc = wave_incl_scan(cnt, OpSum());
+  if (bg_lane() == 63) shs[bg_wave()] = inc;
+  __syncthreads();
+  uint32_t tot = 0, wpre = 0;
+#pragma unroll
+  for (int q = 0; q < NT / 64; ++q) {
+    const uint32_t x = shs[q];
+    if (q < bg_wave()) wpre += x;
+    tot += x;
+  }
+  uint32_t o = wpre + inc - cnt + (has0 ? 1u : 0u);
+  if (threadIdx.x == 0 && has0) ls[0] = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    for (uint32_t m = nlg[g]; m; m &= m - 1) {
+      if (o < cap) ls[o] = (uint16_t)(threadIdx.x * (TT / NT) + 32 * g + bgp_ctz(m) + 1);
+      ++o;
+    }
+  __syncthreads();
+  return tot + (has0 ? 1u : 0u);
+}
+template <int NT>
+__device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
+                                                    ParseLdsT<1>& S, const TileRegsN<NT>& R, int64_t& last_end,
+                                                    bg_dstatus* st) {
+  ParseBuf& B = S.b[0];
+  clear_halo(B);
+  store_tile_n<NT>(B.buf, R);
+  __syncthreads();
+  constexpr int G = TT / NT / 32;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {  // classify this thread's bytes once (SWAR), publish the masks
+    const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
+    const uint32_t W[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t ws, dg;
+    bgp_classify8(W, ws, dg);
+    B.wsm[threadIdx.x * G + g] = ws;
+    B.dgm[threadIdx.x * G + g] = dg;
+  }
+  {  // the halo after the tile (as prologue_core)
+    constexpr uint32_t HD = (HA + 32) / 4;
+    static_assert(HD <= NT, "halo dwords per thread");
+    if (threadIdx.x < HD) {
+      const uint32_t x = reinterpret_cast<const uint32_t*>(&B.buf[HB + TT])[threadIdx.x];
+      uint32_t w4, d4;
+      bgp_classify(x, w4, d4);
+      const uint32_t sh = 4 * (threadIdx.x & 7);
+      if (w4) atomicOr(&B.wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
+      if (d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
+      const uint32_t m = nl_mask4(x);
+      if (m) atomicMin(&B.hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
+    }
+  }
+  bool has0;
+  const uint32_t L = tile_line_starts_n<NT>(R, B.buf, t0, S.lst, LCAP + 1, S.shs, has0);
+  if (L > LCAP) {
+    if (threadIdx.x == 0) bg_report(st, 0, ERR_PARSE);
+    return L;
+  }
+  TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
+  last_end = L == 0 ? -1
+             : (B.buf[HB + TT - 1] == '\n') ? t0 + TT - 1
+             : (B.hnl != ~0u ? t0 + B.hnl : find_nl(T, t0 + TT + HA + 32));
+  return L;
+}
+
+template <int NT>
+struct SetLdsN {
+  uint64_t xe[2][NT / 64], xk[2][NT / 64];
+  uint32_t xc[2][NT / 64];
+  uint64_t klast[2];
+};
+
+// set_rounds with NT lines per round
+template <int NT, typename V>
+__device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* lst, const TileText& T,
+                                             const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
+                                             uint32_t L, int64_t last_end, int64_t gbase,
+                                             uint64_t base, int64_t* __restrict__ LCS,
+                                             int64_t* __restrict__ LCE, SetLdsN<NT>& X, uint64_t& nc,
+                                             V& carry_e, bg_dstatus* st) {
+  constexpr bool NARROW = sizeof(V) == 4;
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t lt = (1ULL << lane) - 1;
+  V carry_k = 0;
+  const uint32_t rounds = (L + NT - 1) / NT;
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t k = j * NT + threadIdx.x;
+    int64_t ks = 0, ke = 0;
+    const bool valid = k < L && set_row(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
+    V K = 0, E = 0;
+    if (valid) {
+      if (NARROW) {
+        const uint64_t ce = (uint64_t)(ke & BG_COORD_MASK) + 1;
+        if (ce >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
+        K = (V)((uint64_t)(ks & BG_COORD_MASK) + 1);
+        E = (V)ce;
+      } else {
+        K = (V)ks + 1;
+        E = (V)ke + 1;
+      }
+    }
+    const V ie = wave_incl_max_v(E);
+    const V pk = wave_shr1_v(K);
+    const int p = j & 1;
+    if (lane == 63) { X.xe[p][w] = ie; X.xk[p][w] = K; }
+    __syncthreads();
+    V pe = carry_e, te = carry_e;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) {
+      const V x = (V)X.xe[p][q];
+      if (q < w) pe = max(pe, x);
+      te = max(te, x);
+    }
+    const V prevK = lane ? pk : (w ? (V)X.xk[p][w - 1] : carry_k);
+    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
+    const V ex_e = max(pe, wave_shr1_v(ie));
+    const bool open = valid && K > ex_e;
+    const uint64_t bal = __ballot(open);
+    if (lane == 0) X.xc[p][w] = (uint32_t)__popcll(bal);
+    if (k + 2 >= L && k < L) X.klast[L - 1 - k] = K;
+    __syncthreads();
+    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) {
+      if (q < w) pos += X.xc[p][q];
+      tot += X.xc[p][q];
+    }
+    if (open && pos < SCAP) {
+      LCS[base + pos] = ks;
+      if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);
+    }
+    carry_e = te;
+    carry_k = (V)X.xk[p][NT / 64 - 1];
+    nc += tot;
+  }
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) BG_SET_WAVES k_parse_set_n(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+  __shared__ ParseLdsT<1> S;
+  __shared__ SetLdsN<NT> X;
+  const uint32_t tile = blockIdx.x;
+  const int64_t t0 = (int64_t)tile * TT;
+  const uint64_t base = (uint64_t)tile * SCAP;
+  if (threadIdx.x == 0) X.klast[0] = X.klast[1] = 0;
+  int64_t last_end = -1;
+  uint32_t L;
+  {
+    TileRegsN<NT> TR;
+    load_tile_n<NT>(txt, nb, t0, TR);
+    L = tile_prologue_n<NT>(txt, nb, t0, S, TR, last_end, st);
+  }
+  if (L > LCAP) {
+    if (threadIdx.x == 0) {
+      TS.tmax[tile] = TS.tlast[tile] = LLONG_MIN;
+      TS.base[tile] = base;
+      TS.nloc[tile] = 0;
+      TS.nrow[tile] = 0;
+    }
+    return;
+  }
+  const ParseBuf& B = S.b[0];
+  const uint32_t rl = runlo[tile], rh = runhi[tile];
+  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
+  uint64_t nc = 0;
+  uint64_t cmax = 0;
+  int64_t gbase = 0;
+  if (rl == rh) {
+    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
+    uint32_t ce = 0;
+    set_rounds_n<NT, uint32_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
+    cmax = ce;
+  } else {
+    set_rounds_n<NT, uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (nc > SCAP) {
+      atomicOr(&st->flags, BG_SET_OVERFLOW);
+      nc = 0;
+    }
+    if (nc > 0) LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
+    const uint64_t kmax = X.klast[0] ? X.klast[0] : X.klast[1];
+    TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
+    TS.base[tile] = base;
+    TS.nloc[tile] = nc;
+    TS.nrow[tile] = L - ((L > 0 && last_end < 0) ? 1 : 0);
+  }
+}
+
 // per tile: sort check against the nearest earlier tile with rows (every tile is sorted
 // inside, or has reported it), how many local components the running max M of the
 // earlier tiles absorbs (mex = exclusive prefix max of tmax; the local starts increase,
@@ -1483,8 +1725,16 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
       !S.tcnt || !S.absorbed || !S.cnt)
     return BG_E_NOMEM;
   SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt};
-  BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-            S.lcs, S.lce, TS, st);
+  static const int set_nt = [] {  // BEDGPU_SET_NT=256: the 256-thread kernel (A/B)
+    const char* e = getenv("BEDGPU_SET_NT");
+    return (e && atoi(e) == 256) ? 256 : 128;
+  }();
+  if (set_nt == 128)
+    BG_LAUNCH(c, "k_parse_set", k_parse_set_n<128>, dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st);
+  else
+    BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st);
   BG_HIP(c, hipGetLastError());
   if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
   BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, BG_NT)), dim3(BG_NT), S.lcs, TS,
