@@ -1305,8 +1305,9 @@ __device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* 
   }
 }
 
+// (LDS holds 11 of these workgroups per CU: 5-6 waves per SIMD)
 template <int NT>
-__global__ void __launch_bounds__(NT) BG_SET_WAVES k_parse_set_n(
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_set_n(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
