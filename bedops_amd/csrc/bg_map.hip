@@ -478,44 +478,102 @@ __device__ __forceinline__ double readlane_f64(double v, int j) {
 }
 
 // one wavefront folds the whole event stream in order: SA[k] = sum_ after event k
-// (QA: squareSum_); `s += x` with x = -score for a Delete is exactly `sum_ -= score`
+// (QA: squareSum_); `s += x` with x = -score for a Delete is exactly `sum_ -= score`.
+// The fold is a chain of dependent FP64 adds, so nothing else may sit on it: blocks of
+// MC_BLK events are staged in LDS by all 64 lanes (coalesced loads issued one block AHEAD,
+// in flight while the chain runs), lane 0 alone walks the block (an LDS read that does not
+// depend on the sum, the add, an LDS write of the partial sum), and the partial sums go
+// back to HBM coalesced. (Round 2 broadcast each event with two v_readlane and captured
+// the sum with a lane select: five VALU ops per event around the add, 4 ns per event.)
+#define MC_BLK 1024
+#define MC_G 32  // values lane 0 holds in registers per half-step of the chain
+// lane 0's fold of one staged block: the values of the next MC_G events are read from LDS
+// into registers before the adds of the current MC_G (two register sets, no copies)
+template <bool SQ>
+__device__ __forceinline__ void mev_fold(const double* xs, const double* ys, double* ss, double* qs,
+                                         double& s, double& q) {
+  double a[MC_G], b[MC_G], ay[MC_G], by[MC_G];
+#pragma unroll
+  for (int j = 0; j < MC_G; ++j) {
+    a[j] = xs[j];
+    if (SQ) ay[j] = ys[j];
+  }
+  for (int g = 0; g < MC_BLK; g += 2 * MC_G) {
+#pragma unroll
+    for (int j = 0; j < MC_G; ++j) {
+      b[j] = xs[g + MC_G + j];
+      if (SQ) by[j] = ys[g + MC_G + j];
+    }
+#pragma unroll
+    for (int j = 0; j < MC_G; ++j) {
+      s += a[j];
+      ss[g + j] = s;
+      if (SQ) {
+        q += ay[j];
+        qs[g + j] = q;
+      }
+    }
+    if (g + 2 * MC_G < MC_BLK) {
+#pragma unroll
+      for (int j = 0; j < MC_G; ++j) {
+        a[j] = xs[g + 2 * MC_G + j];
+        if (SQ) ay[j] = ys[g + 2 * MC_G + j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MC_G; ++j) {
+      s += b[j];
+      ss[g + MC_G + j] = s;
+      if (SQ) {
+        q += by[j];
+        qs[g + MC_G + j] = q;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(64) k_mev_chain(const double* __restrict__ X,
                                                   const double* __restrict__ X2, uint64_t E,
                                                   double* __restrict__ SA, double* __restrict__ QA) {
+  __shared__ double xs[MC_BLK], ys[MC_BLK], ss[MC_BLK], qs[MC_BLK];
+  constexpr int PER = MC_BLK / 64;
   const int lane = threadIdx.x;
-  double s = 0.0, q = 0.0;
-  for (uint64_t b = 0; b < E; b += 64) {
-    const uint64_t k = b + lane;
-    const double x = k < E ? X[k] : 0.0;
-    const double x2 = (X2 && k < E) ? X2[k] : 0.0;
-    double ms = 0.0, mq = 0.0;
-    if (b + 64 <= E) {
-      if (X2) {
+  const bool sq = X2 != nullptr;
+  double s = 0.0, q = 0.0;  // lane 0's running sums
+  double px[PER], py[PER];
+  auto fetch = [&](uint64_t b) {
 #pragma unroll
-        for (int j = 0; j < 64; ++j) {
-          s += readlane_f64(x, j);
-          q += readlane_f64(x2, j);
-          if (lane == j) { ms = s; mq = q; }
-        }
-      } else {
+    for (int i = 0; i < PER; ++i) {
+      const uint64_t k = b + (uint64_t)i * 64 + lane;
+      px[i] = k < E ? X[k] : 0.0;
+      py[i] = (sq && k < E) ? X2[k] : 0.0;
+    }
+  };
+  fetch(0);
+  for (uint64_t b = 0; b < E; b += MC_BLK) {
 #pragma unroll
-        for (int j = 0; j < 64; ++j) {
-          s += readlane_f64(x, j);
-          if (lane == j) ms = s;
-        }
-      }
-    } else {
-      const int nb = (int)(E - b);
-      for (int j = 0; j < nb; ++j) {
-        s += readlane_f64(x, j);
-        if (X2) q += readlane_f64(x2, j);
-        if (lane == j) { ms = s; mq = q; }
+    for (int i = 0; i < PER; ++i) {
+      xs[i * 64 + lane] = px[i];
+      ys[i * 64 + lane] = py[i];
+    }
+    __syncthreads();
+    if (b + MC_BLK < E) fetch(b + MC_BLK);  // the next block in flight during the fold
+    // the last block is padded with +0.0 events: they only follow every real event, and
+    // the sums after them are never stored
+    if (lane == 0) {
+      if (sq) mev_fold<true>(xs, ys, ss, qs, s, q);
+      else mev_fold<false>(xs, ys, ss, qs, s, q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const uint64_t k = b + (uint64_t)i * 64 + lane;
+      if (k < E) {
+        SA[k] = ss[i * 64 + lane];
+        if (QA) QA[k] = qs[i * 64 + lane];
       }
     }
-    if (k < E) {
-      SA[k] = ms;
-      if (QA) QA[k] = mq;
-    }
+    __syncthreads();  // the next block's staging overwrites xs/ss
   }
 }
 
