@@ -176,7 +176,9 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
       in[f].on_device = 1;
     }
     bg_set* set = NULL;
+    if (!rc) cli_mark("  copies");
     if (!rc) rc = bg_load(ctx, nf, in, &set);
+    if (!rc) cli_mark("  load");
     if (!rc) rc = op(oparg, ctx, set, &res[g]);
     uint64_t n = 0;
     const char* t = NULL;

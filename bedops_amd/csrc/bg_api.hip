@@ -48,7 +48,13 @@ void* bg_alloc(bg_ctx* c, size_t bytes) {
     got = c->free_list[best].bytes;
     c->free_list.erase(c->free_list.begin() + best);
   } else {
-    if (hipMalloc(&p, bytes) != hipSuccess) {
+    const auto ta = std::chrono::steady_clock::now();
+    const hipError_t me = hipMalloc(&p, bytes);
+    if (c->stats) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+      if (ms > 2.0) fprintf(stderr, "bedgpu alloc %.1f MB took %.1f ms\n", bytes / 1e6, ms);
+    }
+    if (me != hipSuccess) {
       (void)hipGetLastError();
       // drop the cache and retry once
       hipStreamSynchronize(c->stream);
