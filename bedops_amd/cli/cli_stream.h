@@ -97,15 +97,19 @@ static void* stream_plan_run(void* unused) {
   for (int f = 0; f < nf; ++f)
     for (int k = 0; k < SP.runs[f].n; ++k)
       bytes[sh_gindex(gn, ngc, SP.runs[f].r[k].name)] += SP.runs[f].r[k].b - SP.runs[f].r[k].a;
-  /* consecutive chromosomes, a group closed once it holds total / G bytes */
+  /* consecutive chromosomes, a group closed once it holds total / G bytes; the first group
+   * only total / (G * BEDGPU_STREAM_FIRST) (default 4), so the output queue starts early
+   * and the fixed costs of the first copies are paid on little data */
   int* first = (int*)calloc((size_t)ngc + 1, sizeof(int)); /* group -> first chromosome */
   int ng = 0;
   uint64_t acc = 0;
   const uint64_t target = total / (uint64_t)G;
+  const long F = stream_env("BEDGPU_STREAM_FIRST", 4);
+  const uint64_t target0 = target / (uint64_t)(F < 1 ? 1 : F);
   for (int g = 0; g < ngc; ++g) {
     if (acc == 0) first[ng++] = g;
     acc += bytes[g];
-    if (acc >= target) acc = 0;
+    if (acc >= (ng == 1 ? target0 : target)) acc = 0;
   }
   first[ng] = ngc;
   if (ng >= 2) {

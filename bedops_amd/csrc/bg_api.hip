@@ -169,7 +169,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
     return BG_E_HIP;
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess ||
+      hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess || hipMalloc(&c->warm, 256) != hipSuccess ||
       hipHostMalloc(&c->hstat, sizeof(bg_dstatus), hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     delete c;
@@ -195,6 +195,7 @@ extern "C" void bg_close(bg_ctx* c) {
   for (auto& p : c->prof_pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
   for (auto e : c->prof_events) hipEventDestroy(e);
   hipFree(c->dstat);
+  hipFree(c->warm);
   hipHostFree(c->hstat);
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
   for (auto e : c->ring_ev)
@@ -380,7 +381,16 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
 // driver's own.
 #define BG_RING_SLOTS 16
 #define BG_WR_SLOTS 8  // after the ring's slots: the output queue's (bg_writer)
-#define BG_RING_CH (4ull << 20)
+// slot bytes: BEDGPU_RING_MB (1..16, default 2); pinning cost grows with the slot size
+static uint64_t ring_ch() {
+  static const uint64_t v = [] {
+    const char* s = getenv("BEDGPU_RING_MB");
+    const long m = s ? atol(s) : 2;
+    return (uint64_t)(m < 1 ? 1 : (m > 16 ? 16 : m)) << 20;
+  }();
+  return v;
+}
+#define BG_RING_CH ring_ch()
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -393,12 +403,22 @@ static int ring_alloc(bg_ctx* c) {
   std::vector<hipEvent_t> ev(BG_RING_SLOTS + BG_WR_SLOTS, nullptr);
   std::atomic<int> bad{0};
   std::vector<std::thread> th;
+  static const bool warm = [] {  // BEDGPU_RING_WARM=0: no warm-up copy
+    const char* s = getenv("BEDGPU_RING_WARM");
+    return !(s && strcmp(s, "0") == 0);
+  }();
   for (int k = 0; k < BG_RING_SLOTS + BG_WR_SLOTS; ++k)
     th.emplace_back([&, k]() {
       if (hipSetDevice(c->device) != hipSuccess ||
           hipHostMalloc((void**)&ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
-          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess)
+          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
         bad = 1;
+        return;
+      }
+      // the runtime's first host->device copy on the stream costs ~15 ms more than the
+      // next ones (measured): take it here, while the other slots are being pinned
+      if (k == 0 && warm && c->warm)
+        (void)hipMemcpyAsync(c->warm, ring[0], 256, hipMemcpyHostToDevice, c->stream);
     });
   for (auto& x : th) x.join();
   if (bad) {
@@ -417,7 +437,7 @@ static int ring_alloc(bg_ctx* c) {
     c->cstream = nullptr;  // one copy stream
   }
   if (c->stats)
-    fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", BG_RING_SLOTS + BG_WR_SLOTS,
+    fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", (int)(BG_RING_SLOTS + BG_WR_SLOTS),
             (unsigned long long)(BG_RING_CH >> 20), now_ms() - t0);
   return 0;
 }

@@ -77,6 +77,7 @@ struct bg_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
+  void* warm = nullptr;         // device scratch of the ring's warm-up copy
   bg_dstatus* hstat = nullptr;  // pinned host mirror
   // caching allocator: free blocks by size; live blocks -> their size (per context, so
   // contexts on different devices can be driven from different host threads)
