@@ -486,14 +486,22 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   const int per = BG_RING_SLOTS / TT_;  // slots per thread
   std::mutex mu;
   std::atomic<int> bad{0};
+  std::atomic<int64_t> t_wait{0}, t_copy{0};  // stats: ns in event waits / memcpy, all threads
   auto worker = [&](int t) {
     if (hipSetDevice(c->device) != hipSuccess) { bad = 1; return; }
     uint64_t j = 0;
     for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T, ++j) {
       const int sl = t * per + (int)(j % per);
+      const auto a0 = std::chrono::steady_clock::now();
       if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = 1; return; }
       const uint64_t off = k * BG_RING_CH, len = std::min<uint64_t>(BG_RING_CH, n - off);
+      const auto a1 = std::chrono::steady_clock::now();
       memcpy(c->ring[sl], src + off, len);
+      if (c->stats) {
+        const auto a2 = std::chrono::steady_clock::now();
+        t_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(a1 - a0).count();
+        t_copy += std::chrono::duration_cast<std::chrono::nanoseconds>(a2 - a1).count();
+      }
       hipStream_t cs = (c->cstream && (k & 1)) ? c->cstream : c->stream;
       std::lock_guard<std::mutex> g(mu);
       if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, cs) != hipSuccess ||
@@ -506,6 +514,7 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   const double t0 = now_ms();
   std::vector<std::thread> th;
   for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
+  const double t_spawn = now_ms();
   worker(0);
   for (auto& x : th) x.join();
   if (c->cstream && nch > 1 &&  // later work on ctx's stream waits for the second stream's copies
@@ -514,8 +523,8 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   if (c->stats) {  // the last copies drained (stats runs only: this waits)
     const double t1 = now_ms();
     hipStreamSynchronize(c->stream);
-    fprintf(stderr, "bedgpu ring   %.1f MB: copies issued %.3f ms, drained %.3f ms\n", n / 1e6, t1 - t0,
-            now_ms() - t0);
+    fprintf(stderr, "bedgpu ring   %.1f MB: copies issued %.3f ms, drained %.3f ms (threads: %.1f ms waiting, %.1f ms copying; spawn %.3f ms)\n",
+            n / 1e6, t1 - t0, now_ms() - t0, t_wait / 1e6, t_copy / 1e6, t_spawn - t0);
   }
   return bad ? bg_fail(c, BG_E_HIP, "staging ring copy") : 0;
 }
