@@ -476,6 +476,23 @@ static int copy_streams() {
   }();
   return v;
 }
+static int copy_kernel() {
+  static const int v = [] {
+    const char* s = getenv("BEDGPU_COPY_KERNEL");
+    return s ? atoi(s) : 0;
+  }();
+  return v;
+}
+// one chunk of pinned host memory -> device, read by the CUs over the link (16-byte loads;
+// len and both pointers are 16-byte aligned except the chunk's tail)
+__global__ void k_pull(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len) {
+  const uint64_t n16 = len / 16;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  const uint64_t t = n16 * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < len && blockIdx.x == 0) dst[t] = src[t];
+}
 static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   if (!n) return 0;
   int rc = ring_get(c);
@@ -503,8 +520,16 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
         t_copy += std::chrono::duration_cast<std::chrono::nanoseconds>(a2 - a1).count();
       }
       hipStream_t cs = (c->cstream && (k & 1)) ? c->cstream : c->stream;
+      // BEDGPU_COPY_KERNEL: 1 = every chunk pulled by a kernel reading the pinned slot over
+      // the link, 2 = chunks on the second stream by kernel, the others by the DMA engine
+      const int ck = copy_kernel();
+      const bool by_kernel = ck == 1 || (ck == 2 && cs != c->stream);
       std::lock_guard<std::mutex> g(mu);
-      if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, cs) != hipSuccess ||
+      if (by_kernel) {
+        const unsigned nb = (unsigned)std::min<uint64_t>(1024, (len + 16 * 256 - 1) / (16 * 256));
+        hipLaunchKernelGGL(k_pull, dim3(nb), dim3(256), 0, cs, (uint8_t*)(dst + off), (const uint8_t*)c->ring[sl], len);
+      }
+      if ((!by_kernel && hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, cs) != hipSuccess) ||
           hipEventRecord(c->ring_ev[sl], cs) != hipSuccess) {
         bad = 1;
         return;
