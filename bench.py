@@ -255,6 +255,11 @@ def e2e_cli(W, paths, rows, td, runs=3, devices=None):
         env["BEDGPU_DEVICES"] = devices
     times, logs = [], []
     for i in range(runs):
+        # runs start 0.5 s apart: the drop-in returns once its output is written and its GPU
+        # worker tears down detached (bedops_amd/cli/cli_common.h cli_detach, 60-100 ms in the
+        # kernel driver); a run started inside that window would pay for it in HIP init
+        if i:
+            time.sleep(0.5)
         with open(out, "wb") as fo:
             t0 = time.perf_counter()
             r = subprocess.run([exe, *args, *paths], stdout=fo, stderr=subprocess.PIPE, env=env)
