@@ -397,6 +397,15 @@ static double now_ms() {
 // pins the ring's slots, one thread each (bg_open runs this on a thread of its own, so the
 // pinning overlaps whatever the caller does next)
 static int copy_streams();
+// BEDGPU_EVENT_BLOCK=1: slot events wait by sleeping (hipEventBlockingSync) instead of
+// polling, leaving the CPU quota to the threads that copy
+static bool event_block() {
+  static const bool v = [] {
+    const char* s = getenv("BEDGPU_EVENT_BLOCK");
+    return s && strcmp(s, "1") == 0;
+  }();
+  return v;
+}
 static int ring_alloc(bg_ctx* c) {
   const double t0 = now_ms();
   std::vector<char*> ring(BG_RING_SLOTS + BG_WR_SLOTS, nullptr);
@@ -411,7 +420,8 @@ static int ring_alloc(bg_ctx* c) {
     th.emplace_back([&, k]() {
       if (hipSetDevice(c->device) != hipSuccess ||
           hipHostMalloc((void**)&ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
-          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming | (event_block() ? hipEventBlockingSync : 0)) !=
+              hipSuccess) {
         bad = 1;
         return;
       }
