@@ -397,12 +397,13 @@ static double now_ms() {
 // pins the ring's slots, one thread each (bg_open runs this on a thread of its own, so the
 // pinning overlaps whatever the caller does next)
 static int copy_streams();
-// BEDGPU_EVENT_BLOCK=1: slot events wait by sleeping (hipEventBlockingSync) instead of
-// polling, leaving the CPU quota to the threads that copy
+// slot events wait by sleeping (hipEventBlockingSync) instead of polling, leaving the
+// box's CPU quota (16 CPUs) to the copying threads and the output writer; the copies are
+// DMA-bound either way (profiles/r03_e2e/var_i5_summary.txt). BEDGPU_EVENT_BLOCK=0: poll
 static bool event_block() {
   static const bool v = [] {
     const char* s = getenv("BEDGPU_EVENT_BLOCK");
-    return s && strcmp(s, "1") == 0;
+    return !(s && strcmp(s, "0") == 0);
   }();
   return v;
 }
@@ -468,11 +469,12 @@ static int ring_get(bg_ctx* c) {
 // host -> device through the ring: T threads copy chunks of `src` into their slots (CPU
 // memcpy from cached pages) and queue the slot's DMA on ctx's stream, reusing a slot once its
 // event says the previous DMA out of it has completed
-// (BEDGPU_RING_THREADS: 1..32, default 16)
+// (BEDGPU_RING_THREADS: 1..16, default 8: the copies are DMA-bound, threads wait ~80% of
+// the time with 16)
 static int ring_threads() {
   static const int t = [] {
     const char* s = getenv("BEDGPU_RING_THREADS");
-    const int v = s ? atoi(s) : 16;
+    const int v = s ? atoi(s) : 8;
     return v < 1 ? 1 : (v > BG_RING_SLOTS ? BG_RING_SLOTS : v);
   }();
   return t;

@@ -22,6 +22,7 @@ fi
 for V in ${VARIANTS:-"default:"}; do
   lab=${V%%:*}; envs=${V#*:}; envs=${envs//,/ }
   for k in 1 2 3; do
+    sleep 0.5  # as bench.py: a detached worker's driver teardown is not charged to the next run
     env $envs BEDGPU_STATS=1 timeout -k 10 120 python3 tools/e2e_time.py $D/out.bed ./bedops_amd/bin/bedops --intersect $D/A.bed $D/B.bed 2> "$O/${lab}_$k.txt" || { cat "$O/${lab}_$k.txt"; exit 1; }
     echo "$lab $k: $(grep -h '^split' "$O/${lab}_$k.txt") | $(grep -h 'bedgpu host' "$O/${lab}_$k.txt" | awk '{printf "%s%s ", $3, $NF}')" >> "$O/summary.txt"
   done
