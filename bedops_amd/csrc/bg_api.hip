@@ -14,11 +14,16 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
 
 #include "bg_internal.h"
+
+static int ring_threads();
+static void pool_start(bg_ctx* c, int n);
+void bg_pool_stop(bg_ctx* c);
 
 int bg_fail(bg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -169,7 +174,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
     return BG_E_HIP;
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess || hipMalloc(&c->warm, 256) != hipSuccess ||
+      hipMalloc(&c->dstat, sizeof(bg_dstatus)) != hipSuccess || hipMalloc(&c->warm, 16u << 20) != hipSuccess ||
       hipHostMalloc(&c->hstat, sizeof(bg_dstatus), hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     delete c;
@@ -188,6 +193,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
 extern "C" void bg_close(bg_ctx* c) {
   if (!c) return;
   if (c->ring_th.joinable()) c->ring_th.join();
+  bg_pool_stop(c);
   hipStreamSynchronize(c->stream);
   for (auto& b : c->free_list) hipFree(b.p);
   for (auto& kv : c->live) hipFree(kv.first);
@@ -428,8 +434,8 @@ static int ring_alloc(bg_ctx* c) {
       }
       // the runtime's first host->device copy on the stream costs ~15 ms more than the
       // next ones (measured): take it here, while the other slots are being pinned
-      if (k == 0 && warm && c->warm)
-        (void)hipMemcpyAsync(c->warm, ring[0], 256, hipMemcpyHostToDevice, c->stream);
+      if (k == 0 && warm && c->warm)  // a full slot: small copies take another path (blit kernel)
+        (void)hipMemcpyAsync(c->warm, ring[0], BG_RING_CH, hipMemcpyHostToDevice, c->stream);
     });
   for (auto& x : th) x.join();
   if (bad) {
@@ -442,6 +448,7 @@ static int ring_alloc(bg_ctx* c) {
   }
   c->ring = ring;
   c->ring_ev = ev;
+  pool_start(c, ring_threads() - 1);
   if (copy_streams() == 2 && (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
                               hipEventCreateWithFlags(&c->cjoin, hipEventDisableTiming) != hipSuccess)) {
     (void)hipGetLastError();
@@ -505,6 +512,69 @@ __global__ void k_pull(uint8_t* __restrict__ dst, const uint8_t* __restrict__ sr
   const uint64_t t = n16 * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < len && blockIdx.x == 0) dst[t] = src[t];
 }
+// The ring's copy threads: started once with the ring (bg_open's thread), parked on a
+// condition variable between calls. (Spawning them per call cost 4-7 ms the first time:
+// thread stacks mapped while HIP was mapping its own memory.)
+struct bg_pool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable go, done;
+  const std::function<void(int)>* job = nullptr;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+};
+static void pool_start(bg_ctx* c, int n) {
+  bg_pool* P = new bg_pool();
+  c->pool = P;
+  for (int t = 1; t <= n; ++t)
+    P->th.emplace_back([c, P, t]() {
+      (void)hipSetDevice(c->device);
+      uint64_t seen = 0;
+      for (;;) {
+        const std::function<void(int)>* job;
+        {
+          std::unique_lock<std::mutex> g(P->mu);
+          P->go.wait(g, [&] { return P->stop || P->gen != seen; });
+          if (P->stop) return;
+          seen = P->gen;
+          job = P->job;
+        }
+        (*job)(t);
+        std::lock_guard<std::mutex> g(P->mu);
+        if (--P->pending == 0) P->done.notify_all();
+      }
+    });
+}
+static void pool_run(bg_ctx* c, const std::function<void(int)>& job) {
+  bg_pool* P = c->pool;
+  if (!P) {  // no pool (not started): run every share here
+    for (int t = 0; t < 16; ++t) job(t);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(P->mu);
+    P->job = &job;
+    P->pending = (int)P->th.size();
+    ++P->gen;
+  }
+  P->go.notify_all();
+  job(0);
+  std::unique_lock<std::mutex> g(P->mu);
+  P->done.wait(g, [&] { return P->pending == 0; });
+}
+void bg_pool_stop(bg_ctx* c) {
+  bg_pool* P = c->pool;
+  if (!P) return;
+  {
+    std::lock_guard<std::mutex> g(P->mu);
+    P->stop = true;
+  }
+  P->go.notify_all();
+  for (auto& x : P->th) x.join();
+  delete P;
+  c->pool = nullptr;
+}
 static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
   if (!n) return 0;
   int rc = ring_get(c);
@@ -549,11 +619,11 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
     }
   };
   const double t0 = now_ms();
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; ++t) th.emplace_back(worker, t);
+  const std::function<void(int)> job = [&](int t) {
+    if (t < T) worker(t);
+  };
+  pool_run(c, job);  // the pool's threads take t = 1..; this thread t = 0
   const double t_spawn = now_ms();
-  worker(0);
-  for (auto& x : th) x.join();
   if (c->cstream && nch > 1 &&  // later work on ctx's stream waits for the second stream's copies
       (hipEventRecord(c->cjoin, c->cstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->cjoin, 0) != hipSuccess))
     bad = 1;

@@ -72,6 +72,7 @@ struct bg_ctx {
   std::vector<hipEvent_t> ring_ev;
   std::thread ring_th;  // bg_open starts pinning the ring; its first use joins
   int ring_rc = 0;
+  struct bg_pool* pool = nullptr;  // the ring's copy threads (bg_api.hip)
   hipStream_t cstream = nullptr;  // second H2D copy stream of the ring (BEDGPU_COPY_STREAMS=2)
   hipEvent_t cjoin = nullptr;     // its copies -> ctx's stream
   hipStream_t stream = nullptr;
