@@ -21,8 +21,10 @@
  * any group (a malformed or unsorted line, a refusal such as bedmap's file-wide decimal
  * sums), the output written so far is truncated away and the caller runs the whole-file
  * path, which reports exactly what a whole-file run reports (messages, line numbers).
- * BEDGPU_STREAM=0 turns it off; BEDGPU_STREAM_GROUPS (default 8) and BEDGPU_STREAM_MIN
- * (bytes of input below which the whole-file path is used, default 256 MiB) size it.
+ * BEDGPU_STREAM=0 turns it off; BEDGPU_STREAM_GROUPS (default 8), BEDGPU_STREAM_MIN
+ * (bytes of input below which the whole-file path is used, default 256 MiB) and
+ * BEDGPU_STREAM_MAX_GB (largest group, default 16: more groups for larger inputs, which
+ * then need not fit in HBM at once) size it.
  */
 #ifndef BEDOPS_AMD_CLI_STREAM_H
 #define BEDOPS_AMD_CLI_STREAM_H
@@ -81,8 +83,13 @@ static void* stream_plan_run(void* unused) {
     total += SP.fm[f].n;
     nruns += SP.runs[f].n;
   }
-  const long G = stream_env("BEDGPU_STREAM_GROUPS", 8);
+  long G = stream_env("BEDGPU_STREAM_GROUPS", 8);
   if (G < 2 || total < (uint64_t)stream_env("BEDGPU_STREAM_MIN", 256L << 20) || nruns < 2) return NULL;
+  /* out of core: no group above BEDGPU_STREAM_MAX_GB (default 16) of text, so inputs larger
+   * than the GPU's memory stream through it (a group is whole chromosomes: one chromosome
+   * of every input must fit) */
+  const uint64_t gmax = (uint64_t)stream_env("BEDGPU_STREAM_MAX_GB", 16) << 30;
+  if (gmax && total / (uint64_t)G > gmax) G = (long)((total + gmax - 1) / gmax);
   /* the global chromosome list in strcmp order, bytes per chromosome over all inputs */
   char(*gn)[BG_CHR_NAME_CAP] = (char(*)[BG_CHR_NAME_CAP])calloc((size_t)nruns, BG_CHR_NAME_CAP);
   int ngc = 0;
