@@ -196,3 +196,39 @@ def test_tmean_long_segment(eng, oracle_bin):
             want, err, rc = oracle(oracle_bin["bedmap"], argv(ops), [rt, mt], td)
             got, _ = gpu(eng, ops, rt, mt)
             assert got == want, ops
+
+
+def test_many_identical_map_rows_stay_fast(eng, oracle_bin):
+    """8000 map rows with the same coordinates (decimal scores, ids in string order): the
+    running sums replay their set order (start, end, full_rest, address) from the
+    precomputed run order (k_ev_rank) instead of a selection per window, so the step stays
+    within 2x of the same number of distinct rows; output equal to the oracle"""
+    import time
+    rng = random.Random(77)
+    n = 8000
+    ref = [("chr1", s, s + 300) for s in range(0, 6000, 30)]
+    rt = randbed.text(ref).encode()
+
+    def mapping(identical):
+        rows = []
+        for k in range(n):
+            s = 1000 if identical else 1000 + (k % 4000)
+            rows.append(("chr1", s, s + 500))
+        rows.sort(key=lambda r: (r[1], r[2]))
+        return "".join(f"{c}\t{s}\t{e}\tid{k}\t{rng.randint(0, 9999) / 100}\n"
+                       for k, (c, s, e) in enumerate(rows)).encode()
+
+    times = {}
+    with tempfile.TemporaryDirectory() as td:
+        for identical in (False, True):
+            mt = mapping(identical)
+            for ops in (["mean", "sum", "variance", "count"], [("tmean", 0.1, 0.2)]):
+                want, err, rc = oracle(oracle_bin["bedmap"], argv(ops), [rt, mt], td)
+                assert rc == 0, err
+                got, _ = gpu(eng, ops, rt, mt)
+                assert got == want, (identical, ops)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                gpu(eng, ["mean", "sum", "variance", "count"], rt, mt)
+            times[identical] = time.perf_counter() - t0
+    assert times[True] <= 2 * times[False] + 0.05, times
