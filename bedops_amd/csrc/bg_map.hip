@@ -371,17 +371,67 @@ struct EvArgs {
   int mapfields;
   const int64_t* addr;  // simulated heap addresses (bg_heap.hip), null: row order
   const uint32_t* ro;   // each run of equal starts in set order (k_ev_rank), null: select
+  const ulonglong2* P;  // first 16 bytes of each row's full_rest(), big-endian, 0-padded (k_ev_keys)
+  const uint32_t* PL;   // full_rest() length
 };
 
 __device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
   return bg_frest_cmp(A.text, A.rest_off, A.rest_len, A.mapfields, a, b);
 }
+// strcmp order of full_rest(a) and full_rest(b) from the 16-byte prefixes; the byte
+// comparison only when both strings run past the prefix and it ties
+__device__ __forceinline__ int ev_rest_cmp_k(const EvArgs& A, uint64_t a, uint64_t b) {
+  const ulonglong2 x = A.P[a], y = A.P[b];
+  if (x.x != y.x) return x.x < y.x ? -1 : 1;
+  if (x.y != y.y) return x.y < y.y ? -1 : 1;
+  const uint32_t la = A.PL[a], lb = A.PL[b];
+  if (min(la, lb) < 16) return la == lb ? 0 : (la < lb ? -1 : 1);
+  return ev_rest_cmp(A, a, b);
+}
 // CoordRestAddressCompare for two rows of equal start
 __device__ __forceinline__ bool ev_less(const EvArgs& A, uint64_t a, uint64_t b) {
   if (A.ME[a] != A.ME[b]) return A.ME[a] < A.ME[b];
-  const int c = ev_rest_cmp(A, a, b);
+  const int c = A.P ? ev_rest_cmp_k(A, a, b) : ev_rest_cmp(A, a, b);
   if (c != 0) return c < 0;
   return bg_maddr(A.addr, a) < bg_maddr(A.addr, b);
+}
+// first index in (m, b] whose start differs from MS[m] (starts are sorted): a gallop, so a
+// lone row costs one load and a run of g equal starts O(log g)
+__device__ __forceinline__ uint64_t ev_run_hi(const int64_t* MS, uint64_t m, uint64_t b) {
+  const int64_t v = MS[m];
+  uint64_t lo = m + 1;
+  if (lo >= b || MS[lo] != v) return lo;
+  uint64_t step = 1;  // MS[lo] == v
+  while (lo + step < b && MS[lo + step] == v) {
+    lo += step;
+    step <<= 1;
+  }
+  uint64_t hi = min(lo + step, b);  // MS[hi] != v, or hi == b
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (MS[mid] == v) lo = mid;
+    else hi = mid;
+  }
+  return hi;
+}
+// first index f <= m with MS[f..m] all equal to MS[m]
+__device__ __forceinline__ uint64_t ev_run_lo(const int64_t* MS, uint64_t m) {
+  const int64_t v = MS[m];
+  if (m == 0 || MS[m - 1] != v) return m;
+  uint64_t hi = m - 1, step = 1;  // MS[hi] == v
+  while (hi >= step && MS[hi - step] == v) {
+    hi -= step;
+    step <<= 1;
+  }
+  // the run starts in (hi - step, hi]; hi - step may be "before 0"
+  uint64_t lo = hi >= step ? hi - step : 0;  // MS[lo] != v unless lo == 0 and it is equal
+  if (lo == 0 && MS[0] == v) return 0;
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (MS[mid] == v) hi = mid;
+    else lo = mid;
+  }
+  return hi;
 }
 // the rows of [a, b) that satisfy `pred`, in set order (rows are start-sorted: only runs of
 // equal starts need ordering). With A.ro each whole run is visited in its precomputed set
@@ -391,14 +441,13 @@ template <typename Pred, typename Emit>
 __device__ __forceinline__ void ev_walk(const EvArgs& A, uint64_t a, uint64_t b, Pred pred, Emit emit) {
   uint64_t m = a;
   while (m < b) {
-    uint64_t g1 = m + 1;
-    while (g1 < b && A.MS[g1] == A.MS[m]) ++g1;
+    const uint64_t g1 = ev_run_hi(A.MS, m, b);
     if (g1 - m == 1) {
       if (pred(m)) emit(m);
     } else if (A.ro) {
-      uint64_t f0 = m, f1 = g1;  // the whole run (the window may cut it)
-      while (f0 > 0 && A.MS[f0 - 1] == A.MS[m]) --f0;
-      while (f1 < A.nm && A.MS[f1] == A.MS[m]) ++f1;
+      // the whole run (the window may cut it)
+      const uint64_t f0 = m == a ? ev_run_lo(A.MS, m) : m;
+      const uint64_t f1 = g1 == b ? ev_run_hi(A.MS, m, A.nm) : g1;
       for (uint64_t q = f0; q < f1; ++q) {
         const uint64_t t = A.ro[q];
         if (t >= m && t < g1 && pred(t)) emit(t);
@@ -433,13 +482,45 @@ __global__ void __launch_bounds__(BG_NT) k_ev_rank(EvArgs A, uint32_t* __restric
     ro[t] = (uint32_t)t;
     return;
   }
-  uint64_t f0 = t, f1 = t + 1;
-  while (f0 > 0 && A.MS[f0 - 1] == s) --f0;
-  while (f1 < A.nm && A.MS[f1] == s) ++f1;
+  const uint64_t f0 = ev_run_lo(A.MS, t), f1 = ev_run_hi(A.MS, t, A.nm);
   uint64_t r = 0;
-  for (uint64_t u = f0; u < f1; ++u)
-    if (u != t && ev_less(A, u, t)) ++r;
+  // (ME, prefix) decide almost every pair: independent loads, no byte walks
+  const int64_t te = A.ME[t];
+  const ulonglong2 tp = A.P[t];
+#pragma unroll 4
+  for (uint64_t u = f0; u < f1; ++u) {
+    const int64_t ue = A.ME[u];
+    const ulonglong2 up = A.P[u];
+    bool less;
+    if (ue != te) less = ue < te;
+    else if (up.x != tp.x) less = up.x < tp.x;
+    else if (up.y != tp.y) less = up.y < tp.y;
+    else less = u != t && ev_less(A, u, t);
+    r += less ? 1 : 0;
+  }
   ro[f0 + r] = (uint32_t)t;
+}
+
+// A.P / A.PL: the first 16 bytes of every map row's full_rest() (big-endian: integer order =
+// strcmp order of the prefixes; 0-padded) and its length
+__global__ void __launch_bounds__(BG_NT) k_ev_keys(EvArgs A, ulonglong2* __restrict__ P, uint32_t* __restrict__ PL) {
+  const uint64_t t = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (t >= A.nm) return;
+  uint64_t hi = 0, lo = 0;
+  uint32_t len = 0;
+  if (A.rest_off) {
+    const char *p1, *p2;
+    uint32_t l1, l2;
+    bg_frest(A.text, A.rest_off, A.rest_len, A.mapfields, t, p1, l1, p2, l2);
+    len = l1 + l2;
+    for (uint32_t q = 0; q < 16 && q < len; ++q) {
+      const uint64_t b = (uint8_t)(q < l1 ? p1[q] : p2[q - l1]);
+      if (q < 8) hi |= b << (56 - 8 * q);
+      else lo |= b << (56 - 8 * (q - 8));
+    }
+  }
+  P[t] = make_ulonglong2(hi, lo);
+  PL[t] = len;
 }
 
 // the visitor events between reference rows i-1 and i, in the reference's order:
@@ -1223,13 +1304,25 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     E.mapfields = mapfields;
     E.addr = res->maddr;
     E.ro = nullptr;
+    E.P = nullptr;
+    E.PL = nullptr;
     uint32_t* ro = nullptr;
+    ulonglong2* pk = nullptr;
+    uint32_t* pl = nullptr;
     if (M->n && M->n < (1ull << 32)) {  // set order of every run of equal map starts
       ro = (uint32_t*)bg_alloc(c, 4 * M->n);
-      if (!ro) rc = BG_E_NOMEM;
+      pk = (ulonglong2*)bg_alloc(c, 16 * M->n);
+      pl = (uint32_t*)bg_alloc(c, 4 * M->n);
+      if (!ro || !pk || !pl) rc = BG_E_NOMEM;
       else {
-        BG_LAUNCH(c, "k_ev_rank", k_ev_rank, dim3(bg_blocks(M->n, BG_NT)), dim3(BG_NT), E, ro);
+        BG_LAUNCH(c, "k_ev_keys", k_ev_keys, dim3(bg_blocks(M->n, BG_NT)), dim3(BG_NT), E, pk, pl);
         rc = bg_hip_ok(c, hipGetLastError());
+        E.P = pk;
+        E.PL = pl;
+        if (!rc) {
+          BG_LAUNCH(c, "k_ev_rank", k_ev_rank, dim3(bg_blocks(M->n, BG_NT)), dim3(BG_NT), E, ro);
+          rc = bg_hip_ok(c, hipGetLastError());
+        }
         E.ro = ro;
       }
     }
@@ -1240,9 +1333,11 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       else
         rc = map_tmean(c, crit, E, res->cnt, opts, res);
     }
-    if (ro) {
+    if (ro || pk || pl) {
       (void)hipStreamSynchronize(c->stream);
       bg_release(c, ro);
+      bg_release(c, pk);
+      bg_release(c, pl);
     }
   }
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
