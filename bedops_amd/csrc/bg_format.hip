@@ -13,6 +13,7 @@
 // %.{p}lf is rendered exactly: the double's binary value times 10^p is rounded half-to-
 // even in 128-bit integer arithmetic, which is what glibc printf does.
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include "bg_internal.h"
@@ -88,19 +89,6 @@ struct FmtArgs {
   uint64_t* stop_out;
 };
 
-// decimal digits of v: compares only, 32-bit ones when v fits (the common case)
-__device__ __forceinline__ int dec_len_u64(uint64_t v) {
-  if ((v >> 32) == 0) {
-    const uint32_t w = (uint32_t)v;
-    return 1 + (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
-           (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
-  }
-  int l = 10;  // v >= 2^32 > 10^9
-  uint64_t p = 10000000000ull;
-#pragma unroll
-  for (int k = 0; k < 10; ++k, p *= 10) l += v >= p;
-  return l;
-}
 __device__ __forceinline__ int dec_len_i32(int32_t v) {
   return v < 0 ? 1 + dec_len_u64((uint64_t)(-(int64_t)v)) : dec_len_u64((uint64_t)v);
 }
@@ -1022,9 +1010,7 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
 // them (k_fmt_write's general form scans once per row stripe and reloads each row to
 // render it)
 __device__ __forceinline__ uint32_t ivl_len(const FmtArgs& A, int64_t s, int64_t e) {
-  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
-  return A.name_len[g] + 3u + (uint32_t)dec_len_u64((uint64_t)(s & BG_COORD_MASK)) +
-         (uint32_t)dec_len_u64((uint64_t)(e & BG_COORD_MASK));
+  return bg_ivl_len(A.name_len, s, e);
 }
 __device__ __forceinline__ void ivl_put(const FmtArgs& A, char* p, int64_t s, int64_t e) {
   const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
@@ -1082,6 +1068,60 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_ivl_write(FmtArgs A, const uint64
   for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
   for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT)
     *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
+}
+
+// a segmented RES_IVL (bg_result::nseg, straight from k_mp_tile): one workgroup per segment,
+// its byte offset and printed size already scanned (seg_boff), so there is no count pass.
+// The segment's pieces (up to BG_SEG_CAP, ~660 for 100M x 100M --intersect) go in rounds of
+// BG_NT, one per thread (coalesced column loads, every lane busy): each round is placed by
+// one block scan, rendered into LDS and streamed out as in k_fmt_ivl_write. toff[k] (the
+// byte offset of row k * FT_TILE, kept for bg_result_chrom_spans) is written by whichever
+// segment holds that row. (Measured on 100M x 100M --intersect, with k_mp_tile's segmented
+// write 0.35 ms: 0.49 ms, against 0.117 + 0.381 ms for the count and write passes over a
+// contiguous result, plus the 0.2 ms count pass of k_mp_tile this layout removes. Dense
+// 512-row tiles located through per-piece byte prefixes: 0.50-0.55 ms with the prefixes
+// making k_mp_tile 0.38-0.39 ms; four pieces per thread in one 32 KiB round: 0.69 ms; two
+// per thread in rounds of 512: 0.56 ms.)
+__global__ void __launch_bounds__(BG_NT) k_fmt_ivl_seg(FmtArgs A, const uint64_t* __restrict__ seg_off,
+                                                       const uint64_t* __restrict__ seg_boff,
+                                                       char* __restrict__ out, uint64_t* __restrict__ toff) {
+  __shared__ uint32_t sh[BG_NT / 64 + 1];
+  __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
+  const uint64_t t = blockIdx.x;
+  const uint64_t c0 = seg_off[t];
+  const uint32_t n = (uint32_t)(seg_off[t + 1] - c0);
+  const int64_t* S = A.s + t * BG_SEG_CAP;
+  const int64_t* E = A.e + t * BG_SEG_CAP;
+  uint64_t dst0 = seg_boff[t];
+  for (uint32_t r0 = 0; r0 < n; r0 += BG_NT) {  // block-uniform trip count
+    const uint32_t j = r0 + threadIdx.x;
+    const bool v = j < n;
+    const int64_t s = v ? S[j] : 0, e = v ? E[j] : 0;
+    const uint32_t l = v ? ivl_len(A, s, e) : 0u;
+    uint32_t tot;
+    const uint32_t my = block_excl_scan(l, OpSum(), 0u, sh, &tot);
+    if (v && (c0 + j) % FT_TILE == 0) toff[(c0 + j) / FT_TILE] = dst0 + my;
+    if (tot > FT_LDS) {  // oversized round (long names): render straight to HBM
+      if (v) ivl_put(A, out + dst0 + my, s, e);
+    } else {
+      const uint32_t skew = (uint32_t)(dst0 & 15);
+      if (v) ivl_put(A, buf + skew + my, s, e);
+      __syncthreads();
+      const uint64_t a0 = dst0, a1 = dst0 + tot;
+      const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;
+      const char* bb = buf + skew;
+      if (al0 >= al1) {
+        for (uint64_t p = a0 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+      } else {
+        for (uint64_t p = a0 + threadIdx.x; p < al0; p += BG_NT) out[p] = bb[p - a0];
+        for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+        for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT)
+          *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
+      }
+    }
+    dst0 += tot;
+    __syncthreads();  // buf and sh are reused by the next round
+  }
 }
 
 // bytes of every FT_TILE-row tile of a RES_IVL result: the same two-rows-per-thread
@@ -1231,6 +1271,24 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   FmtArgs A;
   fill_args(r, A);
   A.stop_row = ~0ULL;
+  if (r->kind == RES_IVL && r->nseg) {  // segmented: sizes known, one pass
+    const unsigned nt = bg_blocks(r->n, FT_TILE);
+    uint64_t total = 0;
+    int rc = bg_fetch_u64(c, r->seg_boff + r->nseg, &total);
+    if (rc) return rc;
+    uint64_t* tb = (uint64_t*)bg_alloc(c, 8ull * (nt ? nt : 1));
+    r->text = (char*)bg_alloc(c, total + 16);
+    if (!tb || !r->text) return BG_E_NOMEM;
+    BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_seg, dim3((unsigned)r->nseg), dim3(BG_NT), A, r->seg_off, r->seg_boff,
+              r->text, tb);
+    BG_HIP(c, hipGetLastError());
+    r->toff = tb;
+    r->nbytes = total;
+    r->formatted = true;
+    if (nbytes) *nbytes = total;
+    bg_mark(c, "format");
+    return 0;
+  }
   const unsigned nb = bg_blocks(r->n, FT_TILE);
   const unsigned nbc = bg_blocks(nb, FC_TILES);
   uint64_t* tb = (uint64_t*)bg_alloc(c, 8ull * (nb ? nb : 1));
@@ -1319,6 +1377,7 @@ extern "C" int bg_result_chrom_spans(bg_ctx* c, bg_result* r, uint64_t* offsets,
   if (cap < nc + 1) return bg_fail(c, BG_E_ARG, "offsets buffer needs nchroms+1 entries");
   int rc = bg_result_format(c, r, nullptr);
   if (rc) return rc;
+  if ((rc = bg_result_compact(c, r))) return rc;  // the row search reads contiguous pieces
   FmtArgs A;
   fill_args(r, A);
   uint64_t* d = (uint64_t*)bg_alloc(c, 8ull * (nc + 1));

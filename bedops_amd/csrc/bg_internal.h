@@ -188,7 +188,18 @@ struct bg_result {
   bool formatted = false;
   bool stopped = false;      // the text ends where the reference throws (BG_E_VISITOR)
   uint64_t* toff = nullptr;  // byte offset of each 1024-row format tile (kept for spans)
+  // RES_IVL straight from a merge-path tile kernel: s/e are SEGMENTED, segment t's pieces at
+  // [t * BG_SEG_CAP, t * BG_SEG_CAP + seg_off[t+1] - seg_off[t]); seg_off / seg_boff are the
+  // exclusive scans of the pieces and printed bytes per segment (nseg + 1 entries). The
+  // formatter reads this layout directly; bg_result_compact makes s/e contiguous
+  uint64_t nseg = 0;
+  uint64_t* seg_off = nullptr;
+  uint64_t* seg_boff = nullptr;
 };
+// pieces per segment of a segmented RES_IVL (= the merge-path tile, bg_setops.hip)
+#define BG_SEG_CAP 1024
+// s/e of a segmented RES_IVL result made contiguous (no-op otherwise)
+int bg_result_compact(bg_ctx* c, bg_result* r);
 
 // workgroups of BG_NT threads of `kern` resident on the whole device at once (persistent
 // grid size; occupancy query x compute units, cached per kernel)
@@ -245,6 +256,10 @@ struct Ivl {
   int64_t* e = nullptr;
   uint64_t n = 0;
   bool owned = false;
+  // segmented layout (bg_result::nseg); owned with s/e
+  uint64_t nseg = 0;
+  uint64_t* seg_off = nullptr;
+  uint64_t* seg_boff = nullptr;
 };
 void ivl_free(bg_ctx* c, Ivl& v);
 int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n);
@@ -288,6 +303,26 @@ static int count_scan_write(bg_ctx* c, unsigned nb, CountFn cf, WriteFn wf, uint
 #define BG_NT 256  // threads per workgroup (4 waves of 64)
 
 __device__ __forceinline__ int bg_lane() { return threadIdx.x & 63; }
+
+// decimal digits of v: compares only, 32-bit ones when v fits (the common case)
+__device__ __forceinline__ int dec_len_u64(uint64_t v) {
+  if ((v >> 32) == 0) {
+    const uint32_t w = (uint32_t)v;
+    return 1 + (w >= 10u) + (w >= 100u) + (w >= 1000u) + (w >= 10000u) + (w >= 100000u) +
+           (w >= 1000000u) + (w >= 10000000u) + (w >= 100000000u) + (w >= 1000000000u);
+  }
+  int l = 10;  // v >= 2^32 > 10^9
+  uint64_t p = 10000000000ull;
+#pragma unroll
+  for (int k = 0; k < 10; ++k, p *= 10) l += v >= p;
+  return l;
+}
+// printed bytes of an interval line "%s\t%lu\t%lu\n" (keys: chrom << BG_KEY_SHIFT | coord)
+__device__ __forceinline__ uint32_t bg_ivl_len(const uint32_t* name_len, int64_t s, int64_t e) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  return name_len[g] + 3u + (uint32_t)dec_len_u64((uint64_t)(s & BG_COORD_MASK)) +
+         (uint32_t)dec_len_u64((uint64_t)(e & BG_COORD_MASK));
+}
 __device__ __forceinline__ int bg_wave() { return threadIdx.x >> 6; }
 
 // inclusive wave (64-lane) scan

@@ -619,6 +619,47 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   return true;
 }
 
+// parse_line_fast from the whitespace mask alone (k_parse_set_n: the tile is classified for
+// whitespace only, half the prologue's work): numbers end at whitespace and their bytes are
+// checked to be digits while they are converted (bgp_fields_ws / bgp_digits_rc); a line this
+// refuses takes the byte path, as in parse_line_fast
+__device__ __forceinline__ bool parse_line_fast_ws(const uint8_t* buf, const uint32_t* wsm, uint32_t q,
+                                                   uint32_t len, Fast& L, bool short8 = false) {
+  BgpFields F;
+  const int r = bgp_fields_ws(mask_window(wsm, q), len, F);
+  if (r != 1) return false;
+  const uint32_t toklen = F.a1 - F.a0;
+  if (toklen > 16 || F.s1 - F.s0 > 12 || F.e1 - F.e0 > 12) return false;
+  const uint32_t b = q + HB;
+  bool ok = true;
+  uint32_t d1, d2, d3;
+  lds12_end(buf, b + F.s1, d1, d2, d3);
+  L.start = bgp_digits_rc(d1, d2, d3, (int)(F.s1 - F.s0), ok);
+  lds12_end(buf, b + F.e1, d1, d2, d3);
+  L.end = bgp_digits_rc(d1, d2, d3, (int)(F.e1 - F.e0), ok);
+  uint64_t lo, hi;
+  if (short8) {
+    if (toklen > 8) return false;
+    lo = lds8(buf, b + F.a0);
+    hi = 0;
+  } else {
+    lds16(buf, b + F.a0, lo, hi);
+  }
+  if (toklen < 16) {
+    if (toklen <= 8) {
+      hi = 0;
+      lo = toklen == 8 ? lo : (lo & ((1ull << (8 * toklen)) - 1));
+    } else {
+      hi &= (1ull << (8 * (toklen - 8))) - 1;
+    }
+  }
+  L.tlo = lo;
+  L.thi = hi;
+  L.toklen = toklen;
+  L.rest = F.e1;
+  return ok;
+}
+
 // BED5 fast path: "<ws> id <ws> score" after the end field, score a plain unsigned
 // integer of <= 12 digits followed by whitespace or the line end (the common bedmap map
 // file); anything else (signs, decimals, exponents, long fields) takes the byte path.
@@ -892,6 +933,12 @@ struct SetTiles {
 // one line -> keys; false if the line is not a row (dropped tail, blank, error: reported).
 // Row numbers are not known here (no scout pass): errors are reported as row 0 and
 // bg_load re-reads the input with its row columns to report the exact line.
+// ONE: the tile lies inside one chromosome run (rl == rh), so the run and its token are
+// workgroup-uniform (scalar loads, no per-lane run search)
+#ifndef BG_EXP_SET
+#define BG_EXP_SET 0
+#endif
+template <bool ONE = false, bool WSO = false>
 __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, const TileText& T,
                                         const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
                                         uint32_t k, uint32_t L, int64_t last_end, int64_t& ks,
@@ -899,12 +946,20 @@ __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, 
   const int64_t ls = t0 + lst[k];
   const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
   if (le < 0) return false;  // the unterminated last line (dropped, Bed.hpp:244-255 + feof)
-  const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+#if BG_EXP_SET == 2
+  {  // experiment: no field parsing (round machinery only)
+    ks = ls;
+    ke = ls + 1;
+    return true;
+  }
+#endif
+  const uint32_t run = ONE ? rl : ((rl == rh) ? rl : run_of(R, ls, rl, rh));
   const RunInfo& I = R.info[run];
   uint64_t start, end;
   Fast F;
-  if (parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
-      F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
+  const bool fast = WSO ? parse_line_fast_ws(B.buf, B.wsm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8)
+                        : parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8);
+  if (fast && F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
     start = F.start;
     end = F.end;
   } else {
@@ -1188,7 +1243,9 @@ __device__ __forceinline__ uint32_t tile_line_starts_n(const TileRegsN<NT>& R, c
   __syncthreads();
   return tot + (has0 ? 1u : 0u);
 }
-template <int NT>
+// WSO: whitespace masks only (parse_line_fast_ws): one multiply per two dwords instead of
+// one per dword plus the digit classes
+template <int NT, bool WSO = false>
 __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
                                                     ParseLdsT<1>& S, const TileRegsN<NT>& R, int64_t& last_end,
                                                     bg_dstatus* st) {
@@ -1201,10 +1258,15 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
   for (int g = 0; g < G; ++g) {  // classify this thread's bytes once (SWAR), publish the masks
     const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
     const uint32_t W[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t ws, dg;
-    bgp_classify8(W, ws, dg);
-    B.wsm[threadIdx.x * G + g] = ws;
-    B.dgm[threadIdx.x * G + g] = dg;
+    if (WSO) {
+      B.wsm[threadIdx.x * G + g] = bgp_ws8(W[0], W[1]) | (bgp_ws8(W[2], W[3]) << 8) |
+                                   (bgp_ws8(W[4], W[5]) << 16) | (bgp_ws8(W[6], W[7]) << 24);
+    } else {
+      uint32_t ws, dg;
+      bgp_classify8(W, ws, dg);
+      B.wsm[threadIdx.x * G + g] = ws;
+      B.dgm[threadIdx.x * G + g] = dg;
+    }
   }
   {  // the halo after the tile (as prologue_core)
     constexpr uint32_t HD = (HA + 32) / 4;
@@ -1215,7 +1277,7 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
       bgp_classify(x, w4, d4);
       const uint32_t sh = 4 * (threadIdx.x & 7);
       if (w4) atomicOr(&B.wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
-      if (d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
+      if (!WSO && d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
       const uint32_t m = nl_mask4(x);
       if (m) atomicMin(&B.hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
     }
@@ -1241,7 +1303,7 @@ struct SetLdsN {
 };
 
 // set_rounds with NT lines per round
-template <int NT, typename V>
+template <int NT, typename V, bool WSO>
 __device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* lst, const TileText& T,
                                              const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
                                              uint32_t L, int64_t last_end, int64_t gbase,
@@ -1256,7 +1318,7 @@ __device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* 
   for (uint32_t j = 0; j < rounds; ++j) {
     const uint32_t k = j * NT + threadIdx.x;
     int64_t ks = 0, ke = 0;
-    const bool valid = k < L && set_row(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
+    const bool valid = k < L && set_row<NARROW, WSO>(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
     V K = 0, E = 0;
     if (valid) {
       if (NARROW) {
@@ -1306,7 +1368,7 @@ __device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* 
 }
 
 // (LDS holds 11 of these workgroups per CU: 5-6 waves per SIMD)
-template <int NT>
+template <int NT, bool WSO = true>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_set_n(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
@@ -1322,7 +1384,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
   {
     TileRegsN<NT> TR;
     load_tile_n<NT>(txt, nb, t0, TR);
-    L = tile_prologue_n<NT>(txt, nb, t0, S, TR, last_end, st);
+    L = tile_prologue_n<NT, WSO>(txt, nb, t0, S, TR, last_end, st);
   }
   if (L > LCAP) {
     if (threadIdx.x == 0) {
@@ -1339,13 +1401,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
   uint64_t nc = 0;
   uint64_t cmax = 0;
   int64_t gbase = 0;
+#if BG_EXP_SET == 1
+  if (true) {  // experiment: prologue only
+  } else
+#endif
   if (rl == rh) {
     gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
     uint32_t ce = 0;
-    set_rounds_n<NT, uint32_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
+    set_rounds_n<NT, uint32_t, WSO>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
     cmax = ce;
   } else {
-    set_rounds_n<NT, uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
+    set_rounds_n<NT, uint64_t, WSO>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1730,9 +1796,16 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
     const char* e = getenv("BEDGPU_SET_NT");
     return (e && atoi(e) == 256) ? 256 : 128;
   }();
-  if (set_nt == 128)
-    BG_LAUNCH(c, "k_parse_set", k_parse_set_n<128>, dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st);
+  static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
+    const char* e = getenv("BEDGPU_SET_WS");
+    return !(e && atoi(e) == 0);
+  }();
+  if (set_nt == 128 && set_ws)
+    BG_LAUNCH(c, "k_parse_set", (k_parse_set_n<128, true>), dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi,
+              R, S.lcs, S.lce, TS, st);
+  else if (set_nt == 128)
+    BG_LAUNCH(c, "k_parse_set", (k_parse_set_n<128, false>), dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi,
+              R, S.lcs, S.lce, TS, st);
   else
     BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
               S.lcs, S.lce, TS, st);

@@ -105,6 +105,44 @@ BG_HD uint64_t bgp_digits_r(uint32_t d1, uint32_t d2, uint32_t d3, int L) {
   return (uint64_t)bgp_dig4(d1) * 100000000ull + g23;
 }
 
+// bgp_digits_r plus a check that the L number bytes are all ASCII digits (*ok cleared if
+// not): the whitespace-only field split (bgp_fields_ws) finds number ends at whitespace and
+// leaves the digit test to this
+BG_HD uint64_t bgp_digits_rc(uint32_t d1, uint32_t d2, uint32_t d3, int L, bool& ok) {
+  const int k1 = L >= 12 ? 0 : (L <= 8 ? 4 : 12 - L);
+  const int k2 = L >= 8 ? 0 : (L <= 4 ? 4 : 8 - L);
+  const int k3 = L >= 4 ? 0 : 4 - L;
+  const uint32_t m1 = (uint32_t)(~0ull << (8 * k1));
+  const uint32_t m2 = (uint32_t)(~0ull << (8 * k2));
+  const uint32_t m3 = (uint32_t)(~0ull << (8 * k3));
+  d1 = (d1 & m1) | (0x30303030u & ~m1);
+  d2 = (d2 & m2) | (0x30303030u & ~m2);
+  d3 = (d3 & m3) | (0x30303030u & ~m3);
+  // byte x = d ^ '0' is a digit iff x < 10: bit 7 of x or of (x & 0x7F) + 0x76 flags the rest
+  const uint32_t x1 = d1 ^ 0x30303030u, x2 = d2 ^ 0x30303030u, x3 = d3 ^ 0x30303030u;
+  const uint32_t bad = (x1 | ((x1 & 0x7F7F7F7Fu) + 0x76767676u)) | (x2 | ((x2 & 0x7F7F7F7Fu) + 0x76767676u)) |
+                       (x3 | ((x3 & 0x7F7F7F7Fu) + 0x76767676u));
+  ok = ok && (bad & 0x80808080u) == 0;
+  const uint32_t g23 = bgp_dig4(d2) * 10000u + bgp_dig4(d3);
+  return (uint64_t)bgp_dig4(d1) * 100000000ull + g23;
+}
+
+// bit 7 of each byte of x: the byte is whitespace ({' ', 0x09..0x0D})
+BG_HD uint32_t bgp_ws80(uint32_t x) {
+  const uint32_t hi = x & 0x80808080u;
+  const uint32_t lo7 = x & 0x7F7F7F7Fu;
+  const uint32_t nz20 = ((lo7 ^ 0x20202020u) + 0x7F7F7F7Fu);  // bit 7: byte != ' '
+  const uint32_t ge9 = lo7 + 0x77777777u;
+  const uint32_t ge14 = lo7 + 0x72727272u;
+  return (~nz20 | (ge9 & ~ge14)) & ~hi & 0x80808080u;
+}
+// whitespace classes of two dwords with ONE multiply (the bgp_classify gather with b's flags
+// in a's digit slots): bits 0..3 = bytes of a, 4..7 = bytes of b
+BG_HD uint32_t bgp_ws8(uint32_t a, uint32_t b) {
+  const uint32_t p = ((bgp_ws80(a) >> 7) | (bgp_ws80(b) >> 3)) * 0x00204081u;
+  return (p >> 21) & 0xFFu;
+}
+
 struct BgpFields {
   uint32_t a0, a1;  // chrom token [a0, a1)
   uint32_t s0, s1;  // start digits
@@ -160,6 +198,38 @@ BG_HD int bgp_fields_masks(uint32_t WS, uint32_t DG, uint32_t len, BgpFields& F)
   ok &= ((WS >> (s1 & 31)) & 1u) != 0;   // and ends at whitespace
   ok &= s1 < 31;
   ok &= ((DG >> (e0 & 31)) & 1u) != 0;   // end begins with a digit (may run to the line end)
+  ok &= (s1 - s0 <= 16) & (e1 - e0 <= 16) & (e1 <= len);
+  F.a0 = a0;
+  F.a1 = a1;
+  F.s0 = s0;
+  F.s1 = s1;
+  F.e0 = e0;
+  F.e1 = e1;
+  return ok ? 1 : 0;
+}
+
+// the same fields from the whitespace mask alone: a number runs to the next whitespace (or
+// the line end) and the caller checks its bytes are digits (bgp_digits_rc), so every line
+// this accepts (with the digit check passed) is one bgp_fields_masks accepts with the same
+// fields; a number followed by another non-digit goes to the byte path
+BG_HD int bgp_fields_ws(uint32_t WS, uint32_t len, BgpFields& F) {
+  const uint32_t endm = len < 32 ? (~0u << (len & 31)) : 0u;
+  WS |= endm;
+  const uint32_t NW = ~WS;
+  if (NW == 0) return len <= 32 ? -1 : 0;
+  const uint32_t a0 = bgp_ffbl(NW);
+  const uint32_t m1 = WS & (~0u << a0);
+  const uint32_t a1 = bgp_ffbl(m1);
+  const uint32_t m2 = NW & (~0u << (a1 & 31));
+  const uint32_t s0 = bgp_ffbl(m2);
+  const uint32_t m3 = WS & (~0u << (s0 & 31));
+  const uint32_t s1 = bgp_ffbl(m3);
+  const uint32_t m4 = NW & (~0u << (s1 & 31));
+  const uint32_t e0 = bgp_ffbl(m4);
+  const uint32_t m5 = WS & (~0u << (e0 & 31));
+  const uint32_t e1 = bgp_ffbl(m5);
+  bool ok = (m1 != 0) & (a1 < 31) & (m2 != 0) & (m3 != 0) & (m4 != 0) & (m5 != 0);
+  ok &= s1 < 31;
   ok &= (s1 - s0 <= 16) & (e1 - e0 <= 16) & (e1 <= len);
   F.a0 = a0;
   F.a1 = a1;

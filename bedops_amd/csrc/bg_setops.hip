@@ -194,12 +194,19 @@ enum { MP_INTERSECT = 0, MP_DIFFERENCE = 1 };
 // Y[j0-1 .. j1] (+1 for difference's "next O start"); sentinels outside the arrays.
 //   MP_INTERSECT : X, Y = component lists, keys = starts
 //   MP_DIFFERENCE: X = reference components (key start), Y = other components (key end)
-template <int MODE, bool WRITE>
+//   SEG (with WRITE): no count pass. The tile's pieces go to its own segment
+//     [blockIdx.x * MP_TILE, + count) (a tile of MP_TILE merged elements yields at most
+//     MP_TILE pieces), with the count in cnt[] and the printed bytes in bytes[] (name_len:
+//     the set's chromosome name lengths): a segmented result (bg_result::nseg) that the
+//     formatter reads in place.
+static_assert(MP_TILE == BG_SEG_CAP, "segment capacity = merge-path tile");
+template <int MODE, bool WRITE, bool SEG = false>
 __global__ void __launch_bounds__(BG_NT) k_mp_tile(
     const int64_t* __restrict__ XS, const int64_t* __restrict__ XE, uint64_t nx,
     const int64_t* __restrict__ YS, const int64_t* __restrict__ YE, uint64_t ny,
     const uint64_t* __restrict__ part, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
-    int64_t* __restrict__ OS, int64_t* __restrict__ OE) {
+    int64_t* __restrict__ OS, int64_t* __restrict__ OE, const uint32_t* __restrict__ name_len = nullptr,
+    uint64_t* __restrict__ bytes = nullptr) {
   __shared__ int64_t ls_[MP_TILE + 4];
   __shared__ int64_t le_[MP_TILE + 4];
   __shared__ uint32_t shc[BG_NT / 64 + 1];
@@ -270,12 +277,29 @@ __global__ void __launch_bounds__(BG_NT) k_mp_tile(
     if (threadIdx.x == 0) cnt[blockIdx.x] = btot;
     return;
   }
+  if (SEG) {  // printed bytes of the tile's pieces (the formatter's count pass, here)
+    uint32_t nb = 0;
+#pragma unroll
+    for (int k = 0; k < MP_ITEMS; ++k)
+      if (k < (int)c) nb += bg_ivl_len(name_len, ps[k], pe[k]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nb += __shfl_xor(nb, d, 64);
+    __syncthreads();  // shc reused
+    if (bg_lane() == 0) shc[bg_wave()] = nb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tb = 0;
+      for (int w = 0; w < BG_NT / 64; ++w) tb += shc[w];
+      cnt[blockIdx.x] = btot;
+      bytes[blockIdx.x] = tb;
+    }
+  }
   // stage the tile's pieces in LDS (the input slices are no longer read), then store them
   // with consecutive lanes on consecutive elements
   __syncthreads();
   for (uint32_t k = 0; k < c; ++k) { ls_[o + k] = ps[k]; le_[o + k] = pe[k]; }
   __syncthreads();
-  const uint64_t q = off[blockIdx.x];
+  const uint64_t q = SEG ? (uint64_t)blockIdx.x * MP_TILE : off[blockIdx.x];
   for (uint32_t k = threadIdx.x; k < btot; k += BG_NT) { OS[q + k] = ls_[k]; OE[q + k] = le_[k]; }
 }
 
@@ -532,7 +556,12 @@ __global__ void __launch_bounds__(BG_NT) k_zi_place(const int64_t* __restrict__ 
 // host drivers
 // =====================================================================================
 void ivl_free(bg_ctx* c, Ivl& v) {
-  if (v.owned) { bg_release(c, v.s); bg_release(c, v.e); }
+  if (v.owned) {
+    bg_release(c, v.s);
+    bg_release(c, v.e);
+    bg_release(c, v.seg_off);
+    bg_release(c, v.seg_boff);
+  }
   v = Ivl();
 }
 
@@ -605,10 +634,12 @@ static int merge_sorted(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& z) {
   return 0;
 }
 
-// merge-path tile operation over X and Y (MODE: intersect / difference)
+// merge-path tile operation over X and Y (MODE: intersect / difference). seg: the result
+// is left segmented per tile with its printed byte counts (one pass, no count pass): for a
+// result that goes straight to the formatter (bg_result::nseg)
 template <int MODE>
 static int mp_op(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out, const char* cname,
-                 const char* wname) {
+                 const char* wname, const uint32_t* seg_names = nullptr) {
   const uint64_t nz = x.n + y.n;
   const unsigned nb = bg_blocks(nz, MP_TILE);
   if (nb == 0) return ivl_alloc(c, out, 0);
@@ -618,6 +649,21 @@ static int mp_op(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out, const char* cn
   BG_LAUNCH(c, "k_mp_partition", k_mp_partition, dim3(bg_blocks(nb + 1, 256)), dim3(256), x.s, x.n,
             yk, y.n, nb, part);
   BG_HIP(c, hipGetLastError());
+  if (seg_names) {
+    int rc = ivl_alloc(c, out, nz);
+    out.seg_off = (uint64_t*)bg_alloc(c, 8ull * (nb + 1));
+    out.seg_boff = (uint64_t*)bg_alloc(c, 8ull * (nb + 1));
+    if (rc || !out.seg_off || !out.seg_boff) return BG_E_NOMEM;
+    out.nseg = nb;
+    BG_LAUNCH(c, wname, (k_mp_tile<MODE, true, true>), dim3(nb), dim3(BG_NT), x.s, x.e, x.n, y.s, y.e,
+              y.n, part, out.seg_off, (const uint64_t*)nullptr, out.s, out.e, seg_names, out.seg_boff);
+    BG_HIP(c, hipGetLastError());
+    if ((rc = bg_scan_sum_u64(c, out.seg_off, out.seg_off, nb, out.seg_off + nb))) return rc;
+    if ((rc = bg_scan_sum_u64(c, out.seg_boff, out.seg_boff, nb, out.seg_boff + nb))) return rc;
+    if ((rc = bg_fetch_u64(c, out.seg_off + nb, &out.n))) return rc;
+    bg_release(c, part);
+    return 0;
+  }
   uint64_t total = 0;
   int rc = count_scan_write(
       c, nb,
@@ -705,8 +751,44 @@ bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
   r->n = v.n;
   r->s = v.s;
   r->e = v.e;
+  r->nseg = v.nseg;
+  r->seg_off = v.seg_off;
+  r->seg_boff = v.seg_boff;
   v.owned = false;
   return r;
+}
+
+// segment t's pieces -> [seg_off[t], seg_off[t+1]) of contiguous s/e
+__global__ void __launch_bounds__(BG_NT) k_seg_compact(const int64_t* __restrict__ S, const int64_t* __restrict__ E,
+                                                       const uint64_t* __restrict__ seg_off, int64_t* __restrict__ CS,
+                                                       int64_t* __restrict__ CE) {
+  const uint64_t t = blockIdx.x, c0 = seg_off[t], n = seg_off[t + 1] - c0;
+  for (uint64_t j = threadIdx.x; j < n; j += BG_NT) {
+    CS[c0 + j] = S[t * BG_SEG_CAP + j];
+    CE[c0 + j] = E[t * BG_SEG_CAP + j];
+  }
+}
+
+int bg_result_compact(bg_ctx* c, bg_result* r) {
+  if (!r || r->kind != RES_IVL || !r->nseg) return 0;
+  Ivl w;
+  if (ivl_alloc(c, w, r->n)) {
+    ivl_free(c, w);
+    return BG_E_NOMEM;
+  }
+  BG_LAUNCH(c, "k_seg_compact", k_seg_compact, dim3((unsigned)r->nseg), dim3(BG_NT), r->s, r->e, r->seg_off,
+            w.s, w.e);
+  BG_HIP(c, hipGetLastError());
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  bg_release(c, r->s);
+  bg_release(c, r->e);
+  bg_release(c, r->seg_off);
+  bg_release(c, r->seg_boff);
+  r->s = w.s;
+  r->e = w.e;
+  r->nseg = 0;
+  r->seg_off = r->seg_boff = nullptr;
+  return 0;
 }
 
 int bg_check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf) {
@@ -809,7 +891,10 @@ extern "C" int bg_intersect(bg_ctx* c, bg_set* set, const int* files, int nf, bg
   acc.owned = false;  // comp[0] keeps ownership
   for (int k = 1; k < nf; ++k) {
     Ivl p;
-    if ((rc = mp_op<MP_INTERSECT>(c, acc, comp[k], p, "k_intersect_count", "k_intersect_write")))
+    // the last fold goes straight to the formatter, segmented (unless the zero-length
+    // replay still reads it)
+    const uint32_t* seg = (k + 1 == nf && !zero) ? set->d_name_len : nullptr;
+    if ((rc = mp_op<MP_INTERSECT>(c, acc, comp[k], p, "k_intersect_count", "k_intersect_write", seg)))
       return rc;
     ivl_free(c, acc);
     acc = p;
@@ -829,7 +914,8 @@ extern "C" int bg_difference(bg_ctx* c, bg_set* set, int ref, const int* others,
   Ivl r, o, d;
   if ((rc = bg_table_components(c, set->t[ref], r))) return rc;
   if ((rc = bg_union_components(c, set, others, no, o))) return rc;
-  if ((rc = mp_op<MP_DIFFERENCE>(c, r, o, d, "k_difference_count", "k_difference_write"))) return rc;
+  if ((rc = mp_op<MP_DIFFERENCE>(c, r, o, d, "k_difference_count", "k_difference_write", set->d_name_len)))
+    return rc;
   ivl_free(c, r);
   ivl_free(c, o);
   *out = bg_new_ivl_result(c, set, d);

@@ -53,8 +53,10 @@ REF_BEDMAP_R5M = {"rows": 4999998, "bytes": 54515904, "sha16": "899ec7973e166e2d
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
-            "k_parse_set": "k_parse_set_n<128>" if os.environ.get("BEDGPU_SET_NT") != "256" else "k_parse_set",
-            "k_intersect_count": "k_mp_tile<0, false>", "k_intersect_write": "k_mp_tile<0, true>"}
+            "k_parse_set": ("k_parse_set" if os.environ.get("BEDGPU_SET_NT") == "256" else
+                            "k_parse_set_n<128, false>" if os.environ.get("BEDGPU_SET_WS") == "0" else
+                            "k_parse_set_n<128, true>"),
+            "k_intersect_count": "k_mp_tile<0, false>", "k_intersect_write": "k_mp_tile<0, true, true>"}
 
 
 def log(*a):
