@@ -928,7 +928,15 @@ struct SetTiles {
   uint64_t* nloc;  // local components of the tile
   uint32_t* absorbed;  // local components merged into the component open on entry
   uint64_t* nrow;  // rows of the tile
+  // staging form of the tile: >= 0, a tile inside one chromosome run whose local components
+  // are staged as 32-bit coordinates (LCS/LCE of the tile's slots read as uint32, half the
+  // bytes) under this key prefix; -1, 64-bit keys
+  int64_t* gb;
 };
+// key of local component i of tile t (start: LCS, end: LCE), either staging form
+__device__ __forceinline__ int64_t set_key(const int64_t* X, uint64_t b, int64_t gb, uint64_t i) {
+  return gb >= 0 ? (gb | (int64_t)reinterpret_cast<const uint32_t*>(X + b)[i]) : X[b + i];
+}
 
 // one line -> keys; false if the line is not a row (dropped tail, blank, error: reported).
 // Row numbers are not known here (no scout pass): errors are reported as row 0 and
@@ -1142,6 +1150,7 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
       TS.base[tile] = base;
       TS.nloc[tile] = 0;
       TS.nrow[tile] = 0;
+      TS.gb[tile] = -1;
     }
     return;
   }
@@ -1171,6 +1180,7 @@ __global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
     TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
     TS.base[tile] = base;
     TS.nloc[tile] = nc;
+    TS.gb[tile] = -1;
     TS.nrow[tile] = L - ((L > 0 && last_end < 0) ? 1 : 0);  // (errors fail the load anyway)
   }
 }
@@ -1358,8 +1368,13 @@ __device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* 
       tot += X.xc[p][q];
     }
     if (open && pos < SCAP) {
-      LCS[base + pos] = ks;
-      if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);
+      if (NARROW) {  // 32-bit coordinates (SetTiles::gb)
+        reinterpret_cast<uint32_t*>(LCS + base)[pos] = (uint32_t)(K - 1);
+        if (pos > 0) reinterpret_cast<uint32_t*>(LCE + base)[pos - 1] = (uint32_t)(ex_e - 1);
+      } else {
+        LCS[base + pos] = ks;
+        if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);
+      }
     }
     carry_e = te;
     carry_k = (V)X.xk[p][NT / 64 - 1];
@@ -1392,6 +1407,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
       TS.base[tile] = base;
       TS.nloc[tile] = 0;
       TS.nrow[tile] = 0;
+      TS.gb[tile] = -1;
     }
     return;
   }
@@ -1419,7 +1435,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
       atomicOr(&st->flags, BG_SET_OVERFLOW);
       nc = 0;
     }
-    if (nc > 0) LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    if (nc > 0) {
+      if (rl == rh) reinterpret_cast<uint32_t*>(LCE + base)[nc - 1] = (uint32_t)(cmax - 1);
+      else LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    }
+    TS.gb[tile] = (rl == rh) ? gbase : -1;
     TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
     const uint64_t kmax = X.klast[0] ? X.klast[0] : X.klast[1];
     TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
@@ -1443,21 +1463,29 @@ __global__ void __launch_bounds__(BG_NT) k_set_count(const int64_t* __restrict__
   uint64_t rows = 0;
   if (t < ntiles) {
     const uint64_t b = TS.base[t], n = TS.nloc[t];
+    const int64_t gb = TS.gb[t];
     rows = TS.nrow[t];
+    const int64_t first = n ? set_key(LCS, b, gb, 0) : 0;
     if (n > 0 && t > 0) {
       uint32_t u = t - 1;
       while (u > 0 && TS.tlast[u] == LLONG_MIN) --u;  // tiles without rows (lines > 8 KiB)
-      if (LCS[b] < TS.tlast[u]) bg_report(st, 0, ERR_UNSORTED);  // first row < an earlier row
+      if (first < TS.tlast[u]) bg_report(st, 0, ERR_UNSORTED);  // first row < an earlier row
     }
     const int64_t M = mex[t];
     uint64_t a = 0;
-    if (n && LCS[b] <= M) {
+    if (n && first <= M) {
       uint64_t step = 1;  // gallop, then bisect
-      while (a + step < n && LCS[b + a + step] <= M) {
+      while (a + step < n && set_key(LCS, b, gb, a + step) <= M) {
         a += step;
         step <<= 1;
       }
-      a = upper_bound_in(LCS, b + a + 1, b + min(n, a + step), M) - b;
+      uint64_t lo = a + 1, hi = min(n, a + step);  // first local index in [lo, hi) with key > M
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (set_key(LCS, b, gb, mid) <= M) lo = mid + 1;
+        else hi = mid;
+      }
+      a = lo;
     }
     TS.absorbed[t] = (uint32_t)a;
     cnt[t] = n - a;
@@ -1488,6 +1516,8 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
   // workgroup is independent, instead of a wave waiting on one tile's descriptor first
   __shared__ uint32_t cpre[SW_TILES + 1];
   __shared__ uint64_t src[SW_TILES], dst[SW_TILES];
+  __shared__ uint32_t sab[SW_TILES];       // absorbed local components (the first survivor's index)
+  __shared__ int64_t sgb[SW_TILES];        // staging form (SetTiles::gb)
   __shared__ int64_t first_end[SW_TILES];  // CE value before the tile's first global component
   const uint32_t t0 = blockIdx.x * SW_TILES;
   const uint32_t nt = min((uint32_t)SW_TILES, ntiles - t0);
@@ -1495,11 +1525,13 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
   if (threadIdx.x < nt) {
     const uint32_t t = t0 + threadIdx.x;
     const uint64_t b = TS.base[t], n = TS.nloc[t], a = TS.absorbed[t];
-    const int64_t M = mex[t];
+    const int64_t M = mex[t], gb = TS.gb[t];
     c = (uint32_t)(n - a);
-    src[threadIdx.x] = b + a;
+    src[threadIdx.x] = b;
+    sab[threadIdx.x] = (uint32_t)a;
+    sgb[threadIdx.x] = gb;
     dst[threadIdx.x] = off[t];
-    first_end[threadIdx.x] = (c > 0) ? max(M, a > 0 ? LCE[b + a - 1] : LLONG_MIN) : 0;
+    first_end[threadIdx.x] = (c > 0) ? max(M, a > 0 ? set_key(LCE, b, gb, a - 1) : LLONG_MIN) : 0;
     if (t + 1 == ntiles) {  // the last component ends at the running max of everything
       const uint64_t total = off[t] + c;
       if (total > 0) CE[total - 1] = max(M, TS.tmax[t]);
@@ -1521,9 +1553,10 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
       else hi = mid - 1;
     }
     const uint32_t j = e - cpre[lo];
-    const uint64_t g = dst[lo] + j, sidx = src[lo] + j;
-    CS[g] = LCS[sidx];
-    if (g > 0) CE[g - 1] = j == 0 ? first_end[lo] : LCE[sidx - 1];
+    const uint64_t g = dst[lo] + j, b = src[lo], i = sab[lo] + j;
+    const int64_t gb = sgb[lo];
+    CS[g] = set_key(LCS, b, gb, i);
+    if (g > 0) CE[g - 1] = j == 0 ? first_end[lo] : set_key(LCE, b, gb, i - 1);
   }
 }
 
@@ -1591,6 +1624,7 @@ struct LoadState {
   uint64_t* nloc = nullptr;
   uint64_t* tcnt = nullptr;
   uint32_t* absorbed = nullptr;
+  int64_t* tgb = nullptr;
 };
 
 static void release_state(bg_ctx* c, LoadState& S) {
@@ -1598,7 +1632,8 @@ static void release_state(bg_ctx* c, LoadState& S) {
                   (void*)S.blist, (void*)S.recs,
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
-                  (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed})
+                  (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed,
+                  (void*)S.tgb})
     bg_release(c, p);
   S = LoadState();
 }
@@ -1787,11 +1822,12 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
   S.nloc = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.tcnt = (uint64_t*)bg_alloc(c, 8ull * nt);
   S.absorbed = (uint32_t*)bg_alloc(c, 4ull * nt);
+  S.tgb = (int64_t*)bg_alloc(c, 8ull * nt);
   S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);  // rows per tile
   if (!S.lcs || !S.lce || !S.tmax || !S.tlast || !S.mex || !S.tbase || !S.nloc ||
-      !S.tcnt || !S.absorbed || !S.cnt)
+      !S.tcnt || !S.absorbed || !S.cnt || !S.tgb)
     return BG_E_NOMEM;
-  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt};
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
   static const int set_nt = [] {  // BEDGPU_SET_NT=256: the 256-thread kernel (A/B)
     const char* e = getenv("BEDGPU_SET_NT");
     return (e && atoi(e) == 256) ? 256 : 128;
