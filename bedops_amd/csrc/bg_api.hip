@@ -310,6 +310,11 @@ extern "C" int bg_set_restrict_chrom(bg_ctx* c, bg_set* s, const char* chrom) {
 
 extern "C" int bg_result_rows(const bg_result* r, uint64_t* rows) {
   if (!r || !rows) return BG_E_ARG;
+  if (r->n_pending) {  // a segmented result's count is fetched on first use
+    bg_result* w = const_cast<bg_result*>(r);
+    const int rc = bg_result_resolve_n(w->ctx, w);
+    if (rc) return rc;
+  }
   *rows = r->n;
   return 0;
 }

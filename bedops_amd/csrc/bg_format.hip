@@ -1272,16 +1272,37 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   fill_args(r, A);
   A.stop_row = ~0ULL;
   if (r->kind == RES_IVL && r->nseg) {  // segmented: sizes known, one pass
-    const unsigned nt = bg_blocks(r->n, FT_TILE);
-    uint64_t total = 0;
-    int rc = bg_fetch_u64(c, r->seg_boff + r->nseg, &total);
-    if (rc) return rc;
+    // every piece prints at most name + 3 + two 13-digit coordinates (< 2^40): with that
+    // bound allocated up front, the counts come back with the kernel's completion (one host
+    // round trip per format instead of one before and one after)
+    const uint64_t line_max = (uint64_t)r->set->max_name_len + 3 + 2 * 13;
+    const uint64_t bound = r->seg_nz * line_max;
+    const bool ahead = bound <= (8ull << 30);
+    uint64_t tots[2] = {0, 0};  // pieces, bytes
+    int rc = 0;
+    if (!ahead) {
+      BG_HIP(c, hipMemcpyAsync(&tots[0], r->seg_off + r->nseg, 8, hipMemcpyDeviceToHost, c->stream));
+      BG_HIP(c, hipMemcpyAsync(&tots[1], r->seg_boff + r->nseg, 8, hipMemcpyDeviceToHost, c->stream));
+      BG_HIP(c, hipStreamSynchronize(c->stream));
+      r->n = tots[0];
+      r->n_pending = false;
+    }
+    const unsigned nt = bg_blocks(ahead ? r->seg_nz : r->n, FT_TILE);
     uint64_t* tb = (uint64_t*)bg_alloc(c, 8ull * (nt ? nt : 1));
-    r->text = (char*)bg_alloc(c, total + 16);
+    r->text = (char*)bg_alloc(c, (ahead ? bound : tots[1]) + 16);
     if (!tb || !r->text) return BG_E_NOMEM;
     BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_seg, dim3((unsigned)r->nseg), dim3(BG_NT), A, r->seg_off, r->seg_boff,
               r->text, tb);
     BG_HIP(c, hipGetLastError());
+    if (ahead) {
+      BG_HIP(c, hipMemcpyAsync(&tots[0], r->seg_off + r->nseg, 8, hipMemcpyDeviceToHost, c->stream));
+      BG_HIP(c, hipMemcpyAsync(&tots[1], r->seg_boff + r->nseg, 8, hipMemcpyDeviceToHost, c->stream));
+      BG_HIP(c, hipStreamSynchronize(c->stream));
+      r->n = tots[0];
+      r->n_pending = false;
+    }
+    (void)rc;
+    const uint64_t total = tots[1];
     r->toff = tb;
     r->nbytes = total;
     r->formatted = true;

@@ -195,7 +195,11 @@ struct bg_result {
   uint64_t nseg = 0;
   uint64_t* seg_off = nullptr;
   uint64_t* seg_boff = nullptr;
+  uint64_t seg_nz = 0;     // pieces the segments can hold (the merged elements)
+  bool n_pending = false;  // n is still only on the device (seg_off[nseg]): bg_result_resolve_n
 };
+// n of a segmented result fetched from the device when still pending
+int bg_result_resolve_n(bg_ctx* c, bg_result* r);
 // pieces per segment of a segmented RES_IVL (= the merge-path tile, bg_setops.hip)
 #define BG_SEG_CAP 1024
 // s/e of a segmented RES_IVL result made contiguous (no-op otherwise)
@@ -260,6 +264,8 @@ struct Ivl {
   uint64_t nseg = 0;
   uint64_t* seg_off = nullptr;
   uint64_t* seg_boff = nullptr;
+  uint64_t seg_nz = 0;
+  bool n_pending = false;
 };
 void ivl_free(bg_ctx* c, Ivl& v);
 int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n);

@@ -660,7 +660,11 @@ static int mp_op(bg_ctx* c, const Ivl& x, const Ivl& y, Ivl& out, const char* cn
     BG_HIP(c, hipGetLastError());
     if ((rc = bg_scan_sum_u64(c, out.seg_off, out.seg_off, nb, out.seg_off + nb))) return rc;
     if ((rc = bg_scan_sum_u64(c, out.seg_boff, out.seg_boff, nb, out.seg_boff + nb))) return rc;
-    if ((rc = bg_fetch_u64(c, out.seg_off + nb, &out.n))) return rc;
+    // the piece count stays on the device: the formatter fetches it with the byte count after
+    // its kernel (no host round trip in between)
+    out.n = 0;
+    out.seg_nz = nz;
+    out.n_pending = true;
     bg_release(c, part);
     return 0;
   }
@@ -754,6 +758,8 @@ bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v) {
   r->nseg = v.nseg;
   r->seg_off = v.seg_off;
   r->seg_boff = v.seg_boff;
+  r->seg_nz = v.seg_nz;
+  r->n_pending = v.n_pending;
   v.owned = false;
   return r;
 }
@@ -769,8 +775,17 @@ __global__ void __launch_bounds__(BG_NT) k_seg_compact(const int64_t* __restrict
   }
 }
 
+int bg_result_resolve_n(bg_ctx* c, bg_result* r) {
+  if (!r || !r->n_pending) return 0;
+  const int rc = bg_fetch_u64(c, r->seg_off + r->nseg, &r->n);
+  if (!rc) r->n_pending = false;
+  return rc;
+}
+
 int bg_result_compact(bg_ctx* c, bg_result* r) {
   if (!r || r->kind != RES_IVL || !r->nseg) return 0;
+  int rc = bg_result_resolve_n(c, r);
+  if (rc) return rc;
   Ivl w;
   if (ivl_alloc(c, w, r->n)) {
     ivl_free(c, w);
