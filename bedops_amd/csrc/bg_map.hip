@@ -808,6 +808,56 @@ __device__ __forceinline__ double tm_iround(double d) {
   const double d1 = ceil(d);
   return (d >= 0) ? ((d1 - d > 0.5) ? floor(d) : d1) : ((d1 - d >= 0.5) ? floor(d) : d1);
 }
+// the sorted window's element moves, TM_B at a time (all loads of a batch issued before its
+// stores: one HBM round trip per TM_B elements instead of per element; a window of 10^4
+// equal-coordinate rows took 3-4 s one element at a time)
+#define TM_B 16
+// [p, n) -> [p + 1, n + 1), from the top
+__device__ __forceinline__ void tm_shift_up(double* V, uint64_t* X, uint64_t p, uint64_t n) {
+  uint64_t t = n;  // next destination + 1
+  while (t >= p + 1 + TM_B) {
+    double v[TM_B];
+    uint64_t x[TM_B];
+#pragma unroll
+    for (int i = 0; i < TM_B; ++i) {
+      v[i] = V[t - 1 - i];
+      x[i] = X[t - 1 - i];
+    }
+#pragma unroll
+    for (int i = 0; i < TM_B; ++i) {
+      V[t - i] = v[i];
+      X[t - i] = x[i];
+    }
+    t -= TM_B;
+  }
+  for (; t > p; --t) {
+    V[t] = V[t - 1];
+    X[t] = X[t - 1];
+  }
+}
+// [p + 1, n) -> [p, n - 1), from the bottom
+__device__ __forceinline__ void tm_shift_down(double* V, uint64_t* X, uint64_t p, uint64_t n) {
+  uint64_t t = p;  // next destination
+  while (t + 1 + TM_B <= n) {
+    double v[TM_B];
+    uint64_t x[TM_B];
+#pragma unroll
+    for (int i = 0; i < TM_B; ++i) {
+      v[i] = V[t + 1 + i];
+      x[i] = X[t + 1 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < TM_B; ++i) {
+      V[t + i] = v[i];
+      X[t + i] = x[i];
+    }
+    t += TM_B;
+  }
+  for (; t + 1 < n; ++t) {
+    V[t] = V[t + 1];
+    X[t] = X[t + 1];
+  }
+}
 template <int CRIT>
 __global__ void k_tm_replay(EvArgs A, TmArgs T, const uint64_t* __restrict__ seg, uint64_t nseg,
                             const uint64_t* __restrict__ soff, double* __restrict__ SV,
@@ -846,14 +896,14 @@ __global__ void k_tm_replay(EvArgs A, TmArgs T, const uint64_t* __restrict__ seg
     const uint64_t p = rank(v, (uint64_t)bg_maddr(A.addr, m));
     if (T.lower) mark_del(L, p, v);
     mark_del(U, p, v);
-    for (uint64_t t = p; t + 1 < n; ++t) { V[t] = V[t + 1]; X[t] = X[t + 1]; }
+    tm_shift_down(V, X, p, n);
     --n;
   };
   auto add = [&](uint64_t m) {
     const double v = A.SC[m];
     const uint64_t am = (uint64_t)bg_maddr(A.addr, m);
     const uint64_t p = rank(v, am);
-    for (uint64_t t = n; t > p; --t) { V[t] = V[t - 1]; X[t] = X[t - 1]; }
+    tm_shift_up(V, X, p, n);
     V[p] = v;
     X[p] = am;
     ++n;
