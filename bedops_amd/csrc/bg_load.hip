@@ -30,6 +30,8 @@
 #include <cstring>
 #include <map>
 
+#include <type_traits>
+
 #include "bg_internal.h"
 #include "bg_parse.h"
 
@@ -735,6 +737,25 @@ struct ParseLdsT {
   uint32_t shs[BG_NT / 64 + 1];
 };
 
+// k_parse_set_n's whitespace-only layout: no digit bitmap, and line starts for up to
+// LCAP_WS lines (8 KiB of lines averaging >= 8 bytes; a tile of shorter lines reports a
+// parse error and the load is redone with row columns, as any set-path refusal): 2.1 KiB
+// less LDS per workgroup, 13 instead of 11 workgroups per CU
+#define LCAP_WS 1024
+struct ParseBufWs {
+  __attribute__((aligned(16))) uint8_t buf[LBUF];
+  uint32_t wsm[TT / 32 + HA / 32 + 1];
+  uint32_t hnl;
+};
+struct ParseLdsWs {
+  ParseBufWs b[1];
+  uint16_t lst[LCAP_WS + 1];
+  uint32_t shs[BG_NT / 64 + 1];
+};
+__device__ __forceinline__ void clear_halo(ParseBufWs& B) {
+  if (threadIdx.x == 0) B.hnl = ~0u;
+  if (threadIdx.x < (HA + 32) / 32) B.wsm[TT / 32 + threadIdx.x] = 0;
+}
 // the halo words of B's bitmaps start empty (LDS atomics in prologue_core), hnl unset
 __device__ __forceinline__ void clear_halo(ParseBuf& B) {
   if (threadIdx.x == 0) B.hnl = ~0u;
@@ -946,8 +967,8 @@ __device__ __forceinline__ int64_t set_key(const int64_t* X, uint64_t b, int64_t
 #ifndef BG_EXP_SET
 #define BG_EXP_SET 0
 #endif
-template <bool ONE = false, bool WSO = false>
-__device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, const TileText& T,
+template <bool ONE = false, bool WSO = false, typename BufT = ParseBuf>
+__device__ __forceinline__ bool set_row(const BufT& B, const uint16_t* lst, const TileText& T,
                                         const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
                                         uint32_t k, uint32_t L, int64_t last_end, int64_t& ks,
                                         int64_t& ke, bg_dstatus* st) {
@@ -965,8 +986,9 @@ __device__ __forceinline__ bool set_row(const ParseBuf& B, const uint16_t* lst, 
   const RunInfo& I = R.info[run];
   uint64_t start, end;
   Fast F;
-  const bool fast = WSO ? parse_line_fast_ws(B.buf, B.wsm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8)
-                        : parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8);
+  bool fast;
+  if constexpr (WSO) fast = parse_line_fast_ws(B.buf, B.wsm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8);
+  else fast = parse_line_fast(B.buf, B.wsm, B.dgm, lst[k], (uint32_t)(le - ls), F, I.tlen <= 8);
   if (fast && F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi) {
     start = F.start;
     end = F.end;
@@ -1255,11 +1277,12 @@ __device__ __forceinline__ uint32_t tile_line_starts_n(const TileRegsN<NT>& R, c
 }
 // WSO: whitespace masks only (parse_line_fast_ws): one multiply per two dwords instead of
 // one per dword plus the digit classes
-template <int NT, bool WSO = false>
+template <int NT, bool WSO, typename LdsT>
 __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
-                                                    ParseLdsT<1>& S, const TileRegsN<NT>& R, int64_t& last_end,
+                                                    LdsT& S, const TileRegsN<NT>& R, int64_t& last_end,
                                                     bg_dstatus* st) {
-  ParseBuf& B = S.b[0];
+  constexpr uint32_t CAP = WSO ? LCAP_WS : LCAP;
+  auto& B = S.b[0];
   clear_halo(B);
   store_tile_n<NT>(B.buf, R);
   __syncthreads();
@@ -1268,7 +1291,7 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
   for (int g = 0; g < G; ++g) {  // classify this thread's bytes once (SWAR), publish the masks
     const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
     const uint32_t W[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    if (WSO) {
+    if constexpr (WSO) {
       B.wsm[threadIdx.x * G + g] = bgp_ws8(W[0], W[1]) | (bgp_ws8(W[2], W[3]) << 8) |
                                    (bgp_ws8(W[4], W[5]) << 16) | (bgp_ws8(W[6], W[7]) << 24);
     } else {
@@ -1287,14 +1310,15 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
       bgp_classify(x, w4, d4);
       const uint32_t sh = 4 * (threadIdx.x & 7);
       if (w4) atomicOr(&B.wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
-      if (!WSO && d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
+      if constexpr (!WSO)
+        if (d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
       const uint32_t m = nl_mask4(x);
       if (m) atomicMin(&B.hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
     }
   }
   bool has0;
-  const uint32_t L = tile_line_starts_n<NT>(R, B.buf, t0, S.lst, LCAP + 1, S.shs, has0);
-  if (L > LCAP) {
+  const uint32_t L = tile_line_starts_n<NT>(R, B.buf, t0, S.lst, CAP + 1, S.shs, has0);
+  if (L > CAP) {
     if (threadIdx.x == 0) bg_report(st, 0, ERR_PARSE);
     return L;
   }
@@ -1313,8 +1337,8 @@ struct SetLdsN {
 };
 
 // set_rounds with NT lines per round
-template <int NT, typename V, bool WSO>
-__device__ __forceinline__ void set_rounds_n(const ParseBuf& B, const uint16_t* lst, const TileText& T,
+template <int NT, typename V, bool WSO, typename BufT>
+__device__ __forceinline__ void set_rounds_n(const BufT& B, const uint16_t* lst, const TileText& T,
                                              const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
                                              uint32_t L, int64_t last_end, int64_t gbase,
                                              uint64_t base, int64_t* __restrict__ LCS,
@@ -1388,7 +1412,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
-  __shared__ ParseLdsT<1> S;
+  using LdsT = std::conditional_t<WSO, ParseLdsWs, ParseLdsT<1>>;
+  constexpr uint32_t CAP = WSO ? LCAP_WS : LCAP;
+  __shared__ LdsT S;
   __shared__ SetLdsN<NT> X;
   const uint32_t tile = blockIdx.x;
   const int64_t t0 = (int64_t)tile * TT;
@@ -1401,7 +1427,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     load_tile_n<NT>(txt, nb, t0, TR);
     L = tile_prologue_n<NT, WSO>(txt, nb, t0, S, TR, last_end, st);
   }
-  if (L > LCAP) {
+  if (L > CAP) {
     if (threadIdx.x == 0) {
       TS.tmax[tile] = TS.tlast[tile] = LLONG_MIN;
       TS.base[tile] = base;
@@ -1411,7 +1437,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     }
     return;
   }
-  const ParseBuf& B = S.b[0];
+  const auto& B = S.b[0];
   const uint32_t rl = runlo[tile], rh = runhi[tile];
   const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
   uint64_t nc = 0;
