@@ -992,6 +992,7 @@ extern "C" void bg_result_free(bg_result* r) {
   bg_release(c, r->e);
   bg_release(c, r->seg_off);
   bg_release(c, r->seg_boff);
+  bg_release(c, r->tbytes);
   bg_release(c, r->rows);
   bg_release(c, r->rlen);
   bg_release(c, r->cnt);

@@ -1349,7 +1349,10 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!tb || !d_tot) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   BG_HIP(c, hipMemsetAsync(&c->dstat->stop_row, 0xff, 8, c->stream));
-  if (nb) {
+  static_assert(FT_TILE == BG_FMT_TILE, "format tile");
+  if (nb && A.kind == RES_ROWS && r->tbytes) {  // summed by bg_element_of's compaction
+    BG_HIP(c, hipMemcpyAsync(tb, r->tbytes, 8ull * nb, hipMemcpyDeviceToDevice, c->stream));
+  } else if (nb) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_ivl_count, dim3(nb), dim3(BG_NT), A, tb); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;

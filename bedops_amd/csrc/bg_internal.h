@@ -188,6 +188,9 @@ struct bg_result {
   bool formatted = false;
   bool stopped = false;      // the text ends where the reference throws (BG_E_VISITOR)
   uint64_t* toff = nullptr;  // byte offset of each 1024-row format tile (kept for spans)
+  // RES_ROWS from bg_element_of: printed bytes of every BG_FMT_TILE-row format tile, summed
+  // while the rows were compacted (the formatter's count pass, done already); null: count
+  uint64_t* tbytes = nullptr;
   // RES_IVL straight from a merge-path tile kernel: s/e are SEGMENTED, segment t's pieces at
   // [t * BG_SEG_CAP, t * BG_SEG_CAP + seg_off[t+1] - seg_off[t]); seg_off / seg_boff are the
   // exclusive scans of the pieces and printed bytes per segment (nseg + 1 entries). The
@@ -200,6 +203,8 @@ struct bg_result {
 };
 // n of a segmented result fetched from the device when still pending
 int bg_result_resolve_n(bg_ctx* c, bg_result* r);
+// rows per format tile (bg_format.hip FT_TILE)
+#define BG_FMT_TILE 512
 // pieces per segment of a segmented RES_IVL (= the merge-path tile, bg_setops.hip)
 #define BG_SEG_CAP 1024
 // s/e of a segmented RES_IVL result made contiguous (no-op otherwise)

@@ -336,7 +336,9 @@ __global__ void __launch_bounds__(BG_NT) k_element_flags(
     const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
     const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
     const uint64_t* __restrict__ P, double thres, int use_pct, int invert,
-    uint8_t* __restrict__ flag) {
+    uint8_t* __restrict__ flag, const uint32_t* __restrict__ name_len = nullptr,
+    const uint32_t* __restrict__ rest_len = nullptr, uint16_t* __restrict__ blen = nullptr,
+    unsigned int* __restrict__ blen_ovf = nullptr) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
   __shared__ int64_t xs[EF_SLICE], xe[EF_SLICE];
@@ -389,6 +391,11 @@ __global__ void __launch_bounds__(BG_NT) k_element_flags(
     keep = invert ? !is_el : is_el;
   }
   flag[r] = keep ? 1 : 0;
+  if (blen && keep) {  // the kept row's printed length "%s\t%lu\t%lu%s\n" (k_compact_rows_bytes)
+    const uint32_t l = bg_ivl_len(name_len, s, e) + rest_len[r];
+    if (l > 0xFFFFu) atomicOr(blen_ovf, 1u);
+    blen[r] = (uint16_t)l;
+  }
 }
 
 #define CF_ITEMS 16
@@ -571,6 +578,70 @@ int ivl_alloc(bg_ctx* c, Ivl& v, uint64_t n) {
   v.e = (int64_t*)bg_alloc(c, 8 * (n ? n : 1));
   v.owned = true;
   return (v.s && v.e) ? 0 : BG_E_NOMEM;
+}
+
+// k_compact_flags' write pass that also sums the kept rows' printed lengths (blen) per
+// output format tile of BG_FMT_TILE rows: a wave's kept rows of one ballot are consecutive
+// outputs spanning at most two tiles, lane 0 carries a running (tile, bytes) pair and adds
+// it to tb[] when the tile changes (a few atomics per 1024 input rows)
+__global__ void __launch_bounds__(BG_NT) k_compact_rows_bytes(const uint8_t* __restrict__ flag,
+                                                              const uint16_t* __restrict__ blen, uint64_t n,
+                                                              const uint64_t* __restrict__ off,
+                                                              uint64_t* __restrict__ rows,
+                                                              unsigned long long* __restrict__ tb) {
+  __shared__ uint32_t wc[BG_NT / 64];
+  const int lane = bg_lane(), w = bg_wave();
+  const uint64_t wbase = (uint64_t)blockIdx.x * CF_TILE + (uint64_t)w * 64 * CF_ITEMS;
+  uint64_t bal[CF_ITEMS];
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < CF_ITEMS; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    bal[k] = __ballot(i < n && flag[i]);
+    c += __popcll(bal[k]);
+  }
+  if (lane == 0) wc[w] = c;
+  __syncthreads();
+  uint64_t q = off[blockIdx.x];
+  for (int v = 0; v < w; ++v) q += wc[v];
+  const uint64_t lt = (1ULL << lane) - 1;
+  uint64_t ct = ~0ULL, cs = 0;  // lane 0's open (tile, bytes)
+#pragma unroll
+  for (int k = 0; k < CF_ITEMS; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * 64 + lane;
+    const bool mine = (bal[k] >> lane) & 1ULL;
+    const uint64_t qi = q + __popcll(bal[k] & lt);
+    uint32_t l = 0;
+    if (mine) {
+      rows[qi] = i;
+      l = blen[i];
+    }
+    if (bal[k]) {
+      const uint64_t t0 = q / BG_FMT_TILE;
+      const bool hi = mine && qi / BG_FMT_TILE != t0;
+      uint32_t s0 = hi ? 0u : l, s1 = hi ? l : 0u;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        s0 += __shfl_xor(s0, d, 64);
+        s1 += __shfl_xor(s1, d, 64);
+      }
+      if (lane == 0) {
+        if (ct != t0) {
+          if (ct != ~0ULL && cs) atomicAdd(&tb[ct], (unsigned long long)cs);
+          ct = t0;
+          cs = 0;
+        }
+        cs += s0;
+        if (s1) {
+          if (cs) atomicAdd(&tb[ct], (unsigned long long)cs);
+          ct = t0 + 1;
+          cs = s1;
+        }
+      }
+    }
+    q += __popcll(bal[k]);
+  }
+  if (lane == 0 && ct != ~0ULL && cs) atomicAdd(&tb[ct], (unsigned long long)cs);
 }
 
 // indices i with flag[i] != 0, in order (count -> scan -> write)
@@ -950,6 +1021,12 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   uint64_t* P = (uint64_t*)bg_alloc(c, 8 * (o.n + 1));
   uint8_t* flag = (uint8_t*)bg_alloc(c, R->n ? R->n : 1);
   if (!P || !flag) return BG_E_NOMEM;
+  // the kept rows' printed lengths, summed per format tile during the compaction (no
+  // formatter count pass) when the table keeps its remainders (row results print them)
+  uint16_t* blen = R->rest_len ? (uint16_t*)bg_alloc(c, 2 * (R->n ? R->n : 1)) : nullptr;
+  unsigned int* ovf = blen ? (unsigned int*)bg_alloc(c, 4) : nullptr;
+  if (blen && !ovf) return BG_E_NOMEM;
+  if (ovf) BG_HIP(c, hipMemsetAsync(ovf, 0, 4, c->stream));
   if (o.n) {
     BG_LAUNCH(c, "k_lengths", k_lengths, dim3(bg_blocks(o.n, BG_NT)), dim3(BG_NT), o.s, o.e, o.n, P);
     BG_HIP(c, hipGetLastError());
@@ -957,15 +1034,48 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   if ((rc = bg_scan_sum_u64(c, P, P, o.n, P + o.n))) return rc;
   if (R->n) {
     BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
-              R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag);
+              R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag, set->d_name_len, R->rest_len,
+              blen, ovf);
     BG_HIP(c, hipGetLastError());
   }
   uint64_t total = 0;
   uint64_t* rows = nullptr;
-  rc = bg_compact_flags(c, flag, R->n, &rows, &total);
+  uint64_t* tbytes = nullptr;
+  if (!blen) {
+    rc = bg_compact_flags(c, flag, R->n, &rows, &total);
+  } else {
+    const unsigned nb = bg_blocks(R->n, CF_TILE);
+    rc = count_scan_write(
+        c, nb,
+        [&](uint64_t* cnt) {
+          BG_LAUNCH(c, "k_compact_flags_count", k_compact_flags<false>, dim3(nb), dim3(BG_NT), flag, R->n, cnt,
+                    (const uint64_t*)nullptr, (uint64_t*)nullptr);
+        },
+        [&](uint64_t* off, uint64_t tot) -> int {
+          rows = (uint64_t*)bg_alloc(c, 8 * (tot ? tot : 1));
+          const uint64_t nt = bg_blocks(tot, BG_FMT_TILE);
+          tbytes = (uint64_t*)bg_alloc(c, 8 * (nt ? nt : 1));
+          if (!rows || !tbytes) return BG_E_NOMEM;
+          BG_HIP(c, hipMemsetAsync(tbytes, 0, 8 * (nt ? nt : 1), c->stream));
+          if (nb)
+            BG_LAUNCH(c, "k_compact_rows_bytes", k_compact_rows_bytes, dim3(nb), dim3(BG_NT), flag, blen, R->n,
+                      off, rows, (unsigned long long*)tbytes);
+          return 0;
+        },
+        &total);
+    unsigned int h = 0;  // a line over 64 KiB: the formatter counts instead
+    if (!rc) BG_HIP(c, hipMemcpyAsync(&h, ovf, 4, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) BG_HIP(c, hipStreamSynchronize(c->stream));
+    if (h) {
+      bg_release(c, tbytes);
+      tbytes = nullptr;
+    }
+  }
   if (rc) return rc;
   bg_release(c, P);
   bg_release(c, flag);
+  bg_release(c, blen);
+  bg_release(c, ovf);
   ivl_free(c, o);
   bg_result* res = new bg_result();
   res->ctx = c;
@@ -973,6 +1083,7 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   res->kind = RES_ROWS;
   res->n = total;
   res->rows = rows;
+  res->tbytes = tbytes;
   res->tab = ref;
   *out = res;
   bg_mark(c, "element-of");
