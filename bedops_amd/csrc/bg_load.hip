@@ -1954,8 +1954,8 @@ static int build_dictionary(bg_ctx* c, bg_set* s, std::map<std::string, int32_t>
   return 0;
 }
 
-// Three host round trips per call, whatever the number of inputs: run-record counts, run
-// records, final statuses.
+// Two host round trips per call, whatever the number of inputs: run-record counts (with the
+// first records), final statuses (a third, for the rest of the records, only past REC_SPEC).
 #include <chrono>
 static double hp_now() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1987,10 +1987,21 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
   }
   HP("scout");
-  // round trip 1: rows and record counts of every input
+  // round trip 1: rows and record counts of every input, with the first REC_SPEC records
+  // of each copied along speculatively (a genome's inputs have a few dozen: round trip 2,
+  // the rest of the records, is then skipped)
+  constexpr uint32_t REC_SPEC = 256;
+  std::vector<RunRec*> spec(n, nullptr);
+  for (int i = 0; i < n && !rc; ++i) {
+    const uint32_t k = std::min<uint32_t>(REC_SPEC, st[i].rc);
+    if (!st[i].ntiles || !k) continue;
+    spec[i] = (RunRec*)bg_pin_take(c, sizeof(RunRec) * k);
+    if (spec[i]) rc = bg_hip_ok(c, hipMemcpyAsync(spec[i], st[i].recs, sizeof(RunRec) * k, hipMemcpyDeviceToHost, c->stream));
+  }
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hctr, ctr, 64ull * n, hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
   HP("rt1");
+  bool rt2 = false;
   for (int i = 0; i < n && !rc; ++i) {
     LoadState& S = st[i];
     s->t[i]->n = S.ntiles ? hctr[8ull * i] : 0;
@@ -1998,14 +2009,19 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     if (nr > S.rc) { rc = bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input"); break; }
     S.nrec = nr;
     if (!nr) continue;
+    if (spec[i] && nr <= REC_SPEC) {
+      S.hrec = spec[i];
+      continue;
+    }
     RunRec* h = (RunRec*)bg_pin_take(c, sizeof(RunRec) * nr);
     if (!h) { rc = BG_E_NOMEM; break; }
     S.hrec = h;
+    rt2 = true;
     rc = bg_hip_ok(c, hipMemcpyAsync(h, S.recs, sizeof(RunRec) * nr, hipMemcpyDeviceToHost, c->stream));
   }
-  // round trip 2: the run records
+  // round trip 2: the run records (only when an input has more than REC_SPEC)
   HP("rec_copy");
-  if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  if (!rc && rt2) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
   HP("rt2");
   for (int i = 0; i < n && !rc; ++i) rc = runs_one(c, i, inputs[i], s->t[i], st[i]);
   bg_mark(c, "scout");
