@@ -101,9 +101,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(k, "version")) { printf("bedmap\n  version:  %s\n", BEDOPS_AMD_VERSION); return EXIT_SUCCESS; }
     else if (!strcmp(k, "ec") || !strcmp(k, "header")) {
       ec = 1;
-      if (!strcmp(k, "ec")) check = 1;
+      check = 1; /* --header is --ec: errorCheck_ (bedmap/src/Input.hpp:104-106) */
     }
-    else if (!strcmp(k, "faster") || !strcmp(k, "sweep-all")) {}
+    else if (!strcmp(k, "faster")) o.faster = 1;
+    else if (!strcmp(k, "sweep-all")) {}  /* reads the rest of the map file; no output effect */
     else if (!strcmp(k, "delim")) {
       if (set_delim) arg_error("--delim specified multiple times");
       if (a >= argc) arg_error("No output delimiter given");
@@ -271,6 +272,9 @@ int main(int argc, char** argv) {
     else if (is_bp || count == 0) o.criterion = BG_OVR_BP;
   }
   if (o.n_ops == 0) arg_error("No processing option specified (ie; --max).");
+  if (o.faster && !(o.criterion == BG_OVR_BP || o.criterion == BG_OVR_RANGE || o.criterion == BG_OVR_FRAC_BOTH ||
+                    o.criterion == BG_OVR_EXACT))  /* Input.hpp:349 */
+    arg_error("--faster compatible with --range, --bp-ovr, --fraction-both, and --exact only");
   int nf = argc - a;
   if (nf < 1 || nf > 2) arg_error("Need one or two input files");
   for (int i = a; i < argc; ++i) {
@@ -336,7 +340,9 @@ int main(int argc, char** argv) {
   /* --ec: the reference file is B3Rest, the map file B3Rest/B4Rest/B5Rest by the
    * operations' MapFields (Input.hpp:401-418, Bedmap.cpp:601-655) */
   const int mapfields = need5 ? 5 : (need4 ? 4 : 3);
-  if (check) ec_check(PROG, ctx, argv[a], &tr, nf == 1 ? mapfields : 3, 1);
+  /* --faster checks for nested rows too (nestCheck = ProcessMode, Bedmap.cpp:622, 670) */
+  const int nest = o.faster ? BG_CHECK_NEST : 0;
+  if (check) ec_check(PROG, ctx, argv[a], &tr, nf == 1 ? mapfields : 3, 1 | nest);
   if (ec) {
     apply_ec_header(&tr);
     in[0].data = tr.data;
@@ -365,7 +371,7 @@ int main(int argc, char** argv) {
   }
   {
     if (read_input_chrom(ctx, argv[a + 1], chrom, check || ec, &tm, &in[1])) arg_error("Unable to read the map file");
-    if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1);
+    if (check) ec_check(PROG, ctx, argv[a + 1], &tm, mapfields, 1 | nest);
     if (ec) {
       apply_ec_header(&tm);
       in[1].data = tm.data;

@@ -206,7 +206,7 @@ int main(int argc, char** argv) {
     const char* nx = argv[a];
     if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) {
       ec = 1;
-      if (!strcmp(nx, "--ec")) check = 1;
+      check = 1; /* --header is --ec: errorCheck_ (bedops/src/Input.hpp:77-80, closestfeats/src/Input.hpp:64-65) */
     } else if (!strcmp(nx, "--chrom")) {
       if (has_chrom) bad_input("--chrom specified multiple times.");
       if (++a >= argc) bad_input("No value for --chrom given.");

@@ -361,7 +361,7 @@ static inline void ec_check(const char* prog, bg_ctx* ctx, const char* fn, const
   if (rc) die_ctx(prog, ctx, rc);
   if (!cr.row) return;
   char m[2048], b[4096];
-  bg_check_message(t->data + cr.line_off, cr.line_len, cr.code, nfields, has_rest, m, sizeof(m));
+  bg_check_message(t->data + cr.line_off, cr.line_len, cr.code, nfields, has_rest & 1, m, sizeof(m));
   snprintf(b, sizeof(b), "in %s\n%s\nSee row: %llu", fn, m, (unsigned long long)cr.row);
   die_msg(prog, b);
 }

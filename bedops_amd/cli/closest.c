@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
     if (!strcmp(nx, "--version")) { printf("closest-features\n  version:  %s\n", BEDOPS_AMD_VERSION); return EXIT_SUCCESS; }
     if (!strcmp(nx, "--ec") || !strcmp(nx, "--header")) {
       ec = 1;
-      if (!strcmp(nx, "--ec")) check = 1;
+      check = 1; /* --header is --ec: errorCheck_ (bedops/src/Input.hpp:77-80, closestfeats/src/Input.hpp:64-65) */
     }
     else if (!strcmp(nx, "--no-overlaps")) o.no_overlaps = 1;
     else if (!strcmp(nx, "--delim")) {

@@ -23,7 +23,7 @@ enum {
   BGC_M_SIGNEXP, BGC_M_CHAR, BGC_ONLY5, BGC_M_EMPTY, BGC_M_ENDMINUS,
   BGC_ST_TABS, BGC_ST_CHAR, BGC_ST_TWO, BGC_ST_EMPTY, BGC_REST_LONG,
   BGC_UNSORTED_CHR, BGC_UNSORTED_START, BGC_UNSORTED_END, BGC_UNSORTED_REST, BGC_END_LE_START,
-  BGC_HEADER_LATE
+  BGC_HEADER_LATE, BGC_NESTED
 };
 
 #define BGC_MAXCHROMSIZE 127u          // TOKEN_CHR_MAX_LENGTH (BEDOPS.Constants.hpp:32)
@@ -197,8 +197,10 @@ BGC_HD int bgc_line(const char* l, uint32_t sz, int nfields, int has_rest, BgcRo
 }
 
 // the order checks against the previous data row, then end > start (:594-624)
+// (nest: bedmap --faster's nestCheck, :612-615: an end below the previous row's end on the
+// same chromosome, after the sort checks)
 BGC_HD int bgc_order(const char* p, uint32_t pn, const BgcRow& P, const char* l, uint32_t n,
-                     const BgcRow& R, int has_rest) {
+                     const BgcRow& R, int has_rest, int nest = 0) {
   int cmp = 0;
   {  // strcmp of the chromosome names
     const uint32_t m = P.chrom_len < R.chrom_len ? P.chrom_len : R.chrom_len;
@@ -223,6 +225,7 @@ BGC_HD int bgc_order(const char* p, uint32_t pn, const BgcRow& P, const char* l,
         if (c2 < 0) return BGC_UNSORTED_REST;
       }
     }
+    if (nest && R.end < P.end) return BGC_NESTED;
   }
   (void)pn;
   if (R.end <= R.start) return BGC_END_LE_START;

@@ -37,7 +37,7 @@ struct CkArgs {
   const char* t;
   uint64_t nb;
   const uint64_t* base;  // newlines before each tile (exclusive scan)
-  int nfields, has_rest;
+  int nfields, has_rest, nest;
   uint64_t* first_data;  // pass 1 out / pass 2 in: first non-header line (1-based)
   unsigned long long* key;  // pass 2 out: min (line << 8 | code)
   uint64_t target;       // pass 3: the failing line
@@ -84,7 +84,7 @@ __device__ __forceinline__ void ck_one(const CkArgs& A, uint64_t row, uint64_t l
     BgcRow P;
     const uint32_t pn = (uint32_t)(ls - 1 - ps);
     if (bgc_line(A.t + ps, pn, A.nfields, A.has_rest, P) == BGC_OK)
-      err = bgc_order(A.t + ps, pn, P, A.t + ls, (uint32_t)(le - ls), R, A.has_rest);
+      err = bgc_order(A.t + ps, pn, P, A.t + ls, (uint32_t)(le - ls), R, A.has_rest, A.nest);
   } else if (R.end <= R.start) {
     err = BGC_END_LE_START;
   }
@@ -134,7 +134,8 @@ extern "C" int bg_check(bg_ctx* c, const bg_input* in, int nfields, int has_rest
   A.nb = nb;
   A.base = base;
   A.nfields = nfields;
-  A.has_rest = has_rest;
+  A.has_rest = has_rest & 1;
+  A.nest = (has_rest & BG_CHECK_NEST) != 0;
   A.first_data = w;
   A.key = (unsigned long long*)(w + 1);
   A.target = 0;
@@ -175,6 +176,7 @@ extern "C" int bg_check_message(const char* line, uint64_t len, int code, int nf
                                 char* buf, uint64_t cap) {
   if (!buf || cap == 0) return BG_E_ARG;
   BgcRow R;
+  has_rest &= 1;
   if (line) (void)bgc_line(line, (uint32_t)len, nfields, has_rest, R);
   else R.bad = 0;
   char ch[2] = {(char)R.bad, 0};
@@ -235,6 +237,7 @@ extern "C" int bg_check_message(const char* line, uint64_t len, int code, int nf
     case BGC_UNSORTED_REST: m = "Bed file not sorted by information following the 3rd column (columns 1-3 equal to previous row)."; break;
     case BGC_END_LE_START: m = "End coordinates must be greater than start coordinates."; break;
     case BGC_HEADER_LATE: m = "Header found but should be at top of file."; break;
+    case BGC_NESTED: m = "Fully nested component found."; break;
     default: return BG_E_ARG;
   }
   snprintf(buf, cap, "%s", m);

@@ -744,6 +744,9 @@ __device__ __forceinline__ bool elem_better(const FmtArgs& A, int op, uint64_t m
   if (x != y) return mx ? x > y : x < y;
   if (A.s2[m] != A.s2[b]) return mx ? A.s2[m] > A.s2[b] : A.s2[m] < A.s2[b];
   if (A.e2[m] != A.e2[b]) return mx ? A.e2[m] > A.e2[b] : A.e2[m] < A.e2[b];
+  // --faster: rows join the set in file order (no fixWindow), and equal rows join and leave
+  // the deque together: the set keeps the first in file order
+  if (A.crit == BG_OVR_FAST) return m < b;
   const int c = bg_frest_cmp(A.text2, A.rest_off2, A.rest_len2, A.mapfields, m, b);
   return c != 0 ? c < 0 : am < ab;
 }
@@ -1259,7 +1262,7 @@ static void fill_args(bg_result* r, FmtArgs& A) {
       A.maddr = r->maddr;
       A.n2 = M->n;
       A.lrows = r->lrows;
-      A.crit = r->mopts.criterion;
+      A.crit = r->mopts.faster ? BG_OVR_FAST : r->mopts.criterion;  // --faster: the deque is the window
       A.ovr = (int64_t)r->mopts.overlap_bp;
       A.range = (int64_t)r->mopts.range_bp;
       A.perc = r->perc;

@@ -106,9 +106,12 @@ struct RowStr {  // in-class string chunks of a live row: chrom, id, rest, id + 
 
 // host replay of sweep overload 2 (WindowSweepImpl.cpp:168-256) over the keyed rows; addr[m]
 // = the simulated address of map row m's object
+// (fast_crit >= 0: bedmap --faster, the sweep runs with that criterion's Ref2Map / Map2Ref,
+// bg_fs_r2m / bg_fs_m2r)
 static void heap_replay(const int64_t* RS, const int64_t* RE, uint64_t nr, const uint8_t* rflag,
                         bool ref_obj_in_class, const int64_t* MS, const int64_t* ME, uint64_t nm,
-                        const uint8_t* mflag, bool ranged, int64_t range, int64_t* addr) {
+                        const uint8_t* mflag, bool ranged, int64_t range, int64_t* addr, int fast_crit,
+                        int64_t ovr, double perc) {
   HeapClass H;
   std::unordered_map<uint64_t, RowStr> mstr;
   RowStr rstr[2];
@@ -169,7 +172,11 @@ static void heap_replay(const int64_t* RS, const int64_t* RE, uint64_t nr, const
   map_new(0);
   for (uint64_t r = 0; r < nr; ++r) {
     ref_new(r + 1);  // ++refStart
-    while (wh < win.size() && dist(MS[win[wh]], ME[win[wh]], RS[r], RE[r]) < 0) map_del(win[wh++]);
+    auto pop = [&](uint64_t w) {
+      return fast_crit >= 0 ? bg_fs_m2r(fast_crit, ovr, range, perc, MS[w], ME[w], RS[r], RE[r]) < 0
+                            : dist(MS[w], ME[w], RS[r], RE[r]) < 0;
+    };
+    while (wh < win.size() && pop(win[wh])) map_del(win[wh++]);
     if (wh > 4096 && wh * 2 > win.size()) {
       win.erase(win.begin(), win.begin() + (ptrdiff_t)wh);
       wh = 0;
@@ -183,7 +190,8 @@ static void heap_replay(const int64_t* RS, const int64_t* RE, uint64_t nr, const
         m = mi++;
         map_new(mi);  // ++mapFromStart
       }
-      const int v = dist(RS[r], RE[r], MS[m], ME[m]);
+      const int v = fast_crit >= 0 ? bg_fs_r2m(fast_crit, ovr, range, perc, RS[r], RE[r], MS[m], ME[m])
+                                   : dist(RS[r], RE[r], MS[m], ME[m]);
       if (v == 0) win.push_back(m);
       else if (v < 0) {
         cache = (int64_t)m;
@@ -196,9 +204,105 @@ static void heap_replay(const int64_t* RS, const int64_t* RE, uint64_t nr, const
   }
 }
 
+// one file (R == M): sweep overload 1 (WindowSweepImpl.cpp:66-162; Overlapping
+// specialisation WindowSweepImpl.specialize.cpp:40-138, same calls): the iterator's
+// constructor reads row 0 and each ++start the next row; rows are deleted as they leave the
+// deque (pops, and the whole deque when a reference row runs past its end)
+static void heap_replay_single(const int64_t* S, const int64_t* E, uint64_t n, const uint8_t* mflag, bool ranged,
+                               int64_t range, int64_t* addr, int fast_crit, int64_t ovr, double perc) {
+  HeapClass H;
+  std::unordered_map<uint64_t, RowStr> mstr;
+  auto make = [&](uint8_t f, RowStr& s) {
+    for (int q : {0, 1, 2, 3})
+      s.a[q] = (f >> q) & 1 ? H.get() : -1;
+  };
+  auto drop = [&](const RowStr& s) {
+    for (int q : {2, 3, 1, 0})
+      if (s.a[q] >= 0) H.put(s.a[q]);
+  };
+  auto row_new = [&](uint64_t m) {  // m == n: the read past the last row (never freed)
+    addr[m] = H.get();
+    const uint8_t f = m < n ? mflag[m] : 0;
+    if (f) make(f, mstr[m]);
+  };
+  auto row_del = [&](uint64_t m) {
+    if (mflag[m]) {
+      auto it = mstr.find(m);
+      drop(it->second);
+      mstr.erase(it);
+    }
+    H.put(addr[m]);
+  };
+  auto dist = [&](uint64_t a, uint64_t b) -> int {  // the sweep distance (a, b)
+    const int64_t as = S[a], ae = E[a], bs = S[b], be = E[b];
+    const int64_t ca = as >> BG_KEY_SHIFT, cb = bs >> BG_KEY_SHIFT;
+    if (ca != cb) return ca < cb ? -1 : 1;
+    if (ranged) {
+      if (as < be) return (ae + range > bs) ? 0 : -1;
+      return (be + range > as) ? 0 : 1;
+    }
+    const int64_t mn = as > bs ? as : bs, mx = ae < be ? ae : be;
+    if (mx > mn) return 0;
+    return as < bs ? -1 : 1;
+  };
+  auto r2m = [&](uint64_t r, uint64_t b) {
+    return fast_crit >= 0 ? bg_fs_r2m(fast_crit, ovr, range, perc, S[r], E[r], S[b], E[b]) : dist(r, b);
+  };
+  auto m2r = [&](uint64_t w, uint64_t r) {
+    return fast_crit >= 0 ? bg_fs_m2r(fast_crit, ovr, range, perc, S[w], E[w], S[r], E[r]) : dist(w, r);
+  };
+  std::vector<uint64_t> win;
+  size_t wh = 0, index = 0;
+  uint64_t next = 0;
+  int64_t cache = -1;
+  bool reset = true;
+  row_new(0);
+  for (;;) {
+    if (!(next < n || cache >= 0 || win.size() > wh)) break;
+    if (!reset) {
+      const uint64_t cur = win[wh + index];
+      while (win.size() > wh && m2r(win[wh], cur) < 0) {
+        row_del(win[wh++]);
+        --index;
+      }
+      if (wh > 4096 && wh * 2 > win.size()) {
+        win.erase(win.begin(), win.begin() + (ptrdiff_t)wh);
+        wh = 0;
+      }
+    } else if (next >= n && cache < 0) {
+      break;
+    }
+    while (cache >= 0 || next < n) {
+      uint64_t b;
+      if (cache >= 0) {
+        b = (uint64_t)cache;
+        cache = -1;
+      } else {
+        b = next++;
+        row_new(next);  // ++start
+      }
+      if (win.size() == wh || reset || r2m(win[wh + index], b) == 0) {
+        if (reset) {
+          reset = false;
+          index = 0;
+          while (win.size() > wh) row_del(win[wh++]);
+          win.clear();
+          wh = 0;
+        }
+        win.push_back(b);
+      } else {
+        cache = (int64_t)b;
+        break;
+      }
+    }
+    reset = ++index >= win.size() - wh;
+  }
+}
+
 // the simulated address of every map row, on the device (*out, bg_alloc'ed), for bg_map
+// (R == M: one file)
 int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, int fields, bool ranged,
-                 int64_t range, int64_t** out) {
+                 int64_t range, int64_t** out, int fast_crit, int64_t ovr, double perc) {
   *out = nullptr;
   const uint64_t nr = R->n, nm = M->n;
   std::vector<int64_t> hRS(nr), hRE(nr), hMS(nm), hME(nm);
@@ -250,8 +354,11 @@ int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, i
   for (uint64_t r = 0; r < nr; ++r)  // the reference file is read as B3Rest (Bedmap.cpp:624-654)
     rflag[r] = (uint8_t)((in(name_len(hRS[r])) ? 1 : 0) | (in(hrl[r]) ? 4 : 0));
   std::vector<int64_t> addr(nm + 1);
-  heap_replay(hRS.data(), hRE.data(), nr, rflag.data(), hs_chunk(32) == K, hMS.data(), hME.data(), nm,
-              mflag.data(), ranged, range, addr.data());
+  if (R == M)
+    heap_replay_single(hMS.data(), hME.data(), nm, mflag.data(), ranged, range, addr.data(), fast_crit, ovr, perc);
+  else
+    heap_replay(hRS.data(), hRE.data(), nr, rflag.data(), hs_chunk(32) == K, hMS.data(), hME.data(), nm,
+              mflag.data(), ranged, range, addr.data(), fast_crit, ovr, perc);
   int64_t* d = (int64_t*)bg_alloc(c, 8 * (nm ? nm : 1));
   if (!d) return BG_E_NOMEM;
   if (nm) BG_HIP(c, hipMemcpyAsync(d, addr.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));

@@ -23,6 +23,10 @@
 #define BG_KEY_SHIFT 40
 #define BG_COORD_MASK ((1LL << BG_KEY_SHIFT) - 1)
 #define BG_MAX_COORD 999999999999ULL
+// the largest coordinate a keyed row holds: without --ec the reference reads any %lu
+// (Bed.hpp:244-255) and prints it back, so coordinates above MAX_COORD_VALUE
+// (BEDOPS.Constants.hpp:36) but below 2^40 are kept (only --ec rejects them, bg_check)
+#define BG_KEY_COORD_MAX ((1ULL << BG_KEY_SHIFT) - 1)
 #define BG_CHR_MAX 127
 
 // ---------------------------------------------------------------------------------
@@ -442,8 +446,13 @@ __device__ __forceinline__ uint64_t merge_path_xfirst(const int64_t* X, uint64_t
 // bedmap: is map row [ms, me) in S(r) of reference row [s, e)? (keys of one chromosome;
 // criteria of data/bed/BedDistances.hpp, see bg_map.hip). Rows outside the sweep's
 // Overlapping(0) window never are, except under --range (RangedDist sweeps too).
+// BG_OVR_FAST (internal, never in bg_map_opts): bedmap --faster windows, whose members are
+// the sweep's own deque (bg_faster.hip); every candidate in the window range is a member
+// once bg_map_live has said it is in the deque
+#define BG_OVR_FAST 99
 __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, double perc,
                                           int64_t s, int64_t e, int64_t ms, int64_t me) {
+  if (crit == BG_OVR_FAST) return true;
   if (crit == BG_OVR_RANGE) return (s < me) ? (e + range > ms) : (me + range > s);
   const int64_t ov = min(e, me) - max(s, ms);
   if (ov <= 0) return false;
@@ -457,6 +466,84 @@ __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, 
   if (crit == BG_OVR_FRAC_REF) return fr;
   if (crit == BG_OVR_FRAC_EITHER) return fm || fr;
   return fm && fr;
+}
+
+// bedmap --faster: the distance the sweep itself runs with is the criterion's (Bedmap.cpp:
+// 287-290, 728-745; no BedBaseVisitor re-test). Ref2Map(a = reference row, b = map row) and
+// Map2Ref(b, a) of data/bed/BedDistances.hpp, on keyed rows (chromosome ids are in strcmp
+// order, so comparing keys compares chromosomes first):
+//   Overlapping(ovr)  operator() :97-115, both directions the same function;
+//   RangedDist(R)     operator() :57-64;
+//   PercentOverlapBoth Ref2Map :262-272 over PercentOverlapMapping::Ref2Map :141-180 (the
+//                     reference's double arithmetic), Map2Ref = -Ref2Map :278-281;
+//   Exact             Ref2Map :300-309, Map2Ref = -Ref2Map :313-315.
+// Overlapping's last tie (equal rows overlapping by less than ovr) compares heap addresses
+// (:108-110); such a pair never satisfies the criterion, and whichever way the tie falls the
+// sweep's deque ends up the same (the row is deleted now or when the next reference row
+// passes it; no row it holds back could join the current window), so -1 is returned.
+__host__ __device__ __forceinline__ int bg_fs_ovl(int64_t as, int64_t ae, int64_t bs, int64_t be, int64_t ovr) {
+  const int64_t ca = as >> BG_KEY_SHIFT, cb = bs >> BG_KEY_SHIFT;
+  if (ca != cb) return ca > cb ? 1 : -1;
+  const int64_t mn = as > bs ? as : bs, mx = ae < be ? ae : be;
+  if (mx > mn) {
+    if (mx - mn >= ovr) return 0;
+    if (as != bs) return as < bs ? -1 : 1;
+    if (ae != be) return ae < be ? -1 : 1;
+    return -1;
+  }
+  return as < bs ? -1 : 1;
+}
+__host__ __device__ __forceinline__ int bg_fs_ranged(int64_t as, int64_t ae, int64_t bs, int64_t be, int64_t d) {
+  const int64_t ca = as >> BG_KEY_SHIFT, cb = bs >> BG_KEY_SHIFT;
+  if (ca != cb) return ca > cb ? 1 : -1;
+  if (as < be) return (ae + d > bs) ? 0 : -1;
+  return (be + d > as) ? 0 : 1;
+}
+// PercentOverlapMapping::Ref2Map(ref = a, map = b)
+__host__ __device__ __forceinline__ int bg_fs_pmap(int64_t as, int64_t ae, int64_t bs, int64_t be, double perc) {
+  const int64_t ca = as >> BG_KEY_SHIFT, cb = bs >> BG_KEY_SHIFT;
+  if (ca != cb) return ca > cb ? 1 : -1;
+  if (ae < bs) return -1;
+  if (be < as) return 1;
+  if (perc <= 2.220446049250313e-16) return 0;
+  const double tl = (double)(uint64_t)(be - bs);
+  double sz;
+  int dir;
+  if (as <= bs) {
+    sz = (double)(uint64_t)((ae >= be) ? be - bs : ae - bs);
+    dir = -1;
+  } else {
+    sz = (double)(uint64_t)((ae >= be) ? be - as : ae - as);
+    dir = 1;
+  }
+  return (sz / tl >= perc) ? 0 : dir;
+}
+__host__ __device__ __forceinline__ int bg_fs_r2m(int crit, int64_t ovr, int64_t range, double perc, int64_t rs,
+                                                  int64_t re, int64_t ms, int64_t me) {
+  switch (crit) {
+    case BG_OVR_BP: return bg_fs_ovl(rs, re, ms, me, ovr);
+    case BG_OVR_RANGE: return bg_fs_ranged(rs, re, ms, me, range);
+    case BG_OVR_FRAC_BOTH: {
+      const int v1 = bg_fs_pmap(rs, re, ms, me, perc);
+      if (v1) return v1;
+      return -bg_fs_pmap(ms, me, rs, re, perc);
+    }
+    default: {  // BG_OVR_EXACT
+      const int64_t ca = rs >> BG_KEY_SHIFT, cb = ms >> BG_KEY_SHIFT;
+      if (ca != cb) return ca < cb ? -1 : 1;
+      if (rs != ms) return rs < ms ? -1 : 1;
+      if (re != me) return re < me ? -1 : 1;
+      return 0;
+    }
+  }
+}
+__host__ __device__ __forceinline__ int bg_fs_m2r(int crit, int64_t ovr, int64_t range, double perc, int64_t ms,
+                                                  int64_t me, int64_t rs, int64_t re) {
+  switch (crit) {
+    case BG_OVR_BP: return bg_fs_ovl(ms, me, rs, re, ovr);
+    case BG_OVR_RANGE: return bg_fs_ranged(ms, me, rs, re, range);
+    default: return -bg_fs_r2m(crit, ovr, range, perc, rs, re, ms, me);
+  }
 }
 
 // bedmap with zero-length rows: is map row m in reference row r's sweep window at all?
@@ -602,7 +689,10 @@ __device__ __forceinline__ void bg_report(bg_dstatus* st, uint64_t row, int code
 // bg_heap.hip: the reference's heap address of every map row (device array), and whether
 // adjacent map rows tie on (start, end) [+ full_rest()]
 int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, int fields, bool ranged,
-                 int64_t range, int64_t** out);
+                 int64_t range, int64_t** out, int fast_crit = -1, int64_t ovr = 0, double perc = 0.0);
+// bedmap --faster windows (bg_faster.hip)
+int bg_faster_windows(bg_ctx* c, const bg_table* R, const bg_table* M, int crit, int64_t ovr, int64_t range,
+                      double perc, bool single, uint64_t* wlo, uint64_t* whi, int64_t* zin, int64_t* zout);
 int bg_heap_ties(bg_ctx* c, const bg_table* M, int fields, bool rest, bool* any);
 // the address of map row m (row order without a replay)
 __device__ __forceinline__ int64_t bg_maddr(const int64_t* addr, uint64_t m) {

@@ -698,13 +698,14 @@ __device__ __forceinline__ bool parse_score_fast(const uint8_t* buf, const uint3
   return true;
 }
 
-// runs that can occur in each tile: [runlo, runhi] by position
+// runs that can occur in each tile of TB bytes: [runlo, runhi] by position
+template <int TB = TT>
 __global__ void k_run_range(RunTable R, uint32_t ntiles, uint32_t* __restrict__ runlo,
                             uint32_t* __restrict__ runhi) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
-  runlo[t] = run_of(R, (int64_t)t * TT, 0, R.n - 1);
-  runhi[t] = run_of(R, (int64_t)t * TT + TT - 1, 0, R.n - 1);
+  runlo[t] = run_of(R, (int64_t)t * TB, 0, R.n - 1);
+  runhi[t] = run_of(R, (int64_t)t * TB + TB - 1, 0, R.n - 1);
 }
 
 // keys (+ rest span / score) of one parsed row; false if the chromosome does not match
@@ -713,7 +714,7 @@ __device__ __forceinline__ void emit_row(const RunTable& R, uint32_t run, int64_
                                          uint64_t start, uint64_t end, int64_t* KS, int64_t* KE,
                                          bg_dstatus* st, int64_t& key, int64_t& mlen) {
   if (R.info[run].pos == ls) R.row[run] = r;
-  if (end > BG_MAX_COORD || start > end) bg_report(st, r, ERR_RANGE);
+  if (end > BG_KEY_COORD_MAX || start > end) bg_report(st, r, ERR_RANGE);
   if (start == end) atomicOr(&st->flags, 2ULL);
   mlen = max(mlen, (int64_t)(end - start));
   const int64_t g = (int64_t)R.info[run].gid << BG_KEY_SHIFT;
@@ -1006,7 +1007,7 @@ __device__ __forceinline__ bool set_row(const BufT& B, const uint16_t* lst, cons
     start = Ln.start;
     end = Ln.end;
   }
-  if (end > BG_MAX_COORD || start > end) bg_report(st, 0, ERR_RANGE);
+  if (end > BG_KEY_COORD_MAX || start > end) bg_report(st, 0, ERR_RANGE);
   if (start == end) atomicOr(&st->flags, 2ULL);
   const int64_t g = (int64_t)I.gid << BG_KEY_SHIFT;
   ks = g | (int64_t)(start & BG_COORD_MASK);
@@ -1475,6 +1476,200 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
   }
 }
 
+// ---- k_parse_set_w: one wavefront per 4 KiB sub-tile -----------------------------------
+// The same parse and staging as k_parse_set_n, with the tile cut to TW = 4 KiB and owned by
+// ONE wave (64 lanes x 64 bytes): every exchange of the 2-wave kernel (line-start counts, the
+// per-round max of ends, the last key, the opening counts) becomes a DPP step or a readlane
+// into a scalar register, and the workgroup barriers compile to nothing (the workgroup is
+// one wave). The halo mask words and the halo's first '\n' come from the lanes that loaded
+// the halo (a lane pair per mask word, a ballot for the '\n'), without LDS atomics. Sub-tile
+// u stages its local components in slots [u * SCAP_W, u * SCAP_W + SCAP_W) and has its own
+// SetTiles entry: k_set_count / k_set_write treat sub-tiles as tiles.
+#define TW 4096
+#define SCAP_W 256
+#define LCAP_W 512  // lines per sub-tile (4 KiB of lines averaging >= 8 bytes; more: refused)
+struct ParseLdsW {
+  __attribute__((aligned(16))) uint8_t buf[HB + TW + HA + 32];
+  uint32_t wsm[TW / 32 + (HA + 32) / 32 + 1];
+  uint16_t lst[LCAP_W + 1];
+};
+
+__device__ __forceinline__ uint32_t wave_readlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t wave_readlane(uint64_t v, int l) {
+  return ((uint64_t)wave_readlane((uint32_t)(v >> 32), l) << 32) | wave_readlane((uint32_t)v, l);
+}
+
+// 4 dwords -> '\n' flags of their 16 bytes (bit j = byte j)
+__device__ __forceinline__ uint32_t nl16(const uint4 a) {
+  return bgp_group4(nl_mask4(a.x)) | (bgp_group4(nl_mask4(a.y)) << 4) | (bgp_group4(nl_mask4(a.z)) << 8) |
+         (bgp_group4(nl_mask4(a.w)) << 12);
+}
+__device__ __forceinline__ uint32_t ws16(const uint4 a) { return bgp_ws8(a.x, a.y) | (bgp_ws8(a.z, a.w) << 8); }
+
+// prologue of sub-tile t0: LDS staging, whitespace masks, line starts (S.lst). Returns the
+// number of owned lines (> LCAP_W: error reported); last_end as tile_prologue_n.
+__device__ __forceinline__ uint32_t prologue_w(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
+                                               ParseLdsW& S, int64_t& last_end, bg_dstatus* st) {
+  constexpr int HL = (HA + 32) / 16;  // lanes holding 16 halo bytes after the sub-tile
+  static_assert(HL % 2 == 0 && HL < 63, "halo lanes");
+  const int lane = threadIdx.x;
+  uint4 v[4];
+  const int64_t b = t0 + 64 * lane;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = load16(txt, b + 16 * i, nb);
+  uint4 vh = make_uint4(0, 0, 0, 0);
+  if (lane < HL) vh = load16(txt, t0 + TW + 16 * lane, nb);
+  else if (lane == 63) vh = load16(txt, t0 - HB, nb);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
+  if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
+  else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
+  S.wsm[2 * lane] = ws16(v[0]) | (ws16(v[1]) << 16);
+  S.wsm[2 * lane + 1] = ws16(v[2]) | (ws16(v[3]) << 16);
+  {  // halo: lane pairs make its mask words; its first '\n' by ballot
+    const uint32_t h = ws16(vh);
+    const uint32_t hn = __shfl_down(h, 1, 64);
+    if (lane < HL && !(lane & 1)) S.wsm[TW / 32 + lane / 2] = h | (hn << 16);
+    if (lane == HL) S.wsm[TW / 32 + HL / 2] = 0;  // read past the halo by mask_window
+  }
+  const uint32_t hm = lane < HL ? nl16(vh) : 0u;
+  const uint64_t hb = __ballot(hm != 0);
+  int64_t hnl = -1;
+  if (hb) {
+    const int f = __builtin_ctzll(hb);
+    hnl = TW + 16 * f + __builtin_ctz(wave_readlane(hm, f));
+  }
+  const bool has0 = t0 == 0 || (wave_readlane(vh.w, 63) >> 24) == '\n';
+  const bool endnl = (wave_readlane(v[3].w, 63) >> 24) == '\n';
+  uint32_t n0 = nl16(v[0]) | (nl16(v[1]) << 16), n1 = nl16(v[2]) | (nl16(v[3]) << 16);
+  if (lane == 63) n1 &= 0x7FFFFFFFu;  // a '\n' in the last byte starts the next sub-tile's line
+  const uint32_t cnt = (uint32_t)(__popc(n0) + __popc(n1));
+  const uint32_t inc = wave_incl_scan(cnt, OpSum());
+  const uint32_t L = wave_readlane(inc, 63) + (has0 ? 1u : 0u);
+  if (L > LCAP_W) {
+    if (lane == 0) bg_report(st, 0, ERR_PARSE);
+    return L;
+  }
+  uint32_t o = inc - cnt + (has0 ? 1u : 0u);
+  if (lane == 0 && has0) S.lst[0] = 0;
+  for (uint32_t m = n0; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + bgp_ctz(m) + 1);
+  for (uint32_t m = n1; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + 32 + bgp_ctz(m) + 1);
+  __syncthreads();  // (one wave: orders the LDS writes above before the reads below)
+  TileText T{txt, S.buf, t0 - HB, t0 + TW + HA, nb};
+  last_end = L == 0 ? -1 : endnl ? t0 + TW - 1 : (hnl >= 0 ? t0 + hnl : find_nl(T, t0 + TW + HA + 32));
+  return L;
+}
+
+// the rounds of one sub-tile: 64 lines per round, one per lane, in line order (V as
+// set_rounds_n). kl: K (+1 form) of the sub-tile's largest row key.
+template <typename V>
+__device__ __forceinline__ void set_rounds_w(const ParseLdsW& S, const TileText& T, const RunTable& R,
+                                             uint32_t rl, uint32_t rh, int64_t t0, uint32_t L,
+                                             int64_t last_end, int64_t gbase, uint64_t base,
+                                             int64_t* __restrict__ LCS, int64_t* __restrict__ LCE,
+                                             uint64_t& nc, V& carry_e, V& kl, bg_dstatus* st) {
+  constexpr bool NARROW = sizeof(V) == 4;
+  const int lane = threadIdx.x;
+  const uint64_t lt = (1ULL << lane) - 1;
+  V carry_k = 0;
+  const uint32_t rounds = (L + 63) / 64;
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t k = j * 64 + lane;
+    int64_t ks = 0, ke = 0;
+    const bool valid = k < L && set_row<NARROW, true>(S, S.lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
+    V K = 0, E = 0;
+    if (valid) {
+      if (NARROW) {
+        const uint64_t ce = (uint64_t)(ke & BG_COORD_MASK) + 1;
+        if (ce >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
+        K = (V)((uint64_t)(ks & BG_COORD_MASK) + 1);
+        E = (V)ce;
+      } else {
+        K = (V)ks + 1;
+        E = (V)ke + 1;
+      }
+    }
+    const V ie = wave_incl_max_v(E);
+    const V prevK = lane ? wave_shr1_v(K) : carry_k;
+    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
+    const V ex_e = max(carry_e, wave_shr1_v(ie));
+    const bool open = valid && K > ex_e;
+    const uint64_t bal = __ballot(open);
+    const uint64_t pos = nc + __popcll(bal & lt);
+    if (open && pos < SCAP_W) {
+      if (NARROW) {
+        reinterpret_cast<uint32_t*>(LCS + base)[pos] = (uint32_t)(K - 1);
+        if (pos > 0) reinterpret_cast<uint32_t*>(LCE + base)[pos - 1] = (uint32_t)(ex_e - 1);
+      } else {
+        LCS[base + pos] = ks;
+        if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);
+      }
+    }
+    if (j + 1 == rounds) {  // the largest K: the last line's, or the one before when the last
+                            // line is the file's dropped unterminated tail
+      const int ll = (int)(L - 1 - j * 64);
+      const V k1 = wave_readlane(K, ll);
+      kl = k1 ? k1 : (ll > 0 ? wave_readlane(K, ll - 1) : carry_k);
+    }
+    carry_e = max(carry_e, wave_readlane(ie, 63));
+    carry_k = wave_readlane(K, 63);
+    nc += (uint64_t)__popcll(bal);
+  }
+}
+
+__global__ void __launch_bounds__(64) k_parse_set_w(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+  __shared__ ParseLdsW S;
+  const uint32_t u = blockIdx.x;
+  const int64_t t0 = (int64_t)u * TW;
+  const uint64_t base = (uint64_t)u * SCAP_W;
+  int64_t last_end = -1;
+  const uint32_t L = prologue_w(txt, nb, t0, S, last_end, st);
+  if (L > LCAP_W) {
+    if (threadIdx.x == 0) {
+      TS.tmax[u] = TS.tlast[u] = LLONG_MIN;
+      TS.base[u] = base;
+      TS.nloc[u] = 0;
+      TS.nrow[u] = 0;
+      TS.gb[u] = -1;
+    }
+    return;
+  }
+  const uint32_t rl = runlo[u], rh = runhi[u];
+  const TileText T{txt, S.buf, t0 - HB, t0 + TW + HA, nb};
+  uint64_t nc = 0, cmax = 0, kmax = 0;
+  int64_t gbase = 0;
+  if (rl == rh) {
+    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
+    uint32_t ce = 0, kl = 0;
+    set_rounds_w<uint32_t>(S, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, nc, ce, kl, st);
+    cmax = ce;
+    kmax = kl;
+  } else {
+    set_rounds_w<uint64_t>(S, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, nc, cmax, kmax, st);
+  }
+  if (threadIdx.x == 0) {
+    if (nc > SCAP_W) {
+      atomicOr(&st->flags, BG_SET_OVERFLOW);
+      nc = 0;
+    }
+    if (nc > 0) {
+      if (rl == rh) reinterpret_cast<uint32_t*>(LCE + base)[nc - 1] = (uint32_t)(cmax - 1);
+      else LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    }
+    TS.gb[u] = (rl == rh) ? gbase : -1;
+    TS.tmax[u] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
+    TS.tlast[u] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
+    TS.base[u] = base;
+    TS.nloc[u] = nc;
+    TS.nrow[u] = L - ((L > 0 && last_end < 0) ? 1 : 0);
+  }
+}
+
 // per tile: sort check against the nearest earlier tile with rows (every tile is sorted
 // inside, or has reported it), how many local components the running max M of the
 // earlier tiles absorbs (mex = exclusive prefix max of tmax; the local starts increase,
@@ -1603,7 +1798,7 @@ static int report_status(bg_ctx* c, int file, const bg_dstatus& h) {
   switch (code) {
     case ERR_PARSE: what = "malformed BED line (expected: chrom<tab>start<tab>end...)"; break;
     case ERR_CHROM: what = "chromosome name longer than 127 characters"; rc = BG_E_CHROM; break;
-    case ERR_RANGE: what = "coordinate out of range (end < start or > 999999999999)"; rc = BG_E_RANGE; break;
+    case ERR_RANGE: what = "coordinate out of range (end < start or >= 2^40)"; rc = BG_E_RANGE; break;
     case ERR_UNSORTED: what = "input is not sorted (use sort-bed)"; rc = BG_E_UNSORTED; break;
     case ERR_BLANK: what = "blank line inside the data is not supported by the GPU loader"; rc = BG_E_BLANK; break;
     case ERR_SCORE: what = "score column is not a plain decimal number"; rc = BG_E_UNSUPPORTED; break;
@@ -1758,8 +1953,10 @@ static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSta
 }
 
 // run table of one input on the device (+ the runs each tile can hold)
+// (tb: the tile size the per-tile run ranges are for; TW for k_parse_set_w's sub-tiles)
 static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
-                       const std::map<std::string, int32_t>& gid, RunTable& R) {
+                       const std::map<std::string, int32_t>& gid, RunTable& R, int tb = TT) {
+  const uint32_t ntr = tb == TT ? S.ntiles : (uint32_t)bg_blocks(S.nb, (uint64_t)tb);
   const uint32_t nr = (uint32_t)S.run_pos.size();
   RunInfo* info = (RunInfo*)bg_pin_take(c, sizeof(RunInfo) * nr);
   if (!info) {
@@ -1780,14 +1977,16 @@ static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
   }
   S.d_info = (RunInfo*)bg_alloc(c, sizeof(RunInfo) * nr);
   S.d_row = (uint64_t*)bg_alloc(c, 8ull * nr);
-  S.rlo = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
-  S.rhi = (uint32_t*)bg_alloc(c, 4ull * S.ntiles);
+  S.rlo = (uint32_t*)bg_alloc(c, 4ull * ntr);
+  S.rhi = (uint32_t*)bg_alloc(c, 4ull * ntr);
   if (!S.d_info || !S.d_row || !S.rlo || !S.rhi) return BG_E_NOMEM;
   BG_HIP(c, hipMemcpyAsync(S.d_info, info, sizeof(RunInfo) * nr, hipMemcpyHostToDevice, c->stream));
   BG_HIP(c, hipMemsetAsync(S.d_row, 0xff, 8ull * nr, c->stream));
   R = RunTable{S.d_info, S.d_row, nr};
-  BG_LAUNCH(c, "k_run_range", k_run_range, dim3(bg_blocks(S.ntiles, 256)), dim3(256), R, S.ntiles,
-            S.rlo, S.rhi);
+  if (tb == TT)
+    BG_LAUNCH(c, "k_run_range", k_run_range<TT>, dim3(bg_blocks(ntr, 256)), dim3(256), R, ntr, S.rlo, S.rhi);
+  else
+    BG_LAUNCH(c, "k_run_range", k_run_range<TW>, dim3(bg_blocks(ntr, 256)), dim3(256), R, ntr, S.rlo, S.rhi);
   BG_HIP(c, hipGetLastError());
   return 0;
 }
@@ -1830,14 +2029,25 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
                          const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
   T->is_set = true;
   const uint32_t nr = (uint32_t)S.run_pos.size();
-  const uint32_t nt = S.ntiles;
-  const uint64_t cap = nt ? (uint64_t)nt * SCAP : 1;  // components <= staged slots
+  static const int set_nt = [] {  // BEDGPU_SET_NT=64|128|256: the wave / 8 KiB-tile kernels (A/B)
+    const char* e = getenv("BEDGPU_SET_NT");
+    return e ? atoi(e) : 128;
+  }();
+  static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
+    const char* e = getenv("BEDGPU_SET_WS");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool wave = set_nt == 64;
+  // staging units: 4 KiB sub-tiles (k_parse_set_w) or 8 KiB tiles
+  const uint32_t nt = wave ? (uint32_t)bg_blocks(S.nb, (uint64_t)TW) : S.ntiles;
+  const uint64_t scap = wave ? SCAP_W : SCAP;
+  const uint64_t cap = nt ? (uint64_t)nt * scap : 1;  // components <= staged slots
   T->cs = (int64_t*)bg_alloc(c, 8 * cap);
   T->ce = (int64_t*)bg_alloc(c, 8 * cap);
   if (!T->cs || !T->ce) return BG_E_NOMEM;
   if (nt == 0 || nr == 0) return 0;
   RunTable R;
-  int rc = upload_runs(c, T, S, gid, R);
+  int rc = upload_runs(c, T, S, gid, R, wave ? TW : TT);
   if (rc) return rc;
   S.lcs = (int64_t*)bg_alloc(c, 8 * cap);
   S.lce = (int64_t*)bg_alloc(c, 8 * cap);
@@ -1854,15 +2064,10 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
       !S.tcnt || !S.absorbed || !S.cnt || !S.tgb)
     return BG_E_NOMEM;
   SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  static const int set_nt = [] {  // BEDGPU_SET_NT=256: the 256-thread kernel (A/B)
-    const char* e = getenv("BEDGPU_SET_NT");
-    return (e && atoi(e) == 256) ? 256 : 128;
-  }();
-  static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
-    const char* e = getenv("BEDGPU_SET_WS");
-    return !(e && atoi(e) == 0);
-  }();
-  if (set_nt == 128 && set_ws)
+  if (wave)
+    BG_LAUNCH(c, "k_parse_set", k_parse_set_w, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st);
+  else if (set_nt == 128 && set_ws)
     BG_LAUNCH(c, "k_parse_set", (k_parse_set_n<128, true>), dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi,
               R, S.lcs, S.lce, TS, st);
   else if (set_nt == 128)

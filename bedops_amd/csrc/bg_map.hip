@@ -97,11 +97,15 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const int64_t* X, uint32_t l
 
 #define MAP_SLICE 3072  // map starts staged per workgroup (24 KiB of LDS)
 
+// CRIT == BG_OVR_FAST (bedmap --faster, bg_faster.hip): the window [wlo, whi) of every row
+// is an input, its members are the rows that joined the sweep's deque (zin), and no criterion
+// is re-tested
 template <int CRIT, bool ZM, bool LONG>
 __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
   __shared__ int64_t xs[MAP_SLICE];  // the workgroup's candidate starts, when they fit
+  constexpr bool FAST = CRIT == BG_OVR_FAST;
   const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
   const uint64_t r = r0 + threadIdx.x;
   const bool live = r < A.nr;
@@ -110,27 +114,34 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   const int64_t pad = (CRIT == BG_OVR_RANGE) ? A.range : 0;
   const int64_t klo = max(g, s - pad - A.L + 1);                   // non-decreasing in r
   const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad);
-  const int64_t hm = wmax64(live ? khi : LLONG_MIN);
-  if (bg_lane() == 0) wmax[bg_wave()] = hm;
-  __syncthreads();
-  if (threadIdx.x == 0) bnd[0] = lower_bound_i64(A.MS, A.nm, klo);  // row r0 is live
-  if (threadIdx.x == 64) {
-    int64_t m = wmax[0];
-    for (int w = 1; w < BG_NT / 64; ++w) m = max(m, wmax[w]);
-    bnd[1] = lower_bound_i64(A.MS, A.nm, m);
+  uint64_t blo = 0, bhi = 0;
+  if (!FAST) {
+    const int64_t hm = wmax64(live ? khi : LLONG_MIN);
+    if (bg_lane() == 0) wmax[bg_wave()] = hm;
+    __syncthreads();
+    if (threadIdx.x == 0) bnd[0] = lower_bound_i64(A.MS, A.nm, klo);  // row r0 is live
+    if (threadIdx.x == 64) {
+      int64_t m = wmax[0];
+      for (int w = 1; w < BG_NT / 64; ++w) m = max(m, wmax[w]);
+      bnd[1] = lower_bound_i64(A.MS, A.nm, m);
+    }
+    __syncthreads();
+    blo = bnd[0];
+    bhi = max(bnd[0], bnd[1]);
   }
-  __syncthreads();
-  const uint64_t blo = bnd[0], bhi = max(bnd[0], bnd[1]);
   // the slice every row of this workgroup searches: staged in LDS when it fits (a search
   // level then costs an LDS read instead of an L2 round trip)
-  const bool staged = bhi - blo <= MAP_SLICE;
+  const bool staged = !FAST && bhi - blo <= MAP_SLICE;
   if (staged) {
     for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) xs[i] = A.MS[blo + i];
     __syncthreads();
   }
   if (!live) return;
   uint64_t lo, hi;
-  if (staged) {
+  if (FAST) {
+    lo = A.wlo[r];
+    hi = A.whi[r];
+  } else if (staged) {
     const uint32_t n = (uint32_t)(bhi - blo);
     const uint32_t l = lds_lower_bound(xs, 0, n, klo);
     lo = blo + l;
@@ -139,7 +150,7 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
     lo = lower_bound_in(A.MS, blo, bhi, klo);
     hi = lower_bound_in(A.MS, lo, bhi, khi);
   }
-  if (A.wlo) {
+  if (A.wlo && !FAST) {
     A.wlo[r] = lo;
     A.whi[r] = hi;
   }
@@ -373,6 +384,7 @@ struct EvArgs {
   const uint32_t* ro;   // each run of equal starts in set order (k_ev_rank), null: select
   const ulonglong2* P;  // first 16 bytes of each row's full_rest(), big-endian, 0-padded (k_ev_keys)
   const uint32_t* PL;   // full_rest() length
+  const int64_t* zin;   // --faster: rows that joined the deque (zin != INT64_MAX), else null
 };
 
 __device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
@@ -528,6 +540,18 @@ __global__ void __launch_bounds__(BG_NT) k_ev_keys(EvArgs A, ulonglong2* __restr
 // then (c) the Adds of S(r_i) \ S(r_{i-1})
 template <int CRIT, typename Del, typename Add>
 __device__ __forceinline__ void ev_events(const EvArgs& A, uint64_t i, bool dels, Del emit_del, Add emit_add) {
+  if constexpr (CRIT == BG_OVR_FAST) {
+    // --faster: the visitors see the sweep's own calls (no BedBaseVisitor in between): the
+    // front pops [f_{i-1}, f_i) (WindowSweepImpl.cpp:207-211; one file :92-96 and the whole
+    // deque on a restart :132-136), then each row read into the deque (:219-221; :139-140),
+    // both in file order
+    if (i > 0 && dels)
+      for (uint64_t m = A.wlo[i - 1]; m < A.wlo[i]; ++m)
+        if (A.zin[m] != INT64_MAX) emit_del(m);
+    for (uint64_t m = i ? A.whi[i - 1] : 0; m < A.whi[i]; ++m)
+      if (A.zin[m] != INT64_MAX) emit_add(m);
+    return;
+  }
   const int64_t s = A.RS[i], e = A.RE[i];
   const int64_t g = s & ~BG_COORD_MASK;
   const int64_t R = (CRIT == BG_OVR_RANGE) ? A.range : 0;
@@ -740,6 +764,7 @@ static int map_running_sums(bg_ctx* c, int crit, const EvArgs& A, bool need_sq, 
     case BG_OVR_FRAC_MAP: return map_running_sums_t<BG_OVR_FRAC_MAP>(c, A, need_sq, res);
     case BG_OVR_FRAC_EITHER: return map_running_sums_t<BG_OVR_FRAC_EITHER>(c, A, need_sq, res);
     case BG_OVR_FRAC_BOTH: return map_running_sums_t<BG_OVR_FRAC_BOTH>(c, A, need_sq, res);
+    case BG_OVR_FAST: return map_running_sums_t<BG_OVR_FAST>(c, A, need_sq, res);
     default: return map_running_sums_t<BG_OVR_EXACT>(c, A, need_sq, res);
   }
 }
@@ -781,8 +806,9 @@ __global__ void k_tm_seg(EvArgs A, uint64_t* __restrict__ flag) {
     const uint64_t lo = max(A.wlo[i], A.wlo[i - 1]), hi = min(A.whi[i], A.whi[i - 1]);
     if ((ps & ~BG_COORD_MASK) == g)
       for (uint64_t m = lo; m < hi; ++m)
-        if ((A.MS[m] & ~BG_COORD_MASK) == g && bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]) &&
-          bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m])) {
+        if ((A.MS[m] & ~BG_COORD_MASK) == g && (CRIT != BG_OVR_FAST || A.zin[m] != INT64_MAX) &&
+            bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]) &&
+            bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m])) {
         st = 0;
         break;
       }
@@ -998,6 +1024,7 @@ static int map_tmean(bg_ctx* c, int crit, const EvArgs& A, const int32_t* cnt, c
     case BG_OVR_FRAC_MAP: return map_tmean_t<BG_OVR_FRAC_MAP>(c, A, cnt, o, res);
     case BG_OVR_FRAC_EITHER: return map_tmean_t<BG_OVR_FRAC_EITHER>(c, A, cnt, o, res);
     case BG_OVR_FRAC_BOTH: return map_tmean_t<BG_OVR_FRAC_BOTH>(c, A, cnt, o, res);
+    case BG_OVR_FAST: return map_tmean_t<BG_OVR_FAST>(c, A, cnt, o, res);
     default: return map_tmean_t<BG_OVR_EXACT>(c, A, cnt, o, res);
   }
 }
@@ -1155,6 +1182,10 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (need_sum || need_ext) mapfields = 5;  // score operations read the map as B5Rest
   if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
   const int crit = opts->criterion;
+  const bool faster = opts->faster != 0;
+  // Input.hpp:349: --faster needs a symmetric criterion the sweep can run with
+  if (faster && crit != BG_OVR_BP && crit != BG_OVR_RANGE && crit != BG_OVR_FRAC_BOTH && crit != BG_OVR_EXACT)
+    return bg_fail(c, BG_E_ARG, "--faster compatible with --range, --bp-ovr, --fraction-both, and --exact only");
   double perc = 1.0;
   switch (crit) {
     case BG_OVR_BP:
@@ -1179,16 +1210,16 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   // decimal scores: the running doubles are replayed in event order (map_running_sums)
   const bool decimal = need_sum && !M->score_int;
   const bool need_sq = (need & NEED_SQ) != 0;
-  if (ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
+  if (!faster && ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
     return bg_fail(c, BG_E_UNSUPPORTED, "single-file bedmap over zero-length rows is not on the GPU path");
   if (decimal && opts->shard)
     return bg_fail(c, BG_E_UNSUPPORTED, "decimal-score running sums span every chromosome: not on a chromosome shard");
-  if (tmean) {
+  if (tmean && !faster) {
     if (R->has_zero_len || M->has_zero_len)
       return bg_fail(c, BG_E_UNSUPPORTED, "--tmean with zero-length rows is not on the GPU path of bedmap");
   }
   if (decimal) {
-    if (R->has_zero_len || M->has_zero_len)
+    if (!faster && (R->has_zero_len || M->has_zero_len))
       return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores with zero-length rows are not on the GPU path of bedmap --mean/--sum/--variance/--stdev/--cv");
     if (!M->rest_off)
       return bg_fail(c, BG_E_ARG, "non-integer scores under --mean/--sum/--variance/--stdev/--cv need the map file loaded as BG_BED5_REST (equal rows are ordered by id and remainder)");
@@ -1223,6 +1254,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       return BG_E_NOMEM;
     }
   }
+  if (faster) need |= NEED_WIN;  // the windows are the sweep's (bg_faster.hip), kept for every use
   if (need & NEED_WIN) {
     res->wlo = (uint64_t*)bg_alloc(c, 8 * n1);
     res->whi = (uint64_t*)bg_alloc(c, 8 * n1);
@@ -1238,7 +1270,19 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   // zero-length rows change the sweep window under Overlapping(0); RangedDist (--range)
   // treats them as ordinary rows
-  if (crit != BG_OVR_RANGE && (R->has_zero_len || M->has_zero_len)) {
+  if (faster) {
+    const uint64_t m1 = M->n ? M->n : 1;
+    res->zin = (int64_t*)bg_alloc(c, 8 * m1);
+    res->zout = (int64_t*)bg_alloc(c, 8 * m1);
+    int rf = (!res->zin || !res->zout) ? BG_E_NOMEM
+                                       : bg_faster_windows(c, R, M, crit, (int64_t)opts->overlap_bp,
+                                                           (int64_t)opts->range_bp, perc, ref == map, res->wlo,
+                                                           res->whi, res->zin, res->zout);
+    if (rf) {
+      bg_result_free(res);
+      return rf;
+    }
+  } else if (crit != BG_OVR_RANGE && (R->has_zero_len || M->has_zero_len)) {
     int rz = map_zero_prep(c, R, M, res);
     if (rz) {
       bg_result_free(res);
@@ -1258,7 +1302,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   // rows longer than BG_LONG_THR get per-length-class windows (bg_map_cands), so a few
   // chromosome-length rows do not widen every reference row's window; the zero-length
   // and running-double replays enumerate one contiguous window and keep the global bound
-  if (M->maxlen > BG_LONG_THR && !res->zin && !decimal && !tmean) {
+  if (M->maxlen > BG_LONG_THR && !res->zin && !decimal && !tmean && !faster) {
     int rl = map_long_rows(c, M, res);
     if (rl) {
       bg_result_free(res);
@@ -1295,7 +1339,8 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false>), g, b, A);               \
     }                                                                                      \
   } while (0)
-    switch (crit) {
+    switch (faster ? BG_OVR_FAST : crit) {
+      case BG_OVR_FAST: BG_LAUNCH(c, "k_map_ops", (k_map_ops<BG_OVR_FAST, true, false>), g, b, A); break;
       case BG_OVR_BP: BG_MAP_LAUNCH(BG_OVR_BP); break;
       case BG_OVR_RANGE: BG_MAP_LAUNCH(BG_OVR_RANGE); break;
       case BG_OVR_FRAC_REF: BG_MAP_LAUNCH(BG_OVR_FRAC_REF); break;
@@ -1308,8 +1353,8 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   }
   int rc = bg_hip_ok(c, hipGetLastError());
   // equal map rows are ordered by the reference's heap addresses (bg_heap.hip): replay them
-  // when an operation can see such a tie (two-file mode; single-file mode keeps row order)
-  if (!rc && ref != map && R->n && M->n) {
+  // when an operation can see such a tie (both modes: one file replays sweep overload 1)
+  if (!rc && R->n && M->n) {
     bool want = false, all = false, echo = false, rest_ties = false;
     for (int k = 0; k < opts->n_ops; ++k) {
       const int op = opts->ops[k];
@@ -1331,7 +1376,8 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     }
     if (!rc && want) {
       if (opts->shard) rc = bg_fail(c, BG_E_UNSUPPORTED, "address-ordered ties span every chromosome: not on a chromosome shard");
-      else rc = bg_heap_addr(c, set, R, M, mapfields, crit == BG_OVR_RANGE, (int64_t)opts->range_bp, &res->maddr);
+      else rc = bg_heap_addr(c, set, R, M, mapfields, crit == BG_OVR_RANGE, (int64_t)opts->range_bp, &res->maddr,
+                             faster ? crit : -1, (int64_t)opts->overlap_bp, perc);
     }
   }
   if (!rc && (decimal || tmean) && R->n) {
@@ -1356,6 +1402,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     E.ro = nullptr;
     E.P = nullptr;
     E.PL = nullptr;
+    E.zin = faster ? res->zin : nullptr;
     uint32_t* ro = nullptr;
     ulonglong2* pk = nullptr;
     uint32_t* pl = nullptr;
@@ -1376,12 +1423,13 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
         E.ro = ro;
       }
     }
-    if (!rc && decimal) rc = map_running_sums(c, crit, E, need_sq, res);
+    const int ecrit = faster ? BG_OVR_FAST : crit;
+    if (!rc && decimal) rc = map_running_sums(c, ecrit, E, need_sq, res);
     if (!rc && tmean) {
       if (!M->rest_off)
         rc = bg_fail(c, BG_E_ARG, "--tmean needs the map file loaded as BG_BED5_REST (equal rows are ordered by id and remainder)");
       else
-        rc = map_tmean(c, crit, E, res->cnt, opts, res);
+        rc = map_tmean(c, ecrit, E, res->cnt, opts, res);
     }
     if (ro || pk || pl) {
       (void)hipStreamSynchronize(c->stream);

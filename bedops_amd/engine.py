@@ -93,7 +93,8 @@ class _MapOpts(ctypes.Structure):
                 ("delim", ctypes.c_char * 16), ("criterion", ctypes.c_int),
                 ("range_bp", ctypes.c_uint64), ("fraction", ctypes.c_double),
                 ("multidelim", ctypes.c_char * 16), ("op_arg", ctypes.c_double * 16),
-                ("op_arg2", ctypes.c_double * 16), ("shard", ctypes.c_int)]
+                ("op_arg2", ctypes.c_double * 16), ("shard", ctypes.c_int),
+                ("faster", ctypes.c_int)]
 
 
 class _ClosestOpts(ctypes.Structure):
@@ -445,7 +446,8 @@ class Engine:
 
     # -------------------------------------------------------------- bedmap
     def map_op(self, s, ops, ref=0, map_=1, overlap_bp=1, precision=6, delim="|",
-               skip_unmapped=False, criterion="bp-ovr", value=None, multidelim=";", sci=False):
+               skip_unmapped=False, criterion="bp-ovr", value=None, multidelim=";", sci=False,
+               faster=False):
         """bedmap <ops> on loaded set `s` (ref/map file indices) -> Result.
         criterion: "bp-ovr" (value = overlap_bp), "range" (value = bp), "fraction-ref",
         "fraction-map", "fraction-either", "fraction-both" (value = fraction), "exact"."""
@@ -467,13 +469,14 @@ class Engine:
             o.range_bp = int(value)
         elif criterion.startswith("fraction"):
             o.fraction = float(value)
+        o.faster = 1 if faster else 0
         h = ctypes.c_void_p()
         self._check(self.L.bg_map(self.ctx, s.h, ref, map_, ctypes.byref(o), ctypes.byref(h)))
         return Result(self, h)
 
     def bedmap(self, ops, ref_text, map_text=None, overlap_bp=1, precision=6, delim="|",
                skip_unmapped=False, chrom=None, criterion="bp-ovr", value=None, multidelim=";",
-               sci=False):
+               sci=False, faster=False):
         names = [op[0] if isinstance(op, tuple) else op for op in ops]
         need5 = any(op in SCORE_OPS for op in names)
         mrest = any(op in MAP_REST_OPS for op in names)
@@ -489,7 +492,7 @@ class Engine:
             if chrom:
                 s.restrict_chrom(chrom)
             r = self.map_op(s, ops, 0, 0 if single else 1, overlap_bp, precision, delim,
-                            skip_unmapped, criterion, value, multidelim, sci)
+                            skip_unmapped, criterion, value, multidelim, sci, faster)
             try:
                 return r.text()
             finally:

@@ -50,6 +50,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # reference bedops output for A100M x B100M
 REF_INTERSECT = {"rows": 38507974, "bytes": 917848625, "sha16": "2495074965b49d74"}
 REF_BEDMAP_R5M = {"rows": 4999998, "bytes": 54515904, "sha16": "899ec7973e166e2d"}
+# every workload's full-size output from the genuine reference, one process on the whole
+# files (tools/pin_fullsize.py run in the build container -> tests/golden/ref_fullsize.json)
+try:
+    with open(os.path.join(ROOT, "tests", "golden", "ref_fullsize.json")) as _f:
+        REF_FULL = {k: v["output"] for k, v in json.load(_f).items()}
+except OSError:
+    REF_FULL = {}
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
@@ -148,20 +155,20 @@ WORKLOADS = {
                           "intersect -> BED text in HBM"},
     "element-of": {"gen": [(44, 3), (45, 3)], "rows": [200_000_000, 200_000_000],
                    "kinds": [1, 3], "oracle": "bedops_oracle", "args": ["-e", "1"], "cli": "bedops",
-                   "ref": None,
+                   "ref": REF_FULL.get("element-of"),
                    "desc": "bedops --element-of 1 A.bed B.bed (configs[3] shape, 200M x 200M)"},
     "bedmap": {"gen": [(7, 3), (8, 5)], "rows": [50_000_000, 500_000_000], "kinds": [0, 2],
                "oracle": "bedmap_oracle", "args": ["--count", "--mean"], "cli": "bedmap",
-               "ref": None, "desc": "bedmap --count --mean ref.bed map.bed (configs[2], 50M x 500M "
+               "ref": REF_FULL.get("bedmap"), "desc": "bedmap --count --mean ref.bed map.bed (configs[2], 50M x 500M "
                                     "BED5 map)"},
     "bedmap-decimal": {"gen": [(7, 3), (8, 6)], "rows": [5_000_000, 50_000_000], "kinds": [0, 4],
                        "oracle": "bedmap_oracle", "args": ["--count", "--mean"], "cli": "bedmap",
-                       "ref": None,
+                       "ref": REF_FULL.get("bedmap-decimal"),
                        "desc": "bedmap --count --mean ref.bed map.bed, decimal scores (running "
                                "double replayed in the reference's event order; 5M x 50M)"},
     "closest": {"gen": [(46, 3), (47, 3)], "rows": [10_000_000, 1_000_000_000], "kinds": [1, 1],
                 "oracle": "closest_oracle", "args": ["--closest"], "cli": "closest-features",
-                "ref": None, "desc": "closest-features --closest query.bed ref.bed (configs[4], "
+                "ref": REF_FULL.get("closest"), "desc": "closest-features --closest query.bed ref.bed (configs[4], "
                                      "10M x 1B)"},
 }
 

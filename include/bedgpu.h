@@ -102,6 +102,9 @@ typedef struct bg_map_opts {
   int shard;           /* 1: the set holds some chromosomes of the inputs (multi-GPU shard):
                           results that depend on other chromosomes (decimal-score running
                           sums, one double across the file) are refused, BG_E_UNSUPPORTED */
+  int faster;          /* --faster: the sweep runs with the criterion itself and no window
+                          re-test (Bedmap.cpp:287-290, 728-745); criterion BG_OVR_BP / RANGE /
+                          FRAC_BOTH / EXACT only (bedmap/src/Input.hpp:349), else BG_E_ARG */
 } bg_map_opts;
 /* operations (applications/bed/bedmap/src/TDefs.hpp:70-103; option names
  * interfaces/general-headers/algorithm/visitors/helpers/NamedVisitors.hpp:52-178) */
@@ -198,7 +201,9 @@ int bg_set_pad(bg_ctx* ctx, bg_set* set, int file, int lpad, int rpad);
  * input checked on the GPU; row = 0 when the file passes, else the first failing line
  * (1-based, headers counted), its code and byte range (and the line before it).
  * nfields: 3 (BED3 types), 5 (bedmap's map file under score operations); has_rest: the
- * reader keeps the remainder (B3Rest). */
+ * reader keeps the remainder (B3Rest), or'ed with BG_CHECK_NEST for bedmap --faster's
+ * nested-row check (bed_check_iterator nestCheck, BedCheckIterator.hpp:612-615). */
+#define BG_CHECK_NEST 2
 typedef struct bg_check_result {
   uint64_t row;
   int code;

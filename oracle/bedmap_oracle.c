@@ -138,11 +138,37 @@ static int crit_m2r(int64_t m, int64_t r) {
     default: return d_overlap(a, b, OVR);
   }
 }
-/* the sweep distance: Overlapping(0), or RangedDist(R) for --range */
+/* the criterion's own Ref2Map(ref, map) (--faster sweeps with it, Bedmap.cpp:287-290):
+ * Overlapping / RangedDist operator() (:97-115, :57-64); PercentOverlapBoth::Ref2Map
+ * (:268-276); Exact::Ref2Map (:300-309) */
+static int crit_r2m(int64_t r, int64_t m) {
+  row_t a = R_(r), b = M_(m);
+  switch (CRIT) {
+    case C_RANGE: return d_ranged(a, b);
+    case C_FBOTH: {
+      int v1 = d_pmap(a, b);
+      if (v1 != 0) return v1;
+      return -d_pmap(b, a);
+    }
+    case C_EXACT: {
+      int v = chrom_cmp(a.c, b.c);
+      if (v) return v;
+      if (a.s != b.s) return a.s < b.s ? -1 : 1;
+      if (a.e != b.e) return a.e < b.e ? -1 : 1;
+      return 0;
+    }
+    default: return d_overlap(a, b, OVR);
+  }
+}
+/* the sweep distance: Overlapping(0), or RangedDist(R) for --range; with --faster the
+ * criterion itself (Bedmap.cpp:728-745) */
+static int FASTER; /* --faster: no BedBaseVisitor, the visitors see the sweep's calls */
 static int sweep_r2m(int64_t r, int64_t m) {
+  if (FASTER) return crit_r2m(r, m);
   return CRIT == C_RANGE ? d_ranged(R_(r), M_(m)) : d_overlap(R_(r), M_(m), 0);
 }
 static int sweep_m2r(int64_t m, int64_t r) {
+  if (FASTER) return crit_m2r(m, r);
   return CRIT == C_RANGE ? d_ranged(M_(m), R_(r)) : d_overlap(M_(m), R_(r), 0);
 }
 
@@ -682,13 +708,30 @@ static void ref_new(int64_t r) {
 }
 
 static oset_t vcache, lst, ev;
-/* BedBaseVisitor::OnDelete (:145-154) */
+/* one file under the Overlapping specialisation: rows shorter than the required overlap
+ * reach no visitor (WindowSweepImpl.specialize.cpp:66-67, 110-111) */
+static int f_visible(int64_t m) { return !SINGLE || CRIT != C_BP || MAP->end[m] - MAP->start[m] >= (FASTER ? OVR : 0); }
+/* BedBaseVisitor::OnDelete (:145-154); --faster: MultiVisitor's Delete straight away */
 static void on_delete(int64_t m) {
+  if (FASTER) {
+    if (f_visible(m)) { os_erase(&VWIN, m); v_del(m); }
+    return;
+  }
   if (os_erase(&VWIN, m)) v_del(m);
   else os_erase(&vcache, m);
 }
-/* BedBaseVisitor::OnDone: fixWindow (deletions first, then insertions), then DoneReference */
+/* BedBaseVisitor::OnAdd (:139-143, into its cache); --faster: MultiVisitor's Add */
+static void on_add(int64_t m) {
+  if (FASTER) {
+    if (f_visible(m)) { os_insert(&VWIN, m); v_add(m); }
+    return;
+  }
+  os_insert(&vcache, m);
+}
+/* BedBaseVisitor::OnDone: fixWindow (deletions first, then insertions), then DoneReference;
+ * --faster: DoneReference on the window as the sweep left it */
 static void on_done(int64_t r) {
+  if (FASTER) { v_done(r); return; }
   lst.n = 0;
   ev.n = 0;
   for (int64_t i = 0; i < VWIN.n;) {
@@ -785,6 +828,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(o, "--chrom") && a < argc) only_chrom = argv[a++];
     else if (!strcmp(o, "--sci")) SCI = 1;
     else if (!strcmp(o, "--skip-unmapped")) SKIP_UNMAPPED = 1;
+    else if (!strcmp(o, "--faster")) FASTER = 1;
     else if (!strcmp(o, "--ec") || !strcmp(o, "--header") || !strcmp(o, "--sweep-all")) {}
     else { fprintf(stderr, "bedmap_oracle: unsupported option %s\n", o); return 2; }
   }
@@ -828,27 +872,37 @@ int main(int argc, char** argv) {
   if (SINGLE) { /* sweep() overload 1, WindowSweepImpl.cpp:66-162 */
     int64_t wh = 0, wt = 0, index = 0, next = 0, cache = -1, cur = -1;
     int reset = 1;
+    /* heap addresses: the iterator reads one row ahead (its constructor reads row 0, each
+     * ++start the next); the sweep deletes rows as they leave the deque */
+    ADDR = (int64_t*)calloc((size_t)map.n + 1, sizeof(int64_t));
+    MMEM = (rowmem_t*)calloc((size_t)map.n + 1, sizeof(rowmem_t));
+    map_new(0);
     for (;;) {
       if (!(next < map.n || cache >= 0 || wt > wh)) break;
       if (!reset) {
         cur = win[wh + index]; /* OnStart */
-        while (wt > wh && sweep_m2r(win[wh], cur) < 0) { on_delete(win[wh++]); --index; }
+        while (wt > wh && sweep_m2r(win[wh], cur) < 0) {
+          on_delete(win[wh]);
+          row_del(&MMEM[win[wh]], MAPFIELDS);
+          ++wh;
+          --index;
+        }
       } else if (next >= map.n && cache < 0) {
         break; /* OnEnd; the rest of the window is deleted on behalf of no reference */
       }
       while (cache >= 0 || next < map.n) {
         int64_t b;
         if (cache >= 0) { b = cache; cache = -1; }
-        else b = next++;
+        else { b = next++; map_new(next); } /* ++start */
         if (wt == wh || reset || sweep_r2m(win[wh + index], b) == 0) {
           if (reset) {
             reset = 0;
             index = 0;
             cur = b; /* OnStart(bPtr) */
-            while (wt > wh) on_delete(win[wh++]);
+            while (wt > wh) { on_delete(win[wh]); row_del(&MMEM[win[wh]], MAPFIELDS); ++wh; }
           }
           win[wt++] = b;
-          os_insert(&vcache, b); /* OnAdd */
+          on_add(b); /* OnAdd */
         } else {
           cache = b;
           break;
@@ -874,7 +928,7 @@ int main(int argc, char** argv) {
         if (cache >= 0) { m = cache; cache = -1; }
         else { m = mi++; map_new(mi); } /* ++mapFromStart */
         int v = sweep_r2m(r, m);
-        if (v == 0) { win[wt++] = m; os_insert(&vcache, m); } /* OnAdd -> cache_ */
+        if (v == 0) { win[wt++] = m; on_add(m); } /* OnAdd -> cache_ */
         else if (v < 0) { cache = m; break; }
         else row_del(&MMEM[m], MAPFIELDS);
       }

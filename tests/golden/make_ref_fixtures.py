@@ -312,7 +312,77 @@ def ec():
     s.save()
 
 
+# ------------------------------------------------------------------------------- --faster
+def _flat(rng, n, span, maxlen, chroms=randbed.CHROMS):
+    """sorted rows with no row nested in another (starts and ends both increase)"""
+    out = []
+    for c in sorted(set(rng.choice(chroms) for _ in range(6)), key=str.encode):
+        s_, e_ = 0, 0
+        for _ in range(n // 3):
+            s_ += rng.randint(0, max(1, span // n))
+            e_ = max(e_ + rng.randint(0, 3), s_ + rng.randint(1, maxlen))
+            out.append((c, s_, e_))
+    return _srt(out)
+
+
+FASTER_OPSETS = [["count", "sum", "min", "max", "indicator"],
+                 ["bases", "bases-uniq", "mean", "echo-ref-size"],
+                 ["echo-map", "echo-map-id", "echo-map-size", "count"],
+                 ["echo-map-score", "echo-overlap-size", "echo-map-range"],
+                 ["median", "stdev", ("kth", 0.3), "mad"],
+                 ["min-element", "max-element", "count"],
+                 [("tmean", 0.1, 0.2), "wmean", "sum"]]
+FASTER_CRITS = [[], ["--bp-ovr", "7"], ["--range", "25"], ["--fraction-both", "0.3"], ["--exact"]]
+
+
+def faster():
+    """bedmap --faster (Bedmap.cpp:287-290, 585-594, 728-745): the sweep runs with the
+    criterion itself and no BedBaseVisitor re-test; Input.hpp:349 rejects the other criteria;
+    --ec adds the nested-row check (BedCheckIterator.hpp:612-615)"""
+    s = Suite("faster")
+    for ci, copt in enumerate(FASTER_CRITS):
+        rng = random.Random(zlib.crc32(repr(("faster", ci)).encode()))
+        for shape in ("flat", "nested", "dup"):
+            if shape == "flat":
+                ref, mp = _flat(rng, 240, 3000, 60), _flat(rng, 600, 3000, 40)
+            else:
+                ref = randbed.rows(rng, rng.choice([60, 240]), span=3000, maxlen=rng.choice([30, 120]))
+                mp = randbed.rows(rng, rng.choice([200, 600]), span=3000, maxlen=rng.choice([20, 80]))
+                if shape == "dup":  # exact matches and equal rows
+                    mp = _srt(mp + ref[::2] + ref[::5])
+            g = s.group(randbed.text(ref, rest="cols", rng=rng), _int_map(rng, mp))
+            for ops in FASTER_OPSETS:
+                s.run("bedmap", ["--faster"] + opargs(ops) + copt, g)
+            s.run("bedmap", ["--faster", "--count", "--sum", "--skip-unmapped", "--delim", ";"] + copt, g)
+            s.run("bedmap", ["--faster", "--count", "--mean", "--echo-map-id"] + copt, g, files=[1])  # one file
+        # zero-length rows
+        ref = randbed.rows(rng, 200, span=600, maxlen=40, zero_frac=0.1)
+        mp = randbed.rows(rng, 300, span=600, maxlen=30, zero_frac=0.1)
+        g = s.group(randbed.text(ref, rest="cols", rng=rng), _int_map(rng, mp))
+        for ops in (["count", "sum", "max"], ["echo-map", "bases-uniq"]):
+            s.run("bedmap", ["--faster"] + opargs(ops) + copt, g)
+            s.run("bedmap", ["--faster"] + opargs(ops) + copt, g, files=[1])
+        # decimal scores: the running doubles in the sweep's own call order
+        ref = randbed.rows(rng, 150, span=2000, maxlen=60)
+        mp = _srt(randbed.rows(rng, 400, span=2000, maxlen=60))
+        g = s.group(randbed.text(ref), _decimal_map(rng, mp))
+        s.run("bedmap", ["--faster", "--count", "--mean", "--sum", "--variance", "--prec", "9"] + copt, g)
+    # the criteria --faster rejects (Input.hpp:349), and the nested-row check under --ec
+    g = s.group("chr1\t1\t100\nchr1\t5\t10\nchr1\t50\t60\n", "chr1\t7\t8\nchr1\t55\t58\n")
+    for copt in ([], ["--fraction-ref", "0.5"], ["--fraction-map", "0.5"], ["--fraction-either", "0.5"],
+                 ["--fraction-both", "0.5"], ["--range", "3"], ["--exact"], ["--bp-ovr", "2"]):
+        s.run("bedmap", ["--faster", "--count"] + copt, g)
+        s.run("bedmap", ["--count"] + copt, g)
+    s.run("bedmap", ["--faster", "--ec", "--count"], g)
+    s.run("bedmap", ["--faster", "--ec", "--count"], g, files=[1, 0])
+    s.run("bedmap", ["--faster", "--ec", "--echo", "--count"], g, files=[1])
+    g = s.group("chr1\t1\t10\nchr1\t5\t20\nchr2\t1\t5\n", "chr1\t2\t3\nchr1\t4\t30\nchr2\t0\t1\n")
+    s.run("bedmap", ["--faster", "--ec", "--count", "--echo-map"], g)
+    s.run("bedmap", ["--faster", "--header", "--count"], g)
+    s.save()
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec"]
+    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec", "faster"]
     for w in which:
         globals()[w]()

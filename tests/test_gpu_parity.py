@@ -182,6 +182,56 @@ def test_random_bedmap_ops_criteria_vs_oracle(eng, oracle_bin, crit, val):
                 assert got == want, (crit, val, ops, trial)
 
 
+# bedmap --faster (Bedmap.cpp:287-290, 728-745): the sweep runs with the criterion and the
+# visitors see its own calls; the GPU replays it as two one-integer chains (bg_faster.hip).
+# Shapes: rows without nesting (what --faster is for), nested rows, duplicates, zero-length
+# rows, a chromosome-long reference row (forces the chains' fix-up and serial passes).
+FASTER_CRITS = [("bp-ovr", 1), ("bp-ovr", 7), ("range", 25), ("fraction-both", "0.3"), ("exact", None)]
+
+
+def _flat_rows(rng, n, span, maxlen):
+    out, s_, e_ = [], 0, 0
+    for _ in range(n):
+        s_ += rng.randint(0, max(1, 2 * span // max(n, 1)))
+        e_ = max(e_ + rng.randint(0, 3), s_ + rng.randint(1, maxlen))
+        out.append(("chr1", s_, e_))
+    return out
+
+
+@pytest.mark.parametrize("crit,val", FASTER_CRITS)
+def test_bedmap_faster_vs_oracle(eng, oracle_bin, crit, val):
+    rng = random.Random(zlib.crc32(repr(("faster", crit, val)).encode()))
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(10):
+            shape = trial % 5
+            if shape == 0:
+                ref, mp = _flat_rows(rng, 3000, 200000, 90), _flat_rows(rng, 9000, 200000, 40)
+            else:
+                ref = randbed.rows(rng, rng.choice([1, 40, 600, 3000]), span=rng.choice([300, 5000]),
+                                   maxlen=rng.choice([10, 80, 300]), zero_frac=0.1 if shape == 3 else 0.0)
+                mp = randbed.rows(rng, rng.choice([1, 60, 900, 4000]), span=rng.choice([300, 5000]),
+                                  maxlen=rng.choice([10, 80, 300]), zero_frac=0.1 if shape == 3 else 0.0)
+                if shape == 2:
+                    mp = sorted(mp + ref[::2] + ref[::3], key=lambda r: (r[0].encode(), r[1], r[2]))
+                if shape == 4:  # a chromosome-long row ahead of everything
+                    ref = sorted(ref + [("chr1", 0, 6000)], key=lambda r: (r[0].encode(), r[1], r[2]))
+            rt = randbed.text(ref, rest="cols", rng=rng).encode()
+            mt = "".join(f"{c}\t{s}\t{e}\tid{i % 37}\t{rng.randint(0, 999)}" + ("\tx\t+" if i % 3 == 0 else "")
+                         + "\n" for i, (c, s, e) in enumerate(mp)).encode()
+            copt = [f"--{crit}"] + ([str(val)] if val is not None else [])
+            kw = {"overlap_bp": val} if crit == "bp-ovr" else {"criterion": crit, "value": val}
+            for ops in (["count", "sum", "min", "max", "indicator"], ["bases", "bases-uniq", "mean"],
+                        ["echo-map-id", "echo-map-score", "echo-overlap-size"], ["median", "stdev"],
+                        ["min-element", "count"]):
+                if ops[0] == "median" and len(mp) > 1500:
+                    continue
+                args = ["--faster"] + [f"--{o}" for o in ops] + copt
+                want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
+                assert eng.bedmap(ops, rt, mt, faster=True, **kw) == want, (crit, val, ops, trial)
+                want = run_oracle(oracle_bin["bedmap"], args, [mt], td)  # one file
+                assert eng.bedmap(ops, mt, None, faster=True, **kw) == want, ("single", crit, val, ops, trial)
+
+
 @pytest.mark.parametrize("crit,val", MAP_CRITS)
 def test_bedmap_zero_length_rows_vs_oracle(eng, oracle_bin, crit, val):
     """zero-length reference/map rows change the reference's sweep window (deleted, popped and

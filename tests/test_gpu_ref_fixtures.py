@@ -18,13 +18,19 @@ pytestmark = pytest.mark.gpu
 # non-zero, nothing on stdout) instead of guessing. (suite, case index)
 OUTSIDE_CONTRACT = {("closest", 90), ("closest", 91), ("closest", 92),  # unsorted candidate file
                     ("ec", 6), ("ec", 20), ("ec", 27), ("ec", 34), ("ec", 41), ("ec", 55), ("ec", 62),
-                    ("ec", 69), ("ec", 76), ("ec", 104)}
+                    ("ec", 69), ("ec", 76)}
+# (ec 104, a sorted row at 10^12 > MAX_COORD_VALUE: the reference prints it without --ec, and
+# so does the GPU path for any coordinate below the 2^40 key limit)
 # the heap-address replay's known residual (tests/test_ref_fixtures.py KNOWN): the GPU follows
 # the oracle's model there, which the reference's malloc_consolidate departs from
-KNOWN = {("bedmap", 160)}
+KNOWN = {("bedmap", 160),
+         # one file, B3Rest map rows (48-byte chunks, the size of a std::set node): the
+         # visitors' set nodes (OvrUnique, EchoMapBed) share the rows' chunk class, which the
+         # model does not replay, and --echo-map lists equal rows in address order
+         ("faster", 62), ("faster", 126)}
 
 CHUNK = 40
-_SIZES = {"closest": 96, "bedmap": 313, "decimal": 124, "sortbed": 6, "ec": 112}
+_SIZES = {"closest": 96, "bedmap": 313, "decimal": 124, "sortbed": 6, "ec": 112, "faster": 181}
 PARAMS = [(s, i) for s, n in _SIZES.items() for i in range(0, n, CHUNK)]
 
 
@@ -42,7 +48,7 @@ def test_gpu_cli_reproduces_reference(gpu_bin, suite, start):
             if rc == 0 or out:
                 bad.append((k, c["args"], f"outside the sorted contract: rc {rc}, {len(out)} bytes out"))
             continue
-        d = R.compare(gpu_bin[c["tool"]], fx, c, check_stderr=(suite == "ec" or c["rc"] != 0))
+        d = R.compare(gpu_bin[c["tool"]], fx, c, check_stderr=(suite == "ec" or c["rc"] != 0 or "--ec" in c["args"]))
         if d:
             bad.append((k, c["args"], d[:240]))
     assert not bad, bad

@@ -18,7 +18,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # reference orders equal-coordinate map rows by heap address; the model replays glibc's
 # tcache/fast-bin reuse but not malloc_consolidate, which this case's 150-row window
 # triggers when the heap grows. (suite, case index)
-KNOWN = {("bedmap", 160)}
+KNOWN = {("bedmap", 160),
+         # one file, B3Rest map rows (48-byte chunks, the size of a std::set node): the
+         # visitors' set nodes (OvrUnique, EchoMapBed) share the rows' chunk class, which the
+         # model does not replay, and --echo-map lists equal rows in address order
+         ("faster", 62), ("faster", 126)}
 
 
 def _bin(oracle_bin, tool):
@@ -26,12 +30,16 @@ def _bin(oracle_bin, tool):
                        "sortbed": "sortbed"}[tool]]
 
 
-@pytest.mark.parametrize("suite", ["closest", "bedmap", "decimal", "sortbed"])
+@pytest.mark.parametrize("suite", ["closest", "bedmap", "decimal", "sortbed", "faster"])
 def test_oracle_reproduces_reference(oracle_bin, suite):
     fx = R.load(suite)
     bad = []
     for k, c in enumerate(fx["cases"]):
         if (suite, k) in KNOWN:
+            continue
+        # argument errors and --ec checks are the drop-in CLI's (tests/test_gpu_ref_fixtures.py);
+        # the oracle restates the sweeps
+        if c["rc"] != 0 or "--ec" in c["args"] or "--header" in c["args"]:
             continue
         d = R.compare(_bin(oracle_bin, c["tool"]), fx, c, check_stderr=False)
         if d:
