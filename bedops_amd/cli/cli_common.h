@@ -414,8 +414,14 @@ static void maybe_stats(bg_ctx* ctx) {
  * A worker that fails (die_msg, a crash) is waited for and its status mirrored.
  * BEDGPU_DETACH=0, or BEDGPU_FULL_EXIT=1 (profilers), keep everything in one process. */
 #include <signal.h>
+#include <sys/prctl.h>
 #include <sys/wait.h>
 static int CLI_DETACH_FD = -1;
+static pid_t CLI_WORKER = 0;
+/* the front process forwards termination signals to the worker (whose exit it mirrors) */
+static void cli_forward_signal(int sig) {
+  if (CLI_WORKER > 0) kill(CLI_WORKER, sig);
+}
 static inline int cli_env_on(const char* name) {
   const char* s = getenv(name);
   return s && *s && strcmp(s, "0") != 0;
@@ -436,9 +442,22 @@ static inline void cli_detach(void) {
   if (pid == 0) { /* the worker */
     close(p[0]);
     CLI_DETACH_FD = p[1];
+    /* a front process killed outright (SIGKILL) takes the worker with it; cleared again in
+     * fast_exit once the output is complete */
+    prctl(PR_SET_PDEATHSIG, SIGKILL);
+    if (getppid() == 1) _exit(EXIT_FAILURE);
     return;
   }
   close(p[1]);
+  CLI_WORKER = pid;
+  {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_handler = cli_forward_signal;
+    sigemptyset(&sa.sa_mask);
+    const int sigs[4] = {SIGTERM, SIGINT, SIGHUP, SIGQUIT};
+    for (int k = 0; k < 4; ++k) sigaction(sigs[k], &sa, NULL);
+  }
   close(0); /* stdin belongs to the worker ('-' inputs) */
   unsigned char st = 0;
   ssize_t r;
@@ -465,6 +484,7 @@ static inline void fast_exit(void) {
   /* BEDGPU_FULL_EXIT=1: tear down normally (profilers write their traces at exit) */
   if (cli_env_on("BEDGPU_FULL_EXIT")) return;
   if (CLI_DETACH_FD >= 0) { /* output complete: release the front process (cli_detach) */
+    prctl(PR_SET_PDEATHSIG, 0);  /* the teardown outlives the front process */
     close(1);
     close(2);
     const unsigned char ok = EXIT_SUCCESS;

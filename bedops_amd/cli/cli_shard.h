@@ -12,8 +12,10 @@
  *      mappings (bg_file_image: page-cache pages, nothing read whole into or pinned in host
  *      memory) through its context's pinned ring over its own link, and runs load ->
  *      operation -> format on its own host thread;
- *   4. bg_group_gather reassembles the texts on device 0 in strcmp chromosome order over
- *      RCCL, and device 0 streams them to stdout.
+ *   4. stdout a regular file: each device writes its chromosomes' text spans straight to
+ *      their offsets in the output (D2H over its own link, pwrite), so the output leaves
+ *      over every device's link at once; otherwise (pipes) bg_group_gather reassembles the
+ *      texts on device 0 in strcmp chromosome order over RCCL and device 0 streams them.
  * Inputs that are not regular files (stdin, pipes), inputs the host checks cannot split
  * cleanly (blank or out-of-order chromosome lines), a group that cannot be opened (fewer
  * GPUs than listed, RCCL unavailable) and any error inside a shard fall back to the
@@ -197,6 +199,25 @@ static void* shard_worker(void* p) {
   return NULL;
 }
 
+/* one device's chromosome spans, each at its offset in the output file */
+typedef struct {
+  shard_job_t* J;
+  const int* owner;
+  const uint64_t* pos; /* output offset of each global chromosome (relative to off0) */
+  int ngc;
+  off_t off0;
+  int rc;
+} sh_write_job_t;
+static void* shard_writer(void* p) {
+  sh_write_job_t* W = (sh_write_job_t*)p;
+  shard_job_t* J = W->J;
+  W->rc = bg_bind(J->ctx);
+  for (int g = 0; g < W->ngc && !W->rc; ++g)
+    if (W->owner[g] == J->dev && J->len[g])
+      W->rc = bg_pwrite_device(J->ctx, J->text + J->off[g], J->len[g], 1, (int64_t)(W->off0 + (off_t)W->pos[g]));
+  return NULL;
+}
+
 /* Runs the operation on every device of BEDGPU_DEVICES (>= 2 entries) and writes the
  * reassembled output to fd 1. Returns 0 when done, 1 when the caller should take the
  * one-device path instead (nothing written, no input consumed). */
@@ -312,7 +333,40 @@ static int shard_run(const char* prog, int nf, const bg_input* proto, const char
   cli_mark("shards");
   for (int f = 0; f < nf; ++f) bg_file_image_close(&fm[f]); /* the loads have synchronised */
   int done = 0;
-  if (!failed) {
+  /* stdout a regular file: every device writes its own chromosomes' spans at their offsets
+   * in the output (D2H over its own link, pwrite), no gather; anything else (pipes,
+   * terminals, appends; BEDGPU_SHARD_GATHER=1): the RCCL gather to device 0 below */
+  struct stat ost;
+  const int ofl = fcntl(1, F_GETFL);
+  const off_t off0 = lseek(1, 0, SEEK_CUR);
+  const int direct = !failed && fstat(1, &ost) == 0 && S_ISREG(ost.st_mode) && ofl >= 0 && !(ofl & O_APPEND) &&
+                     off0 >= 0 && !cli_env_on("BEDGPU_SHARD_GATHER");
+  if (direct) {
+    uint64_t* pos = (uint64_t*)calloc((size_t)ngc + 1, sizeof(uint64_t));
+    for (int g = 0; g < ngc; ++g) pos[g + 1] = pos[g] + J[owner[g]].len[g];
+    sh_write_job_t* W = (sh_write_job_t*)calloc((size_t)nd, sizeof(sh_write_job_t));
+    for (int d = 0; d < nd; ++d) {
+      W[d].J = &J[d];
+      W[d].owner = owner;
+      W[d].pos = pos;
+      W[d].ngc = ngc;
+      W[d].off0 = off0;
+      pthread_create(&th[d], NULL, shard_writer, &W[d]);
+    }
+    int wrc = 0, wd = 0;
+    for (int d = 0; d < nd; ++d) {
+      pthread_join(th[d], NULL);
+      if (W[d].rc && !wrc) { wrc = W[d].rc; wd = d; }
+    }
+    cli_mark("write");
+    if (wrc) die_ctx(prog, J[wd].ctx, wrc);
+    if (lseek(1, off0 + (off_t)pos[ngc], SEEK_SET) < 0) die_msg(prog, "seek failed on the output file");
+    free(pos);
+    free(W);
+    maybe_stats(bg_group_ctx(grp, 0));
+    fast_exit();
+    done = 1;
+  } else if (!failed) {
     const char** texts = (const char**)calloc((size_t)nd, sizeof(char*));
     const uint64_t** offs = (const uint64_t**)calloc((size_t)nd, sizeof(uint64_t*));
     const uint64_t** lens = (const uint64_t**)calloc((size_t)nd, sizeof(uint64_t*));

@@ -148,6 +148,16 @@ static int stream_prepare(int nf, const char* const* paths) {
   struct stat st;
   const int fl = fcntl(1, F_GETFL);
   if (fstat(1, &st) != 0 || !S_ISREG(st.st_mode) || fl < 0 || (fl & O_APPEND)) return 0;
+  {  /* the size test of the plan, up front: small inputs keep the whole-file path and its
+        prefetch of the mappings during HIP initialisation */
+    uint64_t total = 0;
+    for (int f = 0; f < nf; ++f) {
+      struct stat si;
+      if (strcmp(paths[f], "-") == 0 || stat(paths[f], &si) != 0 || !S_ISREG(si.st_mode)) return 0;
+      total += (uint64_t)si.st_size;
+    }
+    if (total < (uint64_t)stream_env("BEDGPU_STREAM_MIN", 256L << 20)) return 0;
+  }
   SP.nf = nf;
   SP.paths = paths;
   if (pthread_create(&SP.th, NULL, stream_plan_run, NULL) != 0) return 0;
@@ -177,6 +187,9 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   void** d = (void**)calloc((size_t)nf, sizeof(void*));
   uint64_t freed = 0;
   int rc = 0;
+  /* the group's input blocks go back to the cache stream-ordered (the next group's copies
+   * are queued after its kernels on ctx's stream); a second copy stream needs the host wait */
+  const int ordered = stream_env("BEDGPU_COPY_STREAMS", 1) < 2;
   for (int g = 0; g < ng && !rc; ++g) {
     for (int f = 0; f < nf && !rc; ++f) {
       const uint64_t a = SP.ga[(size_t)g * nf + f], b = SP.gb[(size_t)g * nf + f];
@@ -200,7 +213,8 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
      * freed blocks to the next group's copies, ordered after this group's kernels) */
     bg_set_free(set);
     for (int f = 0; f < nf; ++f) {
-      bg_device_free(ctx, d[f]);
+      if (ordered) bg_device_release(ctx, d[f]);
+      else bg_device_free(ctx, d[f]);
       d[f] = NULL;
     }
     const uint64_t done = bg_writer_done(w);
@@ -222,7 +236,9 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
     if (s && *s && strcmp(s, "0") != 0)
       fprintf(stderr, "bedgpu: chromosome-group pipeline stopped (%d/%d: %s); whole-file path\n", rc, wrc,
               bg_last_error(ctx));
-    if (ftruncate(1, off0) != 0 || lseek(1, off0, SEEK_SET) < 0) return 1;
+    /* never write the whole-file output after leftover group output */
+    if (ftruncate(1, off0) != 0 || lseek(1, off0, SEEK_SET) < 0)
+      die_msg(CLI_PROG, "cannot truncate the output file to rerun the whole-file path");
     return 1;
   }
   return 0;

@@ -727,16 +727,17 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
 // stream 88-165 ms, pwrite from 4 threads ~105 ms, a shared mapping of the file filled by DMA
 // 128 ms (page allocation through faults does not scale with threads: 285 ms with 4).
 // Anything else (pipes, terminals, appends): the same chunks written in order by one thread.
+// (at >= 0: pwrite(2) at that offset and leave the file position alone: bg_pwrite_device)
 #define BG_WR_THREADS 4
-static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd) {
+static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd, off_t at = -1) {
   int rc = ring_get(c);
   if (rc) return rc;
   struct stat st;
   const int fl = fcntl(fd, F_GETFL);
-  const off_t off0 = lseek(fd, 0, SEEK_CUR);
+  const off_t off0 = at >= 0 ? at : lseek(fd, 0, SEEK_CUR);
   const char* par = getenv("BEDGPU_WRITE_PAR");  // 0: one thread, write(2)
-  const bool pw = fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && fl >= 0 && !(fl & O_APPEND) && off0 >= 0 &&
-                  !(par && strcmp(par, "0") == 0);
+  const bool pw = at >= 0 || (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && fl >= 0 && !(fl & O_APPEND) &&
+                              off0 >= 0 && !(par && strcmp(par, "0") == 0));
   const uint64_t CH = BG_RING_CH, nch = (n + CH - 1) / CH;
   const int T = pw ? (int)std::min<uint64_t>(BG_WR_THREADS, nch) : 1;
   const int per = BG_RING_SLOTS / BG_WR_THREADS;
@@ -778,9 +779,18 @@ static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd) {
   hipStreamSynchronize(c->stream);
   if (bad == 2) return bg_fail(c, BG_E_IO, std::string("write failed: ") + strerror(errno));
   if (bad) return bg_fail(c, BG_E_HIP, "bg_write_device copy");
-  if (pw && lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
+  if (pw && at < 0 && lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
     return bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
   return 0;
+}
+
+// n bytes of device memory to the regular file fd at offset `at` (pwrite: the file position
+// is not used or moved), so several devices can write their parts of one output at once
+extern "C" int bg_pwrite_device(bg_ctx* c, const void* d, uint64_t n, int fd, int64_t at) {
+  if (!c || (!d && n) || at < 0) return BG_E_ARG;
+  if (n == 0) return 0;
+  bg_bind(c);
+  return write_device_ring(c, d, n, fd, (off_t)at);
 }
 
 // streams n bytes of device memory to fd (write_device_ring)

@@ -82,6 +82,11 @@ struct bg_group {
   std::vector<ncclComm_t> comm;  // one per local member (empty: no RCCL, single process)
   int nranks = 1;                // global members
   int rank0 = 0;                 // global index of local member 0
+  // BEDGPU_RCCL_SELF=1 on a one-member group: a one-rank communicator, and member 0's own
+  // runs go through ncclSend/ncclRecv to itself instead of device copies, so the
+  // communicator branch of bg_group_gather (all-reduce of the sizes, grouped send/recv,
+  // group error paths) runs on a one-GPU machine (tests/test_gpu_shard.py)
+  bool self = false;
 };
 
 static int nccl_fail(bg_ctx* c, ncclResult_t r, const char* what) {
@@ -120,7 +125,9 @@ extern "C" int bg_group_open(bg_group** out, const int* devices, int n) {
     g->ctx.push_back(c);
   }
   g->nranks = n;
-  if (distinct && n > 1) {
+  const char* se = getenv("BEDGPU_RCCL_SELF");
+  g->self = n == 1 && se && strcmp(se, "0") != 0;
+  if ((distinct && n > 1) || g->self) {
     if (!rccl().ok) {
       bg_fail(g->ctx[0], BG_E_HIP, "RCCL unavailable: " + rccl().err);
       bg_group_close(g);
@@ -150,13 +157,22 @@ extern "C" int bg_group_open_rank(bg_group** out, int device, const void* uid, i
   g->ctx.push_back(c);
   g->nranks = nranks;
   g->rank0 = rank;
-  if (nranks > 1) {
+  const char* se = getenv("BEDGPU_RCCL_SELF");
+  g->self = nranks == 1 && se && strcmp(se, "0") != 0;
+  if (nranks > 1 || g->self) {
     if (!rccl().ok) {
       bg_group_close(g);
       return BG_E_HIP;
     }
     ncclUniqueId id;
-    memcpy(&id, uid, sizeof(id));
+    if (g->self) {  // a one-rank group has no peer to share an id with
+      if (ncclGetUniqueId(&id) != ncclSuccess) {
+        bg_group_close(g);
+        return BG_E_HIP;
+      }
+    } else {
+      memcpy(&id, uid, sizeof(id));
+    }
     g->comm.resize(1);
     if (ncclCommInitRank(&g->comm[0], nranks, id, rank) != ncclSuccess) {
       g->comm.clear();
@@ -284,7 +300,7 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
   for (const Run& r : runs) {
     const int k = r.owner - g->rank0;
     if (k < 0 || k >= nl) continue;
-    if (!root || (!g->comm.empty() && r.owner != 0)) continue;
+    if (!root || (!g->comm.empty() && (r.owner != 0 || g->self))) continue;
     bg_ctx* c = g->ctx[k];
     bg_bind(c0);
     const void* src = text[k] + off[k][r.first];
@@ -293,7 +309,7 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
   }
   if (!g->comm.empty()) {
     bool any = false;
-    for (const Run& r : runs) any = any || r.owner != 0;
+    for (const Run& r : runs) any = any || r.owner != 0 || g->self;
     if (any) {
       int rc = 0;
       ncclResult_t e = ncclGroupStart();
@@ -301,7 +317,7 @@ extern "C" int bg_group_gather(bg_group* g, int nchrom, const char* const* text,
       if (!started) rc = nccl_fail(c0, e, "ncclGroupStart");
       for (size_t i = 0; i < runs.size() && !rc; ++i) {
         const Run& r = runs[i];
-        if (r.owner == 0) continue;
+        if (r.owner == 0 && !g->self) continue;
         const int ks = r.owner - g->rank0;
         if (ks >= 0 && ks < nl) {
           e = ncclSend(text[ks] + off[ks][r.first], r.bytes, ncclChar, 0, g->comm[ks], g->ctx[ks]->stream);
@@ -341,5 +357,12 @@ extern "C" void bg_device_free(bg_ctx* c, void* p) {
   if (!c || !p) return;
   bg_bind(c);
   hipStreamSynchronize(c->stream);
+  bg_release(c, p);
+}
+
+// stream-ordered: the block returns to ctx's cache at once, and whatever reuses it is queued
+// on ctx's stream after the work already there (no host wait)
+extern "C" void bg_device_release(bg_ctx* c, void* p) {
+  if (!c || !p) return;
   bg_release(c, p);
 }

@@ -250,41 +250,75 @@ def _phases(stderr):
     return {"host_ms": host, "stage_ms": stage}
 
 
-def e2e_cli(W, paths, rows, td, runs=3, devices=None):
+def _run_pipe(argv, env):
+    """one CLI run with stdout to a pipe read (and hashed) by this process; (seconds, sha16,
+    bytes, rc, stderr). The clock stops when the process has exited and the pipe is drained."""
+    h = hashlib.sha256()
+    n = 0
+    t0 = time.perf_counter()
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
+    import threading
+    err = []
+    th = threading.Thread(target=lambda: err.append(p.stderr.read()))
+    th.start()
+    while True:
+        b = p.stdout.read(1 << 22)
+        if not b:
+            break
+        h.update(b)
+        n += len(b)
+    rc = p.wait()
+    th.join()
+    return time.perf_counter() - t0, h.hexdigest()[:16], n, rc, b"".join(err)
+
+
+def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", extra_env=None):
     """the drop-in CLI, file -> file: `bedops_amd/bin/<tool> <args> <files> > out`, input files
     in the page cache, process start + HIP init + reads + device work + output write all
     inside the wall clock. Median of `runs`, with the BEDGPU_STATS phase
-    marks of the median run. devices: BEDGPU_DEVICES for the sharded drop-in (None: 1 GPU)."""
+    marks of the median run. devices: BEDGPU_DEVICES for the sharded drop-in (None: 1 GPU).
+    spacing: seconds between runs (0: back to back, as a shell script of consecutive
+    commands runs them); sink "pipe": stdout to a pipe this process drains (`| consumer`);
+    extra_env: e.g. BEDGPU_DETACH=0 (the process lifetime includes the GPU teardown)."""
     exe = os.path.join(ROOT, "bedops_amd", "bin", W["cli"])
     out = os.path.join(td, "cli_out.bed")
     args = W["args"] if W["cli"] != "closest-features" else ["--closest"]
     env = {k: v for k, v in os.environ.items() if k != "BEDGPU_DEVICES"}
     env["BEDGPU_STATS"] = "1"
+    env.update(extra_env or {})
     if devices:
         env["BEDGPU_DEVICES"] = devices
-    times, logs = [], []
+    times, logs, sha, nbytes = [], [], None, None
     for i in range(runs):
-        # runs start 0.5 s apart: the drop-in returns once its output is written and its GPU
-        # worker tears down detached (bedops_amd/cli/cli_common.h cli_detach, 60-100 ms in the
-        # kernel driver); a run started inside that window would pay for it in HIP init
-        if i:
-            time.sleep(0.5)
-        with open(out, "wb") as fo:
-            t0 = time.perf_counter()
-            r = subprocess.run([exe, *args, *paths], stdout=fo, stderr=subprocess.PIPE, env=env)
-            dt = time.perf_counter() - t0
-        if r.returncode != 0:
-            raise RuntimeError(f"CLI failed: {r.stderr.decode(errors='replace')[-2000:]}")
+        # by default runs start 0.5 s apart: the drop-in returns once its output is written
+        # and its GPU worker tears down detached (bedops_amd/cli/cli_common.h cli_detach,
+        # 60-100 ms in the kernel driver); a run started inside that window pays for it in HIP
+        # init (measured separately with spacing=0)
+        if i and spacing:
+            time.sleep(spacing)
+        if sink == "pipe":
+            dt, sha, nbytes, rc, err = _run_pipe([exe, *args, *paths], env)
+        else:
+            with open(out, "wb") as fo:
+                t0 = time.perf_counter()
+                r = subprocess.run([exe, *args, *paths], stdout=fo, stderr=subprocess.PIPE, env=env)
+                dt = time.perf_counter() - t0
+            rc, err = r.returncode, r.stderr
+        if rc != 0:
+            raise RuntimeError(f"CLI failed: {err.decode(errors='replace')[-2000:]}")
         times.append(dt)
-        logs.append(r.stderr.decode(errors="replace"))
-        log(f"e2e run {i}: {dt:.3f} s")
+        logs.append(err.decode(errors="replace"))
+        log(f"e2e run {i} ({sink}, spacing {spacing}, {extra_env or ''}): {dt:.3f} s")
     med = _median(times)
-    sha, nbytes = _sha16_file(out), os.path.getsize(out)
-    os.unlink(out)
+    if sink != "pipe":
+        sha, nbytes = _sha16_file(out), os.path.getsize(out)
+        os.unlink(out)
+    envs = " ".join(f"{k}={v}" for k, v in (extra_env or {}).items())
     rec = {"value": rows / med, "unit": "intervals/s", "median_s": round(med, 4),
-           "runs_s": [round(t, 4) for t in times],
-           "command": f"{'BEDGPU_DEVICES=' + devices + ' ' if devices else ''}"
-                      f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> > out",
+           "runs_s": [round(t, 4) for t in times], "spacing_s": spacing, "sink": sink,
+           "command": f"{'BEDGPU_DEVICES=' + devices + ' ' if devices else ''}{envs + ' ' if envs else ''}"
+                      f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> "
+                      f"{'| reader' if sink == 'pipe' else '> out'}",
            "output_sha16": sha, "output_bytes": nbytes,
            "phases": _phases(logs[times.index(med)])}
     return rec
@@ -563,6 +597,8 @@ def main():
 
     if rank != 0:
         grp.close()
+        # (rank 0 times the sharded drop-in once every rank has released its group)
+        dist.barrier()
         dist.destroy_process_group()
         return
 
@@ -596,14 +632,41 @@ def main():
                 "bytes_per_launch": int(per_launch), "rank": 0}
 
     e2e = cpu = e2e_sh = None
+    if world > 1:
+        # N GPUs: the shipped drop-in itself over the same N devices (BEDGPU_DEVICES=0..N-1,
+        # one process driving them, chromosome shards, per-device output writes), file ->
+        # file, a fresh child process started after every rank has released its group
+        grp.close()
+        grp = None
+        dist.barrier()
+        if not args.no_e2e and args.scale == 1.0 and not args.load_only and not args.weak:
+            with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as td:
+                paths, nrows = write_inputs(L, W, td)
+                e2e_sh = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs,
+                                 devices=",".join(str(d) for d in range(world)))
+                if W["ref"]:
+                    e2e_sh["matches_reference"] = e2e_sh["output_sha16"] == W["ref"]["sha16"]
+                for p in paths:
+                    os.unlink(p)
     if world == 1 and args.scale == 1.0 and not args.load_only and (
             not args.no_e2e or not args.no_cpu_baseline):
         with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as td:
             paths, nrows = write_inputs(L, W, td)
             if not args.no_e2e:
                 e2e = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs)
+                # the same command back to back (no spacing: the previous run's detached GPU
+                # teardown overlaps the next run's HIP init), with the GPU teardown inside the
+                # process lifetime (BEDGPU_DETACH=0), and with stdout to a pipe
+                variants = {"back_to_back": {"spacing": 0},
+                            "no_detach": {"extra_env": {"BEDGPU_DETACH": "0"}},
+                            "pipe": {"sink": "pipe"}}
+                for name, kw in variants.items():
+                    v = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs, **kw)
+                    e2e[name] = {k: v[k] for k in ("median_s", "runs_s", "command", "output_sha16")}
+                    e2e[name]["value"] = round(v["value"], 1)
                 if W["ref"]:
-                    e2e["matches_reference"] = e2e["output_sha16"] == W["ref"]["sha16"]
+                    e2e["matches_reference"] = all(x == W["ref"]["sha16"] for x in
+                                                   [e2e["output_sha16"]] + [e2e[n]["output_sha16"] for n in variants])
                 if args.e2e_devices:
                     e2e_sh = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs, devices=args.e2e_devices)
                     if W["ref"]:
@@ -611,11 +674,16 @@ def main():
             if not args.no_cpu_baseline:
                 info = cpu_info()
                 workers = args.cpu_workers or max(1, min(info["affinity_cpus"], 25))
+                # cores the fan-out can actually use: its processes, bounded by the CPUs visible
+                # and by the cgroup quota
+                eff = min(workers, info["affinity_cpus"],
+                          int(info["cgroup_cpu_quota"]) if info["cgroup_cpu_quota"] else workers)
                 fan = cpu_fanout_ref(L, W, paths, nrows, td, workers, args.cpu_fanout_runs) \
                     if _ref_exe(W) else None
                 single = cpu_single(W, paths, nrows, td, args.cpu_single_runs)
                 top = fan or single
-                cpu = {"value": top["value"], "unit": "intervals/s", "cores": top["cores"],
+                cpu = {"value": top["value"], "unit": "intervals/s",
+                       "cores": eff if fan else top["cores"], "processes": top["cores"],
                        "kind": top["kind"], "sample": top["sample"], **info,
                        "single": single, "fanout": fan}
             for p in paths:
@@ -643,11 +711,17 @@ def main():
         "e2e_intervals_per_s": round(e2e["value"], 1) if e2e else None,
         "e2e": e2e,
         "e2e_sharded": e2e_sh,
+        "e2e_sharded_intervals_per_s": round(e2e_sh["value"], 1) if e2e_sh else None,
         "gpu_vs_cpu": round(e2e["value"] / cpu["value"], 2) if (cpu and e2e) else None,
         "gpu_vs_cpu_single": round(e2e["value"] / cpu["single"]["value"], 2) if (cpu and e2e) else None,
-        "gpu_vs_cpu_scope": ("file->file CLI (median) vs the reference file->file: gpu_vs_cpu "
-                             "against run (ii) (--chrom fan-out), gpu_vs_cpu_single against run (i) "
-                             "(one process)") if (cpu and e2e) else None,
+        "gpu_vs_cpu_back_to_back": round(e2e["back_to_back"]["value"] / cpu["value"], 2)
+        if (cpu and e2e and "back_to_back" in e2e) else None,
+        "gpu_vs_cpu_scope": ("file->file CLI (median of runs 0.5 s apart, the front process's "
+                             "lifetime) vs the reference file->file: gpu_vs_cpu against run (ii) "
+                             "(--chrom fan-out), gpu_vs_cpu_single against run (i) (one process), "
+                             "gpu_vs_cpu_back_to_back: runs back to back against run (ii); "
+                             "e2e.no_detach includes the GPU teardown, e2e.pipe writes to a pipe")
+        if (cpu and e2e) else None,
         "parity": verify,
         "kernels_first_step_ms": {k: round(v[1], 4) for k, v in
                                   sorted(first.items(), key=lambda kv: -kv[1][1])},
@@ -656,7 +730,8 @@ def main():
         line["kernels_ms_per_step"] = {k: round(v[1] / args.steps, 4) for k, v in
                                        sorted(prof.items(), key=lambda kv: -kv[1][1])}
     print(json.dumps(line), flush=True)
-    grp.close()
+    if grp:
+        grp.close()
     if dist:
         dist.destroy_process_group()
 

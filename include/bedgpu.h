@@ -241,6 +241,9 @@ void bg_result_free(bg_result* res);
  * pwrite(2) of DMA'd chunks (BEDGPU_WRITE_PAR=0: not), anything else by double-buffered D2H
  * + write(2) */
 int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
+/* n bytes of device memory to the regular file fd at byte offset `at` (pwrite; the file
+ * position is neither used nor moved): the multi-GPU drop-in's per-device output parts */
+int bg_pwrite_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd, int64_t at);
 /* read a regular file into a new device buffer of ctx's device (its host image DMA'd to HBM,
  * see bg_file_image below); load it with bg_input.on_device = 1, free with bg_device_free.
  * Replaces the reader side of allocate_iterator_starch_bed for plain BED files
@@ -311,6 +314,9 @@ void bg_group_close(bg_group* g);
 int bg_group_gather(bg_group* g, int nchrom, const char* const* text, const uint64_t* const* off,
                     const uint64_t* const* len, char** out, uint64_t* out_len);
 void bg_device_free(bg_ctx* ctx, void* dptr);
+/* bg_device_free without the host wait: the block is reused only by work queued later on
+ * ctx's stream (so not with a second copy stream, BEDGPU_COPY_STREAMS=2) */
+void bg_device_release(bg_ctx* ctx, void* dptr);
 /* host byte ranges copied back to back into one new device buffer of ctx's device (a
  * file's chromosome shard, then loaded with bg_input.on_device = 1) */
 int bg_device_gather_host(bg_ctx* ctx, int n, const void* const* parts, const uint64_t* lens,

@@ -215,3 +215,70 @@ def test_closest_sharded_equals_single_device(gpu_bin, oracle_bin, case):
                 got = _cli(gpu_bin["closest"], case + files, devs)
                 assert got.returncode == 0, got.stderr
                 assert got.stdout == want, (case, trial, devs)
+
+
+def test_group_gather_through_rccl_self_communicator(oracle_bin, monkeypatch):
+    """BEDGPU_RCCL_SELF=1: a one-member group gets a one-rank RCCL communicator and sends its
+    own chromosome runs to itself (ncclAllReduce of the sizes, grouped ncclSend/ncclRecv), so
+    bg_group_gather's communicator branch runs on this one-GPU box; the reassembled text must
+    equal a single run"""
+    from bedops_amd.engine import BED3_SET, Group
+    from bedops_amd.shard import member_spans, strcmp_order
+
+    monkeypatch.setenv("BEDGPU_RCCL_SELF", "1")
+    rng = random.Random(9)
+    texts = [randbed.text(randbed.rows(rng, 5000, chroms=CHROMS, span=30000, maxlen=90)).encode()
+             for _ in range(2)]
+    gnames = strcmp_order({ln.split(b"\t", 1)[0].decode(): 1 for t in texts for ln in t.splitlines()})
+    for single in (True, False):
+        g = Group(devices=[0]) if single else Group(device=0, uid=bytes(128), nranks=1, rank=0)
+        try:
+            eng = g.engines[0]
+            s = eng.load([(x, BED3_SET) for x in texts])
+            r = eng.op("-i", s, [0, 1])
+            r.format()
+            dptr, _ = r.device_text()
+            names = s.chroms()
+            offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
+            out, n = g.gather(len(gnames), [(dptr, offs, lens)])
+            with tempfile.TemporaryFile() as fo:
+                eng.write_device(out, n, fo.fileno())
+                fo.seek(0)
+                got = fo.read()
+            eng.device_free(out)
+            r.free()
+            s.free()
+        finally:
+            g.close()
+        with tempfile.TemporaryDirectory() as td:
+            paths = []
+            for i, t in enumerate(texts):
+                p = os.path.join(td, f"in{i}.bed")
+                open(p, "wb").write(t)
+                paths.append(p)
+            want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE, check=True).stdout
+        assert got == want, single
+
+
+def test_sharded_cli_writes_each_device_part_at_its_offset(gpu_bin, oracle_bin, tmp_path):
+    """stdout a regular file: every shard writes its chromosomes' spans straight to their
+    offsets (bg_pwrite_device), no gather; a pipe keeps the gather. Both equal the oracle,
+    also after bytes already in the file (the output starts at the file position)"""
+    rng = random.Random(13)
+    a = str(tmp_path / "a.bed")
+    b = str(tmp_path / "b.bed")
+    open(a, "w").write(randbed.text(randbed.rows(rng, 20000, chroms=CHROMS, span=200000, maxlen=90)))
+    open(b, "w").write(randbed.text(randbed.rows(rng, 20000, chroms=CHROMS, span=200000, maxlen=90)))
+    want = subprocess.run([oracle_bin["bedops"], "-i", a, b], stdout=subprocess.PIPE, check=True).stdout
+    env = dict(os.environ, BEDGPU_DEVICES="0,0,0", BEDGPU_STATS="1")
+    out = str(tmp_path / "out.bed")
+    with open(out, "wb") as fo:
+        fo.write(b"head\n")
+        fo.flush()
+        r = subprocess.run([gpu_bin["bedops"], "-i", a, b], stdout=fo, stderr=subprocess.PIPE, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert open(out, "rb").read() == b"head\n" + want
+    assert b"shards" in r.stderr  # the sharded path ran (cli_mark)
+    r = subprocess.run([gpu_bin["bedops"], "-i", a, b], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
+                       timeout=120)
+    assert r.returncode == 0 and r.stdout == want, r.stderr
