@@ -18,9 +18,9 @@ all: lib cli tools oracle
 
 lib: $(LIB)
 cli: $(CLIS)
-tools: tools/build/libbedgen.so tools/build/bedgen
+tools: tools/build/libbedgen.so tools/build/bedgen tools/build/heap_replay_check
 
-$(OBJ)/%.o: $(SRC)/%.hip $(SRC)/bg_internal.h include/bedgpu.h
+$(OBJ)/%.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/bedgpu.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -47,6 +47,11 @@ tools/build/libbedgen.so: tools/bedgen.c
 tools/build/bedgen: tools/bedgen.c
 	@mkdir -p tools/build
 	$(CC) -O3 -fopenmp -DBEDGEN_MAIN -o $@ $<
+
+# the host heap replay (bg_heap_replay.h) on the CPU, checked against the oracle's addresses
+tools/build/heap_replay_check: tools/heap_replay_check.cpp $(SRC)/bg_heap_replay.h $(SRC)/bg_internal.h include/bedgpu.h
+	@mkdir -p tools/build
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle

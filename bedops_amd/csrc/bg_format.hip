@@ -87,6 +87,9 @@ struct FmtArgs {
   int single, has_elem;
   uint64_t stop_row;
   uint64_t* stop_out;
+  // each line's length from the count pass (RES_MAP / RES_CLOSEST): the write pass places
+  // the lines without rendering them once more just to measure them
+  uint32_t* rowlen;
 };
 
 __device__ __forceinline__ int dec_len_i32(int32_t v) {
@@ -978,7 +981,9 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __rest
 #pragma unroll 2
     for (int k = 0; k < FT_TILE / 64; ++k) {
       const uint64_t row = base + (uint64_t)k * 64;
+      const uint64_t n0 = co.n;
       if (row < A.n && !render<KIND>(A, row, co)) bg_report(st, row, ERR_RANGE);
+      if (A.rowlen && row < A.n) A.rowlen[row] = (uint32_t)(co.n - n0);
       if (KIND == RES_MAP && A.has_elem && row < A.n && A.cnt[row] <= 0)
         atomicMin(&st->stop_row, (unsigned long long)row);
     }
@@ -1002,7 +1007,10 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     CountOut co;
-    if (row < A.n) render<KIND>(A, row, co);
+    if (row < A.n) {
+      if (A.rowlen) co.n = A.rowlen[row];
+      else render<KIND>(A, row, co);
+    }
     uint64_t st;
     my[k] = tot + block_excl_scan(co.n, OpSum(), (uint64_t)0, sh, &st);
     tot += st;
@@ -1353,6 +1361,9 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
   BG_HIP(c, hipMemsetAsync(&c->dstat->stop_row, 0xff, 8, c->stream));
   static_assert(FT_TILE == BG_FMT_TILE, "format tile");
+  if ((A.kind == RES_MAP || A.kind == RES_CLOSEST) && r->n) {
+    A.rowlen = (uint32_t*)bg_alloc(c, 4 * r->n);  // (null: the write pass measures again)
+  }
   if (nb && A.kind == RES_ROWS && r->tbytes) {  // summed by bg_element_of's compaction
     BG_HIP(c, hipMemcpyAsync(tb, r->tbytes, 8ull * nb, hipMemcpyDeviceToDevice, c->stream));
   } else if (nb) {
@@ -1393,6 +1404,7 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   }
   r->toff = tb;
   bg_release(c, d_tot);
+  bg_release(c, A.rowlen);  // (stream-ordered: reused only by later work on c's stream)
   if (d_stop) {
     rc = bg_fetch_u64(c, d_stop, &total);
     bg_release(c, d_stop);

@@ -450,11 +450,11 @@ __device__ __forceinline__ uint64_t merge_path_xfirst(const int64_t* X, uint64_t
 // the sweep's own deque (bg_faster.hip); every candidate in the window range is a member
 // once bg_map_live has said it is in the deque
 #define BG_OVR_FAST 99
-__device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, double perc,
-                                          int64_t s, int64_t e, int64_t ms, int64_t me) {
+__host__ __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_t range, double perc,
+                                                   int64_t s, int64_t e, int64_t ms, int64_t me) {
   if (crit == BG_OVR_FAST) return true;
   if (crit == BG_OVR_RANGE) return (s < me) ? (e + range > ms) : (me + range > s);
-  const int64_t ov = min(e, me) - max(s, ms);
+  const int64_t ov = (e < me ? e : me) - (s > ms ? s : ms);
   if (ov <= 0) return false;
   if (crit == BG_OVR_BP) return ov >= ovr;
   if (crit == BG_OVR_EXACT) return ms == s && me == e;
@@ -688,8 +688,19 @@ __device__ __forceinline__ void bg_report(bg_dstatus* st, uint64_t row, int code
 
 // bg_heap.hip: the reference's heap address of every map row (device array), and whether
 // adjacent map rows tie on (start, end) [+ full_rest()]
-int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, int fields, bool ranged,
-                 int64_t range, int64_t** out, int fast_crit = -1, int64_t ovr = 0, double perc = 0.0);
+// (the replayed run: the visitors' criterion and its parameters, --faster, --skip-unmapped and
+// the operations in command-line order)
+struct bg_heap_spec {
+  int crit = 0;
+  bool faster = false;
+  int64_t ovr = 0, range = 0;
+  double perc = 1.0;
+  bool skip_unmapped = false;
+  int nops = 0;
+  const int* ops = nullptr;
+};
+int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, int fields,
+                 const bg_heap_spec* spec, int64_t** out);
 // bedmap --faster windows (bg_faster.hip)
 int bg_faster_windows(bg_ctx* c, const bg_table* R, const bg_table* M, int crit, int64_t ovr, int64_t range,
                       double perc, bool single, uint64_t* wlo, uint64_t* whi, int64_t* zin, int64_t* zout);

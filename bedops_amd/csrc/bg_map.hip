@@ -1376,8 +1376,18 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     }
     if (!rc && want) {
       if (opts->shard) rc = bg_fail(c, BG_E_UNSUPPORTED, "address-ordered ties span every chromosome: not on a chromosome shard");
-      else rc = bg_heap_addr(c, set, R, M, mapfields, crit == BG_OVR_RANGE, (int64_t)opts->range_bp, &res->maddr,
-                             faster ? crit : -1, (int64_t)opts->overlap_bp, perc);
+      else {
+        bg_heap_spec hs;
+        hs.crit = crit;
+        hs.faster = faster;
+        hs.ovr = (int64_t)opts->overlap_bp;
+        hs.range = (int64_t)opts->range_bp;
+        hs.perc = perc;
+        hs.skip_unmapped = opts->skip_unmapped != 0;
+        hs.nops = opts->n_ops;
+        hs.ops = opts->ops;
+        rc = bg_heap_addr(c, set, R, M, mapfields, &hs, &res->maddr);
+      }
     }
   }
   if (!rc && (decimal || tmean) && R->n) {

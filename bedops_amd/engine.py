@@ -31,6 +31,9 @@ SCORE_OPS = ("mean", "sum", "min", "max", "echo-map-score", "median", "kth", "va
 # operations (CoordRestAddressCompare: id + remainder)
 MAP_REST_OPS = ("echo-map", "echo-map-id", "echo-map-id-uniq", "mean", "sum", "variance", "stdev",
                 "cv", "min-element", "max-element", "min-element-rand", "max-element-rand", "tmean")
+# operations that can see the reference's heap-address order of equal rows (bedmap.c addr_ops)
+ADDR_OPS = ("wmean", "tmean", "echo-map", "echo-map-id", "echo-map-score", "echo-map-size",
+            "echo-overlap-size", "min-element", "max-element", "min-element-rand", "max-element-rand")
 OVR_CRITERIA = {"bp-ovr": 0, "range": 1, "fraction-ref": 2, "fraction-map": 3,
                 "fraction-either": 4, "fraction-both": 5, "exact": 6}
 
@@ -487,7 +490,9 @@ class Engine:
         if single:
             s = self.load([(ref_text, mkind)])
         else:
-            s = self.load([(ref_text, BED3_REST if "echo" in names else BED3), (map_text, mkind)])
+            # the reference rows' remainders size their strings in the heap replay (bg_heap.hip)
+            rrest = "echo" in names or any(op in ADDR_OPS for op in names)
+            s = self.load([(ref_text, BED3_REST if rrest else BED3), (map_text, mkind)])
         try:
             if chrom:
                 s.restrict_chrom(chrom)

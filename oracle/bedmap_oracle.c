@@ -60,8 +60,11 @@ typedef struct { int c; uint64_t s, e; int64_t id; } row_t;
 static int64_t* ADDR; /* simulated heap address of each map row (NULL: row index) */
 #define A_(m) (ADDR ? ADDR[m] : (m))
 static int SINGLE; /* single-file mode: the reference rows are the map rows (same objects) */
-static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], SINGLE ? r : -1 - r}; return x; }
-static row_t M_(int64_t m) { row_t x = {MAP->chrom[m], MAP->start[m], MAP->end[m], m}; return x; }
+/* Overlapping's last tie-break compares the two rows' addresses (BedDistances.hpp:108-110):
+ * the simulated heap address of a map row, and of the live reference row (two are alive) */
+static int64_t REFA[2];
+static row_t R_(int64_t r) { row_t x = {REF->chrom[r], REF->start[r], REF->end[r], SINGLE ? A_(r) : REFA[r & 1]}; return x; }
+static row_t M_(int64_t m) { row_t x = {MAP->chrom[m], MAP->start[m], MAP->end[m], A_(m)}; return x; }
 static int chrom_cmp(int a, int b) {
   if (a == b) return 0;
   int v = strcmp(POOL.names[a], POOL.names[b]);
@@ -385,7 +388,134 @@ static int tm_done(tmean_t* t, double* out) {
   return 1;
 }
 
+/* std::set node traffic. A B3Rest map row (32-byte object) shares the 48-byte chunk class with
+ * the 40-byte _Rb_tree_node<MapType*> of every set the sweep's visitors keep, so for B3Rest maps
+ * the address of a row depends on those nodes too (B4Rest / B5Rest rows use 64-byte chunks and
+ * are not disturbed). Modelled containers:
+ *   BedBaseVisitor's cache_ / win_ (BedBaseVisitor.hpp:139-153, fixWindow :185-211; the list
+ *     nodes of fixWindow use 32-byte chunks and are left out);
+ *   EchoMapBed / EchoMapIntersectLength / OvrAggregate: one node per Add (EchoMapBedVisitor.hpp:49-55,
+ *     EchoMapIntersectLengthVisitor.hpp:56-62, OvrAggregateVisitor.hpp:57-67);
+ *   OvrUnique(-Fract): a set keyed on coordinates (GenomicCompare), so rows with equal
+ *     coordinates share one node, stored by the first of them (OvrUniqueVisitor.hpp:51-58). */
+#define NODE_REQ 40
+static heapsim_t HS;
+static int NODES_ON;
+static int64_t *NCACHE, *NWIN, *CREP; /* CREP: first row with the same coordinates */
+static int64_t *NV[64], *HOLD[64];
+static int vset(int v) {
+  switch (v) {
+    case V_ECHO_MAP: case V_ECHO_MAP_ID: case V_ECHO_MAP_SCORE: case V_ECHO_MAP_SIZE: case V_ECHO_MAP_RANGE:
+    case V_ECHO_MAP_ID_UNIQ: case V_ECHO_OVERLAP_SIZE: case V_BASES: return 1;
+    case V_BASES_UNIQ: case V_BASES_UNIQ_F: return 2;
+  }
+  return 0;
+}
+static void nodes_init(int64_t n) {
+  NODES_ON = 1;
+  NCACHE = (int64_t*)malloc((size_t)(n + 1) * 8);
+  NWIN = (int64_t*)malloc((size_t)(n + 1) * 8);
+  CREP = (int64_t*)malloc((size_t)(n + 1) * 8);
+  for (int64_t m = 0; m <= n; ++m) NCACHE[m] = NWIN[m] = -1;
+  for (int64_t m = 0; m < n; ++m)
+    CREP[m] = (m && MAP->chrom[m] == MAP->chrom[m - 1] && MAP->start[m] == MAP->start[m - 1] &&
+               MAP->end[m] == MAP->end[m - 1]) ? CREP[m - 1] : m;
+  for (int q = 0; q < NVIS; ++q) {
+    if (!vset(VIS[q])) continue;
+    NV[q] = (int64_t*)malloc((size_t)(n + 1) * 8);
+    HOLD[q] = (int64_t*)malloc((size_t)(n + 1) * 8);
+    for (int64_t m = 0; m <= n; ++m) NV[q][m] = -1;
+  }
+}
+static void n_new(int64_t* s, int64_t k) { s[k] = hs_malloc(&HS, NODE_REQ); }
+static void n_free(int64_t* s, int64_t k) {
+  if (s[k] >= 0) { hs_free(&HS, NODE_REQ, s[k]); s[k] = -1; }
+}
+/* MultiVisitor::Add / Delete: each visitor in command-line order (MultiVisitor.hpp:71-81) */
+static void vis_add(int64_t m) {
+  for (int q = 0; q < NVIS; ++q) {
+    const int k = vset(VIS[q]);
+    if (k == 1) n_new(NV[q], m);
+    else if (k == 2 && NV[q][CREP[m]] < 0) { n_new(NV[q], CREP[m]); HOLD[q][CREP[m]] = m; }
+  }
+}
+static void vis_del(int64_t m) {
+  for (int q = 0; q < NVIS; ++q) {
+    const int k = vset(VIS[q]);
+    if (k == 1) n_free(NV[q], m);
+    else if (k == 2) n_free(NV[q], CREP[m]);
+  }
+}
+/* a temporary copy of a row (of `fields` columns + rest). Copy constructors allocate chrom_
+ * (Bed.hpp:70-72), id_ (B4/B5, :404), then rest_ and fullrest_ (B3Rest :291-294, B4Rest
+ * :509-512); B5Rest's copy constructor sizes rest_ / fullrest_ as strlen(p + 1), one byte
+ * short of the string (Bed.hpp:757-759; for an empty string the length read past it is taken
+ * as 0: such an allocation is in the smallest chunk class either way). The destructor frees
+ * rest_, fullrest_, id_, then chrom_ (Bed.hpp:622-626 / 876-881, 477-480, 100-104). */
+typedef struct { int64_t c, i, r, f; size_t lc, li, lr, lf; int fields; } tmprow_t;
+static size_t slen(const char* p) { return p ? strlen(p) : 0; }
+static void tmp_sizes(tmprow_t* t, const bedfile_t* f, int64_t i, int copy) {
+  const size_t c = strlen(POOL.names[f->chrom[i]]), d = t->fields >= 4 ? slen(f->id[i]) : 0;
+  const size_t r = f->rest ? slen(f->rest[i]) : 0;
+  t->lc = c + 1;
+  t->li = d + 1;
+  if (copy && t->fields == 5) {
+    t->lr = r ? r - 1 : 0;
+    t->lf = d + r ? d + r - 1 : 0;
+  } else {
+    t->lr = r + 1;
+    t->lf = d + r + 1;
+  }
+}
+static void tmp_copy(tmprow_t* t, const bedfile_t* f, int64_t i, int fields) {
+  t->fields = fields;
+  tmp_sizes(t, f, i, 1);
+  t->c = hs_malloc(&HS, t->lc);
+  if (fields >= 4) t->i = hs_malloc(&HS, t->li);
+  t->r = hs_malloc(&HS, t->lr);
+  if (fields >= 4) t->f = hs_malloc(&HS, t->lf);
+}
+/* operator=: chrom_ (Bed.hpp:92-97), id_ (:468-474), then rest_ / fullrest_ freed and
+ * re-allocated (:304-312, :609-619, :864-874) */
+static void tmp_assign(tmprow_t* t, const bedfile_t* f, int64_t i) {
+  tmprow_t n = *t;
+  tmp_sizes(&n, f, i, 0);
+  hs_free(&HS, t->lc, t->c);
+  t->c = hs_malloc(&HS, n.lc);
+  if (t->fields >= 4) { hs_free(&HS, t->li, t->i); t->i = hs_malloc(&HS, n.li); }
+  hs_free(&HS, t->lr, t->r);
+  if (t->fields >= 4) hs_free(&HS, t->lf, t->f);
+  t->r = hs_malloc(&HS, n.lr);
+  if (t->fields >= 4) t->f = hs_malloc(&HS, n.lf);
+  t->lc = n.lc; t->li = n.li; t->lr = n.lr; t->lf = n.lf;
+}
+static void tmp_drop(const tmprow_t* t) {
+  hs_free(&HS, t->lr, t->r);
+  if (t->fields >= 4) { hs_free(&HS, t->lf, t->f); hs_free(&HS, t->li, t->i); }
+  hs_free(&HS, t->lc, t->c);
+}
+/* EchoMapIntersectLength::DoneReference (EchoMapIntersectLengthVisitor.hpp:64-73): per map
+ * row a copy of the reference row, and a std::vector<long> growing 1, 2, 4, 8, ... */
+static void heap_intersect_lengths(int64_t r) {
+  int64_t buf = -1;
+  size_t cap = 0;
+  for (int64_t k = 0; k < VWIN.n; ++k) {
+    tmprow_t t;
+    tmp_copy(&t, REF, r, SINGLE ? MAPFIELDS : 3);
+    if ((size_t)k == cap) { /* _M_realloc_insert: allocate, move, free the old buffer */
+      const size_t nc = cap ? 2 * cap : 1;
+      const int64_t nb = hs_malloc(&HS, nc * 8);
+      if (cap) hs_free(&HS, cap * 8, buf);
+      buf = nb;
+      cap = nc;
+    }
+    tmp_drop(&t);
+  }
+  if (cap) hs_free(&HS, cap * 8, buf);
+}
+
 static void v_add(int64_t m) {
+  if (NODES_ON) vis_add(m);
   ++count_;
   if (MAP->score) {
     sum_ += MAP->score[m]; sq_ += MAP->score[m] * MAP->score[m]; ++counter_;
@@ -395,6 +525,7 @@ static void v_add(int64_t m) {
   ++cnt_;
 }
 static void v_del(int64_t m) {
+  if (NODES_ON) vis_del(m);
   --count_;
   if (MAP->score) {
     sum_ -= MAP->score[m]; sq_ -= MAP->score[m] * MAP->score[m]; --counter_;
@@ -424,13 +555,18 @@ static uint64_t ovr_len(uint64_t as, uint64_t ae, uint64_t bs, uint64_t be) {
   return mx > mn ? mx - mn : 0;
 }
 /* OvrUnique::DoneReference, OvrUniqueVisitor.hpp:62-78 (its set is in genomic order) */
-static unsigned int ovr_uniq(int64_t r) {
+static unsigned int ovr_uniq(int q, int64_t r) {
   unsigned int ovr = 0;
   if (VWIN.n == 0) return 0;
+  /* the set holds one row per distinct coordinates (GenomicCompare): equal rows are adjacent
+   * in the window's order; the temporary is a copy of the row the set stored */
+  tmprow_t t;
+  if (NODES_ON) tmp_copy(&t, MAP, HOLD[q][CREP[VWIN.v[0]]], MAPFIELDS);
   uint64_t ts = MAP->start[VWIN.v[0]], te = MAP->end[VWIN.v[0]];
   const uint64_t rs = REF->start[r], re = REF->end[r];
   for (int64_t i = 1; i < VWIN.n; ++i) {
     const uint64_t s = MAP->start[VWIN.v[i]], e = MAP->end[VWIN.v[i]];
+    if (s == MAP->start[VWIN.v[i - 1]] && e == MAP->end[VWIN.v[i - 1]]) continue;
     if (ovr_len(ts, te, s, e)) {
       ts = ts < s ? ts : s;
       te = te > e ? te : e;
@@ -438,9 +574,11 @@ static unsigned int ovr_uniq(int64_t r) {
       ovr += (unsigned int)ovr_len(ts, te, rs, re);
       ts = s;
       te = e;
+      if (NODES_ON) tmp_assign(&t, MAP, HOLD[q][CREP[VWIN.v[i]]]);
     }
   }
   ovr += (unsigned int)ovr_len(ts, te, rs, re);
+  if (NODES_ON) tmp_drop(&t);
   return ovr;
 }
 /* one map row as its type prints it: B3Rest "%s\t%lu\t%lu%s", B4Rest "...\t%s%s",
@@ -567,9 +705,9 @@ static void v_done(int64_t r) {
         printf("%lu", o);
         break;
       }
-      case V_BASES_UNIQ: printf("%u", ovr_uniq(r)); break;
+      case V_BASES_UNIQ: printf("%u", ovr_uniq(i, r)); break;
       case V_BASES_UNIQ_F:
-        put_real((double)ovr_uniq(r) / (double)(REF->end[r] - REF->start[r]));
+        put_real((double)ovr_uniq(i, r) / (double)(REF->end[r] - REF->start[r]));
         break;
       case V_ECHO:
         if (SINGLE) { print_map_row(r); break; } /* the row as its (map) type prints it */
@@ -649,7 +787,15 @@ static void v_done(int64_t r) {
         break;
       }
       case V_ECHO_MAP: case V_ECHO_MAP_ID: case V_ECHO_MAP_SCORE: case V_ECHO_MAP_SIZE:
-      case V_ECHO_OVERLAP_SIZE: case V_ECHO_MAP_RANGE: echo_map(VIS[i], r); break;
+      case V_ECHO_OVERLAP_SIZE: case V_ECHO_MAP_RANGE:
+        if (NODES_ON && VIS[i] == V_ECHO_OVERLAP_SIZE) heap_intersect_lengths(r);
+        if (NODES_ON && VIS[i] == V_ECHO_MAP_RANGE && VWIN.n) { /* PrintGenomicRange's copy, ProcessBedVisitorRow.hpp:446 */
+          tmprow_t t;
+          tmp_copy(&t, MAP, VWIN.v[0], MAPFIELDS);
+          tmp_drop(&t);
+        }
+        echo_map(VIS[i], r);
+        break;
       case V_ECHO_NAME:
         printf("%s:%" PRIu64 "-%" PRIu64, POOL.names[REF->chrom[r]], REF->start[r], REF->end[r]);
         break;
@@ -672,7 +818,6 @@ static double parse_frac(const char* v) {
  * re-allocates chrom_ and id_, then rest_ and fullrest_ (B4/B5: id + rest); the destructor
  * frees rest_, fullrest_, id_, chrom_, then the object */
 typedef struct { int64_t o, c, i, r, f; size_t lc, li, lr; } rowmem_t;
-static heapsim_t HS;
 static void row_new(rowmem_t* x, int fields, size_t lc, size_t li, size_t lr) {
   x->lc = lc; x->li = li; x->lr = lr;
   x->o = hs_malloc(&HS, fields == 3 ? 32 : (fields == 4 ? 48 : 56));
@@ -705,9 +850,10 @@ static void ref_new(int64_t r) {
     row_new(&RMEM[r & 1], 3, strlen(POOL.names[REF->chrom[r]]), 0, REF->rest ? strlen(REF->rest[r]) : 0);
   else
     row_new(&RMEM[r & 1], 3, 0, 0, 0);
+  REFA[r & 1] = RMEM[r & 1].o;
 }
 
-static oset_t vcache, lst, ev;
+static oset_t vcache, lst, ev, dl;
 /* one file under the Overlapping specialisation: rows shorter than the required overlap
  * reach no visitor (WindowSweepImpl.specialize.cpp:66-67, 110-111) */
 static int f_visible(int64_t m) { return !SINGLE || CRIT != C_BP || MAP->end[m] - MAP->start[m] >= (FASTER ? OVR : 0); }
@@ -717,8 +863,13 @@ static void on_delete(int64_t m) {
     if (f_visible(m)) { os_erase(&VWIN, m); v_del(m); }
     return;
   }
-  if (os_erase(&VWIN, m)) v_del(m);
-  else os_erase(&vcache, m);
+  if (os_erase(&VWIN, m)) {
+    v_del(m);
+    if (NODES_ON) n_free(NWIN, m);
+  } else {
+    os_erase(&vcache, m);
+    if (NODES_ON) n_free(NCACHE, m);
+  }
 }
 /* BedBaseVisitor::OnAdd (:139-143, into its cache); --faster: MultiVisitor's Add */
 static void on_add(int64_t m) {
@@ -727,6 +878,7 @@ static void on_add(int64_t m) {
     return;
   }
   os_insert(&vcache, m);
+  if (NODES_ON) n_new(NCACHE, m);
 }
 /* BedBaseVisitor::OnDone: fixWindow (deletions first, then insertions), then DoneReference;
  * --faster: DoneReference on the window as the sweep left it */
@@ -744,7 +896,12 @@ static void on_done(int64_t r) {
     } else ++i;
   }
   sort_rless(ev.v, ev.n);
-  for (int64_t i = 0; i < ev.n; ++i) v_del(ev.v[i]);
+  for (int64_t i = 0; i < ev.n; ++i) {
+    v_del(ev.v[i]);
+    if (NODES_ON) n_free(NWIN, ev.v[i]); /* Delete, lst.push_back, win_.erase */
+  }
+  dl.n = 0;
+  for (int64_t i = 0; i < ev.n; ++i) ev_push(&dl, ev.v[i]);
   ev.n = 0;
   for (int64_t i = 0; i < vcache.n;) {
     int64_t m = vcache.v[i];
@@ -756,14 +913,20 @@ static void on_done(int64_t r) {
     } else ++i;
   }
   sort_rless(ev.v, ev.n);
-  for (int64_t i = 0; i < ev.n; ++i) v_add(ev.v[i]);
+  for (int64_t i = 0; i < ev.n; ++i) {
+    v_add(ev.v[i]);
+    if (NODES_ON) { n_new(NWIN, ev.v[i]); n_free(NCACHE, ev.v[i]); } /* Add, win_.insert, cache_.erase */
+  }
   for (int64_t i = 0; i < lst.n; ++i) os_insert(&vcache, lst.v[i]);
+  if (NODES_ON)
+    for (int64_t i = 0; i < dl.n; ++i) n_new(NCACHE, dl.v[i]); /* cache_.insert(lst), in list order */
   v_done(r);
 }
 
 int main(int argc, char** argv) {
   int a = 1, need5 = 0, need4 = 0, rest = 0;
   const char* only_chrom = NULL;
+  const char* dump_addr = NULL;
   static const struct { const char* name; int v; int score; } OPS[] = {
       {"--count", V_COUNT, 0},         {"--mean", V_MEAN, 1},           {"--sum", V_SUM, 1},
       {"--min", V_MIN, 1},             {"--max", V_MAX, 1},             {"--indicator", V_INDICATOR, 0},
@@ -829,6 +992,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(o, "--sci")) SCI = 1;
     else if (!strcmp(o, "--skip-unmapped")) SKIP_UNMAPPED = 1;
     else if (!strcmp(o, "--faster")) FASTER = 1;
+    else if (!strcmp(o, "--dump-addr") && a < argc) dump_addr = argv[a++]; /* the replayed addresses */
     else if (!strcmp(o, "--ec") || !strcmp(o, "--header") || !strcmp(o, "--sweep-all")) {}
     else { fprintf(stderr, "bedmap_oracle: unsupported option %s\n", o); return 2; }
   }
@@ -841,7 +1005,8 @@ int main(int argc, char** argv) {
   if (!fr || (!SINGLE && !fm)) { fprintf(stderr, "bedmap_oracle: cannot open input\n"); return 2; }
   MAPFIELDS = need5 ? 5 : (need4 ? 4 : 3);
   if (!SINGLE) {
-    read_bed3(fr, &POOL, &ref, rest);
+    read_bed3(fr, &POOL, &ref, 1); /* rest_ kept for --echo and for its heap size */
+    (void)rest;
     fr = fm;
   }
   if (need5) read_bed5(fr, &POOL, &map);
@@ -865,6 +1030,7 @@ int main(int argc, char** argv) {
   }
   REF = SINGLE ? &map : &ref;
   MAP = &map;
+  nodes_init(map.n);
   static char obuf[1 << 20];
   setvbuf(stdout, obuf, _IOFBF, sizeof(obuf));
 
@@ -937,5 +1103,11 @@ int main(int argc, char** argv) {
     }
   }
   fflush(stdout);
+  if (dump_addr) {
+    FILE* fa = fopen(dump_addr, "w");
+    if (!fa) return 2;
+    for (int64_t m = 0; m < map.n; ++m) fprintf(fa, "%" PRId64 "\n", ADDR[m]);
+    fclose(fa);
+  }
   return 0;
 }

@@ -15,9 +15,11 @@
  * LIFO fast bin; a malloc that misses the cache pops the fast bin and stashes the rest of
  * that bin into the cache (_int_malloc's fastbin path); a miss on both takes fresh memory
  * from the top of the heap (increasing addresses). Chunk size = request + 8 rounded up to
- * 16, at least 32. Only the row objects and their strings are modelled: the other heap
- * users of the sweep (std::set nodes, deque blocks) use other chunk sizes than B4Rest /
- * B5Rest row objects (48 / 56 bytes -> 64-byte chunks), so they do not disturb those.
+ * 16, at least 32. Modelled (oracle/bedmap_oracle.c): the row objects and their strings,
+ * the std::set nodes of BedBaseVisitor and of the visitors keeping one per row or per
+ * coordinates (40 bytes: the 48-byte chunks of B3Rest row objects), and DoneReference's
+ * temporaries (row copies, EchoMapIntersectLength's vector). Not modelled: the sweep's deque
+ * blocks and fixWindow's list nodes (other chunk sizes than any row object's).
  * Not modelled: malloc_consolidate (only when the heap grows while fast bins are occupied, or
  * on large requests), which a multi-megabyte sweep window can trigger.
  */

@@ -23,11 +23,7 @@ OUTSIDE_CONTRACT = {("closest", 90), ("closest", 91), ("closest", 92),  # unsort
 # so does the GPU path for any coordinate below the 2^40 key limit)
 # the heap-address replay's known residual (tests/test_ref_fixtures.py KNOWN): the GPU follows
 # the oracle's model there, which the reference's malloc_consolidate departs from
-KNOWN = {("bedmap", 160),
-         # one file, B3Rest map rows (48-byte chunks, the size of a std::set node): the
-         # visitors' set nodes (OvrUnique, EchoMapBed) share the rows' chunk class, which the
-         # model does not replay, and --echo-map lists equal rows in address order
-         ("faster", 62), ("faster", 126)}
+KNOWN = {("bedmap", 160)}
 
 CHUNK = 40
 _SIZES = {"closest": 96, "bedmap": 313, "decimal": 124, "sortbed": 6, "ec": 112, "faster": 181}

@@ -18,11 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # reference orders equal-coordinate map rows by heap address; the model replays glibc's
 # tcache/fast-bin reuse but not malloc_consolidate, which this case's 150-row window
 # triggers when the heap grows. (suite, case index)
-KNOWN = {("bedmap", 160),
-         # one file, B3Rest map rows (48-byte chunks, the size of a std::set node): the
-         # visitors' set nodes (OvrUnique, EchoMapBed) share the rows' chunk class, which the
-         # model does not replay, and --echo-map lists equal rows in address order
-         ("faster", 62), ("faster", 126)}
+KNOWN = {("bedmap", 160)}
 
 
 def _bin(oracle_bin, tool):
