@@ -98,6 +98,10 @@ __device__ __forceinline__ uint32_t cl_pop(ClState& S) {
   }
   return S.c[S.n];
 }
+// entry i of the stack (i < n) without popping
+__device__ __forceinline__ uint32_t cl_peek(const ClState& S, uint32_t i) {
+  return i >= S.n - S.m ? S.l[(i & (CL_D - 1)) * BG_NT] : S.c[i];
+}
 // the whole stack in global memory (snapshots, comparisons)
 __device__ __forceinline__ void cl_flush(ClState& S) {
   for (uint32_t i = S.n - S.m; i < S.n; ++i) S.c[i] = S.l[(i & (CL_D - 1)) * BG_NT];
@@ -166,8 +170,28 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     pcs[i] = A.nc ? A.cs[j] : 0;
     pce[i] = A.nc ? A.ce[j] : 0;
   }
+  // the next SPF stack entries to be popped (top first) and their keys, loaded ahead: a
+  // scan only pops (the kept list is pushed back after it), so the stack entries it will
+  // read are known when it starts (a pop then no longer waits on its candidate's keys)
+#ifndef BG_SPF
+#define BG_SPF 4
+#endif
+#ifndef BG_CL_FAST
+#define BG_CL_FAST true
+#endif
+  constexpr int SPF = BG_SPF;
+  uint32_t sc[SPF];
+  int64_t scs[SPF], sce[SPF];
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
+#pragma unroll
+    for (int i = 0; i < SPF; ++i) {
+      if ((uint32_t)i < S.n) {
+        sc[i] = cl_peek(S, S.n - 1 - i);
+        scs[i] = A.cs[sc[i]];
+        sce[i] = A.ce[sc[i]];
+      }
+    }
     const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
     int64_t ld = D_MINUS, rdist = D_PLUS;
     int64_t left = -1, right = -1, lce = 0;  // lce = ce[left]
@@ -179,12 +203,71 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     if (nk == cap) ovf = true;          \
     else kept.put(nk++, (uint32_t)(x)); \
   } while (0)
+    bool fast = BG_CL_FAST;  // the file's run of rows left of b, once per scan (below)
     for (;;) {
       int64_t c, cs, ce;
+      if (fast && S.n == 0) {
+        // The rows the file holds before the first one reaching past bs (ce <= bs: d < 0, or
+        // an earlier chromosome, skipped) change only (left, ld, lc) and the kept list:
+        //   d >= ld (newleft): reset; left = c; ld = d; lc = 0
+        //   d <  ld (dropL)  : keepL unless lc; lc = 1
+        // (the general chain's outcome for d < 0, below). On the benchmark's inputs this run
+        // is ~70% of the rows read; here it is a compare per row over a batch of `ce` keys
+        // loaded together, instead of the whole chain per row.
+        fast = false;
+        const int64_t gb = bs >> BG_KEY_SHIFT;
+        const uint64_t fp0 = S.fp;
+        for (;;) {
+          const uint64_t f0 = S.fp;
+          if (f0 >= A.nc) break;
+          int64_t v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = A.ce[min(f0 + i, nc1)];
+          int i = 0;
+          for (; i < 8; ++i) {
+            if (f0 + i >= A.nc || v[i] > bs) break;
+            if ((v[i] >> BG_KEY_SHIFT) != gb) continue;  // earlier chromosome: dropped
+            const int64_t d = -((bs - v[i]) + 1);
+            if (d >= ld) {
+              nk = 0;
+              ovf = false;
+              left = (int64_t)(f0 + i);
+              lce = v[i];
+              ld = d;
+              lc = false;
+            } else {
+              if (left >= 0 && !lc) KEEP(left);
+              lc = true;
+            }
+          }
+          S.fp = f0 + i;
+          if (i < 8) break;
+        }
+        if (S.fp != fp0) {  // the file stream's look-ahead restarts at the new position
+#pragma unroll
+          for (int i = 0; i < CPF; ++i) {
+            const uint64_t j = min(S.fp + i, nc1);
+            pcs[i] = A.cs[j];
+            pce[i] = A.ce[j];
+          }
+        }
+      }
       if (S.n) {
-        c = cl_pop(S);
-        cs = A.cs[c];
-        ce = A.ce[c];
+        cl_pop(S);
+        c = sc[0];
+        cs = scs[0];
+        ce = sce[0];
+#pragma unroll
+        for (int i = 0; i + 1 < SPF; ++i) {
+          sc[i] = sc[i + 1];
+          scs[i] = scs[i + 1];
+          sce[i] = sce[i + 1];
+        }
+        if (S.n >= (uint32_t)SPF) {  // the entry SPF - 1 below the new top
+          sc[SPF - 1] = cl_peek(S, S.n - SPF);
+          scs[SPF - 1] = A.cs[sc[SPF - 1]];
+          sce[SPF - 1] = A.ce[sc[SPF - 1]];
+        }
       } else if (S.fp < A.nc) {
         c = (int64_t)S.fp++;
         cs = pcs[0];

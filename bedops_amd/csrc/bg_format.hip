@@ -124,8 +124,15 @@ __device__ __forceinline__ uint32_t dig4_ascii(uint32_t x) {
   return (t | (u << 8)) + 0x30303030u;
 }
 
-// v (< 10^12) as exactly len digits into LDS: three 4-digit groups, then byte stores
+// v (< 10^13, coordinates are < 2^40) as exactly len digits into LDS: three 4-digit groups,
+// then byte stores (a 13th leading digit separately)
 __device__ __forceinline__ void put_u64_lds(char* p, uint64_t v, int len) {
+  if (len > 12) {
+    const uint64_t top = v / 1000000000000ull;
+    *p++ = (char)('0' + top);
+    v -= top * 1000000000000ull;
+    len = 12;
+  }
   uint32_t hi, mid, lo;
   if ((v >> 32) == 0) {
     const uint32_t w = (uint32_t)v;
@@ -396,6 +403,21 @@ __device__ __forceinline__ bool put_real(Out& o, double v, int prec, bool sci) {
   return true;
 }
 
+// put_real's "%.{p}lf" for finite values whose digits fit 64 bits; false otherwise (NaN,
+// infinities and huge values are left to the general formatter, RES_MAP)
+template <typename Out>
+__device__ __forceinline__ bool put_real_fixed(Out& o, double v, int prec) {
+  uint64_t N;
+  bool neg;
+  if (!fixed_digits(v, prec, N, neg)) return false;
+  put_fixed(o, N, neg, prec);
+  return true;
+}
+// RES_MAP formatted without the window / text / element / order-statistic operations and
+// without --sci: a small kernel (the general one holds ~200 VGPRs and spills SGPRs for the
+// operations a run does not use); bg_result_format falls back to RES_MAP on any value this
+// path refuses
+#define RES_MAPS 100
 struct CountOut {  // measures only
   uint64_t n = 0;
   __device__ __forceinline__ void put_at(int, char) {}
@@ -572,11 +594,13 @@ __device__ __forceinline__ void map_window_genomic(const FmtArgs& A, uint64_t k,
     return bg_map_live(A.zin, A.zout, k, m) && bg_map_in(A.crit, A.ovr, A.range, A.perc, s, e, A.s2[m], A.e2[m]);
   };
   uint64_t skip = 0;  // rows below this went out with their tie run
+  // --faster: the window is exactly [wlo, whi) (the sweep's deque), so a tie run is cut to it
+  const uint64_t tend = A.crit == BG_OVR_FAST ? A.whi[k] : A.n2;
   bg_map_cands(A.s2, A.e2, A.wlo[k], A.whi[k], A.lrows, s, e, fmt_pad(A), [&](uint64_t m) {
     if (m < skip) return true;
-    if (A.maddr && m + 1 < A.n2 && A.s2[m + 1] == A.s2[m] && A.e2[m + 1] == A.e2[m]) {
+    if (A.maddr && m + 1 < tend && A.s2[m + 1] == A.s2[m] && A.e2[m + 1] == A.e2[m]) {
       uint64_t t = m + 1;
-      while (t < A.n2 && A.s2[t] == A.s2[m] && A.e2[t] == A.e2[m]) ++t;
+      while (t < tend && A.s2[t] == A.s2[m] && A.e2[t] == A.e2[m]) ++t;
       skip = t;
       bool has = false;
       int64_t last = 0;
@@ -817,7 +841,8 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
     render_closest(A, k, o);
     return true;
   }
-  if (KIND == RES_MAP) {
+  if (KIND == RES_MAP || KIND == RES_MAPS) {
+    constexpr bool FULL = KIND == RES_MAP;  // RES_MAPS: the plain numeric columns only
     // one value per operation (MultiVisitor.hpp:83-98); formats: Count/Indicator "%d",
     // OvrAggregate "%lu", OvrUnique "%u", Echo (ProcessBedVisitorRow.hpp:309-342), the rest
     // "%.{p}lf" or "NAN" (PrintScorePrecision, Formats.hpp:42-50)
@@ -842,7 +867,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         put_u64(o, (uint64_t)A.uniq[k], dec_len_u64((uint64_t)A.uniq[k]));
         continue;
       }
-      if (op == BG_MAP_ECHO) {
+      if (FULL && op == BG_MAP_ECHO) {
         if (A.single) {  // the row as its own (map) type prints it
           if (!put_map_row(A, o, k)) return false;
         } else {
@@ -850,16 +875,16 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         }
         continue;
       }
-      if (is_elem_op(op)) {
+      if (FULL && is_elem_op(op)) {
         if (c <= 0) return true;  // the reference throws here: the line ends unfinished
         if (!put_element(A, o, k, op)) return false;
         continue;
       }
-      if (op == BG_MAP_ECHO_MAP_ID_UNIQ) {
+      if (FULL && op == BG_MAP_ECHO_MAP_ID_UNIQ) {
         put_unique_ids(A, o, k);
         continue;
       }
-      if (op == BG_MAP_ECHO_REF_ROW_ID) {  // PrintRowID: "id-" ++rowID (a static shared by all)
+      if (FULL && op == BG_MAP_ECHO_REF_ROW_ID) {  // PrintRowID: "id-" ++rowID (a static shared by all)
         const uint64_t line = A.rrank ? A.rrank[k] : k;
         uint64_t j = 0;
         for (int q2 = 0; q2 < q; ++q2) j += A.ops[q2] == BG_MAP_ECHO_REF_ROW_ID;
@@ -868,7 +893,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
         put_u64(o, id, dec_len_u64(id));
         continue;
       }
-      if (op >= BG_MAP_ECHO_MAP && op <= BG_MAP_ECHO_MAP_RANGE) {
+      if (FULL && op >= BG_MAP_ECHO_MAP && op <= BG_MAP_ECHO_MAP_RANGE) {
         if (!put_echo_map(A, o, k, op)) return false;
         continue;
       }
@@ -914,7 +939,7 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
           if (mean == 0) { o.put('N'); o.put('A'); o.put('N'); continue; }
           v = v / mean;
         }
-      } else if (op == BG_MAP_MAD) {  // MedianAbsoluteDeviation::DoneReference (:70-110)
+      } else if (FULL && op == BG_MAP_MAD) {  // MedianAbsoluteDeviation::DoneReference (:70-110)
         if (c <= 1) { o.put('N'); o.put('A'); o.put('N'); continue; }
         const double med = window_kth(A, k, (uint32_t)c, 0.5);
         const uint32_t sz = (uint32_t)c;
@@ -927,16 +952,20 @@ __device__ __forceinline__ bool render(const FmtArgs& A, uint64_t k, Out& o) {
           mad = window_rank(A, k, sz / 2, true, med);
         }
         v = mad * (A.op_arg[q] > 0 ? A.op_arg[q] : 1.0);
-      } else if (op == BG_MAP_MEDIAN || op == BG_MAP_KTH) {
+      } else if (FULL && (op == BG_MAP_MEDIAN || op == BG_MAP_KTH)) {
         v = window_kth(A, k, (uint32_t)c, op == BG_MAP_MEDIAN ? 0.5 : A.op_arg[q]);
-      } else if (op == BG_MAP_TMEAN) {
+      } else if (FULL && op == BG_MAP_TMEAN) {
         v = A.tmv[q][k];
-      } else if (op == BG_MAP_WMEAN) {
+      } else if (FULL && op == BG_MAP_WMEAN) {
         v = window_wmean(A, k);
       } else {
         v = (op == BG_MAP_MIN) ? A.vmin[k] : A.vmax[k];
       }
-      if (!put_real(o, v, A.prec, A.sci)) return false;
+      if (FULL) {
+        if (!put_real(o, v, A.prec, A.sci)) return false;
+      } else if (!put_real_fixed(o, v, A.prec)) {
+        return false;  // (the general kind renders this run)
+      }
     }
     o.put('\n');
     return true;
@@ -1303,6 +1332,16 @@ static void fill_args(bg_result* r, FmtArgs& A) {
   }
 }
 
+static bool map_simple_op_host(int op) {
+  switch (op) {
+    case BG_MAP_COUNT: case BG_MAP_INDICATOR: case BG_MAP_BASES: case BG_MAP_BASES_UNIQ: case BG_MAP_BASES_UNIQ_F:
+    case BG_MAP_MEAN: case BG_MAP_SUM: case BG_MAP_VARIANCE: case BG_MAP_STDEV: case BG_MAP_CV: case BG_MAP_MIN:
+    case BG_MAP_MAX: case BG_MAP_ECHO_SIZE: case BG_MAP_ECHO_NAME:
+      return true;
+  }
+  return false;
+}
+
 extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if (!c || !r) return BG_E_ARG;
   if (r->kind == RES_ROWS && !r->set->t[r->tab]->rest_off)
@@ -1364,13 +1403,19 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   if ((A.kind == RES_MAP || A.kind == RES_CLOSEST) && r->n) {
     A.rowlen = (uint32_t*)bg_alloc(c, 4 * r->n);  // (null: the write pass measures again)
   }
+  bool simple = A.kind == RES_MAP && !A.sci && !A.has_elem;
+  for (int k = 0; simple && k < A.nops; ++k) simple = map_simple_op_host(A.ops[k]);
+count_again:
   if (nb && A.kind == RES_ROWS && r->tbytes) {  // summed by bg_element_of's compaction
     BG_HIP(c, hipMemcpyAsync(tb, r->tbytes, 8ull * nb, hipMemcpyDeviceToDevice, c->stream));
   } else if (nb) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_count", k_fmt_ivl_count, dim3(nb), dim3(BG_NT), A, tb); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_ROWS>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
-      case RES_MAP: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
+      case RES_MAP:
+        if (simple) BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAPS>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat);
+        else BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MAP>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat);
+        break;
       case RES_MULTI: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_MULTI>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat); break;
       default: BG_LAUNCH(c, "k_fmt_count", k_fmt_count<RES_CLOSEST>, dim3(nbc), dim3(BG_NT), A, tb, (uint64_t)nb, c->dstat);
     }
@@ -1381,6 +1426,12 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
   uint64_t total = 0;
   BG_HIP(c, hipMemcpyAsync(c->hstat, c->dstat, sizeof(bg_dstatus), hipMemcpyDeviceToHost, c->stream));
   if ((rc = bg_fetch_u64(c, d_tot, &total))) return rc;
+  if (c->hstat->first_bad != ~0ULL && simple) {  // a value the small kernel refuses: the general one
+    simple = false;
+    BG_HIP(c, hipMemsetAsync(&c->dstat->first_bad, 0xff, 8, c->stream));
+    BG_HIP(c, hipMemsetAsync(&c->dstat->stop_row, 0xff, 8, c->stream));
+    goto count_again;
+  }
   if (c->hstat->first_bad != ~0ULL)
     return bg_fail(c, BG_E_UNSUPPORTED, "a value is outside the GPU formatter's range");
   r->text = (char*)bg_alloc(c, total + 16);
@@ -1396,7 +1447,10 @@ extern "C" int bg_result_format(bg_ctx* c, bg_result* r, uint64_t* nbytes) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_write, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       case RES_ROWS: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
-      case RES_MAP: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_MAP:
+        if (simple) BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAPS>, dim3(nb), dim3(BG_NT), A, tb, r->text);
+        else BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text);
+        break;
       case RES_MULTI: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MULTI>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
       default: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, r->text);
     }

@@ -89,6 +89,12 @@ struct bg_group {
   bool self = false;
 };
 
+// a group that cannot be opened has no context to keep the message in: say why on stderr
+static void group_warn(const std::string& m) { fprintf(stderr, "bedgpu: group: %s\n", m.c_str()); }
+static void group_warn_nccl(ncclResult_t r, const char* what) {
+  group_warn(std::string(what) + ": " + (ncclGetErrorString ? ncclGetErrorString(r) : "RCCL error"));
+}
+
 static int nccl_fail(bg_ctx* c, ncclResult_t r, const char* what) {
   return bg_fail(c, BG_E_HIP, std::string("RCCL error: ") + ncclGetErrorString(r) + " in " + what);
 }
@@ -130,11 +136,14 @@ extern "C" int bg_group_open(bg_group** out, const int* devices, int n) {
   if ((distinct && n > 1) || g->self) {
     if (!rccl().ok) {
       bg_fail(g->ctx[0], BG_E_HIP, "RCCL unavailable: " + rccl().err);
+      group_warn("RCCL unavailable: " + rccl().err);
       bg_group_close(g);
       return BG_E_HIP;
     }
     g->comm.resize(n);
-    if (ncclCommInitAll(g->comm.data(), n, devices) != ncclSuccess) {
+    const ncclResult_t ri = ncclCommInitAll(g->comm.data(), n, devices);
+    if (ri != ncclSuccess) {
+      group_warn_nccl(ri, "ncclCommInitAll");
       g->comm.clear();
       bg_group_close(g);
       return BG_E_HIP;
@@ -161,12 +170,15 @@ extern "C" int bg_group_open_rank(bg_group** out, int device, const void* uid, i
   g->self = nranks == 1 && se && strcmp(se, "0") != 0;
   if (nranks > 1 || g->self) {
     if (!rccl().ok) {
+      group_warn("RCCL unavailable: " + rccl().err);
       bg_group_close(g);
       return BG_E_HIP;
     }
     ncclUniqueId id;
     if (g->self) {  // a one-rank group has no peer to share an id with
-      if (ncclGetUniqueId(&id) != ncclSuccess) {
+      const ncclResult_t ru = ncclGetUniqueId(&id);
+      if (ru != ncclSuccess) {
+        group_warn_nccl(ru, "ncclGetUniqueId");
         bg_group_close(g);
         return BG_E_HIP;
       }
@@ -174,7 +186,9 @@ extern "C" int bg_group_open_rank(bg_group** out, int device, const void* uid, i
       memcpy(&id, uid, sizeof(id));
     }
     g->comm.resize(1);
-    if (ncclCommInitRank(&g->comm[0], nranks, id, rank) != ncclSuccess) {
+    const ncclResult_t rr = ncclCommInitRank(&g->comm[0], nranks, id, rank);
+    if (rr != ncclSuccess) {
+      group_warn_nccl(rr, "ncclCommInitRank");
       g->comm.clear();
       bg_group_close(g);
       return BG_E_HIP;

@@ -1048,6 +1048,7 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 #endif
 #define SCAP 512
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
+#define BG_ROW_OVERFLOW 16ULL  // k_parse_n: a tile of more than LCAP_WS lines
 
 __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
   v = max(v, dpp32<0x111, 0xF, true>(v));
@@ -1278,7 +1279,9 @@ __device__ __forceinline__ uint32_t tile_line_starts_n(const TileRegsN<NT>& R, c
 }
 // WSO: whitespace masks only (parse_line_fast_ws): one multiply per two dwords instead of
 // one per dword plus the digit classes
-template <int NT, bool WSO, typename LdsT>
+// (OVF_FLAG: a tile of more than CAP lines sets BG_ROW_OVERFLOW instead of reporting a
+// parse error; bg_load then redoes the load with k_parse)
+template <int NT, bool WSO, typename LdsT, bool OVF_FLAG = false>
 __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
                                                     LdsT& S, const TileRegsN<NT>& R, int64_t& last_end,
                                                     bg_dstatus* st) {
@@ -1320,7 +1323,10 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
   bool has0;
   const uint32_t L = tile_line_starts_n<NT>(R, B.buf, t0, S.lst, CAP + 1, S.shs, has0);
   if (L > CAP) {
-    if (threadIdx.x == 0) bg_report(st, 0, ERR_PARSE);
+    if (threadIdx.x == 0) {
+      if (OVF_FLAG) atomicOr(&st->flags, BG_ROW_OVERFLOW);
+      else bg_report(st, 0, ERR_PARSE);
+    }
     return L;
   }
   TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
@@ -1328,6 +1334,131 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
              : (B.buf[HB + TT - 1] == '\n') ? t0 + TT - 1
              : (B.hnl != ~0u ? t0 + B.hnl : find_nl(T, t0 + TT + HA + 32));
   return L;
+}
+
+// parse_score_fast from the whitespace mask alone: the score's bytes are checked to be
+// digits while they are converted (bgp_digits_rc)
+__device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const uint32_t* wsm, uint32_t q,
+                                                    uint32_t len, uint32_t e1, double& score) {
+  uint32_t WS = mask_window(wsm, q + e1);
+  const uint32_t l2 = len - e1;  // bytes from e1 to the line end
+  if (l2 < 32) WS |= ~0u << l2;  // bytes past the line end act as whitespace
+  if (!(WS & 1u)) return false;  // the end digits must be followed by whitespace
+  const uint32_t NW = ~WS;
+  if (!NW) return false;
+  const uint32_t i0 = bgp_ctz(NW);  // id
+  const uint32_t m1 = WS & (~0u << i0);
+  if (!m1) return false;
+  const uint32_t i1 = bgp_ctz(m1);
+  if (i1 >= 31) return false;
+  const uint32_t m2 = NW & (~0u << i1);
+  if (!m2) return false;
+  const uint32_t c0 = bgp_ctz(m2);  // score
+  if (c0 >= l2) return false;
+  const uint32_t m3 = WS & (~0u << c0);
+  if (!m3) return false;
+  const uint32_t c1 = bgp_ctz(m3);  // whitespace or the line end after the score
+  if (c1 - c0 > 12) return false;
+  uint32_t d1, d2, d3;
+  lds12_end(buf, q + HB + e1 + c1, d1, d2, d3);
+  bool ok = true;
+  const uint64_t v = bgp_digits_rc(d1, d2, d3, (int)(c1 - c0), ok);
+  score = (double)v;
+  return ok;
+}
+
+// Row parse (keys, rest spans, scores) with k_parse_set_n's tile front end: NT threads per
+// 8 KiB tile, the tile classified for whitespace only (tile_prologue_n<NT, true>), fields and
+// digits checked in parse_line_fast_ws / parse_score_fast_ws. Lines the fast path refuses
+// take parse_line_slow in the same loop. Same outputs and error reports as k_parse.
+template <int NT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_n(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
+    int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
+    uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
+    bg_dstatus* st) {
+  __shared__ ParseLdsWs S;
+  constexpr uint32_t NR = LCAP_WS / NT;  // rounds of NT lines at most
+  __shared__ int64_t kfirst[NR][NT / 64], klast[NR][NT / 64];  // keys at the waves' edges
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  int64_t last_end = -1;
+  uint32_t L;
+  {
+    TileRegsN<NT> TR;
+    load_tile_n<NT>(txt, nb, t0, TR);
+    L = tile_prologue_n<NT, true, ParseLdsWs, true>(txt, nb, t0, S, TR, last_end, st);
+  }
+  const auto& B = S.b[0];
+  const bool has0 = (t0 == 0) || B.buf[HB - 1] == '\n';
+  const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1);  // row of the first owned line
+  if (L > LCAP_WS) return;  // (BG_ROW_OVERFLOW: the load is redone with k_parse)
+  const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];
+  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
+  int64_t mlen = 0;
+  const uint32_t rounds = (L + NT - 1) / NT;
+  const int lane = bg_lane(), w = bg_wave();
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t k = j * NT + threadIdx.x;
+    int64_t key = LLONG_MIN;
+    const int64_t ls = k < L ? t0 + S.lst[k] : 0;
+    const uint64_t r = r0 + k;
+    const int64_t le = k >= L ? -1 : (k + 1 < L) ? t0 + S.lst[k + 1] - 1 : last_end;
+    if (k < L && r < nrows && le >= 0) {  // r >= nrows: the unterminated last line (dropped)
+      Fast F;
+      const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+      const RunInfo& I = R.info[run];
+      double sc = 0;
+      if (parse_line_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
+          F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi &&
+          (kind != BG_BED5 || parse_score_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F.rest, sc))) {
+        emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
+        if (rest_off) {
+          rest_off[r] = (uint64_t)(ls + F.rest);
+          rest_len[r] = (uint32_t)(le - ls - F.rest);
+        }
+        if (score) score[r] = sc;
+      } else {  // the full grammar, byte by byte (decimal scores, odd spacing, errors)
+        Line Ln;
+        parse_line_slow(T, ls, le, kind, Ln);
+        if (Ln.err) {
+          if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
+          bg_report(st, r, Ln.err);
+          KS[r] = KE[r] = 0;
+        } else if (Ln.hash != I.hash) {  // a chromosome outside the run order: unsorted input
+          bg_report(st, r, ERR_UNSORTED);
+        } else {
+          emit_row(R, run, ls, r, Ln.start, Ln.end, KS, KE, st, key, mlen);
+          if (rest_off) {
+            rest_off[r] = (uint64_t)Ln.rest;
+            rest_len[r] = (uint32_t)(le - Ln.rest);
+          }
+          if (score) {
+            score[r] = Ln.score;
+            if (!Ln.scoreint) atomicOr(&st->flags, 1ULL);
+          }
+        }
+      }
+    }
+    // sort order inside the tile: each line against the one before it (the lane before, or
+    // across a wave edge after the loop)
+    const int64_t prev = __shfl_up(key, 1, 64);
+    if (lane > 0 && key != LLONG_MIN && prev != LLONG_MIN && key < prev) bg_report(st, r, ERR_UNSORTED);
+    if (lane == 0) kfirst[j][w] = key;
+    if (lane == 63) klast[j][w] = key;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mlen = max(mlen, (int64_t)__shfl_xor(mlen, d, 64));
+  if (bg_lane() == 0 && mlen > *(volatile long long*)&st->maxlen) atomicMax(&st->maxlen, (long long)mlen);
+  __syncthreads();
+  if (threadIdx.x < rounds * (NT / 64)) {  // the first line of each wave's round vs the line before it
+    const uint32_t j = threadIdx.x / (NT / 64), q = threadIdx.x % (NT / 64);
+    const uint32_t k = j * NT + q * 64;
+    if (k > 0 && k < L) {
+      const int64_t a = (q > 0) ? klast[j][q - 1] : klast[j - 1][NT / 64 - 1], b = kfirst[j][q];
+      if (a != LLONG_MIN && b != LLONG_MIN && b < a) bg_report(st, r0 + k, ERR_UNSORTED);
+    }
+  }
 }
 
 template <int NT>
@@ -2012,8 +2143,18 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   RunTable R;
   int rc = upload_runs(c, T, S, gid, R);
   if (rc) return rc;
-  BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
-            S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
+  // k_parse_n (whitespace-only tile front end, 128 threads) unless a load found a tile of very
+  // short lines (BG_ROW_OVERFLOW) and is being redone, or BEDGPU_ROW_PARSE=0
+  static const bool row_n = [] {
+    const char* e = getenv("BEDGPU_ROW_PARSE");
+    return !(e && atoi(e) == 0);
+  }();
+  if (row_n && !c->row_wide)
+    BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
+              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
+  else
+    BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
+              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, st);
@@ -2258,11 +2399,14 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   HP("rt3");
   // a BG_BED3_SET input with an error (its exact line is not known) or a staging overflow:
   // the whole load is redone with that input's row columns (BG_BED3)
-  bool redo = false;
+  bool redo = false, wide = false;
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind == BG_BED3_SET && st[i].ntiles &&
         (hst[i].first_bad != ~0ULL || (hst[i].flags & BG_SET_OVERFLOW)))
       redo = true;
+  // a row input with a tile of more lines than k_parse_n holds: redone with k_parse
+  for (int i = 0; i < n && !rc; ++i)
+    if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && (hst[i].flags & BG_ROW_OVERFLOW)) redo = wide = true;
   for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
   if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies use the pinned staging
   for (auto& S : st) release_state(c, S);
@@ -2274,7 +2418,11 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     std::vector<bg_input> rows(inputs, inputs + n);
     for (auto& in : rows)
       if (in.kind == BG_BED3_SET) in.kind = BG_BED3;
-    return bg_load(c, n, rows.data(), out);
+    const bool w0 = c->row_wide;
+    if (wide) c->row_wide = true;
+    const int rc2 = bg_load(c, n, rows.data(), out);
+    c->row_wide = w0;
+    return rc2;
   }
   for (bg_table* T : s->t)  // keep every column non-null for empty inputs
     if (T->is_set) {

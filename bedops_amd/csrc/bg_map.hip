@@ -1201,6 +1201,11 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
       while (perc > 1) perc /= 10.0;
       perc -= DBL_EPSILON;
       if (perc <= 0.0) perc = DBL_EPSILON;
+      // at perc_ <= DBL_EPSILON Ref2Map is 0 for any pair not strictly apart (:147-150): rows
+      // that only touch the reference row, or have no length, join its window when the sweep's
+      // deque still holds them, which the window kernels (overlap > 0) do not model
+      if (perc <= DBL_EPSILON && !faster)
+        return bg_fail(c, BG_E_UNSUPPORTED, "--fraction-* values below 4.5e-16 are not on the GPU path");
       break;
     case BG_OVR_EXACT: break;
     default: return BG_E_ARG;

