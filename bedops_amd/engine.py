@@ -349,13 +349,15 @@ class Engine:
 
     # -------------------------------------------------------------- loading
     def load(self, inputs):
-        """inputs: list of (data, kind) where data is bytes (host) or (devptr, nbytes)."""
+        """inputs: list of (data, kind) where data is bytes (host), (devptr, nbytes), or
+        (hostptr, nbytes, False): host memory the caller keeps alive until load returns."""
         n = len(inputs)
         arr = (_Input * n)()
         keep = []
         for i, (data, kind) in enumerate(inputs):
             if isinstance(data, tuple):
-                arr[i].data, arr[i].nbytes, arr[i].on_device = data[0], data[1], 1
+                dev = 1 if len(data) < 3 or data[2] else 0
+                arr[i].data, arr[i].nbytes, arr[i].on_device = data[0], data[1], dev
             else:
                 b = ctypes.create_string_buffer(bytes(data), len(data) + 1)
                 keep.append(b)

@@ -11,6 +11,7 @@ engine.Group.gather the way bench.py does under torch.distributed.run.
 import os
 import random
 import subprocess
+import sys
 import tempfile
 import zlib
 
@@ -20,6 +21,7 @@ import randbed
 
 pytestmark = pytest.mark.gpu
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHROMS = ["chr1", "chr10", "chr11", "chr2", "chr20", "chr3", "chrM", "chrX", "chrY"]
 MODES = [["-m"], ["-i"], ["-d"], ["-e", "1"], ["-n", "30%"], ["-c"], ["-c", "-L"], ["-w", "7"],
          ["-s"], ["-p"], ["-u"]]
@@ -217,47 +219,61 @@ def test_closest_sharded_equals_single_device(gpu_bin, oracle_bin, case):
                 assert got.stdout == want, (case, trial, devs)
 
 
-def test_group_gather_through_rccl_self_communicator(oracle_bin, monkeypatch):
+_RCCL_SELF_CHILD = r"""
+import os, random, sys, tempfile
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import randbed
+from bedops_amd.engine import BED3_SET, Group
+from bedops_amd.shard import member_spans, strcmp_order
+chroms = sys.argv[3].split(",")
+rng = random.Random(9)
+texts = [randbed.text(randbed.rows(rng, 5000, chroms=chroms, span=30000, maxlen=90)).encode() for _ in range(2)]
+gnames = strcmp_order({ln.split(b"\t", 1)[0].decode(): 1 for t in texts for ln in t.splitlines()})
+single = sys.argv[2] == "1"
+g = Group(devices=[0]) if single else Group(device=0, uid=bytes(128), nranks=1, rank=0)
+try:
+    eng = g.engines[0]
+    s = eng.load([(x, BED3_SET) for x in texts])
+    r = eng.op("-i", s, [0, 1])
+    r.format()
+    dptr, _ = r.device_text()
+    names = s.chroms()
+    offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
+    out, n = g.gather(len(gnames), [(dptr, offs, lens)])
+    eng.write_device(out, n, 1)
+    eng.device_free(out)
+    r.free()
+    s.free()
+finally:
+    g.close()
+with open(sys.argv[4], "wb") as f:
+    for t in texts:
+        f.write(t + b"\0")
+"""
+
+
+def test_group_gather_through_rccl_self_communicator(oracle_bin, tmp_path):
     """BEDGPU_RCCL_SELF=1: a one-member group gets a one-rank RCCL communicator and sends its
     own chromosome runs to itself (ncclAllReduce of the sizes, grouped ncclSend/ncclRecv), so
     bg_group_gather's communicator branch runs on this one-GPU box; the reassembled text must
-    equal a single run"""
-    from bedops_amd.engine import BED3_SET, Group
-    from bedops_amd.shard import member_spans, strcmp_order
-
-    monkeypatch.setenv("BEDGPU_RCCL_SELF", "1")
-    monkeypatch.setenv("NCCL_DEBUG", "WARN")  # RCCL says why, should the communicator fail
-    rng = random.Random(9)
-    texts = [randbed.text(randbed.rows(rng, 5000, chroms=CHROMS, span=30000, maxlen=90)).encode()
-             for _ in range(2)]
-    gnames = strcmp_order({ln.split(b"\t", 1)[0].decode(): 1 for t in texts for ln in t.splitlines()})
-    for single in (True, False):
-        g = Group(devices=[0]) if single else Group(device=0, uid=bytes(128), nranks=1, rank=0)
-        try:
-            eng = g.engines[0]
-            s = eng.load([(x, BED3_SET) for x in texts])
-            r = eng.op("-i", s, [0, 1])
-            r.format()
-            dptr, _ = r.device_text()
-            names = s.chroms()
-            offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
-            out, n = g.gather(len(gnames), [(dptr, offs, lens)])
-            with tempfile.TemporaryFile() as fo:
-                eng.write_device(out, n, fo.fileno())
-                fo.seek(0)
-                got = fo.read()
-            eng.device_free(out)
-            r.free()
-            s.free()
-        finally:
-            g.close()
-        with tempfile.TemporaryDirectory() as td:
-            paths = []
-            for i, t in enumerate(texts):
-                p = os.path.join(td, f"in{i}.bed")
-                open(p, "wb").write(t)
-                paths.append(p)
-            want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE, check=True).stdout
+    equal a single run. Each case runs in a child process that loads only the library (as the
+    C front-ends do): a process that has also loaded torch's own HIP runtime gives RCCL a
+    second one"""
+    env = dict(os.environ, BEDGPU_RCCL_SELF="1", NCCL_DEBUG="WARN")
+    for single in ("1", "0"):
+        inputs = tmp_path / f"inputs{single}.bin"
+        r = subprocess.run([sys.executable, "-c", _RCCL_SELF_CHILD, ROOT, single, ",".join(CHROMS), str(inputs)],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=240)
+        assert r.returncode == 0, (single, r.stderr.decode(errors="replace")[-3000:])
+        got = r.stdout
+        texts = inputs.read_bytes().split(b"\0")[:2]
+        paths = []
+        for i, t in enumerate(texts):
+            p = tmp_path / f"in{single}_{i}.bed"
+            p.write_bytes(t)
+            paths.append(str(p))
+        want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE, check=True).stdout
         assert got == want, single
 
 
