@@ -260,7 +260,8 @@ def test_group_gather_through_rccl_self_communicator(oracle_bin, tmp_path):
     equal a single run. Each case runs in a child process that loads only the library (as the
     C front-ends do): a process that has also loaded torch's own HIP runtime gives RCCL a
     second one"""
-    env = dict(os.environ, BEDGPU_RCCL_SELF="1", NCCL_DEBUG="WARN")
+    env = dict(os.environ, BEDGPU_RCCL_SELF="1")
+    env.pop("NCCL_DEBUG", None)  # (RCCL prints its log on stdout, where the text goes)
     for single in ("1", "0"):
         inputs = tmp_path / f"inputs{single}.bin"
         r = subprocess.run([sys.executable, "-c", _RCCL_SELF_CHILD, ROOT, single, ",".join(CHROMS), str(inputs)],
