@@ -35,8 +35,8 @@
 
 #include "bg_internal.h"
 
-#define CQ_DEF 32  // ref rows per chunk
-#define CW_DEF 8   // speculative warm-up rows before a chunk (BEDGPU_CLOSEST_CQ/_CW override)
+#define CQ_DEF 24  // ref rows per chunk (10M x 1B sweep: 16-64 rows, 3-8 warm-up rows, profiles/r04_closest_cq.txt)
+#define CW_DEF 4   // speculative warm-up rows before a chunk (BEDGPU_CLOSEST_CQ/_CW override)
 #define CBACK 4096 // at most this many candidates before the warm-up row are re-read
 #define CAP0 256   // initial capacity of the cache stack / kept list (x4 on overflow)
 #define FIX_ROUNDS 8
@@ -98,10 +98,6 @@ __device__ __forceinline__ uint32_t cl_pop(ClState& S) {
   }
   return S.c[S.n];
 }
-// entry i of the stack (i < n) without popping
-__device__ __forceinline__ uint32_t cl_peek(const ClState& S, uint32_t i) {
-  return i >= S.n - S.m ? S.l[(i & (CL_D - 1)) * BG_NT] : S.c[i];
-}
 // the whole stack in global memory (snapshots, comparisons)
 __device__ __forceinline__ void cl_flush(ClState& S) {
   for (uint32_t i = S.n - S.m; i < S.n; ++i) S.c[i] = S.l[(i & (CL_D - 1)) * BG_NT];
@@ -162,6 +158,9 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
 #define BG_CPF 4
 #endif
   constexpr int CPF = BG_CPF;
+#ifndef BG_CL_FAST
+#define BG_CL_FAST true
+#endif
   int64_t pcs[CPF], pce[CPF];
   const uint64_t nc1 = A.nc ? A.nc - 1 : 0;
 #pragma unroll
@@ -170,28 +169,8 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     pcs[i] = A.nc ? A.cs[j] : 0;
     pce[i] = A.nc ? A.ce[j] : 0;
   }
-  // the next SPF stack entries to be popped (top first) and their keys, loaded ahead: a
-  // scan only pops (the kept list is pushed back after it), so the stack entries it will
-  // read are known when it starts (a pop then no longer waits on its candidate's keys)
-#ifndef BG_SPF
-#define BG_SPF 4
-#endif
-#ifndef BG_CL_FAST
-#define BG_CL_FAST true
-#endif
-  constexpr int SPF = BG_SPF;
-  uint32_t sc[SPF];
-  int64_t scs[SPF], sce[SPF];
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
-#pragma unroll
-    for (int i = 0; i < SPF; ++i) {
-      if ((uint32_t)i < S.n) {
-        sc[i] = cl_peek(S, S.n - 1 - i);
-        scs[i] = A.cs[sc[i]];
-        sce[i] = A.ce[sc[i]];
-      }
-    }
     const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
     int64_t ld = D_MINUS, rdist = D_PLUS;
     int64_t left = -1, right = -1, lce = 0;  // lce = ce[left]
@@ -203,89 +182,10 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     if (nk == cap) ovf = true;          \
     else kept.put(nk++, (uint32_t)(x)); \
   } while (0)
-    bool fast = BG_CL_FAST;  // the file's run of rows left of b, once per scan (below)
-    for (;;) {
-      int64_t c, cs, ce;
-      if (fast && S.n == 0) {
-        // The rows the file holds before the first one reaching past bs (ce <= bs: d < 0, or
-        // an earlier chromosome, skipped) change only (left, ld, lc) and the kept list:
-        //   d >= ld (newleft): reset; left = c; ld = d; lc = 0
-        //   d <  ld (dropL)  : keepL unless lc; lc = 1
-        // (the general chain's outcome for d < 0, below). On the benchmark's inputs this run
-        // is ~70% of the rows read; here it is a compare per row over a batch of `ce` keys
-        // loaded together, instead of the whole chain per row.
-        fast = false;
-        const int64_t gb = bs >> BG_KEY_SHIFT;
-        const uint64_t fp0 = S.fp;
-        for (;;) {
-          const uint64_t f0 = S.fp;
-          if (f0 >= A.nc) break;
-          int64_t v[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) v[i] = A.ce[min(f0 + i, nc1)];
-          int i = 0;
-          for (; i < 8; ++i) {
-            if (f0 + i >= A.nc || v[i] > bs) break;
-            if ((v[i] >> BG_KEY_SHIFT) != gb) continue;  // earlier chromosome: dropped
-            const int64_t d = -((bs - v[i]) + 1);
-            if (d >= ld) {
-              nk = 0;
-              ovf = false;
-              left = (int64_t)(f0 + i);
-              lce = v[i];
-              ld = d;
-              lc = false;
-            } else {
-              if (left >= 0 && !lc) KEEP(left);
-              lc = true;
-            }
-          }
-          S.fp = f0 + i;
-          if (i < 8) break;
-        }
-        if (S.fp != fp0) {  // the file stream's look-ahead restarts at the new position
-#pragma unroll
-          for (int i = 0; i < CPF; ++i) {
-            const uint64_t j = min(S.fp + i, nc1);
-            pcs[i] = A.cs[j];
-            pce[i] = A.ce[j];
-          }
-        }
-      }
-      if (S.n) {
-        cl_pop(S);
-        c = sc[0];
-        cs = scs[0];
-        ce = sce[0];
-#pragma unroll
-        for (int i = 0; i + 1 < SPF; ++i) {
-          sc[i] = sc[i + 1];
-          scs[i] = scs[i + 1];
-          sce[i] = sce[i + 1];
-        }
-        if (S.n >= (uint32_t)SPF) {  // the entry SPF - 1 below the new top
-          sc[SPF - 1] = cl_peek(S, S.n - SPF);
-          scs[SPF - 1] = A.cs[sc[SPF - 1]];
-          sce[SPF - 1] = A.ce[sc[SPF - 1]];
-        }
-      } else if (S.fp < A.nc) {
-        c = (int64_t)S.fp++;
-        cs = pcs[0];
-        ce = pce[0];
-#pragma unroll
-        for (int i = 0; i + 1 < CPF; ++i) {
-          pcs[i] = pcs[i + 1];
-          pce[i] = pce[i + 1];
-        }
-        const uint64_t j = min(S.fp + (CPF - 1), nc1);
-        pcs[CPF - 1] = A.cs[j];
-        pce[CPF - 1] = A.ce[j];
-      } else {
-        eof = true;
-        break;
-      }
+    // one candidate through the reference's branch chain; true when the scan of b ends
+    auto step = [&](int64_t c, int64_t cs, int64_t ce) -> bool {
       const int64_t d = cl_dist(cs, ce, bs, be);
-      if (d == D_MINUS) continue;  // earlier chromosome: dropped
+      if (d == D_MINUS) return false;  // earlier chromosome: dropped
       const bool hasL = left >= 0, hasR = right >= 0;
       const bool plus = d == D_PLUS;
       const bool neg = d < 0;
@@ -337,7 +237,64 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
       const bool setright = firstR || hangR || in_a || in_d;
       right = setright ? c : right;
       rdist = firstR ? d : ((hangR || in_a || in_d) ? 0 : rdist);
-      if (plus || pos) break;
+      return plus || pos;
+    };
+    // the next file row (its keys from the look-ahead registers)
+    auto advance = [&]() {
+#pragma unroll
+      for (int i = 0; i + 1 < CPF; ++i) {
+        pcs[i] = pcs[i + 1];
+        pce[i] = pce[i + 1];
+      }
+      const uint64_t j = min(S.fp + (CPF - 1), nc1);
+      pcs[CPF - 1] = A.cs[j];
+      pce[CPF - 1] = A.ce[j];
+    };
+    // The scan in three phases, each run by all lanes of a wave together (lanes whose scan
+    // already ended idle), so a phase costs its longest lane, not the sum of every lane's
+    // phases one after the other:
+    //   A: the cached rows (popped in the reference's order);
+    //   B: the file's run of rows that end at or before bs (d < 0, or an earlier chromosome,
+    //      skipped): they change only (left, ld, lc) and the kept list, as the chain would:
+    //        d >= ld (newleft): reset; left = c; ld = d; lc = 0
+    //        d <  ld (dropL)  : keepL unless lc; lc = 1
+    //      ~70% of the rows read on the benchmark's inputs, at a compare and a select each;
+    //   C: the rest of the file through the chain, up to the row that ends the scan.
+    bool brk = false;
+    while (S.n && !brk) {  // A
+      const int64_t c = cl_pop(S);
+      brk = step(c, A.cs[c], A.ce[c]);
+    }
+    if (BG_CL_FAST && !brk) {  // B
+      const int64_t gb = bs >> BG_KEY_SHIFT;
+      while (S.fp < A.nc && pce[0] <= bs) {
+        const int64_t ce0 = pce[0];
+        const uint64_t c0 = S.fp++;
+        advance();
+        if ((ce0 >> BG_KEY_SHIFT) != gb) continue;  // earlier chromosome: dropped
+        const int64_t d = -((bs - ce0) + 1);
+        if (d >= ld) {
+          nk = 0;
+          ovf = false;
+          left = (int64_t)c0;
+          lce = ce0;
+          ld = d;
+          lc = false;
+        } else {
+          if (left >= 0 && !lc) KEEP(left);
+          lc = true;
+        }
+      }
+    }
+    while (!brk) {  // C
+      if (S.fp >= A.nc) {
+        eof = true;
+        break;
+      }
+      const int64_t c = (int64_t)S.fp++;
+      const int64_t cs = pcs[0], ce = pce[0];
+      advance();
+      brk = step(c, cs, ce);
     }
     if (eof && left >= 0 && !lc) KEEP(left);
     if (eof && right >= 0) KEEP(right);

@@ -30,6 +30,12 @@ for S in $STEPS; do
         python3 -c "import json;d=json.load(open('$O/cab_$n.json'));k=d.get('kernels_first_step_ms',{});print('%-8s step %.1f chunks %s check %s fix %s match %s'%('$n',d['ms_per_step'],k.get('k_closest_chunks'),k.get('k_closest_check'),k.get('k_closest_fix'),d.get('matches_reference')))"
       done
       ;;
+    closest_cq:*)  # closest_cq:CQ:CW with the main library
+      Q=${S#closest_cq:}; CQ=${Q%%:*}; CW=${Q#*:}
+      BEDGPU_CLOSEST_CQ=$CQ BEDGPU_CLOSEST_CW=$CW timeout -k 10 300 python3 bench.py --workload closest --steps 2 \
+        --warmup 1 --no-cpu-baseline --no-e2e > $O/ccq_${CQ}_$CW.json 2> $O/ccq_${CQ}_$CW.err || { echo "closest_cq $CQ $CW FAILED"; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/ccq_${CQ}_$CW.json'));k=d.get('kernels_first_step_ms',{});print('cq %s cw %s step %.1f chunks %s fix %s serial %s'%('$CQ','$CW',d['ms_per_step'],k.get('k_closest_chunks'),k.get('k_closest_fix'),k.get('k_closest_serial')))"
+      ;;
     bench:*)  # bench:W or bench:W:ENV=VAL (one extra environment setting)
       W=${S#bench:}
       E=""
