@@ -426,7 +426,18 @@ static inline int cli_env_on(const char* name) {
   const char* s = getenv(name);
   return s && *s && strcmp(s, "0") != 0;
 }
+/* stdout a pipe: a 1 MiB pipe buffer (F_SETPIPE_SZ; 64 KiB by default) lets each write(2)
+ * of the output hand over 16x more before it waits for the consumer */
+#ifndef F_SETPIPE_SZ
+#define F_SETPIPE_SZ 1031
+#endif
+static inline void cli_pipe_size(void) {
+  struct stat st;
+  if (fstat(1, &st) != 0 || !S_ISFIFO(st.st_mode)) return;
+  if (fcntl(1, F_SETPIPE_SZ, 1 << 20) < 0) (void)fcntl(1, F_SETPIPE_SZ, 256 << 10);
+}
 static inline void cli_detach(void) {
+  cli_pipe_size();
   const char* d = getenv("BEDGPU_DETACH");
   if ((d && !strcmp(d, "0")) || cli_env_on("BEDGPU_FULL_EXIT")) return;
   int p[2];

@@ -17,10 +17,15 @@
  * multi-GPU shards, cli_shard.h, whose run discovery this reuses), so the concatenated
  * group outputs are the whole-file output byte for byte.
  *
- * Used only when stdout is a regular file (seekable, not O_APPEND): if anything fails in
- * any group (a malformed or unsorted line, a refusal such as bedmap's file-wide decimal
- * sums), the output written so far is truncated away and the caller runs the whole-file
- * path, which reports exactly what a whole-file run reports (messages, line numbers).
+ * Stdout a regular file (seekable, not O_APPEND): if anything fails in any group (a
+ * malformed or unsorted line, a refusal such as bedmap's file-wide decimal sums), the output
+ * written so far is truncated away and the caller runs the whole-file path, which reports
+ * exactly what a whole-file run reports (messages, line numbers). Stdout a pipe
+ * (BEDGPU_STREAM_PIPE=0: off): the groups go out in order as they are done; on a failure the
+ * whole-file path runs with its first `sent` bytes dropped (bg_set_output_skip): the groups
+ * already written are exactly that prefix, so a refusal (decimal sums) still ends in the
+ * whole file's bytes; an input error leaves those groups followed by the whole-file path's
+ * message and status (where that path alone prints the message without output).
  * BEDGPU_STREAM=0 turns it off; BEDGPU_STREAM_GROUPS (default 8), BEDGPU_STREAM_MIN
  * (bytes of input below which the whole-file path is used, default 256 MiB) and
  * BEDGPU_STREAM_MAX_GB (largest group, default 16: more groups for larger inputs, which
@@ -43,6 +48,7 @@ typedef struct {
   uint64_t* ga;      /* [g * nf + f]: byte range [ga, gb) of file f in group g */
   uint64_t* gb;
   int ok, started;
+  int pipe;          /* stdout is a pipe: no truncation, see stream_run */
   pthread_t th;
 } stream_plan_t;
 static stream_plan_t SP;
@@ -147,7 +153,9 @@ static int stream_prepare(int nf, const char* const* paths) {
   if (stream_env("BEDGPU_STREAM", 1) == 0) return 0;
   struct stat st;
   const int fl = fcntl(1, F_GETFL);
-  if (fstat(1, &st) != 0 || !S_ISREG(st.st_mode) || fl < 0 || (fl & O_APPEND)) return 0;
+  if (fstat(1, &st) != 0 || fl < 0) return 0;
+  const int is_pipe = S_ISFIFO(st.st_mode) && stream_env("BEDGPU_STREAM_PIPE", 1) != 0;
+  if (!is_pipe && (!S_ISREG(st.st_mode) || (fl & O_APPEND))) return 0;
   {  /* the size test of the plan, up front: small inputs keep the whole-file path and its
         prefetch of the mappings during HIP initialisation */
     uint64_t total = 0;
@@ -160,6 +168,7 @@ static int stream_prepare(int nf, const char* const* paths) {
   }
   SP.nf = nf;
   SP.paths = paths;
+  SP.pipe = is_pipe;
   if (pthread_create(&SP.th, NULL, stream_plan_run, NULL) != 0) return 0;
   SP.started = 1;
   return 1;
@@ -171,7 +180,7 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   if (!SP.started) return 1;
   pthread_join(SP.th, NULL);
   SP.started = 0;
-  const off_t off0 = lseek(1, 0, SEEK_CUR);
+  const off_t off0 = SP.pipe ? 0 : lseek(1, 0, SEEK_CUR);
   if (!SP.ok || off0 < 0) {
     stream_plan_free();
     return 1;
@@ -186,7 +195,8 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   bg_input* in = (bg_input*)calloc((size_t)nf, sizeof(bg_input));
   void** d = (void**)calloc((size_t)nf, sizeof(void*));
   uint64_t freed = 0;
-  int rc = 0;
+  int rc = 0, pushed = 0;
+  uint64_t sent = 0;  /* bytes handed to the output queue */
   /* the group's input blocks go back to the cache stream-ordered (the next group's copies
    * are queued after its kernels on ctx's stream); a second copy stream needs the host wait */
   const int ordered = stream_env("BEDGPU_COPY_STREAMS", 1) < 2;
@@ -209,6 +219,10 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
     if (!rc) rc = bg_result_format(ctx, res[g], &n);
     if (!rc) rc = bg_result_text_device(res[g], &t, &n);
     if (!rc) rc = bg_writer_push(w, t, n);
+    if (!rc) {
+      ++pushed;
+      sent += n;
+    }
     /* the formatted text is all the group leaves behind (the caching allocator hands the
      * freed blocks to the next group's copies, ordered after this group's kernels) */
     bg_set_free(set);
@@ -231,6 +245,13 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   free(in);
   free(d);
   stream_plan_free();
+  if ((rc || wrc) && SP.pipe) {
+    if (wrc) die_msg(CLI_PROG, "cannot write the output");  /* (the consumer went away) */
+    /* the groups written so far are the whole-file output's first `sent` bytes (every
+     * covered operation is chromosome-local): the whole-file path continues after them */
+    if (pushed && bg_set_output_skip(ctx, sent) != 0) die_ctx(CLI_PROG, ctx, rc);
+    return 1;
+  }
   if (rc || wrc) { /* the whole-file path starts over on an empty output */
     const char* s = getenv("BEDGPU_STATS");
     if (s && *s && strcmp(s, "0") != 0)

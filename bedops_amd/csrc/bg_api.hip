@@ -730,6 +730,13 @@ extern "C" int bg_read_file_device(bg_ctx* c, const char* path, void** out, uint
 // (at >= 0: pwrite(2) at that offset and leave the file position alone: bg_pwrite_device)
 #define BG_WR_THREADS 4
 static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd, off_t at = -1) {
+  if (at < 0 && c->out_skip) {  // bg_set_output_skip: this much of the stream is out already
+    const uint64_t k = std::min(c->out_skip, n);
+    c->out_skip -= k;
+    d = (const char*)d + k;
+    n -= k;
+    if (n == 0) return 0;
+  }
   int rc = ring_get(c);
   if (rc) return rc;
   struct stat st;
@@ -781,6 +788,12 @@ static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd, off_t
   if (bad) return bg_fail(c, BG_E_HIP, "bg_write_device copy");
   if (pw && at < 0 && lseek(fd, off0 + (off_t)n, SEEK_SET) < 0)
     return bg_fail(c, BG_E_IO, std::string("seek failed: ") + strerror(errno));
+  return 0;
+}
+
+extern "C" int bg_set_output_skip(bg_ctx* c, uint64_t n) {
+  if (!c) return BG_E_ARG;
+  c->out_skip = n;
   return 0;
 }
 

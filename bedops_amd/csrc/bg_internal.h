@@ -65,6 +65,7 @@ struct bg_buf {
 struct bg_ctx {
   int device = 0;
   bool row_wide = false;  // bg_load: rows parsed by k_parse (a redo after BG_ROW_OVERFLOW)
+  uint64_t out_skip = 0;  // bytes write_device_ring still drops (bg_set_output_skip)
   int ncu = 256;  // compute units
   std::vector<std::pair<const void*, uint32_t>> resident;  // kernel -> resident BG_NT blocks
   // pinned host staging for the loader's small copies (async DMA, no bounce buffer):

@@ -244,6 +244,10 @@ int bg_write_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd);
 /* n bytes of device memory to the regular file fd at byte offset `at` (pwrite; the file
  * position is neither used nor moved): the multi-GPU drop-in's per-device output parts */
 int bg_pwrite_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd, int64_t at);
+/* the next n bytes ctx's bg_write_device / bg_result_write would write are dropped (counted
+ * across calls): a run whose first part already went down a pipe (the drop-ins' chromosome
+ * groups, cli_stream.h) redoes the whole file and continues the output after that part */
+int bg_set_output_skip(bg_ctx* ctx, uint64_t n);
 /* read a regular file into a new device buffer of ctx's device (its host image DMA'd to HBM,
  * see bg_file_image below); load it with bg_input.on_device = 1, free with bg_device_free.
  * Replaces the reader side of allocate_iterator_starch_bed for plain BED files

@@ -180,3 +180,50 @@ def test_detached_teardown_status_and_output(gpu_bin, oracle_bin, tmp_path):
         r = subprocess.run([gpu_bin["bedops"], "-u", bad, b], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            env=env, timeout=120)
         assert r.returncode == 1 and b"Error" in r.stderr and r.stdout == b""
+
+
+def _run_pipe(exe, args, groups, stream=True):
+    env = dict(os.environ, BEDGPU_STATS="1", BEDGPU_STREAM_MIN="0", BEDGPU_STREAM_GROUPS=str(groups),
+               BEDGPU_STREAM="1" if stream else "0")
+    env.pop("BEDGPU_DEVICES", None)
+    r = subprocess.run([exe, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=120)
+    return r.returncode, r.stdout, r.stderr.decode(errors="replace")
+
+
+def test_groups_through_a_pipe(gpu_bin, oracle_bin, tmp_path):
+    """stdout a pipe: the groups go out in order as they are done (bg_writer, 1 MiB pipe
+    buffer); a refusal in a later group (decimal sums) reruns the whole file and continues the
+    output after the groups already written (bg_set_output_skip): the oracle's bytes either way"""
+    rng = random.Random(31)
+    files = [randbed.write(str(tmp_path / f"{k}.bed"),
+                           randbed.text(randbed.rows(rng, 20000, chroms=CHROMS, span=50000)))
+             for k in range(2)]
+    want = subprocess.run([oracle_bin["bedops"], "-i", *files], stdout=subprocess.PIPE, check=True).stdout
+    for groups in (2, 5):
+        rc, got, err = _run_pipe(gpu_bin["bedops"], ["-i", *files], groups)
+        assert rc == 0 and got == want, err
+        assert _streamed(err), err
+    ref = randbed.write(str(tmp_path / "r.bed"), randbed.text(randbed.rows(rng, 3000, chroms=CHROMS, span=8000)))
+    mp = randbed.write(str(tmp_path / "m.bed"),
+                       _scored(rng, randbed.rows(rng, 6000, chroms=CHROMS, span=8000), decimal_from="chrX"))
+    want = subprocess.run([oracle_bin["bedmap"], "--mean", "--sum", ref, mp], stdout=subprocess.PIPE,
+                          check=True).stdout
+    rc, got, err = _run_pipe(gpu_bin["bedmap"], ["--mean", "--sum", ref, mp], 4)
+    assert rc == 0 and got == want, err
+    assert "pipeline stopped" in err
+
+
+def test_error_in_a_later_group_through_a_pipe(gpu_bin, tmp_path):
+    """stdout a pipe and a malformed line in a later group: the groups before it are out
+    already, then the whole-file path's message and exit status"""
+    rng = random.Random(12)
+    rows = randbed.rows(rng, 3000, chroms=["chr1", "chr2", "chr3", "chrX"], span=20000)
+    lines = randbed.text(rows).splitlines(keepends=True)
+    k = next(i for i, ln in enumerate(lines) if ln.startswith("chr3\t"))
+    lines.insert(k + 5, "chr3\t4\tx\n")
+    a = randbed.write(str(tmp_path / "a.bed"), "".join(lines))
+    b = randbed.write(str(tmp_path / "b.bed"), randbed.text(randbed.rows(rng, 2000, chroms=["chr1", "chr3"])))
+    want_rc, _, want_err = _run_pipe(gpu_bin["bedops"], ["-i", a, b], 4, stream=False)
+    rc, got, err = _run_pipe(gpu_bin["bedops"], ["-i", a, b], 4)
+    assert want_rc != 0 and rc == want_rc
+    assert err.splitlines()[-1] == want_err.splitlines()[-1]
