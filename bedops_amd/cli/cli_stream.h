@@ -245,18 +245,18 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   free(in);
   free(d);
   stream_plan_free();
-  if ((rc || wrc) && SP.pipe) {
-    if (wrc) die_msg(CLI_PROG, "cannot write the output");  /* (the consumer went away) */
-    /* the groups written so far are the whole-file output's first `sent` bytes (every
-     * covered operation is chromosome-local): the whole-file path continues after them */
-    if (pushed && bg_set_output_skip(ctx, sent) != 0) die_ctx(CLI_PROG, ctx, rc);
-    return 1;
-  }
   if (rc || wrc) { /* the whole-file path starts over on an empty output */
     const char* s = getenv("BEDGPU_STATS");
     if (s && *s && strcmp(s, "0") != 0)
       fprintf(stderr, "bedgpu: chromosome-group pipeline stopped (%d/%d: %s); whole-file path\n", rc, wrc,
               bg_last_error(ctx));
+    if (SP.pipe) {
+      if (wrc) die_msg(CLI_PROG, "cannot write the output");  /* (the consumer went away) */
+      /* the groups written so far are the whole-file output's first `sent` bytes (every
+       * covered operation is chromosome-local): the whole-file path continues after them */
+      if (pushed && bg_set_output_skip(ctx, sent) != 0) die_ctx(CLI_PROG, ctx, rc);
+      return 1;
+    }
     /* never write the whole-file output after leftover group output */
     if (ftruncate(1, off0) != 0 || lseek(1, off0, SEEK_SET) < 0)
       die_msg(CLI_PROG, "cannot truncate the output file to rerun the whole-file path");

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 batch on the GPU box: the -m gpu tests in TESTS, then each step of STEPS:
 #   settests    tests/test_gpu_setload.py under BEDGPU_SET_NT=64
+#   e2e         bench.py's e2e runs (file, back to back, no detach, pipe)
 #   closest_ab  every build/ab/*/libbedgpu.so on the closest 10M x 1B workload (kernel ms)
 #   bench:W     rocprof kernel table of bench.py --workload W (W = intersect, bedmap, ...)
 #   pmc:W       FETCH_SIZE / WRITE_SIZE passes of bench.py --workload W
@@ -29,6 +30,10 @@ for S in $STEPS; do
           --no-cpu-baseline --no-e2e > $O/cab_$n.json 2> $O/cab_$n.err || { echo "closest_ab $n FAILED"; tail -5 $O/cab_$n.err; exit 1; }
         python3 -c "import json;d=json.load(open('$O/cab_$n.json'));k=d.get('kernels_first_step_ms',{});print('%-8s step %.1f chunks %s check %s fix %s match %s'%('$n',d['ms_per_step'],k.get('k_closest_chunks'),k.get('k_closest_check'),k.get('k_closest_fix'),d.get('matches_reference')))"
       done
+      ;;
+    e2e)  # the default workload with its e2e variants (no CPU baseline)
+      timeout -k 10 600 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/e2e.json 2> $O/e2e.err || { echo "e2e FAILED"; tail -5 $O/e2e.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/e2e.json'));e=d['e2e'];print('e2e', e['median_s'], e['runs_s'], 'b2b', e['back_to_back']['median_s'], 'nodetach', e['no_detach']['median_s'], 'pipe', e['pipe']['median_s'], e['pipe']['runs_s'], 'match', e.get('matches_reference'));print('phases', json.dumps(e.get('phases')))"
       ;;
     closest_cq:*)  # closest_cq:CQ:CW with the main library
       Q=${S#closest_cq:}; CQ=${Q%%:*}; CW=${Q#*:}
