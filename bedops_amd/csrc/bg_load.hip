@@ -2172,7 +2172,7 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
   const uint32_t nr = (uint32_t)S.run_pos.size();
   static const int set_nt = [] {  // BEDGPU_SET_NT=64|128|256: the wave / 8 KiB-tile kernels (A/B)
     const char* e = getenv("BEDGPU_SET_NT");
-    return e ? atoi(e) : 128;
+    return e ? atoi(e) : 64;
   }();
   static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
     const char* e = getenv("BEDGPU_SET_WS");

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Round-4 batch on the GPU box: the -m gpu tests in TESTS, then each step of STEPS:
-#   settests    tests/test_gpu_setload.py under BEDGPU_SET_NT=64
+#   settests    tests/test_gpu_setload.py under BEDGPU_SET_NT=128 (the default is the wave kernel, 64)
 #   e2e         bench.py's e2e runs (file, back to back, no detach, pipe)
 #   closest_ab  every build/ab/*/libbedgpu.so on the closest 10M x 1B workload (kernel ms)
 #   bench:W     rocprof kernel table of bench.py --workload W (W = intersect, bedmap, ...)
-#   pmc:W       FETCH_SIZE / WRITE_SIZE passes of bench.py --workload W
+#   pmc:W       FETCH_SIZE / WRITE_SIZE passes of bench.py --workload W -> per-kernel traffic json
 # Outputs under gpurun_out/r04_<TAG>/. Every GPU step has its own time limit; the script
 # stops at the first failure.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -18,8 +18,8 @@ if [ -n "$TESTS" ]; then
 fi
 for S in $STEPS; do
   case $S in
-    settests)  # the set loader's tests under BEDGPU_SET_NT=64 (the wave-per-sub-tile kernel)
-      BEDGPU_SET_NT=64 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_setload.py -m gpu -x -q --timeout 200 \
+    settests)  # the set loader's tests under BEDGPU_SET_NT=128 (the round-3 8 KiB-tile kernel)
+      BEDGPU_SET_NT=128 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_setload.py -m gpu -x -q --timeout 200 \
         --timeout-method thread > $O/settests.log 2>&1 || { tail -30 $O/settests.log; exit 1; }
       tail -2 $O/settests.log
       ;;
@@ -61,6 +61,8 @@ for S in $STEPS; do
           --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-verify > $O/pmc_${W}_$C.json 2> $O/pmc_${W}_$C.err \
           || { echo "pmc $W $C FAILED"; tail -5 $O/pmc_${W}_$C.err; exit 1; }
       done
+      python3 tools/pmc_traffic.py $O/pmc_${W}_FETCH_SIZE $O/pmc_${W}_WRITE_SIZE $O/pmc_traffic_$W.json || exit 1
+      cp $O/pmc_traffic_$W.json profiles/pmc_traffic_$W.json  # read by the bench steps after this one
       echo "pmc $W done"
       ;;
   esac
