@@ -265,7 +265,10 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
       const int64_t c = cl_pop(S);
       brk = step(c, A.cs[c], A.ce[c]);
     }
-    if (BG_CL_FAST && !brk) {  // B
+#ifndef BG_CL_CB
+#define BG_CL_CB 8
+#endif
+    if (BG_CL_FAST && BG_CL_CB == 0 && !brk) {  // B, one row at a time
       const int64_t gb = bs >> BG_KEY_SHIFT;
       while (S.fp < A.nc && pce[0] <= bs) {
         const int64_t ce0 = pce[0];
@@ -284,6 +287,80 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
           if (left >= 0 && !lc) KEEP(left);
           lc = true;
         }
+      }
+    } else if (BG_CL_FAST && !brk) {  // B in closed form, the file's ends CB at a time
+      // Over the run, the chain's effect is: every row whose end is >= the running maximum
+      // (and >= the current left's, d >= ld) is a new left (reset), every other row a
+      // dropL. So the left afterwards is the LAST row holding the run's largest end M when
+      // M beats the current left, the kept list is reset there, and a row after it keeps
+      // it (lc); otherwise the first row keeps the current left (unless cached) and lc = 1.
+      // Only the ends are needed: CB of them per load, all in flight together.
+      constexpr int CB = BG_CL_CB > 0 ? BG_CL_CB : 2;
+      const int64_t gb = bs >> BG_KEY_SHIFT;
+      uint64_t j = S.fp, jend = A.nc;
+      int64_t M = LLONG_MIN;
+      uint64_t p = 0;
+      bool any = false, after = false, end = false;
+      while (!end && j < A.nc) {
+        const uint64_t base = j & ~(uint64_t)(CB - 1);
+        int64_t v[CB];
+        if (base + CB <= A.nc) {
+          const longlong2* q = reinterpret_cast<const longlong2*>(A.ce + base);
+#pragma unroll
+          for (int i = 0; i < CB / 2; ++i) {
+            const longlong2 t = q[i];
+            v[2 * i] = t.x;
+            v[2 * i + 1] = t.y;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < CB; ++i) v[i] = base + i < A.nc ? A.ce[base + i] : LLONG_MAX;
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+          const uint64_t x = base + i;
+          if (end || x < j) continue;
+          if (v[i] > bs) {  // (LLONG_MAX past the file: its end)
+            end = true;
+            jend = min(x, A.nc);
+            continue;
+          }
+          if ((v[i] >> BG_KEY_SHIFT) != gb) continue;  // earlier chromosome: dropped
+          any = true;
+          if (v[i] >= M) {
+            M = v[i];
+            p = x;
+            after = false;
+          } else {
+            after = true;
+          }
+        }
+        j = base + CB;
+      }
+      S.fp = end ? jend : A.nc;
+      if (any) {
+        const int64_t d = -((bs - M) + 1);
+        if (d >= ld) {
+          nk = 0;
+          ovf = false;
+          left = (int64_t)p;
+          lce = M;
+          ld = d;
+          lc = false;
+          if (after) {
+            KEEP(left);
+            lc = true;
+          }
+        } else {
+          if (left >= 0 && !lc) KEEP(left);
+          lc = true;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CPF; ++i) {  // the look-ahead registers from the new position
+        const uint64_t q = min(S.fp + i, nc1);
+        pcs[i] = A.nc ? A.cs[q] : 0;
+        pce[i] = A.nc ? A.ce[q] : 0;
       }
     }
     while (!brk) {  // C

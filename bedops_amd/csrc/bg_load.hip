@@ -1723,7 +1723,8 @@ __device__ __forceinline__ void set_rounds_w(const ParseLdsW& S, const TileText&
       }
     }
     const V ie = wave_incl_max_v(E);
-    const V prevK = lane ? wave_shr1_v(K) : carry_k;
+    const V pk = wave_shr1_v(K);  // with every lane active: a DPP move reads 0 from a masked lane
+    const V prevK = lane ? pk : carry_k;
     if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
     const V ex_e = max(carry_e, wave_shr1_v(ie));
     const bool open = valid && K > ex_e;
