@@ -669,16 +669,14 @@ __device__ __forceinline__ void mev_fold(const double* xs, const double* ys, dou
   }
 }
 
-// events [k0, E) from the sums (s0, q0) read at S0/Q0 (null: +0.0, the visitors' start)
 __global__ void __launch_bounds__(64) k_mev_chain(const double* __restrict__ X,
-                                                  const double* __restrict__ X2, uint64_t k0, uint64_t E,
-                                                  const double* __restrict__ S0, const double* __restrict__ Q0,
+                                                  const double* __restrict__ X2, uint64_t E,
                                                   double* __restrict__ SA, double* __restrict__ QA) {
   __shared__ double xs[MC_BLK], ys[MC_BLK], ss[MC_BLK], qs[MC_BLK];
   constexpr int PER = MC_BLK / 64;
   const int lane = threadIdx.x;
   const bool sq = X2 != nullptr;
-  double s = S0 ? *S0 : 0.0, q = (sq && Q0) ? *Q0 : 0.0;  // lane 0's running sums
+  double s = 0.0, q = 0.0;  // lane 0's running sums
   double px[PER], py[PER];
   auto fetch = [&](uint64_t b) {
 #pragma unroll
@@ -688,8 +686,8 @@ __global__ void __launch_bounds__(64) k_mev_chain(const double* __restrict__ X,
       py[i] = (sq && k < E) ? X2[k] : 0.0;
     }
   };
-  fetch(k0);
-  for (uint64_t b = k0; b < E; b += MC_BLK) {
+  fetch(0);
+  for (uint64_t b = 0; b < E; b += MC_BLK) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       xs[i * 64 + lane] = px[i];
@@ -714,257 +712,6 @@ __global__ void __launch_bounds__(64) k_mev_chain(const double* __restrict__ X,
     }
     __syncthreads();  // the next block's staging overwrites xs/ss
   }
-}
-
-// ---- the same fold, in parallel and still bit-exact
-// s_k = fl(s_{k-1} + x_k) is a function of the BITS of s_{k-1} and x_k alone, so two folds of
-// the same events that hold the same bits after event k agree on every later sum. The stream
-// is cut into segments of L events, one per lane:
-//   k_ch_tot   each segment's own fold from +0.0 (its total),
-//   k_ch_scan  guessed starts = the exclusive sum of those totals (segment 0: +0.0, exact),
-//   k_ch_run   every segment folds from its guess (sums into SA/QA, its end),
-//   k_ch_fix   (rounds) a segment whose start differs from its predecessor's end refolds from
-//              that end, in 16-event blocks, until a block ends on the bits already stored:
-//              from there on the stored sums are the ones the new start produces.
-// A round that changes no start leaves every segment starting at its predecessor's end: the
-// sequential fold exactly. A rounding difference between a guess and the true start dies out
-// as soon as the sums grow past it (both sides round to the same double), usually within a
-// few events; a difference that survives a whole segment moves one segment per round. After
-// CH_ROUNDS rounds the rest runs on one wavefront (k_mev_chain) from the first segment whose
-// start still changed — every segment before it is final.
-__device__ __forceinline__ bool ch_same(double a, double b) {
-  return __double_as_longlong(a) == __double_as_longlong(b);
-}
-// [a, b) from (s, q); WRITE stores the sums; CHECK stops after the first 16-event block (or
-// tail event) whose sums equal the stored ones bit for bit (returns true then)
-template <bool SQ, bool WRITE, bool CHECK>
-__device__ __forceinline__ bool ch_fold(const double* __restrict__ X, const double* __restrict__ X2,
-                                        uint64_t a, uint64_t b, double* __restrict__ SA,
-                                        double* __restrict__ QA, double& s, double& q) {
-  uint64_t k = a;
-  for (; k + 16 <= b; k += 16) {
-    double v[16], w[16];
-    const double2* px = (const double2*)(X + k);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const double2 t = px[i];
-      v[2 * i] = t.x;
-      v[2 * i + 1] = t.y;
-    }
-    if (SQ) {
-      const double2* py = (const double2*)(X2 + k);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const double2 t = py[i];
-        w[2 * i] = t.x;
-        w[2 * i + 1] = t.y;
-      }
-    }
-    double old = 0.0, oldq = 0.0;
-    if (CHECK) {
-      old = SA[k + 15];
-      if (SQ) oldq = QA[k + 15];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s += v[i];
-      v[i] = s;
-      if (SQ) {
-        q += w[i];
-        w[i] = q;
-      }
-    }
-    if (WRITE) {
-      double2* ps = (double2*)(SA + k);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ps[i] = make_double2(v[2 * i], v[2 * i + 1]);
-      if (SQ) {
-        double2* pq = (double2*)(QA + k);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pq[i] = make_double2(w[2 * i], w[2 * i + 1]);
-      }
-    }
-    if (CHECK && ch_same(s, old) && (!SQ || ch_same(q, oldq))) return true;
-  }
-  for (; k < b; ++k) {
-    double old = 0.0, oldq = 0.0;
-    if (CHECK) {
-      old = SA[k];
-      if (SQ) oldq = QA[k];
-    }
-    s += X[k];
-    if (SQ) q += X2[k];
-    if (WRITE) {
-      SA[k] = s;
-      if (SQ) QA[k] = q;
-    }
-    if (CHECK && ch_same(s, old) && (!SQ || ch_same(q, oldq))) return true;
-  }
-  return false;
-}
-
-struct ChainArgs {
-  const double* X;
-  const double* X2;  // null: no square sums
-  uint64_t E, L, P;  // events, events per segment (a multiple of 16), segments
-  double* SA;
-  double* QA;
-  double* st;  // each segment's start (2P with square sums: [P, 2P) = squares)
-  double* ea;  // segment ends, this round
-  double* eb;  // segment ends, the previous round
-};
-
-template <bool SQ>
-__global__ void __launch_bounds__(BG_NT) k_ch_tot(ChainArgs A, double* __restrict__ T) {
-  const uint64_t j = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (j >= A.P) return;
-  double s = 0.0, q = 0.0;
-  ch_fold<SQ, false, false>(A.X, A.X2, j * A.L, min(A.E, (j + 1) * A.L), nullptr, nullptr, s, q);
-  T[j] = s;
-  if (SQ) T[A.P + j] = q;
-}
-
-// one block: the exclusive running sum of the segment totals = the guessed starts
-#define CH_SCAN_NT 1024
-template <bool SQ>
-__global__ void __launch_bounds__(CH_SCAN_NT) k_ch_scan(ChainArgs A, const double* __restrict__ T) {
-  __shared__ double part[CH_SCAN_NT], partq[CH_SCAN_NT];
-  const uint64_t per = (A.P + CH_SCAN_NT - 1) / CH_SCAN_NT;
-  const uint64_t a = min(A.P, threadIdx.x * per), b = min(A.P, a + per);
-  double s = 0.0, q = 0.0;
-  for (uint64_t j = a; j < b; ++j) {
-    s += T[j];
-    if (SQ) q += T[A.P + j];
-  }
-  part[threadIdx.x] = s;
-  partq[threadIdx.x] = q;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double r = 0.0, rq = 0.0;
-    for (int i = 0; i < CH_SCAN_NT; ++i) {
-      const double x = part[i], xq = partq[i];
-      part[i] = r;
-      partq[i] = rq;
-      r += x;
-      rq += xq;
-    }
-  }
-  __syncthreads();
-  s = part[threadIdx.x];
-  q = partq[threadIdx.x];
-  for (uint64_t j = a; j < b; ++j) {
-    A.st[j] = j ? s : 0.0;  // segment 0 starts where the visitors do
-    if (SQ) A.st[A.P + j] = j ? q : 0.0;
-    s += T[j];
-    if (SQ) q += T[A.P + j];
-  }
-}
-
-template <bool SQ>
-__global__ void __launch_bounds__(BG_NT) k_ch_run(ChainArgs A) {
-  const uint64_t j = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (j >= A.P) return;
-  double s = A.st[j], q = SQ ? A.st[A.P + j] : 0.0;
-  ch_fold<SQ, true, false>(A.X, A.X2, j * A.L, min(A.E, (j + 1) * A.L), A.SA, A.QA, s, q);
-  A.ea[j] = s;
-  if (SQ) A.ea[A.P + j] = q;
-}
-
-// one repair round: ends of the previous round in A.eb, this round's into A.ea;
-// chg[0] += segments whose start changed, chg[1] = min of their indices
-template <bool SQ>
-__global__ void __launch_bounds__(BG_NT) k_ch_fix(ChainArgs A, uint32_t* __restrict__ chg) {
-  const uint64_t j = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  bool changed = false;
-  if (j < A.P) {
-    double n = 0.0, nq = 0.0;
-    if (j) {
-      n = A.eb[j - 1];
-      if (SQ) nq = A.eb[A.P + j - 1];
-    }
-    changed = j && !(ch_same(n, A.st[j]) && (!SQ || ch_same(nq, A.st[A.P + j])));
-    double e = A.eb[j], eq = SQ ? A.eb[A.P + j] : 0.0;
-    if (changed) {
-      A.st[j] = n;
-      if (SQ) A.st[A.P + j] = nq;
-      if (!ch_fold<SQ, true, true>(A.X, A.X2, j * A.L, min(A.E, (j + 1) * A.L), A.SA, A.QA, n, nq)) {
-        e = n;
-        eq = nq;
-      }
-    }
-    A.ea[j] = e;
-    if (SQ) A.ea[A.P + j] = eq;
-  }
-  const uint64_t m = __ballot(changed);
-  if (m && (threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) {
-    atomicAdd(&chg[0], (uint32_t)__popcll(m));
-    atomicMin(&chg[1], (uint32_t)j);
-  }
-}
-
-template <bool SQ>
-static int chain_fold_t(bg_ctx* c, ChainArgs A) {
-  static const uint64_t seg = [] {  // BEDGPU_CHAIN_SEG: events per segment (tests)
-    const char* e = getenv("BEDGPU_CHAIN_SEG");
-    const long v = e ? atol(e) : 256;
-    return (uint64_t)((v < 16 ? 16 : v) + 15) / 16 * 16;
-  }();
-  static const int rmax = [] {  // BEDGPU_CHAIN_ROUNDS: repair rounds before the one-wave tail
-    const char* e = getenv("BEDGPU_CHAIN_ROUNDS");
-    return e ? atoi(e) : 32;
-  }();
-  static const bool log = getenv("BEDGPU_CHAIN_LOG") != nullptr;
-  const uint64_t E = A.E;
-  if (rmax <= 0 || E <= seg) {
-    BG_LAUNCH(c, "k_mev_chain", k_mev_chain, dim3(1), dim3(64), A.X, A.X2, (uint64_t)0, E,
-              (const double*)nullptr, (const double*)nullptr, A.SA, A.QA);
-    return 0;
-  }
-  A.L = seg;
-  A.P = (E + seg - 1) / seg;
-  const uint64_t w = SQ ? 2 : 1;
-  double* T = (double*)bg_alloc(c, 8 * w * A.P);
-  A.st = (double*)bg_alloc(c, 8 * w * A.P);
-  A.ea = (double*)bg_alloc(c, 8 * w * A.P);
-  A.eb = (double*)bg_alloc(c, 8 * w * A.P);
-  uint32_t* chg = (uint32_t*)bg_alloc(c, 8);
-  int rc = 0;
-  if (!T || !A.st || !A.ea || !A.eb || !chg) rc = BG_E_NOMEM;
-  const unsigned nb = bg_blocks(A.P, BG_NT);
-  if (!rc) {
-    BG_LAUNCH(c, "k_ch_tot", k_ch_tot<SQ>, dim3(nb), dim3(BG_NT), A, T);
-    BG_LAUNCH(c, "k_ch_scan", k_ch_scan<SQ>, dim3(1), dim3(CH_SCAN_NT), A, (const double*)T);
-    BG_LAUNCH(c, "k_ch_run", k_ch_run<SQ>, dim3(nb), dim3(BG_NT), A);
-    rc = bg_hip_ok(c, hipGetLastError());
-  }
-  int r = 0;
-  uint32_t h[2] = {0, 0};
-  for (; !rc && r < rmax; ++r) {
-    std::swap(A.ea, A.eb);  // the ends just computed are the previous round's
-    if ((rc = bg_hip_ok(c, hipMemsetAsync(chg, 0, 4, c->stream)))) break;
-    if ((rc = bg_hip_ok(c, hipMemsetAsync(chg + 1, 0xff, 4, c->stream)))) break;
-    BG_LAUNCH(c, "k_ch_fix", k_ch_fix<SQ>, dim3(nb), dim3(BG_NT), A, chg);
-    if ((rc = bg_hip_ok(c, hipMemcpyAsync(h, chg, 8, hipMemcpyDeviceToHost, c->stream)))) break;
-    if ((rc = bg_hip_ok(c, hipStreamSynchronize(c->stream)))) break;
-    if (h[0] == 0) break;
-  }
-  const bool tail = !rc && h[0] != 0;
-  if (tail) {  // segments [0, h[1]) are final; the rest in order from h[1]'s true start
-    const uint64_t j = h[1];
-    BG_LAUNCH(c, "k_mev_chain", k_mev_chain, dim3(1), dim3(64), A.X, A.X2, j * A.L, E,
-              (const double*)(A.ea + j - 1), SQ ? (const double*)(A.ea + A.P + j - 1) : nullptr, A.SA, A.QA);
-    rc = bg_hip_ok(c, hipGetLastError());
-  }
-  if (log)
-    fprintf(stderr, "bedgpu chain: %llu events, %llu segments of %llu, %d rounds, tail from %lld\n",
-            (unsigned long long)E, (unsigned long long)A.P, (unsigned long long)A.L, r + (h[0] == 0),
-            tail ? (long long)h[1] * (long long)A.L : -1LL);
-  bg_release(c, T);  // (stream-ordered reuse)
-  bg_release(c, A.st);
-  bg_release(c, A.ea);
-  bg_release(c, A.eb);
-  bg_release(c, chg);
-  return rc;
 }
 
 // each row's running sums after its last event (0 before any event: the visitors start at 0)
@@ -998,11 +745,7 @@ static int map_running_sums_t(bg_ctx* c, const EvArgs& A, bool need_sq, bg_resul
   if (!X || !SA || (need_sq && (!X2 || !QA))) return BG_E_NOMEM;
   BG_LAUNCH(c, "k_mev_write", (k_mev<CRIT, true>), dim3(nb), dim3(BG_NT), A, (uint64_t*)nullptr,
             (const uint64_t*)off, X, X2);
-  if (E) {
-    ChainArgs C{X, X2, E, 0, 0, SA, QA, nullptr, nullptr, nullptr};
-    rc = need_sq ? chain_fold_t<true>(c, C) : chain_fold_t<false>(c, C);
-    if (rc) return rc;
-  }
+  if (E) BG_LAUNCH(c, "k_mev_chain", k_mev_chain, dim3(1), dim3(64), X, X2, E, SA, QA);
   BG_LAUNCH(c, "k_mev_pick", k_mev_pick, dim3(nb), dim3(BG_NT), off, nr, SA, QA, res->dsum, res->dsq);
   BG_HIP(c, hipGetLastError());
   bg_release(c, off);

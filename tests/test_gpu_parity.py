@@ -362,35 +362,6 @@ def test_bedmap_decimal_drift_fixture(eng):
         assert got == c["expect"].encode(), c["name"]
 
 
-@pytest.mark.parametrize("seg,rounds", [(16, 32), (16, 1), (32, 2), (16, 0)])
-def test_bedmap_decimal_segmented_fold_vs_oracle(gpu_bin, oracle_bin, tmp_path, seg, rounds):
-    """the running sums folded in parallel segments (k_ch_*) with guessed starts and repair
-    rounds, with the one-wave tail after `rounds` rounds (0: the one-wave fold alone):
-    byte-equal to the oracle on scores of mixed magnitudes (drift that outlives segments)"""
-    rng = random.Random(seg * 100 + rounds)
-    ref = randbed.rows(rng, 3000, span=20000, maxlen=200)
-    mp = randbed.rows(rng, 6000, span=20000, maxlen=400)
-    r = randbed.write(str(tmp_path / "r.bed"), randbed.text(ref))
-    m = str(tmp_path / "m.bed")
-    with open(m, "wb") as f:
-        f.write(_decimal_map(rng, mp))
-    env = dict(os.environ, BEDGPU_CHAIN_SEG=str(seg), BEDGPU_CHAIN_ROUNDS=str(rounds), BEDGPU_CHAIN_LOG="1")
-    logs = []
-    for args in (["--count", "--mean", "--sum", "--prec", "17"], ["--variance", "--cv", "--prec", "12"],
-                 ["--range", "50", "--sum", "--stdev", "--prec", "9"]):
-        want = subprocess.run([oracle_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE, check=True).stdout
-        got = subprocess.run([gpu_bin["bedmap"]] + args + [r, m], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                             env=env, check=True)
-        assert got.stdout == want, args
-        logs.append(got.stderr.decode())
-    chain = [ln for t in logs for ln in t.splitlines() if ln.startswith("bedgpu chain:")]
-    if rounds:
-        assert len(chain) == 3, logs
-        assert all(f"segments of {seg}," in ln for ln in chain), chain
-        if rounds == 1:  # a guess's drift outlives one repair round somewhere
-            assert any("tail from -1" not in ln for ln in chain), chain
-
-
 def test_bedmap_cli_overlap_options(gpu_bin, oracle_bin, tmp_path):
     rng = random.Random(5)
     ref = randbed.rows(rng, 300, span=3000, maxlen=100)
