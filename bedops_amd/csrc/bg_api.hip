@@ -351,6 +351,24 @@ extern "C" int bg_result_copy_text(bg_ctx* c, bg_result* r, char* host, uint64_t
 //   - the round-2 pread ring: needed extra copy streams (8-40 ms each to create, more to
 //     tear down at exit) and could not start before HIP was up.
 // ---------------------------------------------------------------------------------------
+// BEDGPU_RD_PREAD=1: a file image's chunks are read into the slots with pread(2) (the kernel
+// copies from the page cache; no page faults on the mapping) instead of memcpy from the mapping
+static bool rd_pread() {
+  static const bool v = [] {
+    const char* s = getenv("BEDGPU_RD_PREAD");
+    return s && strcmp(s, "1") == 0;
+  }();
+  return v;
+}
+// open files of the images (pread sources, BEDGPU_RD_PREAD), by mapping address
+static std::mutex img_mu;
+static std::unordered_map<const char*, int> img_fd;
+static int image_fd(const bg_file_image* m) {
+  std::lock_guard<std::mutex> g(img_mu);
+  auto it = img_fd.find(m->data);
+  return it == img_fd.end() ? -1 : it->second;
+}
+
 extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
   if (!path || !m) return BG_E_ARG;
   memset(m, 0, sizeof(*m));
@@ -378,6 +396,11 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
       return BG_E_IO;
     }
     m->data = (const char*)p;
+    if (rd_pread()) {
+      std::lock_guard<std::mutex> g(img_mu);
+      img_fd[m->data] = fd;
+      return 0;
+    }
   }
   close(fd);
   return 0;
@@ -580,7 +603,8 @@ void bg_pool_stop(bg_ctx* c) {
   delete P;
   c->pool = nullptr;
 }
-static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
+// fd >= 0: src is the mapping of that file at offset foff (pread source when rd_pread())
+static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = -1, uint64_t foff = 0) {
   if (!n) return 0;
   int rc = ring_get(c);
   if (rc) return rc;
@@ -600,7 +624,20 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n) {
       if (hipEventSynchronize(c->ring_ev[sl]) != hipSuccess) { bad = 1; return; }
       const uint64_t off = k * BG_RING_CH, len = std::min<uint64_t>(BG_RING_CH, n - off);
       const auto a1 = std::chrono::steady_clock::now();
-      memcpy(c->ring[sl], src + off, len);
+      if (fd >= 0) {
+        uint64_t got = 0;
+        while (got < len) {
+          const ssize_t r = pread(fd, c->ring[sl] + got, len - got, (off_t)(foff + off + got));
+          if (r <= 0) {
+            if (r < 0 && errno == EINTR) continue;
+            bad = 1;
+            return;
+          }
+          got += (uint64_t)r;
+        }
+      } else {
+        memcpy(c->ring[sl], src + off, len);
+      }
       if (c->stats) {
         const auto a2 = std::chrono::steady_clock::now();
         t_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(a1 - a0).count();
@@ -676,7 +713,8 @@ extern "C" int bg_file_image_to_device(bg_ctx* c, const bg_file_image* m, uint64
       const hipError_t e = hipMemcpyAsync(d, m->data + off, (size_t)len, hipMemcpyHostToDevice, c->stream);
       if (e != hipSuccess) rc = bg_hip_fail(c, e, "file image copy");
     } else {
-      rc = ring_h2d(c, d, m->data + off, len);
+      const int fd = rd_pread() ? image_fd(m) : -1;
+      rc = ring_h2d(c, d, m->data + off, len, fd, off);
     }
   }
   if (rc) {
@@ -691,6 +729,14 @@ extern "C" int bg_file_image_to_device(bg_ctx* c, const bg_file_image* m, uint64
 extern "C" void bg_file_image_close(bg_file_image* m) {
   if (!m) return;
   if (m->registered) (void)hipHostUnregister((void*)m->data);
+  if (m->data) {
+    std::lock_guard<std::mutex> g(img_mu);
+    auto it = img_fd.find(m->data);
+    if (it != img_fd.end()) {
+      close(it->second);
+      img_fd.erase(it);
+    }
+  }
   if (m->data && m->n) munmap((void*)m->data, (size_t)m->n);
   memset(m, 0, sizeof(*m));
 }

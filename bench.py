@@ -328,7 +328,11 @@ def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", 
                       f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> "
                       f"{'| reader' if sink == 'pipe' else '> out'}",
            "output_sha16": sha, "output_bytes": nbytes,
-           "phases": _phases(logs[times.index(med)])}
+           "phases": _phases(logs[times.index(med)]),
+           # the staging ring's own report of the median run (copy issue / drain times, and
+           # how long its threads waited on DMA vs copied on the CPU)
+           "ring": [ln.strip() for ln in logs[times.index(med)].splitlines()
+                    if ln.startswith("bedgpu ring")][:40]}
     return rec
 
 

@@ -31,9 +31,11 @@ for S in $STEPS; do
         python3 -c "import json;d=json.load(open('$O/cab_$n.json'));k=d.get('kernels_first_step_ms',{});print('%-8s step %.1f chunks %s check %s fix %s match %s'%('$n',d['ms_per_step'],k.get('k_closest_chunks'),k.get('k_closest_check'),k.get('k_closest_fix'),d.get('matches_reference')))"
       done
       ;;
-    e2e)  # the default workload with its e2e variants (no CPU baseline)
-      timeout -k 10 600 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/e2e.json 2> $O/e2e.err || { echo "e2e FAILED"; tail -5 $O/e2e.err; exit 1; }
-      python3 -c "import json;d=json.load(open('$O/e2e.json'));e=d['e2e'];print('e2e', e['median_s'], e['runs_s'], 'b2b', e['back_to_back']['median_s'], 'nodetach', e['no_detach']['median_s'], 'pipe', e['pipe']['median_s'], e['pipe']['runs_s'], 'match', e.get('matches_reference'));print('phases', json.dumps(e.get('phases')))"
+    e2e|e2e:*)  # the default workload with its e2e variants (no CPU baseline); e2e:ENV=VAL
+      E=""; N=e2e
+      case $S in e2e:*) E=${S#e2e:}; N=e2e_$(echo "$E" | tr '=,' '__');; esac
+      env $(echo "$E" | tr "," " ") timeout -k 10 600 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/$N.json 2> $O/$N.err || { echo "$N FAILED"; tail -5 $O/$N.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/$N.json'));e=d['e2e'];print('$N', e['median_s'], e['runs_s'], 'b2b', e['back_to_back']['median_s'], 'nodetach', e['no_detach']['median_s'], 'pipe', e['pipe']['median_s'], e['pipe']['runs_s'], 'match', e.get('matches_reference'));print('phases', json.dumps(e.get('phases')))"
       ;;
     closest_cq:*)  # closest_cq:CQ:CW with the main library
       Q=${S#closest_cq:}; CQ=${Q%%:*}; CW=${Q#*:}
