@@ -15,11 +15,15 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
 
 #include "bg_internal.h"
+
+#define BG_RING_SLOTS 16  // H2D / output staging slots of the ring (below)
+#define BG_WR_SLOTS 8     // after the ring's slots: the output queue's (bg_writer)
 
 static int ring_threads();
 static void pool_start(bg_ctx* c, int n);
@@ -206,8 +210,9 @@ extern "C" void bg_close(bg_ctx* c) {
   for (auto& ch : c->pin_chunks) hipHostFree(ch.first);
   for (auto e : c->ring_ev)
     if (e) hipEventDestroy(e);
-  for (auto p : c->ring)
-    if (p) hipHostFree(p);
+  for (size_t k = c->ring_base ? BG_RING_SLOTS : 0; k < c->ring.size(); ++k)
+    if (c->ring[k]) hipHostFree(c->ring[k]);
+  if (c->ring_base) hipHostFree(c->ring_base);
   if (c->cjoin) hipEventDestroy(c->cjoin);
   if (c->cstream) hipStreamDestroy(c->cstream);
   hipStreamDestroy(c->stream);
@@ -413,8 +418,6 @@ extern "C" int bg_file_image_open(const char* path, bg_file_image* m) {
 // images or of output bounce buffers were in use stalled by 250-450 ms per run (the driver
 // evicts and restores the queues when such pages are invalidated); the ring's pages are the
 // driver's own.
-#define BG_RING_SLOTS 16
-#define BG_WR_SLOTS 8  // after the ring's slots: the output queue's (bg_writer)
 // slot bytes: BEDGPU_RING_MB (1..16, default 2); pinning cost grows with the slot size
 static uint64_t ring_ch() {
   static const uint64_t v = [] {
@@ -425,6 +428,18 @@ static uint64_t ring_ch() {
   return v;
 }
 #define BG_RING_CH ring_ch()
+// H2D chunks per DMA: BEDGPU_RING_GROUP (1, 2, 4, 8 or 16; default 4). The threads fill
+// BG_RING_CH chunks, the last filler of a group of consecutive chunks issues ONE copy for
+// the group: measured on the box (tools/h2d_probe.py, profiles/r04_h2d_probe.txt) 2 MiB
+// copies run at ~40 GB/s, 8 MiB and larger at ~57 GB/s
+static int ring_group() {
+  static const int v = [] {
+    const char* s = getenv("BEDGPU_RING_GROUP");
+    const int g = s ? atoi(s) : 4;
+    return (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 4;
+  }();
+  return v;
+}
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -451,10 +466,20 @@ static int ring_alloc(bg_ctx* c) {
     const char* s = getenv("BEDGPU_RING_WARM");
     return !(s && strcmp(s, "0") == 0);
   }();
+  // the H2D slots in ONE allocation, so that consecutive slots take one DMA (ring_h2d's
+  // groups); the output slots one allocation each
+  const bool one = ring_group() > 1;
+  char* base = nullptr;
   for (int k = 0; k < BG_RING_SLOTS + BG_WR_SLOTS; ++k)
     th.emplace_back([&, k]() {
+      char** dst = &ring[k];
+      size_t bytes = BG_RING_CH;
+      if (one && k < BG_RING_SLOTS) {
+        dst = k == 0 ? &base : nullptr;
+        bytes = (size_t)BG_RING_SLOTS * BG_RING_CH;
+      }
       if (hipSetDevice(c->device) != hipSuccess ||
-          hipHostMalloc((void**)&ring[k], BG_RING_CH, hipHostMallocDefault) != hipSuccess ||
+          (dst && hipHostMalloc((void**)dst, bytes, hipHostMallocDefault) != hipSuccess) ||
           hipEventCreateWithFlags(&ev[k], hipEventDisableTiming | (event_block() ? hipEventBlockingSync : 0)) !=
               hipSuccess) {
         bad = 1;
@@ -463,7 +488,7 @@ static int ring_alloc(bg_ctx* c) {
       // the runtime's first host->device copy on the stream costs ~15 ms more than the
       // next ones (measured): take it here, while the other slots are being pinned
       if (k == 0 && warm && c->warm)  // a full slot: small copies take another path (blit kernel)
-        (void)hipMemcpyAsync(c->warm, ring[0], BG_RING_CH, hipMemcpyHostToDevice, c->stream);
+        (void)hipMemcpyAsync(c->warm, one ? base : ring[0], BG_RING_CH, hipMemcpyHostToDevice, c->stream);
     });
   for (auto& x : th) x.join();
   if (bad) {
@@ -472,8 +497,12 @@ static int ring_alloc(bg_ctx* c) {
       if (e) hipEventDestroy(e);
     for (auto p : ring)
       if (p) hipHostFree(p);
+    if (base) hipHostFree(base);
     return BG_E_HIP;
   }
+  if (one)
+    for (int k = 0; k < BG_RING_SLOTS; ++k) ring[k] = base + (size_t)k * BG_RING_CH;
+  c->ring_base = base;
   c->ring = ring;
   c->ring_ev = ev;
   pool_start(c, ring_threads() - 1);
@@ -603,11 +632,91 @@ void bg_pool_stop(bg_ctx* c) {
   delete P;
   c->pool = nullptr;
 }
+// one chunk of the source into a ring slot (memcpy from the mapping, or pread)
+static bool ring_fill(char* slot, const char* src, uint64_t off, uint64_t len, int fd, uint64_t foff) {
+  if (fd < 0) {
+    memcpy(slot, src + off, len);
+    return true;
+  }
+  uint64_t got = 0;
+  while (got < len) {
+    const ssize_t r = pread(fd, slot + got, len - got, (off_t)(foff + off + got));
+    if (r <= 0) {
+      if (r < 0 && errno == EINTR) continue;
+      return false;
+    }
+    got += (uint64_t)r;
+  }
+  return true;
+}
+
+// ring_h2d with G chunks per DMA: chunk k lives in slot (k / G % (SLOTS / G)) * G + k % G, so a
+// group's chunks are contiguous; the thread that completes a group issues its copy and
+// records the group slot's event. A thread refills a group slot only after the group that
+// used it before was issued (subm) and its copy completed (the event).
+static int ring_h2d_grouped(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd, uint64_t foff, int G) {
+  const uint64_t CH = BG_RING_CH, nch = (n + CH - 1) / CH, ngr = (nch + G - 1) / G;
+  const int NGS = BG_RING_SLOTS / G;
+  const int T = (int)std::min<uint64_t>(ring_threads(), nch);
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<int64_t> subm(NGS, -1);  // the last group issued from each group slot (this call)
+  std::unique_ptr<std::atomic<uint32_t>[]> filled(new std::atomic<uint32_t>[ngr]);
+  for (uint64_t g = 0; g < ngr; ++g) filled[g] = 0;
+  std::atomic<int> bad{0};
+  std::atomic<int64_t> t_wait{0}, t_copy{0};
+  auto worker = [&](int t) {
+    if (hipSetDevice(c->device) != hipSuccess) { bad = 1; cv.notify_all(); return; }
+    for (uint64_t k = (uint64_t)t; k < nch && !bad; k += (uint64_t)T) {
+      const uint64_t gk = k / G;
+      const int gs = (int)(gk % NGS), sl = gs * G + (int)(k % G);
+      const auto a0 = std::chrono::steady_clock::now();
+      if (gk >= (uint64_t)NGS) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return subm[gs] >= (int64_t)(gk - NGS) || bad; });
+        if (bad) return;
+      }
+      if (hipEventSynchronize(c->ring_ev[gs * G]) != hipSuccess) { bad = 1; cv.notify_all(); return; }
+      const uint64_t off = k * CH, len = std::min<uint64_t>(CH, n - off);
+      const auto a1 = std::chrono::steady_clock::now();
+      if (!ring_fill(c->ring[sl], src, off, len, fd, foff)) { bad = 1; cv.notify_all(); return; }
+      if (c->stats) {
+        const auto a2 = std::chrono::steady_clock::now();
+        t_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(a1 - a0).count();
+        t_copy += std::chrono::duration_cast<std::chrono::nanoseconds>(a2 - a1).count();
+      }
+      const uint32_t in_group = (uint32_t)std::min<uint64_t>(G, nch - gk * G);
+      if (filled[gk].fetch_add(1) + 1 == in_group) {  // the group is complete: one copy
+        const uint64_t go = gk * G * CH, glen = std::min<uint64_t>((uint64_t)G * CH, n - go);
+        std::lock_guard<std::mutex> g(mu);
+        if (hipMemcpyAsync(dst + go, c->ring[gs * G], glen, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(c->ring_ev[gs * G], c->stream) != hipSuccess)
+          bad = 1;
+        subm[gs] = (int64_t)gk;
+        cv.notify_all();
+      }
+    }
+  };
+  const double t0 = now_ms();
+  const std::function<void(int)> job = [&](int t) {
+    if (t < T) worker(t);
+  };
+  pool_run(c, job);
+  if (c->stats) {
+    const double t1 = now_ms();
+    hipStreamSynchronize(c->stream);
+    fprintf(stderr, "bedgpu ring   %.1f MB: copies issued %.3f ms, drained %.3f ms (threads: %.1f ms waiting, %.1f ms copying; %d chunks per copy)\n",
+            n / 1e6, t1 - t0, now_ms() - t0, t_wait / 1e6, t_copy / 1e6, G);
+  }
+  return bad ? bg_fail(c, BG_E_HIP, "staging ring copy") : 0;
+}
+
 // fd >= 0: src is the mapping of that file at offset foff (pread source when rd_pread())
 static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = -1, uint64_t foff = 0) {
   if (!n) return 0;
   int rc = ring_get(c);
   if (rc) return rc;
+  if (c->ring_base && copy_kernel() == 0 && !c->cstream) return ring_h2d_grouped(c, dst, src, n, fd, foff, ring_group());
   const uint64_t nch = (n + BG_RING_CH - 1) / BG_RING_CH;
   const int TT_ = ring_threads();
   const int T = (int)std::min<uint64_t>(TT_, nch);

@@ -75,6 +75,7 @@ struct bg_ctx {
   // staging ring for bulk host<->device copies (bg_ring_get): driver-allocated pinned slots,
   // so no user-pointer pages the kernel driver could invalidate under running kernels
   std::vector<char*> ring;
+  char* ring_base = nullptr;  // the H2D slots' one allocation (ring[0 .. BG_RING_SLOTS) point into it)
   std::vector<hipEvent_t> ring_ev;
   std::thread ring_th;  // bg_open starts pinning the ring; its first use joins
   int ring_rc = 0;

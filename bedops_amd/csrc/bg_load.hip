@@ -1339,7 +1339,7 @@ __device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ 
 // parse_score_fast from the whitespace mask alone: the score's bytes are checked to be
 // digits while they are converted (bgp_digits_rc)
 __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const uint32_t* wsm, uint32_t q,
-                                                    uint32_t len, uint32_t e1, double& score) {
+                                                    uint32_t len, uint32_t e1, double& score, bool& isint) {
   uint32_t WS = mask_window(wsm, q + e1);
   const uint32_t l2 = len - e1;  // bytes from e1 to the line end
   if (l2 < 32) WS |= ~0u << l2;  // bytes past the line end act as whitespace
@@ -1358,13 +1358,49 @@ __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const ui
   const uint32_t m3 = WS & (~0u << c0);
   if (!m3) return false;
   const uint32_t c1 = bgp_ctz(m3);  // whitespace or the line end after the score
-  if (c1 - c0 > 12) return false;
   uint32_t d1, d2, d3;
+  bool ok = c1 - c0 <= 12;
+  if (ok) {
+    lds12_end(buf, q + HB + e1 + c1, d1, d2, d3);
+    const uint64_t v = bgp_digits_rc(d1, d2, d3, (int)(c1 - c0), ok);
+    score = (double)v;
+    if (ok) return true;
+  }
+  // a decimal "<int digits>.<fraction digits>" (the common bedmap signal column): the value is
+  // m / 10^f with m < 2^53 and f <= 12, one correctly rounded division of exact operands —
+  // parse_score's result (Clinger's fast path), with its trailing-zero rule; a non-integer
+  // clears `isint` (st->flags bit 0, as the byte path sets it). Anything else: the byte path.
+  if (c1 - c0 > 20) return false;
+  uint64_t lo, hi;
+  lds16(buf, q + HB + e1 + c0, lo, hi);
+  const uint64_t x = lo ^ 0x2e2e2e2e2e2e2e2eull, y = hi ^ 0x2e2e2e2e2e2e2e2eull;
+  const uint64_t zx = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+  const uint64_t zy = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+  if (!zx && !zy) return false;
+  const uint32_t dot = zx ? (uint32_t)__builtin_ctzll(zx) / 8 : 8 + (uint32_t)__builtin_ctzll(zy) / 8;
+  const uint32_t ni = dot, nf = c1 - c0 - dot - 1;  // integer / fraction digits
+  if (ni < 1 || ni > 12 || nf < 1 || nf > 12 || ni + nf > 19 || dot >= c1 - c0) return false;
+  ok = true;
+  lds12_end(buf, q + HB + e1 + c0 + dot, d1, d2, d3);
+  const uint64_t vi = bgp_digits_rc(d1, d2, d3, (int)ni, ok);
   lds12_end(buf, q + HB + e1 + c1, d1, d2, d3);
-  bool ok = true;
-  const uint64_t v = bgp_digits_rc(d1, d2, d3, (int)(c1 - c0), ok);
-  score = (double)v;
-  return ok;
+  const uint64_t vf = bgp_digits_rc(d1, d2, d3, (int)nf, ok);
+  if (!ok) return false;
+  const double P10[13] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12};
+  uint64_t m = vi * (uint64_t)P10[nf] + vf;
+  int pw = -(int)nf;
+  while (pw < 0 && m != 0 && m % 10 == 0) {
+    m /= 10;
+    ++pw;
+  }
+  if (m > (1ULL << 53)) return false;
+  if (m == 0 || pw == 0) {  // "0.000", "12.000": integers (parse_score: isint, +0.0)
+    score = (double)m;
+    return true;
+  }
+  score = (double)m / P10[-pw];
+  isint = false;
+  return true;
 }
 
 // Row parse (keys, rest spans, scores) with k_parse_set_n's tile front end: NT threads per
@@ -1396,6 +1432,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
   const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];
   const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
   int64_t mlen = 0;
+  bool nonint = false;  // a decimal score on the fast path (st->flags bit 0, once per wave)
   const uint32_t rounds = (L + NT - 1) / NT;
   const int lane = bg_lane(), w = bg_wave();
   for (uint32_t j = 0; j < rounds; ++j) {
@@ -1409,9 +1446,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
       const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
       const RunInfo& I = R.info[run];
       double sc = 0;
+      bool isint = true;
       if (parse_line_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
           F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi &&
-          (kind != BG_BED5 || parse_score_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F.rest, sc))) {
+          (kind != BG_BED5 || parse_score_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F.rest, sc, isint))) {
+        nonint |= !isint;
         emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
         if (rest_off) {
           rest_off[r] = (uint64_t)(ls + F.rest);
@@ -1447,6 +1486,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     if (lane == 0) kfirst[j][w] = key;
     if (lane == 63) klast[j][w] = key;
   }
+  if (__ballot(nonint) && lane == 0) atomicOr(&st->flags, 1ULL);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) mlen = max(mlen, (int64_t)__shfl_xor(mlen, d, 64));
   if (bg_lane() == 0 && mlen > *(volatile long long*)&st->maxlen) atomicMax(&st->maxlen, (long long)mlen);
