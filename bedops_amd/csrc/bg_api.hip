@@ -22,7 +22,17 @@
 
 #include "bg_internal.h"
 
-#define BG_RING_SLOTS 16  // H2D / output staging slots of the ring (below)
+// H2D / output staging slots of the ring (below): BEDGPU_RING_SLOTS (16; 16..64, rounded to a
+// multiple of 16)
+static int ring_slots() {
+  static const int v = [] {
+    const char* s = getenv("BEDGPU_RING_SLOTS");
+    const int n = s ? atoi(s) : 16;
+    return n < 16 ? 16 : (n > 64 ? 64 : n / 16 * 16);
+  }();
+  return v;
+}
+#define BG_RING_SLOTS ring_slots()
 #define BG_WR_SLOTS 8     // after the ring's slots: the output queue's (bg_writer)
 
 static int ring_threads();
