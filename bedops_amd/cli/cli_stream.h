@@ -113,16 +113,25 @@ static void* stream_plan_run(void* unused) {
   /* consecutive chromosomes, a group closed once it holds total / G bytes; the first group
    * only total / (G * BEDGPU_STREAM_FIRST) (default 4), so the output queue starts early
    * and the fixed costs of the first copies are paid on little data */
+  /* and the last group likewise at most total / (G * BEDGPU_STREAM_LAST) (default 4) when the
+   * chromosomes allow it: the output queue's tail after the last group is that group's text */
   int* first = (int*)calloc((size_t)ngc + 1, sizeof(int)); /* group -> first chromosome */
   int ng = 0;
-  uint64_t acc = 0;
+  uint64_t acc = 0, left = total;
   const uint64_t target = total / (uint64_t)G;
-  const long F = stream_env("BEDGPU_STREAM_FIRST", 4);
+  const long F = stream_env("BEDGPU_STREAM_FIRST", 4), LF = stream_env("BEDGPU_STREAM_LAST", 4);
   const uint64_t target0 = target / (uint64_t)(F < 1 ? 1 : F);
+  const uint64_t target_last = LF > 0 ? target / (uint64_t)LF : 0;
+  int tail = 0;
   for (int g = 0; g < ngc; ++g) {
+    if (!tail && acc && left <= target_last) { /* the rest is small: one group of its own */
+      acc = 0;
+      tail = 1;
+    }
     if (acc == 0) first[ng++] = g;
     acc += bytes[g];
-    if (acc >= (ng == 1 ? target0 : target)) acc = 0;
+    left -= bytes[g];
+    if (!tail && acc >= (ng == 1 ? target0 : target)) acc = 0;
   }
   first[ng] = ngc;
   if (ng >= 2) {
