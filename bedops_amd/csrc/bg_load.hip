@@ -414,10 +414,50 @@ __device__ __forceinline__ bool parse_u64(const TileText& T, int64_t& p, int64_t
   return nd > 0;
 }
 
+// N * 2^e2 (N > 0) rounded to the nearest double, ties to even (normal range only: the
+// callers' |exponents| keep it there)
+__device__ __forceinline__ double round_u128(unsigned __int128 N, int e2) {
+  const uint64_t hi = (uint64_t)(N >> 64), lo = (uint64_t)N;
+  const int lz = hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);
+  N <<= lz;  // top bit at 127
+  e2 -= lz;
+  uint64_t mant = (uint64_t)(N >> 75);  // 53 bits
+  const unsigned __int128 rest = N & (((unsigned __int128)1 << 75) - 1), half = (unsigned __int128)1 << 74;
+  if (rest > half || (rest == half && (mant & 1))) {
+    ++mant;
+    if (mant >> 53) {
+      mant >>= 1;
+      ++e2;
+    }
+  }
+  return ldexp((double)mant, e2 + 75);
+}
+// m * 10^pw correctly rounded for what Clinger's fast path does not cover: m up to 2^64 and
+// -26 <= pw <= 27. pw >= 0: m * 5^pw exactly in 128 bits, times 2^pw. pw < 0: m / 5^k * 2^-k
+// with m scaled to 117 bits, so the quotient keeps >= 55 bits and the remainder is the
+// sticky bit. false outside that range.
+__device__ __forceinline__ bool decimal_exact(uint64_t m, int pw, double& out) {
+  if (pw > 27 || pw < -26) return false;
+  uint64_t f5 = 1;
+  for (int k = 0; k < (pw < 0 ? -pw : pw); ++k) f5 *= 5;
+  if (pw >= 0) {
+    out = round_u128((unsigned __int128)m * f5, pw);
+    return true;
+  }
+  const int s = 117 - (64 - __builtin_clzll(m));
+  const unsigned __int128 num = (unsigned __int128)m << s;
+  const unsigned __int128 q = num / f5, r = num - q * f5;
+  out = round_u128((q << 1) | (r != 0 ? 1 : 0), -s - 1 + pw);
+  return true;
+}
+
 // strtod subset, correctly rounded where it accepts: [+-]digits[.digits][(e|E)[+-]digits]
-// with <= 19 significant digits m and value m * 10^p, |p| <= 22 (Clinger's fast path: one
-// rounding of exact operands), or p up to 37 when m * 10^(p-22) stays an exact integer
-// <= 2^53. Integers up to 2^53 are flagged (exact sums). Anything else -> ERR_SCORE.
+// with <= 19 significant digits m and value m * 10^p, |p| <= 22 and m <= 2^53 (Clinger's
+// fast path: one rounding of exact operands), p up to 37 when m * 10^(p-22) stays an exact
+// integer <= 2^53, otherwise -26 <= p <= 27 by exact 128-bit arithmetic (decimal_exact:
+// e.g. the 17 significant digits of %.17g / repr output). Integers up to 2^53 are flagged
+// (exact sums). Anything else (more than 19 significant digits, larger exponents) ->
+// ERR_SCORE.
 __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64_t le,
                                             double& out, int& isint) {
   bool neg = false;
@@ -462,17 +502,31 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
     out = neg ? -0.0 : 0.0;
     return true;
   }
-  if (m > (1ULL << 53)) return false;
+  if (m > (1ULL << 53) || pw < -22) {  // outside Clinger's fast path: exact 128-bit rounding
+    if (!decimal_exact(m, pw, out)) return false;
+    isint = 0;  // a fraction, or an integer above 2^53 (no exact int64 sums)
+    if (neg) out = -out;
+    return true;
+  }
   if (pw < 0) {
-    if (pw < -22) return false;
     isint = 0;
     out = (double)m / P10[-pw];
   } else {
     if (pw > 22) {  // m * 10^(pw-22) exact and <= 2^53, then one rounding by 1e22
-      for (; pw > 22; --pw) {
-        if (m > (1ULL << 53) / 10) return false;
-        m *= 10;
+      uint64_t mm = m;
+      int pp = pw;
+      for (; pp > 22; --pp) {
+        if (mm > (1ULL << 53) / 10) break;
+        mm *= 10;
       }
+      if (pp > 22) {  // not exact that way
+        if (!decimal_exact(m, pw, out)) return false;
+        isint = 0;
+        if (neg) out = -out;
+        return true;
+      }
+      m = mm;
+      pw = pp;
     }
     // an integer: exact sums need |value| <= 2^53
     uint64_t v = m;

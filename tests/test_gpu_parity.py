@@ -350,6 +350,30 @@ def test_bedmap_decimal_running_sums_vs_oracle(eng, oracle_bin, crit, val):
                 assert eng.bedmap(ops, rt, mt, precision=prec, **kw) == want, (crit, ops, trial)
 
 
+def test_bedmap_decimal_score_spellings_vs_oracle(eng, oracle_bin):
+    """the row parser's decimal fast path (parse_score_fast_ws: `<int>.<frac>` as one
+    correctly rounded division) and every spelling it hands to the byte path: trailing zeros,
+    integers written with a fraction, leading zeros, long fractions, 17-19 significant
+    digits (above 2^53: decimal_exact's 128-bit rounding), signs, exponents, a lone dot side;
+    byte-equal to the oracle for sums, means and extremes"""
+    spell = ["0.000", "12.000", "1.50", "007.25", "5.", ".5", "3.14159265358979", "0.1", "0.2",
+             "0.3", "99.999", "123456789012.5", "1234567.123456789012", "12345678901.12345678",
+             "-1.5", "+2.25", "1e3", "2.5e-2", "10.0001", "4503599627370497.5", "0.000001",
+             "1.0000000000001", "42", "000", "7.7", "100000.00001", "0.30000000000000004",
+             "1.2345678901234567e-05", "9007199254740993", "123456789012345678e-5",
+             "6.0221408570000001e+23", "2.2250738585072014e-10"]
+    rng = random.Random(4242)
+    ref = randbed.rows(rng, 500, chroms=["chr1", "chr2"], span=4000, maxlen=80)
+    mp = randbed.rows(rng, 3000, chroms=["chr1", "chr2"], span=4000, maxlen=80)
+    rt = randbed.text(ref).encode()
+    mt = "".join(f"{c}\t{s}\t{e}\tid{i}\t{spell[i % len(spell)] if i % 3 else rng.choice(spell)}\n"
+                 for i, (c, s, e) in enumerate(mp)).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for ops, prec in ((["count", "sum", "mean"], 6), (["min", "max", "sum"], 17), (["variance", "mean"], 9)):
+            want = run_oracle(oracle_bin["bedmap"], [f"--{o}" for o in ops] + ["--prec", str(prec)], [rt, mt], td)
+            assert eng.bedmap(ops, rt, mt, precision=prec) == want, ops
+
+
 def test_bedmap_decimal_drift_fixture(eng):
     """tests/golden/bedmap_drift.json: running-double drift (2|0.350001 where the exact mean
     is 0.35) and CoordRestAddressCompare order of equal rows"""

@@ -54,7 +54,7 @@ for S in $STEPS; do
       f=$(find $O/prof_$N -name '*kernel_stats.csv' | head -1)
       echo "== $N"
       python3 tools/prof_summary.py "$f" $O/kernel_stats_$N.csv || exit 1
-      python3 -c "import json; d=json.load(open('$O/prof_$N.json')); print('ms/step', d['ms_per_step'], 'match', d.get('matches_reference'), 'frac', d.get('roofline',{}).get('frac'))"
+      python3 -c "import json; d=json.load(open('$O/prof_$N.json')); print('ms/step', d['ms_per_step'], 'match', (d.get('parity') or {}).get('matches_reference'), 'frac', (d.get('roofline') or {}).get('frac'))"
       ;;
     pmc:*)
       W=${S#pmc:}
