@@ -183,6 +183,52 @@ static int stream_prepare(int nf, const char* const* paths) {
   return 1;
 }
 
+/* Read-ahead (BEDGPU_STREAM_AHEAD groups, default 2; 0 = copies in line): a copier thread
+ * issues group g's page-cache -> HBM copies (bg_file_image_copy, the context's prefetch
+ * stream) while the main thread loads, runs and formats earlier groups on ctx's stream, so
+ * the DMA engine never waits for a group's host round trips. The main thread allocates every
+ * group's buffers (the allocator is the main thread's) at most AHEAD groups ahead and fences
+ * ctx's stream on a group's copies (bg_copy_fence) before loading it. */
+typedef struct {
+  bg_ctx* ctx;
+  int nf, ng;
+  void** d;          /* [g * nf + f] device buffers, allocated by the main thread */
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  int alloc_upto;    /* groups [0, alloc_upto) have buffers */
+  int issued;        /* groups [0, issued) have their copies issued and fenced slots recorded */
+  int stop;          /* main thread: stop issuing */
+  int rc;            /* copier's first error */
+  pthread_t th;
+} stream_ahead_t;
+
+static void* stream_copier(void* arg) {
+  stream_ahead_t* A = (stream_ahead_t*)arg;
+  for (int g = 0; g < A->ng; ++g) {
+    pthread_mutex_lock(&A->mu);
+    while (!A->stop && A->alloc_upto <= g) pthread_cond_wait(&A->cv, &A->mu);
+    const int stop = A->stop;
+    pthread_mutex_unlock(&A->mu);
+    if (stop) break;
+    int rc = 0;
+    for (int f = 0; f < A->nf && !rc; ++f) {
+      const uint64_t a = SP.ga[(size_t)g * A->nf + f], b = SP.gb[(size_t)g * A->nf + f];
+      rc = bg_file_image_copy(A->ctx, &SP.fm[f], a, b - a, A->d[(size_t)g * A->nf + f], g);
+    }
+    pthread_mutex_lock(&A->mu);
+    if (rc) {
+      A->rc = rc;
+      A->issued = A->ng;  /* wake the main thread: it stops at this group */
+    } else {
+      A->issued = g + 1;
+    }
+    pthread_cond_broadcast(&A->cv);
+    pthread_mutex_unlock(&A->mu);
+    if (rc) break;
+  }
+  return NULL;
+}
+
 /* Runs the operation group by group on ctx and writes the output to fd 1. Returns 0 when
  * done, 1 when the caller should take the whole-file path (nothing left on fd 1). */
 static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* oparg) {
@@ -209,10 +255,44 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
   /* the group's input blocks go back to the cache stream-ordered (the next group's copies
    * are queued after its kernels on ctx's stream); a second copy stream needs the host wait */
   const int ordered = stream_env("BEDGPU_COPY_STREAMS", 1) < 2;
+  const long ahead = ordered ? stream_env("BEDGPU_STREAM_AHEAD", 0) : 0;
+  stream_ahead_t A;
+  memset(&A, 0, sizeof(A));
+  int copier = 0;
+  if (ahead > 0) {
+    A.ctx = ctx;
+    A.nf = nf;
+    A.ng = ng;
+    A.d = (void**)calloc((size_t)ng * nf, sizeof(void*));
+    pthread_mutex_init(&A.mu, NULL);
+    pthread_cond_init(&A.cv, NULL);
+    for (int g = 0; g < ng && g < ahead + 1 && !rc; ++g) {
+      for (int f = 0; f < nf && !rc; ++f)
+        rc = bg_device_alloc(ctx, SP.gb[(size_t)g * nf + f] - SP.ga[(size_t)g * nf + f] + 64, &A.d[(size_t)g * nf + f]);
+      if (!rc) rc = bg_copy_order(ctx, g);  /* (reused blocks: after ctx's earlier work) */
+      if (!rc) A.alloc_upto = g + 1;
+    }
+    if (!rc) {
+      if (pthread_create(&A.th, NULL, stream_copier, &A) == 0) copier = 1;
+      else rc = -1;
+    }
+  }
   for (int g = 0; g < ng && !rc; ++g) {
+    if (copier) {  /* group g's copies issued by the copier: fence ctx's stream on them */
+      pthread_mutex_lock(&A.mu);
+      while (A.issued <= g) pthread_cond_wait(&A.cv, &A.mu);
+      const int crc = A.rc;
+      pthread_mutex_unlock(&A.mu);
+      rc = crc ? crc : bg_copy_fence(ctx, g);
+    }
     for (int f = 0; f < nf && !rc; ++f) {
       const uint64_t a = SP.ga[(size_t)g * nf + f], b = SP.gb[(size_t)g * nf + f];
-      rc = bg_file_image_to_device(ctx, &SP.fm[f], a, b - a, &d[f]);
+      if (copier) {
+        d[f] = A.d[(size_t)g * nf + f];
+        A.d[(size_t)g * nf + f] = NULL;
+      } else {
+        rc = bg_file_image_to_device(ctx, &SP.fm[f], a, b - a, &d[f]);
+      }
       in[f] = proto[f];
       in[f].data = d[f];
       in[f].nbytes = b - a;
@@ -236,9 +316,23 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
      * freed blocks to the next group's copies, ordered after this group's kernels) */
     bg_set_free(set);
     for (int f = 0; f < nf; ++f) {
-      if (ordered) bg_device_release(ctx, d[f]);
-      else bg_device_free(ctx, d[f]);
+      if (d[f]) {
+        if (ordered) bg_device_release(ctx, d[f]);
+        else bg_device_free(ctx, d[f]);
+      }
       d[f] = NULL;
+    }
+    if (copier && !rc && g + ahead + 1 < ng) {  /* buffers for the group AHEAD + 1 on */
+      const int q = (int)(g + ahead + 1);
+      for (int f = 0; f < nf && !rc; ++f)
+        rc = bg_device_alloc(ctx, SP.gb[(size_t)q * nf + f] - SP.ga[(size_t)q * nf + f] + 64, &A.d[(size_t)q * nf + f]);
+      /* the blocks may be group g's, released just above: the copier's DMA into them waits
+       * for everything queued on ctx's stream so far */
+      if (!rc) rc = bg_copy_order(ctx, q);
+      pthread_mutex_lock(&A.mu);
+      if (!rc) A.alloc_upto = q + 1;
+      pthread_cond_broadcast(&A.cv);
+      pthread_mutex_unlock(&A.mu);
     }
     const uint64_t done = bg_writer_done(w);
     while (freed < done) bg_result_free(res[freed++]);
@@ -247,6 +341,22 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
       snprintf(m, sizeof(m), "group%d", g);
       cli_mark(m);
     }
+  }
+  if (copier) {  /* stop the copier, wait for its last copies, free what it did not hand over */
+    pthread_mutex_lock(&A.mu);
+    A.stop = 1;
+    pthread_cond_broadcast(&A.cv);
+    pthread_mutex_unlock(&A.mu);
+    pthread_join(A.th, NULL);
+    for (int g = 0; g < A.issued && g < ng; ++g) (void)bg_copy_fence(ctx, g);
+    (void)bg_sync(ctx);
+  }
+  if (A.d) {
+    for (size_t k = 0; k < (size_t)ng * nf; ++k)
+      if (A.d[k]) bg_device_release(ctx, A.d[k]);
+    free(A.d);
+    pthread_mutex_destroy(&A.mu);
+    pthread_cond_destroy(&A.cv);
   }
   const int wrc = bg_writer_close(w);
   while (freed < (uint64_t)ng) bg_result_free(res[freed++]);

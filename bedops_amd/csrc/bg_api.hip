@@ -225,6 +225,10 @@ extern "C" void bg_close(bg_ctx* c) {
   if (c->ring_base) hipHostFree(c->ring_base);
   if (c->cjoin) hipEventDestroy(c->cjoin);
   if (c->cstream) hipStreamDestroy(c->cstream);
+  if (c->pstream) hipStreamSynchronize(c->pstream);
+  for (auto e : c->copy_ev) hipEventDestroy(e);
+  for (auto e : c->order_ev) hipEventDestroy(e);
+  if (c->pstream) hipStreamDestroy(c->pstream);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -664,7 +668,8 @@ static bool ring_fill(char* slot, const char* src, uint64_t off, uint64_t len, i
 // group's chunks are contiguous; the thread that completes a group issues its copy and
 // records the group slot's event. A thread refills a group slot only after the group that
 // used it before was issued (subm) and its copy completed (the event).
-static int ring_h2d_grouped(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd, uint64_t foff, int G) {
+static int ring_h2d_grouped(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd, uint64_t foff, int G,
+                            hipStream_t cs) {
   const uint64_t CH = BG_RING_CH, nch = (n + CH - 1) / CH, ngr = (nch + G - 1) / G;
   const int NGS = BG_RING_SLOTS / G;
   const int T = (int)std::min<uint64_t>(ring_threads(), nch);
@@ -699,8 +704,8 @@ static int ring_h2d_grouped(bg_ctx* c, char* dst, const char* src, uint64_t n, i
       if (filled[gk].fetch_add(1) + 1 == in_group) {  // the group is complete: one copy
         const uint64_t go = gk * G * CH, glen = std::min<uint64_t>((uint64_t)G * CH, n - go);
         std::lock_guard<std::mutex> g(mu);
-        if (hipMemcpyAsync(dst + go, c->ring[gs * G], glen, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-            hipEventRecord(c->ring_ev[gs * G], c->stream) != hipSuccess)
+        if (hipMemcpyAsync(dst + go, c->ring[gs * G], glen, hipMemcpyHostToDevice, cs) != hipSuccess ||
+            hipEventRecord(c->ring_ev[gs * G], cs) != hipSuccess)
           bad = 1;
         subm[gs] = (int64_t)gk;
         cv.notify_all();
@@ -714,7 +719,7 @@ static int ring_h2d_grouped(bg_ctx* c, char* dst, const char* src, uint64_t n, i
   pool_run(c, job);
   if (c->stats) {
     const double t1 = now_ms();
-    hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(cs);
     fprintf(stderr, "bedgpu ring   %.1f MB: copies issued %.3f ms, drained %.3f ms (threads: %.1f ms waiting, %.1f ms copying; %d chunks per copy)\n",
             n / 1e6, t1 - t0, now_ms() - t0, t_wait / 1e6, t_copy / 1e6, G);
   }
@@ -726,7 +731,8 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = 
   if (!n) return 0;
   int rc = ring_get(c);
   if (rc) return rc;
-  if (c->ring_base && copy_kernel() == 0 && !c->cstream) return ring_h2d_grouped(c, dst, src, n, fd, foff, ring_group());
+  if (c->ring_base && copy_kernel() == 0 && !c->cstream)
+    return ring_h2d_grouped(c, dst, src, n, fd, foff, ring_group(), c->stream);
   const uint64_t nch = (n + BG_RING_CH - 1) / BG_RING_CH;
   const int TT_ = ring_threads();
   const int T = (int)std::min<uint64_t>(TT_, nch);
@@ -842,6 +848,82 @@ extern "C" int bg_file_image_to_device(bg_ctx* c, const bg_file_image* m, uint64
     return rc;
   }
   *out = d;
+  return 0;
+}
+
+// prefetch copies: issued by a host thread of the caller's on the context's prefetch stream
+// while ctx's stream runs earlier groups' kernels; bg_copy_fence orders ctx's stream after a
+// slot's copies (the caller's thread that launches kernels calls it, once the copy was issued)
+extern "C" int bg_device_alloc(bg_ctx* c, uint64_t n, void** out) {
+  if (!c || !out) return BG_E_ARG;
+  bg_bind(c);
+  *out = bg_alloc(c, n ? n : 1);
+  return *out ? 0 : BG_E_NOMEM;
+}
+
+extern "C" int bg_file_image_copy(bg_ctx* c, const bg_file_image* m, uint64_t off, uint64_t len, void* dst,
+                                  int slot) {
+  if (!c || !m || !dst || slot < 0 || slot >= 65536 || off > m->n || len > m->n - off) return BG_E_ARG;
+  bg_bind(c);
+  hipStream_t ps = nullptr;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->copy_mu);
+    if (!c->pstream && hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking) != hipSuccess) {
+      c->pstream = nullptr;
+      return BG_E_HIP;
+    }
+    while ((int)c->copy_ev.size() <= slot) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return BG_E_HIP;
+      c->copy_ev.push_back(e);
+    }
+    ps = c->pstream;
+    ev = c->copy_ev[slot];
+    // the destination may be a block ctx's stream used before (the caching allocator):
+    // the copies start after the position bg_copy_order recorded for this slot
+    if (slot < (int)c->order_set.size() && c->order_set[slot] &&
+        hipStreamWaitEvent(ps, c->order_ev[slot], 0) != hipSuccess)
+      return BG_E_HIP;
+  }
+  int rc = 0;
+  if (len) {
+    if ((rc = ring_get(c))) return rc;
+    if (c->ring_base && copy_kernel() == 0) {
+      const int fd = rd_pread() ? image_fd(m) : -1;
+      rc = ring_h2d_grouped(c, (char*)dst, m->data + off, len, fd, off, ring_group(), ps);
+    } else if (hipMemcpyAsync(dst, m->data + off, (size_t)len, hipMemcpyHostToDevice, ps) != hipSuccess) {
+      rc = BG_E_HIP;
+    }
+  }
+  if (!rc && hipEventRecord(ev, ps) != hipSuccess) rc = BG_E_HIP;
+  return rc;
+}
+
+extern "C" int bg_copy_order(bg_ctx* c, int slot) {
+  if (!c || slot < 0 || slot >= 65536) return BG_E_ARG;
+  bg_bind(c);
+  std::lock_guard<std::mutex> g(c->copy_mu);
+  while ((int)c->order_ev.size() <= slot) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return BG_E_HIP;
+    c->order_ev.push_back(e);
+    c->order_set.push_back(0);
+  }
+  if (hipEventRecord(c->order_ev[slot], c->stream) != hipSuccess) return BG_E_HIP;
+  c->order_set[slot] = 1;
+  return 0;
+}
+
+extern "C" int bg_copy_fence(bg_ctx* c, int slot) {
+  if (!c || slot < 0) return BG_E_ARG;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->copy_mu);
+    if (slot >= (int)c->copy_ev.size()) return BG_E_ARG;
+    ev = c->copy_ev[slot];
+  }
+  BG_HIP(c, hipStreamWaitEvent(c->stream, ev, 0));
   return 0;
 }
 

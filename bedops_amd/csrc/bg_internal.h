@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <thread>
@@ -81,6 +82,11 @@ struct bg_ctx {
   int ring_rc = 0;
   struct bg_pool* pool = nullptr;  // the ring's copy threads (bg_api.hip)
   hipStream_t cstream = nullptr;  // second H2D copy stream of the ring (BEDGPU_COPY_STREAMS=2)
+  hipStream_t pstream = nullptr;  // prefetch copies (bg_file_image_copy), fenced by slot events
+  std::vector<hipEvent_t> copy_ev;  // bg_file_image_copy slots
+  std::vector<hipEvent_t> order_ev;  // bg_copy_order: ctx's stream position a slot's copies wait for
+  std::vector<char> order_set;
+  std::mutex copy_mu;
   hipEvent_t cjoin = nullptr;     // its copies -> ctx's stream
   hipStream_t stream = nullptr;
   std::string err;

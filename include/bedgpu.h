@@ -269,6 +269,21 @@ int bg_file_image_open(const char* path, bg_file_image* m);
 int bg_file_image_register(bg_file_image* m);
 int bg_file_image_to_device(bg_ctx* ctx, const bg_file_image* m, uint64_t off, uint64_t len, void** dptr);
 void bg_file_image_close(bg_file_image* m);
+/* Prefetch (the chromosome-group pipeline's read-ahead): a host thread of the caller's copies
+ * the next groups while ctx's stream runs the current one.
+ *   bg_device_alloc     a device buffer of ctx (free with bg_device_release / bg_device_free);
+ *                       from the thread that launches ctx's work
+ *   bg_file_image_copy  bytes [off, off + len) of an image into dst on ctx's prefetch stream,
+ *                       then records slot's event (0 <= slot < 65536); any one thread
+ *   bg_copy_order       records ctx's stream position: slot's later copies start after it
+ *                       (call it once slot's buffers are allocated: a buffer may be a block
+ *                       ctx's earlier work used, handed back by the caching allocator)
+ *   bg_copy_fence       ctx's stream waits for slot's last recorded copy (call it after the
+ *                       bg_file_image_copy for that slot returned) */
+int bg_device_alloc(bg_ctx* ctx, uint64_t n, void** dptr);
+int bg_file_image_copy(bg_ctx* ctx, const bg_file_image* m, uint64_t off, uint64_t len, void* dst, int slot);
+int bg_copy_order(bg_ctx* ctx, int slot);
+int bg_copy_fence(bg_ctx* ctx, int slot);
 /* Output queue: texts (device pointers of ctx, e.g. bg_result_text_device) written to fd in
  * the order they are pushed, by a host thread of the queue's own (D2H on its own stream into
  * pinned slots, then write(2)), so output can go out while the caller reads and computes the
