@@ -60,6 +60,28 @@ def test_bedops_groups_equal_oracle(gpu_bin, oracle_bin, tmp_path, mode):
             assert got == want, (mode, trial, groups)
 
 
+@pytest.mark.parametrize("ahead", [1, 2, 5])
+def test_groups_read_ahead_equal_oracle(gpu_bin, oracle_bin, tmp_path, ahead):
+    """BEDGPU_STREAM_AHEAD: a copier thread copies later groups on the prefetch stream while
+    earlier ones run (bg_file_image_copy after bg_copy_order, bg_copy_fence before the load):
+    many small groups, so released blocks come straight back as the next groups' buffers"""
+    rng = random.Random(90 + ahead)
+    files = [randbed.write(str(tmp_path / f"{k}.bed"),
+                           randbed.text(randbed.rows(rng, 30000, chroms=CHROMS, span=60000)))
+             for k in range(2)]
+    os.environ["BEDGPU_STREAM_AHEAD"] = str(ahead)
+    try:
+        for mode in (["-i"], ["-m"], ["-d"]):
+            want = subprocess.run([oracle_bin["bedops"], *mode, *files], stdout=subprocess.PIPE,
+                                  check=True).stdout
+            for groups in (3, 9):
+                rc, got, err = _run(gpu_bin["bedops"], mode + files, str(tmp_path / "o.bed"), groups)
+                assert rc == 0 and got == want, (mode, groups, err[-2000:])
+                assert _streamed(err), err
+    finally:
+        os.environ.pop("BEDGPU_STREAM_AHEAD", None)
+
+
 def test_bedops_groups_actually_stream(gpu_bin, oracle_bin, tmp_path):
     rng = random.Random(3)
     files = [randbed.write(str(tmp_path / f"{k}.bed"),
