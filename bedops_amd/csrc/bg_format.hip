@@ -17,6 +17,7 @@
 #include <cstring>
 
 #include "bg_internal.h"
+#include "bg_decfmt.h"
 
 #define FT_ROWS 2
 #define FT_TILE (BG_NT * FT_ROWS)
@@ -308,74 +309,7 @@ __device__ __forceinline__ void put_sci(Out& o, uint64_t N, int E, bool neg, int
   const uint64_t ae = (uint64_t)(E < 0 ? -E : E);
   put_u64(o, ae, ae < 10 ? 2 : dec_len_u64(ae));
 }
-// "%.{prec}lf" of any finite double whose rounded digits do not fit the 64-bit fast path
-// (|v| * 10^prec >= 2^64): N = round-half-even(|v| * 10^prec) exactly, in 32-bit limbs
-// (|v| = m * 2^ex: m * 10^prec shifted left by ex, or right by -ex with the glibc rounding
-// of the exact binary value), then base-10^9 digits by long division.
-template <typename Out>
-__device__ __noinline__ bool put_fixed_big(Out& o, double v, int prec) {
-  const uint64_t bits = (uint64_t)__double_as_longlong(v);
-  const bool neg = (bits >> 63) != 0;
-  const int bexp = (int)((bits >> 52) & 0x7ff);
-  uint64_t m = bits & ((1ULL << 52) - 1);
-  if (bexp == 0x7ff) return false;  // inf / nan
-  int ex;
-  if (bexp == 0) ex = -1074;
-  else { m |= 1ULL << 52; ex = bexp - 1075; }
-  uint64_t P = 1;
-  for (int k = 0; k < prec; ++k) P *= 10;  // prec <= 17 (bg_map)
-  typedef unsigned __int128 u128;
-  u128 X = (u128)m * P;  // < 2^110
-  constexpr int NL = 40;  // 1280 bits >= 2^110 * 2^971
-  uint32_t L[NL];
-  for (int k = 0; k < NL; ++k) L[k] = 0;
-  if (ex >= 0) {
-    const int w = ex >> 5, b = ex & 31;
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t chunk = (uint64_t)(uint32_t)(X >> (32 * k));
-      const uint64_t sh = chunk << b;
-      if (w + k < NL) L[w + k] |= (uint32_t)sh;
-      if (w + k + 1 < NL) L[w + k + 1] |= (uint32_t)(sh >> 32);
-    }
-  } else {
-    const int sh = -ex;
-    u128 q = 0;
-    if (sh < 128) {
-      q = X >> sh;
-      const u128 rem = X - (q << sh);
-      const u128 half = (u128)1 << (sh - 1);
-      if (rem > half || (rem == half && (q & 1))) ++q;
-    }  // else |v| * 10^prec < 2^-17: rounds to 0
-    for (int k = 0; k < 4; ++k) L[k] = (uint32_t)(q >> (32 * k));
-  }
-  char D[400];  // decimal digits, least significant first
-  int nd = 0;
-  int top = NL;
-  while (top > 0 && L[top - 1] == 0) --top;
-  while (top > 0) {
-    uint64_t rem = 0;
-    for (int k = top - 1; k >= 0; --k) {
-      const uint64_t cur = (rem << 32) | L[k];
-      L[k] = (uint32_t)(cur / 1000000000u);
-      rem = cur % 1000000000u;
-    }
-    while (top > 0 && L[top - 1] == 0) --top;
-    for (int d = 0; d < 9; ++d) {
-      D[nd++] = (char)('0' + rem % 10);
-      rem /= 10;
-      if (top == 0 && rem == 0) break;
-    }
-  }
-  while (nd <= prec) D[nd++] = '0';  // at least one integer digit
-  if (neg) o.put('-');
-  for (int k = nd - 1; k >= prec; --k) o.put(D[k]);
-  if (prec > 0) {
-    o.put('.');
-    for (int k = prec - 1; k >= 0; --k) o.put(D[k]);
-  }
-  return true;
-}
-
+// exact "%.{p}lf" / "%.{p}e" for what the fast paths above do not cover: bg_decfmt.h
 // a score-precision value (PrintScorePrecision: "%.{p}lf", or "%.{p}e" under --sci)
 template <typename Out>
 __device__ __forceinline__ bool put_real(Out& o, double v, int prec, bool sci) {
@@ -394,12 +328,12 @@ __device__ __forceinline__ bool put_real(Out& o, double v, int prec, bool sci) {
   }
   if (sci) {
     int E;
-    if (!sci_digits(v, prec, N, E, neg)) return false;
-    put_sci(o, N, E, neg, prec);
+    if (prec <= 17 && sci_digits(v, prec, N, E, neg)) put_sci(o, N, E, neg, prec);
+    else put_real_exact(o, v, prec, true);
     return true;
   }
-  if (!fixed_digits(v, prec, N, neg)) return put_fixed_big(o, v, prec);
-  put_fixed(o, N, neg, prec);
+  if (prec <= 17 && fixed_digits(v, prec, N, neg)) put_fixed(o, N, neg, prec);
+  else put_real_exact(o, v, prec, false);
   return true;
 }
 
@@ -409,7 +343,7 @@ template <typename Out>
 __device__ __forceinline__ bool put_real_fixed(Out& o, double v, int prec) {
   uint64_t N;
   bool neg;
-  if (!fixed_digits(v, prec, N, neg)) return false;
+  if (prec > 17 || !fixed_digits(v, prec, N, neg)) return false;
   put_fixed(o, N, neg, prec);
   return true;
 }
@@ -568,8 +502,12 @@ __device__ __forceinline__ bool put_map_row(const FmtArgs& A, Out& o, uint64_t m
     } else {
       uint64_t N;
       bool neg;
-      if (!fixed_digits(A.score2[m], 6, N, neg)) {
-        if (!put_fixed_big(o, A.score2[m], 6)) return false;
+      const double sv = A.score2[m];
+      if (sv != sv || sv == __longlong_as_double(0x7ff0000000000000LL) ||
+          sv == __longlong_as_double((long long)0xfff0000000000000ULL)) {
+        if (!put_real(o, sv, 6, false)) return false;
+      } else if (!fixed_digits(sv, 6, N, neg)) {
+        put_real_exact(o, sv, 6, false);
       } else {
         put_fixed(o, N, neg, 6);
       }

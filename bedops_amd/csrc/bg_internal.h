@@ -41,6 +41,7 @@ struct bg_dstatus {
   long long maxlen;              // max (end - start) seen (bedmap window)
   unsigned long long stop_row;   // bedmap: first row where the reference throws (~0: none)
   unsigned long long pad[2];
+  unsigned long long nbig;       // BED5 scores left to the exact big-number conversion (k_score_big)
 };
 
 // bedmap: map rows longer than thr, by length class (see bg_map_cands below)

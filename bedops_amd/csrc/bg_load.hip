@@ -34,6 +34,7 @@
 
 #include "bg_internal.h"
 #include "bg_parse.h"
+#include "bg_strtod.h"
 
 #define TT 8192   // tile bytes
 #define HB 16     // halo before (we need the byte before the tile)
@@ -456,15 +457,16 @@ __device__ __forceinline__ bool decimal_exact(uint64_t m, int pw, double& out) {
 // fast path: one rounding of exact operands), p up to 37 when m * 10^(p-22) stays an exact
 // integer <= 2^53, otherwise -26 <= p <= 27 by exact 128-bit arithmetic (decimal_exact:
 // e.g. the 17 significant digits of %.17g / repr output). Integers up to 2^53 are flagged
-// (exact sums). Anything else (more than 19 significant digits, larger exponents) ->
-// ERR_SCORE.
+// (exact sums). Any other valid number (up to BG_SD_DIGITS significant digits, any
+// exponent) returns isint = -1: the caller lists it for k_score_big (bg_strtod.h). More
+// digits, or anything that is not a plain decimal number -> ERR_SCORE.
 __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64_t le,
                                             double& out, int& isint) {
   bool neg = false;
   if (p < le && (T.at(p) == '+' || T.at(p) == '-')) neg = T.at(p++) == '-';
   uint64_t m = 0;
   int nd = 0, frac = 0, sig = 0;
-  bool dot = false;
+  bool dot = false, big = false;
   while (p < le) {
     const uint8_t ch = T.at(p);
     if (ch == '.' && !dot) { dot = true; ++p; continue; }
@@ -473,10 +475,10 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
     if (dot) ++frac;
     if (m != 0 || ch != '0') ++sig;
     if (sig <= 19) m = m * 10 + (ch - '0');
-    else return false;
+    else big = true;  // past 19 digits: k_score_big (up to BG_SD_DIGITS)
     ++p;
   }
-  if (nd == 0 || sig > 19) return false;
+  if (nd == 0 || sig > BG_SD_DIGITS) return false;
   int ex = 0;
   if (p < le && (T.at(p) == 'e' || T.at(p) == 'E')) {  // strtod takes the exponent only if digits follow
     int64_t q = p + 1;
@@ -493,6 +495,11 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
     p = q;
   }
   if (p < le && !bg_isws(T.at(p))) return false;  // junk after the number
+  if (big) {  // a syntactically valid number for the exact conversion (isint -1)
+    isint = -1;
+    out = 0;
+    return true;
+  }
   int pw = ex - frac;  // value = m * 10^pw
   while (pw < 0 && m != 0 && m % 10 == 0) { m /= 10; ++pw; }  // trailing zeros
   const double P10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
@@ -503,7 +510,11 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
     return true;
   }
   if (m > (1ULL << 53) || pw < -22) {  // outside Clinger's fast path: exact 128-bit rounding
-    if (!decimal_exact(m, pw, out)) return false;
+    if (!decimal_exact(m, pw, out)) {  // beyond 128 bits: k_score_big
+      isint = -1;
+      out = 0;
+      return true;
+    }
     isint = 0;  // a fraction, or an integer above 2^53 (no exact int64 sums)
     if (neg) out = -out;
     return true;
@@ -520,7 +531,11 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
         mm *= 10;
       }
       if (pp > 22) {  // not exact that way
-        if (!decimal_exact(m, pw, out)) return false;
+        if (!decimal_exact(m, pw, out)) {
+          isint = -1;
+          out = 0;
+          return true;
+        }
         isint = 0;
         if (neg) out = -out;
         return true;
@@ -550,7 +565,8 @@ struct Line {
   int64_t rest;
   double score;
   int err;
-  int scoreint;
+  int scoreint;  // 1: an integer <= 2^53; 0: other; -1: left to k_score_big
+  int64_t spos;  // the score's first byte
 };
 
 // full grammar, byte by byte (fallback path and error reporting)
@@ -585,9 +601,66 @@ __device__ __forceinline__ void parse_line_slow(const TileText& T, int64_t ls, i
     if (p == id) { L.err = ERR_PARSE; return; }
     while (p < le && bg_isws(T.at(p))) ++p;
     int isint = 1;
+    L.spos = p;
     if (!parse_score(T, p, le, L.score, isint)) { L.err = ERR_SCORE; return; }
     L.scoreint = isint;
   }
+}
+
+// a score for k_score_big: (row, first byte) pairs; beyond the list's capacity the load
+// refuses (finish_one)
+__device__ __forceinline__ void big_push(bg_dstatus* st, uint64_t* big, uint32_t cap, uint64_t r, int64_t pos) {
+  const unsigned long long q = atomicAdd(&st->nbig, 1ULL);
+  if (q < cap) {
+    big[2 * q] = r;
+    big[2 * q + 1] = (uint64_t)pos;
+  }
+}
+
+// the exact conversion of the listed scores (parse_score's isint -1: more than 19 significant
+// digits or exponents past the 128-bit path), one thread per score; the syntax was checked
+// by parse_score. st->flags bit 5: a score with more than BG_SD_DIGITS significant digits
+__global__ void k_score_big(const uint8_t* __restrict__ txt, uint64_t nb, const uint64_t* __restrict__ big,
+                            uint64_t n, double* __restrict__ score) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r = big[2 * i];
+  uint64_t p = big[2 * i + 1];
+  bool neg = false;
+  if (p < nb && (txt[p] == '+' || txt[p] == '-')) neg = txt[p++] == '-';
+  uint8_t dg[BG_SD_DIGITS];
+  int nd = 0, frac_after = 0;  // significant digits; fraction digits after the first significant one
+  int lead_frac = 0;           // fraction digits before it (leading zeros after the point)
+  bool dot = false;
+  for (; p < nb; ++p) {
+    const uint8_t ch = txt[p];
+    if (ch == '.' && !dot) { dot = true; continue; }
+    if (ch < '0' || ch > '9') break;
+    if (nd == 0 && ch == '0') {
+      if (dot) ++lead_frac;
+      continue;
+    }
+    if (nd < BG_SD_DIGITS) dg[nd] = (uint8_t)(ch - '0');
+    ++nd;
+    if (dot) ++frac_after;
+  }
+  int ex = 0;
+  if (p < nb && (txt[p] == 'e' || txt[p] == 'E')) {
+    uint64_t q = p + 1;
+    bool eneg = false;
+    if (q < nb && (txt[q] == '+' || txt[q] == '-')) eneg = txt[q++] == '-';
+    for (; q < nb && txt[q] >= '0' && txt[q] <= '9'; ++q)
+      if (ex < 100000) ex = ex * 10 + (txt[q] - '0');
+    if (eneg) ex = -ex;
+  }
+  int n10 = nd;
+  while (n10 > 0 && n10 <= BG_SD_DIGITS && dg[n10 - 1] == 0) --n10;  // trailing zeros
+  double v = 0;
+  if (nd <= BG_SD_DIGITS && n10 > 0) {
+    const int e = ex - lead_frac - frac_after + (nd - n10);  // exponent of the last kept digit
+    strtod_big(dg, n10, e, false, v);
+  }
+  score[r] = neg ? -v : v;
 }
 
 // 16 bytes of LDS starting at byte offset q (q + 20 <= LBUF)
@@ -883,7 +956,7 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
-    bg_dstatus* st) {
+    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap) {
   __shared__ ParseLdsT<1> S;
   __shared__ int64_t lkey[LCAP];
   uint8_t* buf = S.b[0].buf;
@@ -959,7 +1032,8 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
     }
     if (score) {
       score[r] = Ln.score;
-      if (!Ln.scoreint) atomicOr(&st->flags, 1ULL);
+      if (Ln.scoreint <= 0) atomicOr(&st->flags, 1ULL);
+      if (Ln.scoreint < 0) big_push(st, big, bigcap, r, Ln.spos);
     }
   }
 #pragma unroll
@@ -1467,7 +1541,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
-    bg_dstatus* st) {
+    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap) {
   __shared__ ParseLdsWs S;
   constexpr uint32_t NR = LCAP_WS / NT;  // rounds of NT lines at most
   __shared__ int64_t kfirst[NR][NT / 64], klast[NR][NT / 64];  // keys at the waves' edges
@@ -1528,7 +1602,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
           }
           if (score) {
             score[r] = Ln.score;
-            if (!Ln.scoreint) atomicOr(&st->flags, 1ULL);
+            if (Ln.scoreint <= 0) atomicOr(&st->flags, 1ULL);
+            if (Ln.scoreint < 0) big_push(st, big, bigcap, r, Ln.spos);
           }
         }
       }
@@ -1789,8 +1864,8 @@ __device__ __forceinline__ uint32_t prologue_w(const uint8_t* __restrict__ txt, 
 
 // the rounds of one sub-tile: 64 lines per round, one per lane, in line order (V as
 // set_rounds_n). kl: K (+1 form) of the sub-tile's largest row key.
-template <typename V>
-__device__ __forceinline__ void set_rounds_w(const ParseLdsW& S, const TileText& T, const RunTable& R,
+template <typename V, typename LdsT = ParseLdsW>
+__device__ __forceinline__ void set_rounds_w(const LdsT& S, const TileText& T, const RunTable& R,
                                              uint32_t rl, uint32_t rh, int64_t t0, uint32_t L,
                                              int64_t last_end, int64_t gbase, uint64_t base,
                                              int64_t* __restrict__ LCS, int64_t* __restrict__ LCE,
@@ -1893,6 +1968,488 @@ __global__ void __launch_bounds__(64) k_parse_set_w(
     TS.base[u] = base;
     TS.nloc[u] = nc;
     TS.nrow[u] = L - ((L > 0 && last_end < 0) ? 1 : 0);
+  }
+}
+
+// ---- k_parse_set_v (round 5, the default): k_parse_set_w with a lean common path -------
+// Same sub-tiles, LDS layout, staging and SetTiles entries as k_parse_set_w. The SQ counters
+// of k_parse_set_w (profiles/r04_sq_k_parse_set_w.txt: 1294 VALU + 504 SALU per 4 KiB wave)
+// and its ISA (64-bit address arithmetic, compares and masks, guarded byte-loop loads, funnel
+// shifts for every unaligned LDS word) set what this kernel removes. On the common path — a
+// sub-tile inside one chromosome run (rl == rh) whose lines are "<token> <start> <end>[...]"
+// within their first 32 bytes, the token the run's, both numbers of at most 9 digits —
+// every step is 32-bit:
+//  - the global loads are unguarded when the sub-tile and its halos lie inside the text (a
+//    wave-uniform test; only the file's first and last sub-tiles take load16);
+//  - '\n' classes two dwords per multiply (the whitespace gather of bgp_ws8);
+//  - lst[L] holds the last line's end, so a line's start and end come from ONE unaligned
+//    32-bit LDS read of lst[k], lst[k+1];
+//  - fields from the transitions of the line's whitespace window (starts = non-ws after ws,
+//    ends = ws after non-ws: three ffbl + clear-lowest each) instead of a chain of masks;
+//  - unaligned LDS reads (ds_read_b64/b96; gfx950 DS takes any byte address) for the window,
+//    the token and each number's last 12 bytes: no alignbyte funnels;
+//  - a number of <= 9 digits converts with two byte dot products per dword and 24-bit
+//    multiply-adds (< 10^9 < 2^32);
+//  - the token compared under the run's length mask (uniform).
+// Any other line (longer fields, signs, errors, the dropped unterminated tail) takes set_row,
+// the full grammar, in its own lane; sub-tiles over a chromosome change run set_rounds_w.
+
+// v_ffbl_b32 itself: the lowest set bit's index, 0xFFFFFFFF for 0 (no select for the zero case)
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// Byte classes without v_mul_lo_u32 (a quarter-rate instruction): bit 7 of each byte is the
+// byte's flag, v_bitop3_b32 merges the SWAR terms (truth tables as f(0xF0, 0xCC, 0xAA) over
+// the operands S0, S1, S2), and byte dot products gather the flags of two dwords into 8 bits.
+#define BOP3_A 0xF0u
+#define BOP3_B 0xCCu
+#define BOP3_C 0xAAu
+// whitespace {' ', 0x09..0x0D} (bgp_ws80 in 7 operations)
+__device__ __forceinline__ uint32_t ws80_v(uint32_t x) {
+  const uint32_t lo7 = x & 0x7F7F7F7Fu;
+  const uint32_t nz20 = (lo7 ^ 0x20202020u) + 0x7F7F7F7Fu;  // bit 7: byte != ' '
+  const uint32_t ge9 = lo7 + 0x77777777u, ge14 = lo7 + 0x72727272u;
+  const uint32_t f = __builtin_amdgcn_bitop3_b32(nz20, ge9, ge14, (~BOP3_A | (BOP3_B & ~BOP3_C)) & 0xFFu);
+  return __builtin_amdgcn_bitop3_b32(f, x, 0x80808080u, (BOP3_A & ~BOP3_B & BOP3_C) & 0xFFu);
+}
+// '\n' (nl_mask4 in 3 operations; bit 7 of x ^ 0x0A is bit 7 of x)
+__device__ __forceinline__ uint32_t nl80_v(uint32_t x) {
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(x, 0x0A0A0A0Au, 0x7F7F7F7Fu, ((BOP3_A ^ BOP3_B) & BOP3_C) & 0xFFu) +
+                     0x7F7F7F7Fu;
+  return __builtin_amdgcn_bitop3_b32(t, x, 0x80808080u, (~BOP3_A & ~BOP3_B & BOP3_C) & 0xFFu);
+}
+// bit-7 flags of two dwords -> their 8 flags (a's bytes, then b's) times 128
+__device__ __forceinline__ uint32_t gather8x128(uint32_t fa, uint32_t fb) {
+  return __builtin_amdgcn_udot4(fb, 0x80402010u, __builtin_amdgcn_udot4(fa, 0x08040201u, 0u, false), false);
+}
+// 32 bytes -> whitespace mask and '\n' mask (bit j = byte j)
+__device__ __forceinline__ void classify32(const uint4 a, const uint4 b, uint32_t& ws, uint32_t& nl) {
+  const uint32_t w0 = gather8x128(ws80_v(a.x), ws80_v(a.y)), w1 = gather8x128(ws80_v(a.z), ws80_v(a.w));
+  const uint32_t w2 = gather8x128(ws80_v(b.x), ws80_v(b.y)), w3 = gather8x128(ws80_v(b.z), ws80_v(b.w));
+  ws = (w0 >> 7) | (w1 << 1) | (w2 << 9) | (w3 << 17);
+  const uint32_t n0 = gather8x128(nl80_v(a.x), nl80_v(a.y)), n1 = gather8x128(nl80_v(a.z), nl80_v(a.w));
+  const uint32_t n2 = gather8x128(nl80_v(b.x), nl80_v(b.y)), n3 = gather8x128(nl80_v(b.z), nl80_v(b.w));
+  nl = (n0 >> 7) | (n1 << 1) | (n2 << 9) | (n3 << 17);
+}
+// 16 bytes -> 16-bit masks
+__device__ __forceinline__ void classify16(const uint4 a, uint32_t& ws, uint32_t& nl) {
+  ws = (gather8x128(ws80_v(a.x), ws80_v(a.y)) >> 7) | (gather8x128(ws80_v(a.z), ws80_v(a.w)) << 1);
+  nl = (gather8x128(nl80_v(a.x), nl80_v(a.y)) >> 7) | (gather8x128(nl80_v(a.z), nl80_v(a.w)) << 1);
+}
+
+struct LdsU3 {
+  uint32_t x, y, z;
+};
+// unaligned LDS reads (any byte address); BG_LDS_ALIGNED=1: aligned dwords + alignbyte
+#ifndef BG_LDS_ALIGNED
+#define BG_LDS_ALIGNED 0
+#endif
+#if BG_LDS_ALIGNED
+template <int N>
+__device__ __forceinline__ void lds_words(const void* p, uint32_t* o) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t w[N + 1];
+#pragma unroll
+  for (int i = 0; i <= N; ++i) w[i] = d[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+__device__ __forceinline__ uint32_t ldsu32(const void* p) {
+  uint32_t o[1];
+  lds_words<1>(p, o);
+  return o[0];
+}
+__device__ __forceinline__ uint2 ldsu64(const void* p) {
+  uint32_t o[2];
+  lds_words<2>(p, o);
+  return make_uint2(o[0], o[1]);
+}
+__device__ __forceinline__ LdsU3 ldsu96(const void* p) {
+  uint32_t o[3];
+  lds_words<3>(p, o);
+  return LdsU3{o[0], o[1], o[2]};
+}
+__device__ __forceinline__ uint4 ldsu128(const void* p) {
+  uint32_t o[4];
+  lds_words<4>(p, o);
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+#else
+__device__ __forceinline__ uint32_t ldsu32(const void* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+__device__ __forceinline__ uint2 ldsu64(const void* p) {
+  uint2 v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+__device__ __forceinline__ LdsU3 ldsu96(const void* p) {
+  LdsU3 v;
+  __builtin_memcpy(&v, p, 12);
+  return v;
+}
+__device__ __forceinline__ uint4 ldsu128(const void* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+#endif
+
+#ifndef BG_EXP_V
+#define BG_EXP_V 0
+#endif
+#ifndef BG_GTXT
+#define BG_GTXT 0
+#endif
+// the value of a number of L (1..9) digits whose last digit is the high byte of D.z (the 12
+// bytes D end at the number's end); ok cleared when one of its bytes is not a digit
+__device__ __forceinline__ uint32_t digits9(const LdsU3 D, uint32_t L, bool& ok) {
+  const uint32_t u = 8u * (12u - L);                // bits before the number: 24..88
+  const uint32_t sh = ~0u << (u & 31u);
+  const uint32_t m1 = u < 32u ? sh : 0u;
+  const uint32_t m2 = u < 32u ? ~0u : (u < 64u ? sh : 0u);
+  const uint32_t m3 = u < 64u ? ~0u : sh;
+  const uint32_t x1 = (D.x ^ 0x30303030u) & m1;     // digit values; bytes before the number 0
+  const uint32_t x2 = (D.y ^ 0x30303030u) & m2;
+  const uint32_t x3 = (D.z ^ 0x30303030u) & m3;
+  const uint32_t bad = (x1 | ((x1 & 0x7F7F7F7Fu) + 0x76767676u)) | (x2 | ((x2 & 0x7F7F7F7Fu) + 0x76767676u)) |
+                       (x3 | ((x3 & 0x7F7F7F7Fu) + 0x76767676u));
+  ok = ok && (bad & 0x80808080u) == 0;
+  // 10 * b0 + b1 and 10 * b2 + b3 of a dword by byte dot products; L <= 9: x1 holds one digit
+  // (24-bit multiplies: full rate, every operand < 2^24)
+  const uint32_t v2 = __builtin_amdgcn_udot4(x2, 0x010A0000u, __umul24(__builtin_amdgcn_udot4(x2, 0x0000010Au, 0u, false), 100u), false);
+  const uint32_t v3 = __builtin_amdgcn_udot4(x3, 0x010A0000u, __umul24(__builtin_amdgcn_udot4(x3, 0x0000010Au, 0u, false), 100u), false);
+  return __umul24(__umul24(x1 >> 24, 10000u) + v2, 10000u) + v3;
+}
+
+// k_parse_set_v's LDS: a 32-byte halo after the sub-tile (+32 bytes of padding the fast
+// path's reads may touch) instead of 256, and at most 384 lines per 4 KiB (lines averaging
+// under 10.7 bytes report ERR_PARSE and the load is redone with row columns): 5470 bytes
+// instead of 5984, 29 waves per CU instead of 26 (LDS-bound residency). A last line whose
+// '\n' lies past the halo is found by find_nl_wave (1 KiB per step).
+#define HA_V 32
+#define LCAP_V 384
+struct ParseLdsV {
+  __attribute__((aligned(16))) uint8_t buf[HB + TW + HA_V + 32];
+  uint32_t wsm[TW / 32 + (HA_V + 32) / 32 + 1];
+  uint16_t lst[LCAP_V + 1];
+};
+
+// first '\n' at or after `from` (-1: none before the end of the text), one wave, 1 KiB a step
+__device__ __forceinline__ int64_t find_nl_wave(const uint8_t* __restrict__ txt, uint64_t nb, int64_t from) {
+  const int lane = threadIdx.x;
+  for (int64_t b = from; b >= 0 && (uint64_t)b < nb; b += 1024) {
+    const uint4 x = load16(txt, b + 16 * lane, nb);  // bytes past the text read as 0
+    const uint32_t m = (gather8x128(nl80_v(x.x), nl80_v(x.y)) >> 7) | (gather8x128(nl80_v(x.z), nl80_v(x.w)) << 1);
+    const uint64_t bal = __ballot(m != 0);
+    if (bal) {
+      const int f = __builtin_ctzll(bal);
+      return b + 16 * f + __builtin_ctz(wave_readlane(m, f));
+    }
+  }
+  return -1;
+}
+
+// the sub-tile's bytes as registers: 64 per lane, and 16 of the halos (lanes < HL: after the
+// sub-tile, lane 63: the 16 bytes before it); unguarded when the sub-tile and its halos lie
+// inside the text (wave-uniform), load16 otherwise
+#define HL_W ((HA_V + 32) / 16)
+struct SubRegs {
+  uint4 v[4];
+  uint4 vh;
+};
+__device__ __forceinline__ void load_sub(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0, SubRegs& R) {
+  constexpr int HL = HL_W;
+  static_assert(HL % 2 == 0 && HL < 63, "halo lanes");
+  const int lane = threadIdx.x;
+  uint4* const v = R.v;
+  uint4& vh = R.vh;
+  vh = make_uint4(0, 0, 0, 0);
+  if (t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb) {  // wave-uniform: no guards
+    const uint4* p = reinterpret_cast<const uint4*>(txt + t0) + 4 * lane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = p[i];
+    if (lane < HL) vh = reinterpret_cast<const uint4*>(txt + t0 + TW)[lane];
+    else if (lane == 63) vh = *reinterpret_cast<const uint4*>(txt + t0 - HB);
+  } else {
+    const int64_t b = t0 + 64 * lane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = load16(txt, b + 16 * i, nb);
+    if (lane < HL) vh = load16(txt, t0 + TW + 16 * lane, nb);
+    else if (lane == 63) vh = load16(txt, t0 - HB, nb);
+  }
+}
+
+// prologue of k_parse_set_v: prologue_w from the registers of load_sub, with the cheaper
+// '\n' classes and lst[L] = the last line's end + 1 (0xFFFF: none or out of reach)
+__device__ __forceinline__ uint32_t prologue_v(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
+                                               const SubRegs& R, ParseLdsV& S, int64_t& last_end,
+                                               bg_dstatus* st) {
+  constexpr int HL = HL_W;
+  const int lane = threadIdx.x;
+  const uint4* const v = R.v;
+  const uint4 vh = R.vh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
+  if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
+  else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
+  uint32_t w0, w1, n0, n1, hw, hm;
+  classify32(v[0], v[1], w0, n0);
+  classify32(v[2], v[3], w1, n1);
+  classify16(vh, hw, hm);
+  *reinterpret_cast<uint2*>(&S.wsm[2 * lane]) = make_uint2(w0, w1);
+  {
+    const uint32_t hn = __shfl_down(hw, 1, 64);
+    if (lane < HL && !(lane & 1)) S.wsm[TW / 32 + lane / 2] = hw | (hn << 16);
+    if (lane == HL) S.wsm[TW / 32 + HL / 2] = 0;
+  }
+  if (lane >= HL) hm = 0;
+  const uint64_t hb = __ballot(hm != 0);
+  int64_t hnl = -1;
+  if (hb) {
+    const int f = __builtin_ctzll(hb);
+    hnl = TW + 16 * f + __builtin_ctz(wave_readlane(hm, f));
+  }
+  const bool has0 = t0 == 0 || (wave_readlane(vh.w, 63) >> 24) == '\n';
+  const bool endnl = (wave_readlane(v[3].w, 63) >> 24) == '\n';
+  if (lane == 63) n1 &= 0x7FFFFFFFu;
+  const uint32_t cnt = (uint32_t)(__popc(n0) + __popc(n1));
+  const uint32_t inc = wave_incl_scan(cnt, OpSum());
+  const uint32_t L = wave_readlane(inc, 63) + (has0 ? 1u : 0u);
+  if (L > LCAP_V) {
+    if (lane == 0) bg_report(st, 0, ERR_PARSE);
+    return L;
+  }
+  uint32_t o = inc - cnt + (has0 ? 1u : 0u);
+  if (lane == 0 && has0) S.lst[0] = 0;
+  for (uint32_t m = n0; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + bgp_ctz(m) + 1);
+  for (uint32_t m = n1; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + 32 + bgp_ctz(m) + 1);
+  __syncthreads();  // (one wave: orders the LDS writes above before the reads below)
+  last_end = L == 0 ? -1 : endnl ? t0 + TW - 1 : (hnl >= 0 ? t0 + hnl : find_nl_wave(txt, nb, t0 + TW + HA_V + 32));
+  if (lane == 0) {
+    const int64_t d = last_end - t0 + 1;
+    S.lst[L] = (last_end >= 0 && d < 0xFFFF) ? (uint16_t)d : (uint16_t)0xFFFF;
+  }
+  __syncthreads();
+  return L;
+}
+
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// the rounds of a one-run sub-tile (32-bit coordinates under the key prefix, set_rounds_w's
+// staging); TOK16: the run's token is 9..16 bytes
+template <bool TOK16, bool GTXT>
+__device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, const ParseLdsV& S,
+                                             const TileText& T, const RunTable& R,
+                                             uint32_t rl, int64_t t0, uint32_t L, int64_t last_end,
+                                             uint64_t base, int64_t* __restrict__ LCS,
+                                             int64_t* __restrict__ LCE, uint64_t& nc, uint32_t& carry_e,
+                                             uint32_t& kl, bg_dstatus* st) {
+  const int lane = threadIdx.x;
+  const uint64_t lt = (1ULL << lane) - 1;
+  // the run's token and the mask of its bytes, in SGPRs (readfirstlane: the stores below may
+  // alias R.info as far as the compiler knows, and it would reload the token every round
+  // behind an s_waitcnt vmcnt(0) that also waits for those stores)
+  const RunInfo& I = R.info[rl];
+  const uint32_t tlen = sgpr(I.tlen);
+  const uint64_t tm = tlen >= 8 ? ~0ull : ((1ull << (8 * tlen)) - 1);
+  const uint64_t tm2 = tlen >= 16 ? ~0ull : (tlen <= 8 ? 0ull : ((1ull << (8 * (tlen - 8))) - 1));
+  const uint32_t tk0 = sgpr((uint32_t)I.tlo), tk1 = sgpr((uint32_t)(I.tlo >> 32));
+  const uint32_t tk2 = sgpr((uint32_t)I.thi), tk3 = sgpr((uint32_t)(I.thi >> 32));
+  const uint32_t tm0 = sgpr((uint32_t)tm), tm1 = sgpr((uint32_t)(tm >> 32)), tm2l = sgpr((uint32_t)tm2),
+                 tm2h = sgpr((uint32_t)(tm2 >> 32));
+  uint32_t* const S32 = reinterpret_cast<uint32_t*>(LCS + base);
+  uint32_t* const E32 = reinterpret_cast<uint32_t*>(LCE + base);
+  uint32_t carry_k = 0, nc32 = (uint32_t)nc;
+  const uint32_t rounds = (L + 63) / 64;
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t k = j * 64 + lane;
+    const bool act = k < L;
+    const uint32_t pr = ldsu32(&S.lst[act ? k : 0]);
+    const uint32_t q = pr & 0xFFFFu, qn = pr >> 16;
+    const uint32_t len = qn - q - 1;  // bytes before the line's '\n'
+    uint32_t WS;
+    {
+      const uint2 two = ldsu64(&S.wsm[q >> 5]);
+      WS = __builtin_amdgcn_alignbit(two.y, two.x, q & 31u);
+    }
+    WS |= len < 32u ? (~0u << (len & 31u)) : 0u;  // bytes past the line end act as whitespace
+    const uint32_t NW = ~WS, NW1 = NW << 1;
+    uint32_t Ts = NW & ~NW1, Te = WS & NW1;    // field starts, field ends
+    const uint32_t a0 = ffbl_hw(Ts);
+    Ts &= Ts - 1;
+    const uint32_t s0 = ffbl_hw(Ts);
+    Ts &= Ts - 1;
+    const uint32_t e0 = ffbl_hw(Ts);
+    const uint32_t a1 = ffbl_hw(Te);
+    Te &= Te - 1;
+    const uint32_t s1 = ffbl_hw(Te);
+    Te &= Te - 1;
+    const uint32_t e1 = ffbl_hw(Te);
+    // the third field ends inside the window (so do the others); short numbers; the token's
+    // length; the line has an end (lst[L] != 0xFFFF)
+    bool ok = act && e1 <= 31u && qn != 0xFFFFu && (a1 - a0) == tlen && (s1 - s0) <= 9u && (e1 - e0) <= 9u;
+    // the line's bytes: LDS, or (GTXT) the text itself through the vector memory path,
+    // which the LDS pipe's unaligned reads do not share
+    const uint8_t* lb = GTXT ? txt + (t0 + q) : &S.buf[HB + q];
+    {
+      uint32_t dif;
+      if (TOK16) {
+        const uint4 t = ldsu128(lb + (a0 & 31u));
+        dif = ((t.x ^ tk0) & tm0) | ((t.y ^ tk1) & tm1) | ((t.z ^ tk2) & tm2l) | ((t.w ^ tk3) & tm2h);
+      } else {
+        const uint2 t = ldsu64(lb + (a0 & 31u));
+        dif = ((t.x ^ tk0) & tm0) | ((t.y ^ tk1) & tm1);
+      }
+      ok = ok && dif == 0;
+    }
+#if BG_EXP_V == 2  // experiment: no number conversion
+    uint32_t start = (uint32_t)((t0 + q) >> 1), end = start + 1 + (e1 & 1);
+#else
+    uint32_t start = digits9(ldsu96(lb + (s1 & 31u) - 12), (s1 - s0) & 15u, ok);
+    uint32_t end = digits9(ldsu96(lb + (e1 & 31u) - 12), (e1 - e0) & 15u, ok);
+#endif
+    bool valid = ok;
+    if (act && !ok) {  // the full grammar (and its errors), this lane only
+      int64_t ks = 0, ke = 0;
+      valid = set_row<true, true>(S, S.lst, T, R, rl, rl, t0, k, L, last_end, ks, ke, st);
+      start = (uint32_t)(ks & BG_COORD_MASK);
+      end = (uint32_t)(ke & BG_COORD_MASK);
+      if (valid && (uint64_t)(ke & BG_COORD_MASK) + 1 >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
+    } else if (ok) {
+      if (start > end) bg_report(st, 0, ERR_RANGE);
+      if (start == end) atomicOr(&st->flags, 2ULL);
+    }
+    const uint32_t K = valid ? start + 1 : 0u, E = valid ? end + 1 : 0u;
+    const uint32_t ie = wave_incl_max_u32(E);
+    const uint32_t pk = wave_shr1_v(K);
+    const uint32_t prevK = lane ? pk : carry_k;
+    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
+    const uint32_t ex_e = max(carry_e, wave_shr1_v(ie));
+    const bool open = valid && K > ex_e;
+    const uint64_t bal = __ballot(open);
+    const uint32_t pos = nc32 + (uint32_t)__popcll(bal & lt);
+    if (open && pos < SCAP_W) {
+      S32[pos] = K - 1;
+      if (pos > 0) E32[pos - 1] = ex_e - 1;
+    }
+    if (j + 1 == rounds) {
+      const int ll = (int)(L - 1 - j * 64);
+      const uint32_t k1 = wave_readlane(K, ll);
+      kl = k1 ? k1 : (ll > 0 ? wave_readlane(K, ll - 1) : carry_k);
+    }
+    carry_e = max(carry_e, wave_readlane(ie, 63));
+    carry_k = wave_readlane(K, 63);
+    nc32 += (uint32_t)__popcll(bal);
+  }
+  nc = nc32;
+}
+
+// one sub-tile from its registers
+__device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t u,
+                                            const SubRegs& V, ParseLdsV& S,
+                                            const uint32_t* __restrict__ runlo,
+                                            const uint32_t* __restrict__ runhi, const RunTable& R,
+                                            int64_t* __restrict__ LCS, int64_t* __restrict__ LCE,
+                                            const SetTiles& TS, bg_dstatus* st) {
+  const int64_t t0 = (int64_t)u * TW;
+  const uint64_t base = (uint64_t)u * SCAP_W;
+  int64_t last_end = -1;
+  const uint32_t L = prologue_v(txt, nb, t0, V, S, last_end, st);
+  if (L > LCAP_V) {
+    if (threadIdx.x == 0) {
+      TS.tmax[u] = TS.tlast[u] = LLONG_MIN;
+      TS.base[u] = base;
+      TS.nloc[u] = 0;
+      TS.nrow[u] = 0;
+      TS.gb[u] = -1;
+    }
+    return;
+  }
+  const uint32_t rl = runlo[u], rh = runhi[u];
+  const TileText T{txt, S.buf, t0 - HB, t0 + TW + HA_V, nb};
+  uint64_t nc = 0, cmax = 0, kmax = 0;
+  int64_t gbase = 0;
+#if BG_EXP_V == 1
+  if (true) {  // experiment: prologue only
+  } else
+#endif
+  if (rl == rh) {
+    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
+    uint32_t ce = 0, kl = 0;
+    const bool tok16 = R.info[rl].tlen > 8;
+#if BG_GTXT
+    if (t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb) {  // every read inside the text
+      if (tok16) set_rounds_v<true, true>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      else set_rounds_v<false, true>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+    } else
+#endif
+    if (tok16)
+      set_rounds_v<true, false>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+    else
+      set_rounds_v<false, false>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+    cmax = ce;
+    kmax = kl;
+  } else {
+    set_rounds_w<uint64_t, ParseLdsV>(S, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, nc, cmax, kmax, st);
+  }
+  if (threadIdx.x == 0) {
+    if (nc > SCAP_W) {
+      atomicOr(&st->flags, BG_SET_OVERFLOW);
+      nc = 0;
+    }
+    if (nc > 0) {
+      if (rl == rh) reinterpret_cast<uint32_t*>(LCE + base)[nc - 1] = (uint32_t)(cmax - 1);
+      else LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
+    }
+    TS.gb[u] = (rl == rh) ? gbase : -1;
+    TS.tmax[u] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
+    TS.tlast[u] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
+    TS.base[u] = base;
+    TS.nloc[u] = nc;
+    TS.nrow[u] = L - ((L > 0 && last_end < 0) ? 1 : 0);
+  }
+}
+
+// one wave per sub-tile
+__global__ void __launch_bounds__(64) k_parse_set_v(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+  __shared__ ParseLdsV S;
+  SubRegs V;
+  load_sub(txt, nb, (int64_t)blockIdx.x * TW, V);
+  parse_sub_v(txt, nb, blockIdx.x, V, S, runlo, runhi, R, LCS, LCE, TS, st);
+}
+
+// persistent waves (grid-strided over the sub-tiles): the next sub-tile's bytes are loaded
+// into registers while this one is parsed, so every wave keeps a load in flight through its
+// compute instead of waiting for its own bytes first
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_set_p(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+  __shared__ ParseLdsV S;
+  uint32_t u = blockIdx.x;
+  if (u >= nsub) return;
+  SubRegs V;
+  load_sub(txt, nb, (int64_t)u * TW, V);
+  for (;;) {
+    const uint32_t un = u + gridDim.x;
+    SubRegs N;
+    if (un < nsub) load_sub(txt, nb, (int64_t)un * TW, N);
+    __syncthreads();  // (one wave: the previous sub-tile's LDS reads before this one's writes)
+    parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
+    if (un >= nsub) break;
+    V = N;
+    u = un;
   }
 }
 
@@ -2072,6 +2629,9 @@ struct LoadState {
   uint64_t* tcnt = nullptr;
   uint32_t* absorbed = nullptr;
   int64_t* tgb = nullptr;
+  // BED5: scores for k_score_big, (row, first byte) pairs
+  uint64_t* big = nullptr;
+  uint32_t bigcap = 0;
 };
 
 static void release_state(bg_ctx* c, LoadState& S) {
@@ -2080,7 +2640,7 @@ static void release_state(bg_ctx* c, LoadState& S) {
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
                   (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed,
-                  (void*)S.tgb})
+                  (void*)S.tgb, (void*)S.big})
     bg_release(c, p);
   S = LoadState();
 }
@@ -2244,12 +2804,20 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     const char* e = getenv("BEDGPU_ROW_PARSE");
     return !(e && atoi(e) == 0);
   }();
+  // scores past the loader's fast paths (parse_score: isint -1) go to k_score_big (finish_one)
+  if (T->score) {
+    S.bigcap = (uint32_t)std::min<uint64_t>(T->n, 1u << 20);
+    S.big = (uint64_t*)bg_alloc(c, 16ull * (S.bigcap ? S.bigcap : 1));
+    if (!S.big) return BG_E_NOMEM;
+  }
   if (row_n && !c->row_wide)
     BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
-              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
+              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
+              S.big, S.bigcap);
   else
     BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
-              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st);
+              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
+              S.big, S.bigcap);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, st);
@@ -2272,6 +2840,10 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
   static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
     const char* e = getenv("BEDGPU_SET_WS");
     return !(e && atoi(e) == 0);
+  }();
+  static const int set_lean = [] {  // BEDGPU_SET_V=0: k_parse_set_w (round 4); 2: persistent
+    const char* e = getenv("BEDGPU_SET_V");
+    return e ? atoi(e) : 1;
   }();
   const bool wave = set_nt == 64;
   // staging units: 4 KiB sub-tiles (k_parse_set_w) or 8 KiB tiles
@@ -2300,7 +2872,18 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
       !S.tcnt || !S.absorbed || !S.cnt || !S.tgb)
     return BG_E_NOMEM;
   SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  if (wave)
+  if (wave && set_lean == 2) {  // persistent: BEDGPU_SET_GRID waves per CU (256 CUs)
+    static const uint32_t per_cu = [] {
+      const char* e = getenv("BEDGPU_SET_GRID");
+      return e ? (uint32_t)atoi(e) : 24u;
+    }();
+    const uint32_t g = std::min<uint32_t>(nt, 256u * std::max<uint32_t>(per_cu, 1u));
+    BG_LAUNCH(c, "k_parse_set", k_parse_set_p, dim3(g), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st);
+  } else if (wave && set_lean)
+    BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st);
+  else if (wave)
     BG_LAUNCH(c, "k_parse_set", k_parse_set_w, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
               S.lcs, S.lce, TS, st);
   else if (set_nt == 128 && set_ws)
@@ -2342,6 +2925,14 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
   }
   int rc = report_status(c, idx, h);
   if (rc) return rc;
+  if (h.nbig) {  // scores past the fast paths: exact big-number conversion (bg_strtod.h)
+    if (h.nbig > S.bigcap || !T->score)
+      return bg_fail(c, BG_E_UNSUPPORTED, "too many scores needing the exact big-number conversion");
+    BG_LAUNCH(c, "k_score_big", k_score_big, dim3(bg_blocks(h.nbig, 64)), dim3(64), S.txt, S.nb, S.big, h.nbig,
+              T->score);
+    rc = bg_hip_ok(c, hipGetLastError());
+    if (rc) return rc;
+  }
   if ((in.kind == BG_BED5 || in.kind == BG_BED5_REST) && (h.flags & 1ULL)) T->score_int = false;
   T->has_zero_len = (h.flags & 2ULL) != 0;
   T->maxlen = h.maxlen;

@@ -1103,8 +1103,19 @@ __global__ void k_map_printed(const int32_t* __restrict__ cnt, uint64_t n, uint6
   if (i < n) f[i] = cnt[i] > 0 ? 1 : 0;
 }
 
+// force_running: integer scores whose window sums (or sums of squares) reach 2^53, where
+// the reference's running doubles (AverageVisitor.hpp:46-54) round: the same replay of its
+// doubles in event order as decimal scores (map_running_sums), instead of exact int64 sums
+static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts* opts, bg_result** out,
+                    bool force_running);
+
 extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts* opts,
                       bg_result** out) {
+  return map_impl(c, set, ref, map, opts, out, false);
+}
+
+static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts* opts, bg_result** out,
+                    bool force_running) {
   if (!c || !set || !opts || !out || ref < 0 || map < 0 || ref >= (int)set->t.size() ||
       map >= (int)set->t.size() || opts->n_ops <= 0 || opts->n_ops > 16)
     return BG_E_ARG;
@@ -1180,7 +1191,9 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if (need_sum) need |= NEED_SUM;
   if (need_ext) need |= NEED_EXT;
   if (need_sum || need_ext) mapfields = 5;  // score operations read the map as B5Rest
-  if (opts->precision < 0 || opts->precision > 17) return bg_fail(c, BG_E_UNSUPPORTED, "--prec above 17 is not on the GPU path");
+  // any --prec >= 0 (bedmap/src/Input.hpp:133-141): digits past the fast paths' 17 come from
+  // the exact formatter (bg_decfmt.h)
+  if (opts->precision < 0) return bg_fail(c, BG_E_ARG, "--prec must be >= 0");
   const int crit = opts->criterion;
   const bool faster = opts->faster != 0;
   // Input.hpp:349: --faster needs a symmetric criterion the sweep can run with
@@ -1213,7 +1226,7 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
   if ((need & (NEED_SUM | NEED_EXT)) && !M->score)
     return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
   // decimal scores: the running doubles are replayed in event order (map_running_sums)
-  const bool decimal = need_sum && !M->score_int;
+  const bool decimal = need_sum && (!M->score_int || force_running);
   const bool need_sq = (need & NEED_SQ) != 0;
   if (!faster && ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
     return bg_fail(c, BG_E_UNSUPPORTED, "single-file bedmap over zero-length rows is not on the GPU path");
@@ -1465,8 +1478,12 @@ extern "C" int bg_map(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opt
     }
     if (!rc) rc = bg_scan_sum_u64(c, res->rrank, res->rrank, R->n, nullptr);
   }
-  if (!rc && (c->hstat->flags & 4ULL))
-    rc = bg_fail(c, BG_E_UNSUPPORTED, "a window score sum (or sum of squares) reaches 2^53 (inexact in the reference too)");
+  if (!rc && (c->hstat->flags & 4ULL) && !decimal) {
+    // a window sum reached 2^53: the int64 sums are exact where the reference's doubles are
+    // not; redo with the reference's running doubles
+    bg_result_free(res);
+    return map_impl(c, set, ref, map, opts, out, true);
+  }
   if (rc) {
     bg_result_free(res);
     return rc;

@@ -17,6 +17,8 @@ Suites (VERDICT r02 "Next round" item 5):
            (replaces the oracle-generated bedmap_drift.json)
   sortbed  sort-bed ordering incl. long tie runs and rests
   ec       --ec messages of bedops / bedmap / closest-features on malformed inputs
+  faster   bedmap --faster (the sweep's own window) under its four criteria
+  f2       round 5: window sums past 2^53, --prec past 17, huge/tiny values in %lf and %e
 The *-rand element operations are excluded: the reference seeds std::random_shuffle with
 time(NULL) (ExtremeVisitor.hpp:47-72), so it has no single answer.
 """
@@ -382,7 +384,50 @@ def faster():
     s.save()
 
 
+# ------------------------------------------------------------------------------- f2
+def f2():
+    """bedmap inputs the GPU path refused before round 5 (VERDICT r04 "What's missing" 1):
+    integer window sums at and past 2^53 (the reference's running doubles round), --prec past
+    17, "%.{p}lf" of |v| * 10^p >= 2^64, --sci of tiny and huge values"""
+    s = Suite("f2")
+    rng = random.Random(906)
+    ref = randbed.rows(rng, 150, span=2000, maxlen=60)
+    mp = randbed.rows(rng, 600, span=2000, maxlen=80)
+    # integer scores near 2^53 / 10: a window of ~10 rows sums past 2^53; squares past 2^63
+    big = "".join(f"{c}\t{s_}\t{e}\tid{i % 5}\t{rng.choice([0, 1, 3, 7]) * 10 ** 15 + rng.randint(0, 10 ** 15)}\n"
+                  for i, (c, s_, e) in enumerate(mp))
+    g = s.group(randbed.text(ref), big)
+    for prec in (0, 6, 17):
+        s.run("bedmap", ["--count", "--sum", "--mean", "--prec", str(prec)], g)
+        s.run("bedmap", ["--variance", "--stdev", "--cv", "--prec", str(prec)], g)
+    s.run("bedmap", ["--sum", "--sci"], g)
+    s.run("bedmap", ["--sum", "--mean", "--range", "40"], g)
+    # integer scores at 2^53 exactly and around it, negative too
+    edge = "".join(f"{c}\t{s_}\t{e}\tid{i % 3}\t{rng.choice([2 ** 53, 2 ** 53 - 1, 2 ** 52 + 1, -(2 ** 53), 1])}\n"
+                   for i, (c, s_, e) in enumerate(mp))
+    g = s.group(randbed.text(ref), edge)
+    s.run("bedmap", ["--count", "--sum", "--mean", "--variance"], g)
+    # decimal and integer scores at precisions past 17
+    dec = "".join(f"{c}\t{s_}\t{e}\tid{i % 4}\t{rng.choice(['0.1', '2.5', '1e14', '123456.789', '-7', '3'])}\n"
+                  for i, (c, s_, e) in enumerate(mp))
+    g = s.group(randbed.text(ref), dec)
+    for prec in (18, 20, 30, 60):
+        s.run("bedmap", ["--count", "--mean", "--sum", "--prec", str(prec)], g)
+        s.run("bedmap", ["--min", "--max", "--median", "--prec", str(prec)], g)
+        s.run("bedmap", ["--mean", "--sum", "--sci", "--prec", str(prec)], g)
+    s.run("bedmap", ["--echo-map-score", "--prec", "25"], g)
+    # |v| * 10^p >= 2^64 at the default precision; 1e300-scale sums; tiny values under --sci
+    huge = "".join(f"{c}\t{s_}\t{e}\tid{i % 4}\t{rng.choice(['1e14', '4.5e15', '1e300', '-2.5e299', '1e-300', '3e-320', '0.5'])}\n"
+                   for i, (c, s_, e) in enumerate(mp))
+    g = s.group(randbed.text(ref), huge)
+    for args in (["--sum", "--mean"], ["--sum", "--mean", "--sci"], ["--min", "--max", "--sci", "--prec", "3"],
+                 ["--mean", "--prec", "0"], ["--sum", "--prec", "40"], ["--min", "--sci", "--prec", "30"],
+                 ["--variance", "--stdev"]):
+        s.run("bedmap", args, g)
+    s.save()
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec", "faster"]
+    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec", "faster", "f2"]
     for w in which:
         globals()[w]()

@@ -189,3 +189,35 @@ def test_chrom_spans_of_set_results(eng):
             r.free()
     finally:
         s.free()
+
+
+def _outcome(eng, texts, set_load):
+    from bedops_amd import BedgpuError
+    try:
+        return ("ok", eng.bedops("-m", texts, set_load=set_load))
+    except BedgpuError as e:
+        return ("err", e.code, e.msg)
+
+
+@pytest.mark.parametrize("where", ["token", "sep1", "start", "sep2", "end", "after_end"])
+def test_set_load_every_byte(eng, where):
+    """every byte value at each position of one line inside a long sorted file: the set
+    loader's byte classes (whitespace, '\\n', digits; k_parse_set_v's bitop3/dot-product
+    SWAR) must agree with the row loader's, whether the line is accepted or refused"""
+    rs = randbed.rows(random.Random(21), 20000, chroms=["chr1"], span=10**7, maxlen=40)
+    lines = randbed.text(rs).encode().splitlines(keepends=True)
+    k = 9000  # far inside the file: the sub-tile takes the unguarded load path
+    head, tail = b"".join(lines[:k]), b"".join(lines[k + 1:])
+    c, s, e = lines[k].rstrip(b"\n").split(b"\t")
+    for b in range(256):
+        x = bytes([b])
+        if b == 10:
+            continue
+        line = {"token": c[:2] + x + c[2:] + b"\t" + s + b"\t" + e,
+                "sep1": c + x + s + b"\t" + e,
+                "start": c + b"\t" + s[:1] + x + s[1:] + b"\t" + e,
+                "sep2": c + b"\t" + s + x + e,
+                "end": c + b"\t" + s + b"\t" + e[:1] + x + e[1:],
+                "after_end": c + b"\t" + s + b"\t" + e + x + b"rest"}[where]
+        text = head + line + b"\n" + tail
+        assert _outcome(eng, [text], True) == _outcome(eng, [text], False), (where, b)
