@@ -464,11 +464,16 @@ __host__ __device__ __forceinline__ bool bg_map_in(int crit, int64_t ovr, int64_
                                                    int64_t s, int64_t e, int64_t ms, int64_t me) {
   if (crit == BG_OVR_FAST) return true;
   if (crit == BG_OVR_RANGE) return (s < me) ? (e + range > ms) : (me + range > s);
+  // Exact (:300-309) compares coordinates only: a zero-length row matches its equal (it can
+  // be a window member only in one-file mode, where the row itself is in the deque)
+  if (crit == BG_OVR_EXACT) return ms == s && me == e;
+  // perc_ <= DBL_EPSILON: PercentOverlapMapping::Ref2Map is 0 for every pair not strictly
+  // apart (:147-150), rows that only touch or have no length included (each fraction
+  // variant reduces to that test then)
+  if (crit != BG_OVR_BP && perc <= 2.220446049250313e-16) return !(e < ms || me < s);
   const int64_t ov = (e < me ? e : me) - (s > ms ? s : ms);
   if (ov <= 0) return false;
   if (crit == BG_OVR_BP) return ov >= ovr;
-  if (crit == BG_OVR_EXACT) return ms == s && me == e;
-  if (perc <= 2.220446049250313e-16) return true;  // DBL_EPSILON
   // sz of BedDistances.hpp:160-174 is the overlap length for overlapping rows
   const bool fm = (double)ov / (double)(me - ms) >= perc;  // relative to the map row
   const bool fr = (double)ov / (double)(e - s) >= perc;    // relative to the ref row

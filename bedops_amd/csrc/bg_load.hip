@@ -2105,8 +2105,12 @@ __device__ __forceinline__ uint4 ldsu128(const void* p) {
 #ifndef BG_EXP_V
 #define BG_EXP_V 0
 #endif
+// BG_GTXT (default 1): an interior sub-tile is not staged in LDS; its lines' token and
+// numbers are read from the text through the vector memory path (the unaligned LDS reads
+// were the LDS pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave), 3% faster on
+// MI355X; 0 stages every sub-tile (A/B)
 #ifndef BG_GTXT
-#define BG_GTXT 0
+#define BG_GTXT 1
 #endif
 // the value of a number of L (1..9) digits whose last digit is the high byte of D.z (the 12
 // bytes D end at the number's end); ok cleared when one of its bytes is not a digit
@@ -2157,6 +2161,20 @@ __device__ __forceinline__ int64_t find_nl_wave(const uint8_t* __restrict__ txt,
   return -1;
 }
 
+// the sub-tile and its halos lie inside the text (wave-uniform): unguarded loads, and every
+// read of the line bytes may go to the text itself
+__device__ __forceinline__ bool sub_inb(int64_t t0, uint64_t nb) {
+  return t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb;
+}
+// what set_row / set_rounds_w read a sub-tile's lines through: its bytes from offset t0 - HB
+// (the LDS copy, or the text itself for an interior sub-tile under BG_GTXT), whitespace
+// masks and line starts (LDS)
+struct SubView {
+  const uint8_t* buf;
+  const uint32_t* wsm;
+  const uint16_t* lst;
+};
+
 // the sub-tile's bytes as registers: 64 per lane, and 16 of the halos (lanes < HL: after the
 // sub-tile, lane 63: the 16 bytes before it); unguarded when the sub-tile and its halos lie
 // inside the text (wave-uniform), load16 otherwise
@@ -2172,7 +2190,7 @@ __device__ __forceinline__ void load_sub(const uint8_t* __restrict__ txt, uint64
   uint4* const v = R.v;
   uint4& vh = R.vh;
   vh = make_uint4(0, 0, 0, 0);
-  if (t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb) {  // wave-uniform: no guards
+  if (sub_inb(t0, nb)) {  // wave-uniform: no guards
     const uint4* p = reinterpret_cast<const uint4*>(txt + t0) + 4 * lane;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = p[i];
@@ -2196,10 +2214,12 @@ __device__ __forceinline__ uint32_t prologue_v(const uint8_t* __restrict__ txt, 
   const int lane = threadIdx.x;
   const uint4* const v = R.v;
   const uint4 vh = R.vh;
+  if (!sub_inb(t0, nb) || !BG_GTXT) {  // interior sub-tiles are read from the text itself
 #pragma unroll
-  for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
-  if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
-  else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
+    if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
+    else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
+  }
   uint32_t w0, w1, n0, n1, hw, hm;
   classify32(v[0], v[1], w0, n0);
   classify32(v[2], v[3], w1, n1);
@@ -2247,7 +2267,7 @@ __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return (uint32_t)__builti
 // staging); TOK16: the run's token is 9..16 bytes
 template <bool TOK16, bool GTXT>
 __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, const ParseLdsV& S,
-                                             const TileText& T, const RunTable& R,
+                                             const SubView& SV, const TileText& T, const RunTable& R,
                                              uint32_t rl, int64_t t0, uint32_t L, int64_t last_end,
                                              uint64_t base, int64_t* __restrict__ LCS,
                                              int64_t* __restrict__ LCE, uint64_t& nc, uint32_t& carry_e,
@@ -2298,7 +2318,7 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     bool ok = act && e1 <= 31u && qn != 0xFFFFu && (a1 - a0) == tlen && (s1 - s0) <= 9u && (e1 - e0) <= 9u;
     // the line's bytes: LDS, or (GTXT) the text itself through the vector memory path,
     // which the LDS pipe's unaligned reads do not share
-    const uint8_t* lb = GTXT ? txt + (t0 + q) : &S.buf[HB + q];
+    const uint8_t* lb = GTXT ? txt + (t0 + q) : &SV.buf[HB + q];
     {
       uint32_t dif;
       if (TOK16) {
@@ -2319,7 +2339,7 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     bool valid = ok;
     if (act && !ok) {  // the full grammar (and its errors), this lane only
       int64_t ks = 0, ke = 0;
-      valid = set_row<true, true>(S, S.lst, T, R, rl, rl, t0, k, L, last_end, ks, ke, st);
+      valid = set_row<true, true>(SV, S.lst, T, R, rl, rl, t0, k, L, last_end, ks, ke, st);
       start = (uint32_t)(ks & BG_COORD_MASK);
       end = (uint32_t)(ke & BG_COORD_MASK);
       if (valid && (uint64_t)(ke & BG_COORD_MASK) + 1 >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
@@ -2374,7 +2394,9 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
     return;
   }
   const uint32_t rl = runlo[u], rh = runhi[u];
-  const TileText T{txt, S.buf, t0 - HB, t0 + TW + HA_V, nb};
+  const bool direct = BG_GTXT && sub_inb(t0, nb);  // line bytes from the text (not staged)
+  const SubView SV{direct ? txt + (t0 - HB) : S.buf, S.wsm, S.lst};
+  const TileText T{txt, SV.buf, t0 - HB, t0 + TW + HA_V, nb};
   uint64_t nc = 0, cmax = 0, kmax = 0;
   int64_t gbase = 0;
 #if BG_EXP_V == 1
@@ -2386,19 +2408,19 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
     uint32_t ce = 0, kl = 0;
     const bool tok16 = R.info[rl].tlen > 8;
 #if BG_GTXT
-    if (t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb) {  // every read inside the text
-      if (tok16) set_rounds_v<true, true>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
-      else set_rounds_v<false, true>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+    if (direct) {  // every read inside the text
+      if (tok16) set_rounds_v<true, true>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      else set_rounds_v<false, true>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
     } else
 #endif
     if (tok16)
-      set_rounds_v<true, false>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      set_rounds_v<true, false>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
     else
-      set_rounds_v<false, false>(txt, S, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      set_rounds_v<false, false>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
     cmax = ce;
     kmax = kl;
   } else {
-    set_rounds_w<uint64_t, ParseLdsV>(S, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, nc, cmax, kmax, st);
+    set_rounds_w<uint64_t, SubView>(SV, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, nc, cmax, kmax, st);
   }
   if (threadIdx.x == 0) {
     if (nc > SCAP_W) {
@@ -2419,14 +2441,28 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
 }
 
 // one wave per sub-tile
+// pfd > 0: after its own loads, the wave touches every 128-byte line of sub-tile u + pfd
+// (one dword per line, 35 lanes), which a wave starting about one wave lifetime later
+// will parse: its loads then hit L2 / the Infinity Cache instead of waiting out HBM latency
+// (SQ: 2830 of a wave's 5465 quad-cycles were waits, 2029 of them before the first byte in
+// a loads-only variant). The touched dwords are consumed (pf_sink, null at run time) so the
+// loads are real; they are waited for only at the end, long after they landed.
 __global__ void __launch_bounds__(64) k_parse_set_v(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
-    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
+    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st, uint32_t pfd,
+    uint32_t* __restrict__ pf_sink) {
   __shared__ ParseLdsV S;
   SubRegs V;
   load_sub(txt, nb, (int64_t)blockIdx.x * TW, V);
+  uint32_t pf = 0;
+  if (pfd) {
+    const uint64_t a = ((uint64_t)blockIdx.x + pfd) * TW + 128u * threadIdx.x;
+    if (threadIdx.x < (TW + HA_V + 32 + 127) / 128 && a + 4 <= nb)
+      pf = *reinterpret_cast<const uint32_t*>(txt + a);
+  }
   parse_sub_v(txt, nb, blockIdx.x, V, S, runlo, runhi, R, LCS, LCE, TS, st);
+  if (pf_sink) pf_sink[threadIdx.x] = pf;
 }
 
 // persistent waves (grid-strided over the sub-tiles): the next sub-tile's bytes are loaded
@@ -2880,9 +2916,14 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
     const uint32_t g = std::min<uint32_t>(nt, 256u * std::max<uint32_t>(per_cu, 1u));
     BG_LAUNCH(c, "k_parse_set", k_parse_set_p, dim3(g), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
               S.lcs, S.lce, TS, st);
-  } else if (wave && set_lean)
+  } else if (wave && set_lean) {
+    static const uint32_t pfd = [] {  // BEDGPU_SET_PF: prefetch distance in sub-tiles (0: off)
+      const char* e = getenv("BEDGPU_SET_PF");
+      return e ? (uint32_t)atoi(e) : 0u;
+    }();
     BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st);
+              S.lcs, S.lce, TS, st, pfd, (uint32_t*)nullptr);
+  }
   else if (wave)
     BG_LAUNCH(c, "k_parse_set", k_parse_set_w, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
               S.lcs, S.lce, TS, st);

@@ -68,6 +68,7 @@ struct MapArgs {
   LongRows lrows;      // rows longer than L by length class (bg_map_cands); L = its threshold
   const int64_t* zin;  // zero-length rows: window membership (bg_map_live), else null
   const int64_t* zout;
+  int64_t touch;       // 1: rows that only touch the reference row can be in S(r) (tiny fractions)
   bg_dstatus* st;
 };
 
@@ -112,8 +113,10 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   const int64_t s = live ? A.RS[r] : 0, e = live ? A.RE[r] : 0;
   const int64_t g = s & ~BG_COORD_MASK;  // the row's chromosome in key space
   const int64_t pad = (CRIT == BG_OVR_RANGE) ? A.range : 0;
-  const int64_t klo = max(g, s - pad - A.L + 1);                   // non-decreasing in r
-  const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad);
+  const int64_t klo = max(g, s - pad - A.L + 1 - A.touch);          // non-decreasing in r
+  // (--exact: a zero-length row matches rows starting at its end, itself in one-file mode;
+  // tiny fractions: rows touching either end)
+  const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad + (CRIT == BG_OVR_EXACT ? 1 : A.touch));
   uint64_t blo = 0, bhi = 0;
   if (!FAST) {
     const int64_t hm = wmax64(live ? khi : LLONG_MIN);
@@ -309,6 +312,77 @@ __global__ void k_mz_member(const int64_t* __restrict__ RS, const int64_t* __res
   zout[m] = k < nzr ? (int64_t)zr[k] : (int64_t)nr;
 }
 
+// One file (sweep overload 1, WindowSweepImpl.specialize.cpp:40-138, run with Overlapping(0)
+// under every criterion but --range, Bedmap.cpp:108-152): the deque after row i's pops and
+// reads is [f_i, p_i) (every row joins it), the --faster replay's own chains with the sweep
+// distance Overlapping(0) (bg_faster_windows); f and p never decrease, so row m is a member
+// for the rows i with f_i <= m < p_i: mz_in = the first i with p_i > m, mz_out = the first
+// i with f_i > m. BedBaseVisitor then re-tests each member with the criterion (fixWindow,
+// BedBaseVisitor.hpp:184-215), as k_map_ops does for bg_map_live members.
+__global__ void k_mz_single(const uint64_t* __restrict__ f, const uint64_t* __restrict__ p, uint64_t n,
+                            int64_t* __restrict__ zin, int64_t* __restrict__ zout) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  zin[m] = (int64_t)upper_bound_i64((const int64_t*)p, n, (int64_t)m);
+  zout[m] = (int64_t)upper_bound_i64((const int64_t*)f, n, (int64_t)m);
+}
+static int map_zero_prep_single(bg_ctx* c, const bg_table* R, bg_result* res) {
+  const uint64_t n = R->n;
+  if (!n) return 0;
+  res->zin = (int64_t*)bg_alloc(c, 8 * n);
+  res->zout = (int64_t*)bg_alloc(c, 8 * n);
+  uint64_t* f = (uint64_t*)bg_alloc(c, 8 * n);
+  uint64_t* p = (uint64_t*)bg_alloc(c, 8 * n);
+  int64_t* j0 = (int64_t*)bg_alloc(c, 8 * n);
+  int64_t* j1 = (int64_t*)bg_alloc(c, 8 * n);
+  int rc = (!res->zin || !res->zout || !f || !p || !j0 || !j1) ? BG_E_NOMEM : 0;
+  if (!rc) rc = bg_faster_windows(c, R, R, BG_OVR_BP, 0, 0, 1.0, true, f, p, j0, j1);
+  if (!rc) {
+    BG_LAUNCH(c, "k_mz_single", k_mz_single, dim3(bg_blocks(n, BG_NT)), dim3(BG_NT), f, p, n, res->zin, res->zout);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  bg_release(c, f);
+  bg_release(c, p);
+  bg_release(c, j0);
+  bg_release(c, j1);
+  return rc;
+}
+
+// Two files under a tiny fraction (perc_ <= DBL_EPSILON): S(r) takes every deque member
+// not strictly apart from r, so the windows are the sweep's deque (overload 2 under
+// Overlapping(0), Bedmap.cpp:108-138): [f_i, p_i) over the rows that joined it, from the
+// --faster replay's chains; a joined row m is a member for i in [first p_i > m, first f_i > m)
+__global__ void k_mz_deque(const uint64_t* __restrict__ f, const uint64_t* __restrict__ p, uint64_t nr,
+                           const int64_t* __restrict__ joined, uint64_t nm, int64_t* __restrict__ zin,
+                           int64_t* __restrict__ zout) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  zin[m] = joined[m] == INT64_MAX ? INT64_MAX : (int64_t)upper_bound_i64((const int64_t*)p, nr, (int64_t)m);
+  zout[m] = (int64_t)upper_bound_i64((const int64_t*)f, nr, (int64_t)m);
+}
+static int map_deque_prep(bg_ctx* c, const bg_table* R, const bg_table* M, bg_result* res) {
+  const uint64_t nr = R->n, nm = M->n;
+  if (!nr || !nm) return 0;
+  res->zin = (int64_t*)bg_alloc(c, 8 * nm);
+  res->zout = (int64_t*)bg_alloc(c, 8 * nm);
+  uint64_t* f = (uint64_t*)bg_alloc(c, 8 * nr);
+  uint64_t* p = (uint64_t*)bg_alloc(c, 8 * nr);
+  int64_t* j0 = (int64_t*)bg_alloc(c, 8 * nm);
+  int64_t* j1 = (int64_t*)bg_alloc(c, 8 * nm);
+  int rc = (!res->zin || !res->zout || !f || !p || !j0 || !j1) ? BG_E_NOMEM : 0;
+  if (!rc) rc = bg_faster_windows(c, R, M, BG_OVR_BP, 0, 0, 1.0, false, f, p, j0, j1);
+  if (!rc) {
+    BG_LAUNCH(c, "k_mz_deque", k_mz_deque, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), f, p, nr, j0, nm, res->zin,
+              res->zout);
+    rc = bg_hip_ok(c, hipGetLastError());
+  }
+  bg_release(c, f);
+  bg_release(c, p);
+  bg_release(c, j0);
+  bg_release(c, j1);
+  return rc;
+}
+
 static int map_zero_prep(bg_ctx* c, const bg_table* R, const bg_table* M, bg_result* res) {
   const uint64_t nr = R->n, nm = M->n;
   if (!nr || !nm) return 0;
@@ -385,7 +459,15 @@ struct EvArgs {
   const ulonglong2* P;  // first 16 bytes of each row's full_rest(), big-endian, 0-padded (k_ev_keys)
   const uint32_t* PL;   // full_rest() length
   const int64_t* zin;   // --faster: rows that joined the deque (zin != INT64_MAX), else null
+  // zero-length rows (not --faster): map row m is a sweep-window member of the reference rows
+  // [mz_in[m], mz_out[m]) only (k_mz_member, k_mz_single), else null
+  const int64_t* mz_in;
+  const int64_t* mz_out;
+  bool mz_exact;  // the membership is the deque itself (one file; tiny fractions): pops = leaving it
 };
+__device__ __forceinline__ bool ev_live(const EvArgs& A, uint64_t r, uint64_t m) {
+  return bg_map_live(A.mz_in, A.mz_out, r, m);
+}
 
 __device__ __forceinline__ int ev_rest_cmp(const EvArgs& A, uint64_t a, uint64_t b) {
   return bg_frest_cmp(A.text, A.rest_off, A.rest_len, A.mapfields, a, b);
@@ -561,15 +643,21 @@ __device__ __forceinline__ void ev_events(const EvArgs& A, uint64_t i, bool dels
   const uint64_t plo = hp ? A.wlo[i - 1] : 0, phi = hp ? A.whi[i - 1] : 0;
   uint64_t f = lo;  // first candidate of r_i that the sweep cannot pop
   while (f < hi && A.ME[f] + R <= s) ++f;
+  // S(r) = the sweep-window members (every candidate, or the zero-length replay's [mz_in,
+  // mz_out)) that meet the criterion; the sweep itself deletes the rows it pops at r_i and,
+  // with zero-length rows, every member whose window membership ends at r_i (a zero-length
+  // reference row's pops, WindowSweepImpl.cpp:207-211; one file, a restart :132-136)
   auto in_prev = [&](uint64_t m) {
-    return hp && m >= plo && m < phi && bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m]);
+    return hp && m >= plo && m < phi && ev_live(A, i - 1, m) &&
+           bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m]);
   };
   auto in_cur = [&](uint64_t m) {
-    return (A.MS[m] & ~BG_COORD_MASK) == g &&
+    return (A.MS[m] & ~BG_COORD_MASK) == g && ev_live(A, i, m) &&
            bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]);
   };
   auto popped = [&](uint64_t m) {
-    return m < f && ((A.ME[m] & ~BG_COORD_MASK) != g || A.ME[m] + R <= s);
+    if (A.mz_exact) return !ev_live(A, i, m);
+    return (m < f && ((A.ME[m] & ~BG_COORD_MASK) != g || A.ME[m] + R <= s)) || (A.mz_in && !ev_live(A, i, m));
   };
   if (hp && dels) {
     for (uint64_t m = plo; m < phi; ++m)  // (a) in deque (file) order
@@ -807,6 +895,7 @@ __global__ void k_tm_seg(EvArgs A, uint64_t* __restrict__ flag) {
     if ((ps & ~BG_COORD_MASK) == g)
       for (uint64_t m = lo; m < hi; ++m)
         if ((A.MS[m] & ~BG_COORD_MASK) == g && (CRIT != BG_OVR_FAST || A.zin[m] != INT64_MAX) &&
+            (CRIT == BG_OVR_FAST || (ev_live(A, i, m) && ev_live(A, i - 1, m))) &&
             bg_map_in(CRIT, A.ovr, A.range, A.perc, s, e, A.MS[m], A.ME[m]) &&
             bg_map_in(CRIT, A.ovr, A.range, A.perc, ps, pe, A.MS[m], A.ME[m])) {
         st = 0;
@@ -1215,10 +1304,8 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
       perc -= DBL_EPSILON;
       if (perc <= 0.0) perc = DBL_EPSILON;
       // at perc_ <= DBL_EPSILON Ref2Map is 0 for any pair not strictly apart (:147-150): rows
-      // that only touch the reference row, or have no length, join its window when the sweep's
-      // deque still holds them, which the window kernels (overlap > 0) do not model
-      if (perc <= DBL_EPSILON && !faster)
-        return bg_fail(c, BG_E_UNSUPPORTED, "--fraction-* values below 4.5e-16 are not on the GPU path");
+      // that only touch the reference row, or have no length, are in S(r) while the sweep's
+      // deque still holds them: the windows are then the deque itself (map_deque_prep)
       break;
     case BG_OVR_EXACT: break;
     default: return BG_E_ARG;
@@ -1227,18 +1314,11 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
     return bg_fail(c, BG_E_ARG, "score operations need the map file loaded as BG_BED5");
   // decimal scores: the running doubles are replayed in event order (map_running_sums)
   const bool decimal = need_sum && (!M->score_int || force_running);
+  const bool tiny = !faster && crit >= BG_OVR_FRAC_REF && crit <= BG_OVR_FRAC_BOTH && perc <= DBL_EPSILON;
   const bool need_sq = (need & NEED_SQ) != 0;
-  if (!faster && ref == map && crit != BG_OVR_RANGE && R->has_zero_len)
-    return bg_fail(c, BG_E_UNSUPPORTED, "single-file bedmap over zero-length rows is not on the GPU path");
   if (decimal && opts->shard)
     return bg_fail(c, BG_E_UNSUPPORTED, "decimal-score running sums span every chromosome: not on a chromosome shard");
-  if (tmean && !faster) {
-    if (R->has_zero_len || M->has_zero_len)
-      return bg_fail(c, BG_E_UNSUPPORTED, "--tmean with zero-length rows is not on the GPU path of bedmap");
-  }
   if (decimal) {
-    if (!faster && (R->has_zero_len || M->has_zero_len))
-      return bg_fail(c, BG_E_UNSUPPORTED, "non-integer map scores with zero-length rows are not on the GPU path of bedmap --mean/--sum/--variance/--stdev/--cv");
     if (!M->rest_off)
       return bg_fail(c, BG_E_ARG, "non-integer scores under --mean/--sum/--variance/--stdev/--cv need the map file loaded as BG_BED5_REST (equal rows are ordered by id and remainder)");
     need &= ~(NEED_SUM | NEED_SQ);
@@ -1300,8 +1380,8 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
       bg_result_free(res);
       return rf;
     }
-  } else if (crit != BG_OVR_RANGE && (R->has_zero_len || M->has_zero_len)) {
-    int rz = map_zero_prep(c, R, M, res);
+  } else if (tiny || (crit != BG_OVR_RANGE && (R->has_zero_len || M->has_zero_len))) {
+    int rz = ref == map ? map_zero_prep_single(c, R, res) : tiny ? map_deque_prep(c, R, M, res) : map_zero_prep(c, R, M, res);
     if (rz) {
       bg_result_free(res);
       return rz;
@@ -1331,6 +1411,7 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
   }
   A.ovr = (int64_t)opts->overlap_bp;
   A.range = (int64_t)opts->range_bp;
+  A.touch = tiny ? 1 : 0;
   A.perc = perc;
   A.need = need;
   A.cnt = res->cnt;
@@ -1431,6 +1512,9 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
     E.P = nullptr;
     E.PL = nullptr;
     E.zin = faster ? res->zin : nullptr;
+    E.mz_in = faster ? nullptr : res->zin;  // the zero-length replay's windows (else null)
+    E.mz_out = faster ? nullptr : res->zout;
+    E.mz_exact = !faster && res->zin && (ref == map || tiny);
     uint32_t* ro = nullptr;
     ulonglong2* pk = nullptr;
     uint32_t* pl = nullptr;

@@ -424,6 +424,45 @@ def f2():
                  ["--mean", "--prec", "0"], ["--sum", "--prec", "40"], ["--min", "--sci", "--prec", "30"],
                  ["--variance", "--stdev"]):
         s.run("bedmap", args, g)
+    # zero-length rows: single-file mode (sweep overload 1 under Overlapping(0) + fixWindow),
+    # and decimal running sums / --tmean over zero-length rows in either mode
+    crits = [[], ["--bp-ovr", "3"], ["--fraction-map", "0.5"], ["--fraction-both", "0.3"], ["--exact"],
+             ["--fraction-either", "0.6"]]
+    for trial in range(3):
+        rng = random.Random(zlib.crc32(repr(("f2-zero", trial)).encode()))
+        rows = randbed.rows(rng, 400, span=rng.choice([400, 1500]), maxlen=rng.choice([20, 60]),
+                            zero_frac=rng.choice([0.1, 0.3]))
+        ints = _int_map(rng, rows)
+        decs = _decimal_map(rng, rows)
+        gi, gd = s.group(ints), s.group(decs)
+        for copt in crits:
+            s.run("bedmap", ["--count", "--sum", "--mean", "--max", "--echo-map-id", "--bases"] + copt, gi)
+            s.run("bedmap", ["--echo", "--echo-map", "--indicator", "--median"] + copt, gi)
+            s.run("bedmap", ["--count", "--mean", "--sum", "--variance", "--prec", "9"] + copt, gd)
+            s.run("bedmap", [["--tmean", "0.1", "0.2"][0], "0.1", "0.2", "--wmean", "--count"] + copt, gd)
+        ref = randbed.rows(rng, 200, span=rng.choice([400, 1500]), maxlen=40, zero_frac=0.2)
+        g2 = s.group(randbed.text(ref), decs)
+        for copt in crits:
+            s.run("bedmap", ["--count", "--mean", "--sum", "--stdev", "--prec", "12"] + copt, g2)
+            s.run("bedmap", ["--tmean", "0", "0.25", "--count"] + copt, g2)
+    # --fraction-* at or below 2 * DBL_EPSILON: every deque member not strictly apart from the
+    # reference row (touching rows, zero-length rows) is in S(r); 5e-16 is just above
+    for trial in range(2):
+        rng = random.Random(zlib.crc32(repr(("f2-tiny", trial)).encode()))
+        rows = randbed.rows(rng, 300, span=600, maxlen=30, zero_frac=0.15 * trial)
+        # adjacent rows: some rows start exactly where others end
+        rows = _srt(rows + [(c, e, e + rng.randint(0, 10)) for c, s_, e in rows[::4]])
+        mp = randbed.rows(rng, 400, span=600, maxlen=40, zero_frac=0.1)
+        mp = _srt(mp + [(c, e, e + 3) for c, s_, e in rows[::5]])
+        gt = s.group(randbed.text(rows), _int_map(rng, mp))
+        gd = s.group(randbed.text(rows), _decimal_map(rng, mp))
+        g1 = s.group(_int_map(rng, rows))
+        for frac in ("0.0000000000000001", "0.0000000000000002", "0.0000000000000004", "0.0000000000000005"):
+            for kind in ("fraction-map", "fraction-ref", "fraction-either", "fraction-both"):
+                s.run("bedmap", ["--count", "--sum", "--echo-map-id", "--bases", f"--{kind}", frac], gt)
+                s.run("bedmap", ["--count", "--echo-map", f"--{kind}", frac], g1)
+            s.run("bedmap", ["--count", "--mean", "--prec", "10", "--fraction-map", frac], gd)
+            s.run("bedmap", ["--tmean", "0.1", "0.1", "--fraction-both", frac], gd)
     s.save()
 
 

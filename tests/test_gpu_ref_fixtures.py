@@ -26,7 +26,7 @@ OUTSIDE_CONTRACT = {("closest", 90), ("closest", 91), ("closest", 92),  # unsort
 KNOWN = {("bedmap", 160)}
 
 CHUNK = 40
-_SIZES = {"closest": 96, "bedmap": 313, "decimal": 124, "sortbed": 6, "ec": 112, "faster": 181, "f2": 29}
+_SIZES = {"closest": 96, "bedmap": 313, "decimal": 124, "sortbed": 6, "ec": 112, "faster": 181, "f2": 217}
 PARAMS = [(s, i) for s, n in _SIZES.items() for i in range(0, n, CHUNK)]
 
 
