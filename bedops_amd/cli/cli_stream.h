@@ -183,7 +183,8 @@ static int stream_prepare(int nf, const char* const* paths) {
   return 1;
 }
 
-/* Read-ahead (BEDGPU_STREAM_AHEAD groups, default 2; 0 = copies in line): a copier thread
+/* Read-ahead (BEDGPU_STREAM_AHEAD groups, default 0 = copies in line; off by default: on the
+ * 16-CPU box it saved ~30 ms of copies and cost as much in kernel and writer time): a copier thread
  * issues group g's page-cache -> HBM copies (bg_file_image_copy, the context's prefetch
  * stream) while the main thread loads, runs and formats earlier groups on ctx's stream, so
  * the DMA engine never waits for a group's host round trips. The main thread allocates every

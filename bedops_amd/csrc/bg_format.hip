@@ -25,6 +25,8 @@
 
 struct FmtArgs {
   int kind;
+  bg_dstatus* st;   // the write pass's checks (BG_FMT_MISMATCH)
+  uint64_t total;   // bytes of the whole text (the write pass's bound)
   // intervals / rows
   const int64_t* s;
   const int64_t* e;
@@ -374,6 +376,22 @@ __device__ __forceinline__ void put_coord(LdsOut& o, uint64_t v, int len) {
   }
 }
 __device__ __forceinline__ void put_coord(CountOut& o, uint64_t, int len) { o.adv(len); }
+// a row rendered straight to HBM (oversized tiles): writes stop at the row's counted end, so
+// a row that renders longer than the count pass measured (its inputs changed in between)
+// cannot write past its slot or the text buffer; the mismatch is reported (BG_FMT_MISMATCH)
+struct BoundOut {
+  char* p;
+  char* lim;
+  __device__ __forceinline__ void put_at(int k, char c) {
+    if (p + k < lim) p[k] = c;
+  }
+  __device__ __forceinline__ void adv(int k) { p += k; }
+  __device__ __forceinline__ void put(char c) {
+    if (p < lim) *p = c;
+    ++p;
+  }
+};
+__device__ __forceinline__ void put_coord(BoundOut& o, uint64_t v, int len) { put_u64(o, v, len); }
 
 template <typename Out>
 __device__ __forceinline__ void put_i64(Out& o, int64_t v) {
@@ -984,12 +1002,18 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
     if (KIND == RES_MAP && row == A.stop_row) *A.stop_out = toff[blockIdx.x] + my[k] + co.n;
   }
   const uint64_t dst0 = toff[blockIdx.x];
+  bool mismatch = false;  // a row rendered to another length than it was placed with
   if (tot > FT_LDS) {  // oversized tile (long names / rests): render straight to HBM
     for (int k = 0; k < FT_ROWS; ++k) {
       const uint64_t row = base + (uint64_t)k * BG_NT;
-      LdsOut o{out + dst0 + my[k]};
-      if (row < A.n) render<KIND>(A, row, o);
+      if (row >= A.n) continue;
+      const uint64_t len = A.rowlen ? A.rowlen[row] : 0;
+      char* const p0 = out + dst0 + my[k];
+      BoundOut o{p0, A.rowlen ? p0 + len : out + A.total};
+      render<KIND>(A, row, o);
+      mismatch |= A.rowlen && (uint64_t)(o.p - p0) != len;
     }
+    if (mismatch && A.st) atomicOr(&A.st->flags, BG_FMT_MISMATCH);
     return;
   }
   // stage with the same alignment mod 16 as the destination, so every aligned 16-byte
@@ -998,8 +1022,12 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     LdsOut o{buf + skew + my[k]};
-    if (row < A.n) render<KIND>(A, row, o);
+    if (row < A.n) {
+      render<KIND>(A, row, o);
+      mismatch |= A.rowlen && (uint64_t)(o.p - (buf + skew + my[k])) != A.rowlen[row];
+    }
   }
+  if (mismatch && A.st) atomicOr(&A.st->flags, BG_FMT_MISMATCH);
   __syncthreads();
   // stream buf[skew, skew + tot) -> out[dst0, dst0 + tot)
   const uint64_t a0 = dst0, a1 = dst0 + tot;
@@ -1374,6 +1402,9 @@ count_again:
     return bg_fail(c, BG_E_UNSUPPORTED, "a value is outside the GPU formatter's range");
   r->text = (char*)bg_alloc(c, total + 16);
   if (!r->text) return BG_E_NOMEM;
+  A.st = c->dstat;
+  A.total = total;
+  if (A.rowlen) BG_HIP(c, hipMemsetAsync(&c->dstat->flags, 0, 8, c->stream));
   uint64_t* d_stop = nullptr;
   if (c->hstat->stop_row != ~0ULL) {  // the text ends inside this row (k_fmt_write finds where)
     A.stop_row = c->hstat->stop_row;
@@ -1393,6 +1424,12 @@ count_again:
       default: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_CLOSEST>, dim3(nb), dim3(BG_NT), A, tb, r->text);
     }
     BG_HIP(c, hipGetLastError());
+    if (A.rowlen) {  // rows placed by the count pass's lengths must render to exactly those
+      uint64_t fl = 0;
+      if ((rc = bg_fetch_u64(c, (const uint64_t*)&c->dstat->flags, &fl))) return rc;
+      if (fl & BG_FMT_MISMATCH)
+        return bg_fail(c, BG_E_INTERNAL, "formatter: a row rendered to another length than counted (its inputs changed between the passes)");
+    }
   }
   r->toff = tb;
   bg_release(c, d_tot);

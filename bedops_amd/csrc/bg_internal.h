@@ -54,6 +54,10 @@ struct LongRows {
   int64_t thr;
 };
 
+// bg_dstatus.flags bit: a formatter row rendered to another length than its count pass
+// measured (its inputs changed between the passes); the result is refused, not written
+#define BG_FMT_MISMATCH 64ULL
+
 enum { ERR_PARSE = 1, ERR_CHROM = 2, ERR_RANGE = 3, ERR_UNSORTED = 4, ERR_BLANK = 5, ERR_SCORE = 6 };
 
 // ---------------------------------------------------------------------------------

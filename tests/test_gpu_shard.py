@@ -97,15 +97,52 @@ def test_cli_sharded_stdin_and_missing_devices_fall_back(gpu_bin, oracle_bin, tm
     assert got.returncode == 0 and got.stdout == wantm, got.stderr
 
 
-def test_engine_group_gather_equals_single_run(oracle_bin):
-    """bench.py's multi-rank step on one GPU: each member loads only its chromosomes,
-    intersects, formats; Group.gather reassembles on member 0"""
-    from bedops_amd.engine import BED3_SET, Group
+# bench.py's workloads (WORKLOADS / run_op): input kinds and the step's operation
+BENCH_STEPS = {
+    "intersect": ([3, 3], lambda eng, s: eng.op("-i", s, [0, 1])),
+    "element-of": ([1, 3], lambda eng, s: eng.op("-e", s, [0, 1], "1")),
+    "bedmap": ([0, 2], lambda eng, s: eng.map_op(s, ["count", "mean"], 0, 1)),
+    "closest": ([1, 1], lambda eng, s: eng.closest_op(s, 0, 1, shortest=True)),
+}
+
+
+def _bench_texts(rng, workload):
+    a = randbed.rows(rng, 3000, chroms=CHROMS, span=20000, maxlen=90)
+    b = randbed.rows(rng, 6000 if workload != "closest" else 12000, chroms=CHROMS, span=20000, maxlen=90)
+    if workload == "bedmap":  # BED5 map rows, integer scores (configs[2])
+        mt = "".join(f"{c}\t{st}\t{e}\tid{i}\t{rng.randint(0, 999)}\n" for i, (c, st, e) in enumerate(b))
+        return [randbed.text(a).encode(), mt.encode()]
+    return [randbed.text(a).encode(), randbed.text(b).encode()]
+
+
+def _step_text(eng, workload, texts):
+    kinds, op = BENCH_STEPS[workload]
+    s = eng.load([(t, k) for t, k in zip(texts, kinds)])
+    r = op(eng, s)
+    r.format()
+    return s, r
+
+
+@pytest.mark.parametrize("workload", sorted(BENCH_STEPS))
+def test_engine_group_gather_equals_single_run(workload):
+    """bench.py's multi-rank step on one GPU, for every workload it times: each member loads
+    only its chromosomes (LPT owner), runs the workload's operation, formats in HBM;
+    Group.gather reassembles on member 0 (member_spans in strcmp order) — byte-identical to the
+    one-engine run of the same step (which the reference-fixture and full-size tests pin)"""
+    from bedops_amd import Engine
+    from bedops_amd.engine import Group
     from bedops_amd.shard import assign, member_spans, strcmp_order
 
-    rng = random.Random(5)
-    texts = [randbed.text(randbed.rows(rng, 4000, chroms=CHROMS, span=20000, maxlen=90)).encode()
-             for _ in range(2)]
+    rng = random.Random(zlib.crc32(workload.encode()))
+    texts = _bench_texts(rng, workload)
+    e1 = Engine(0)
+    try:
+        s1, r1 = _step_text(e1, workload, texts)
+        want = r1.text()
+        r1.free()
+        s1.free()
+    finally:
+        e1.close()
     weights = {}
     for t in texts:
         for ln in t.splitlines(keepends=True):
@@ -120,9 +157,7 @@ def test_engine_group_gather_equals_single_run(oracle_bin):
             for m, eng in enumerate(g.engines):
                 shard = [b"".join(ln for ln in t.splitlines(keepends=True)
                                   if owner[ln.split(b"\t", 1)[0].decode()] == m) for t in texts]
-                s = eng.load([(x, BED3_SET) for x in shard])
-                r = eng.op("-i", s, [0, 1])
-                r.format()
+                s, r = _step_text(eng, workload, shard)
                 dptr, _ = r.device_text()
                 names = s.chroms()
                 offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
@@ -139,15 +174,55 @@ def test_engine_group_gather_equals_single_run(oracle_bin):
                 s.free()
         finally:
             g.close()
-        with tempfile.TemporaryDirectory() as td:
-            paths = []
-            for i, t in enumerate(texts):
-                p = os.path.join(td, f"{i}.bed")
-                open(p, "wb").write(t)
-                paths.append(p)
-            want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE,
-                                  check=True).stdout
-        assert got == want, world
+        assert got == want, (workload, world)
+
+
+def test_engine_group_intersect_matches_oracle(oracle_bin):
+    """the gathered intersect (bench.py's headline step) against the oracle itself"""
+    from bedops_amd.engine import Group
+    from bedops_amd.shard import assign, member_spans, strcmp_order
+
+    rng = random.Random(5)
+    texts = [randbed.text(randbed.rows(rng, 4000, chroms=CHROMS, span=20000, maxlen=90)).encode()
+             for _ in range(2)]
+    weights = {}
+    for t in texts:
+        for ln in t.splitlines(keepends=True):
+            c = ln.split(b"\t", 1)[0].decode()
+            weights[c] = weights.get(c, 0) + len(ln)
+    gnames = strcmp_order(weights)
+    owner, _ = assign(weights, 3)
+    g = Group(devices=[0] * 3)
+    try:
+        parts, keep = [], []
+        for m, eng in enumerate(g.engines):
+            shard = [b"".join(ln for ln in t.splitlines(keepends=True)
+                              if owner[ln.split(b"\t", 1)[0].decode()] == m) for t in texts]
+            s, r = _step_text(eng, "intersect", shard)
+            dptr, _ = r.device_text()
+            names = s.chroms()
+            offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
+            parts.append((dptr, offs, lens))
+            keep.append((s, r))
+        out, n = g.gather(len(gnames), parts)
+        with tempfile.TemporaryFile() as fo:
+            g.engines[0].write_device(out, n, fo.fileno())
+            fo.seek(0)
+            got = fo.read()
+        g.engines[0].device_free(out)
+        for s, r in keep:
+            r.free()
+            s.free()
+    finally:
+        g.close()
+    with tempfile.TemporaryDirectory() as td:
+        paths = []
+        for i, t in enumerate(texts):
+            p = os.path.join(td, f"{i}.bed")
+            open(p, "wb").write(t)
+            paths.append(p)
+        want = subprocess.run([oracle_bin["bedops"], "-i", *paths], stdout=subprocess.PIPE, check=True).stdout
+    assert got == want
 
 
 MAP_CASES = [

@@ -82,6 +82,32 @@ def test_groups_read_ahead_equal_oracle(gpu_bin, oracle_bin, tmp_path, ahead):
         os.environ.pop("BEDGPU_STREAM_AHEAD", None)
 
 
+@pytest.mark.parametrize("ops", [["--bp-ovr", "5", "--median", "--indicator"],
+                                 ["--fraction-ref", "0.5", "--mean", "--echo-map-range"],
+                                 ["--range", "20", "--count", "--min-element", "--skip-unmapped"]])
+def test_bedmap_groups_read_ahead_equal_oracle(gpu_bin, oracle_bin, tmp_path, ops):
+    """the bedmap cases that faulted under read-ahead in round 4 (test_bedmap_groups_equal_oracle
+    ops2..ops4 with BEDGPU_STREAM_AHEAD on): a group's text is copied on the prefetch stream
+    after the previous group's kernels released its blocks (bg_copy_order), and the formatter's
+    write pass checks every row against its count (BG_FMT_MISMATCH) instead of trusting it"""
+    rng = random.Random(zlib.crc32(repr(("ahead", ops)).encode()))
+    ref = randbed.write(str(tmp_path / "r.bed"),
+                        randbed.text(randbed.rows(rng, 3000, chroms=CHROMS, span=8000), rest="cols", rng=rng))
+    mp = randbed.write(str(tmp_path / "m.bed"),
+                       _scored(rng, randbed.rows(rng, 6000, chroms=CHROMS[:7], span=8000)))
+    for ahead in (1, 2, 5):
+        os.environ["BEDGPU_STREAM_AHEAD"] = str(ahead)
+        try:
+            for args in (ops + [ref, mp], ops + [mp]):
+                want = subprocess.run([oracle_bin["bedmap"], *args], stdout=subprocess.PIPE, check=True).stdout
+                for groups in (2, 5):
+                    rc, got, err = _run(gpu_bin["bedmap"], args, str(tmp_path / "o.bed"), groups)
+                    assert rc == 0, err[-2000:]
+                    assert got == want, (args, groups, ahead)
+        finally:
+            os.environ.pop("BEDGPU_STREAM_AHEAD", None)
+
+
 def test_bedops_groups_actually_stream(gpu_bin, oracle_bin, tmp_path):
     rng = random.Random(3)
     files = [randbed.write(str(tmp_path / f"{k}.bed"),
