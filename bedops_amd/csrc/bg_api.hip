@@ -77,6 +77,7 @@ void* bg_alloc(bg_ctx* c, size_t bytes) {
       (void)hipGetLastError();
       // drop the cache and retry once
       hipStreamSynchronize(c->stream);
+      if (c->sstream) hipStreamSynchronize(c->sstream);
       for (auto& b : c->free_list) hipFree(b.p);
       c->free_list.clear();
       if (hipMalloc(&p, bytes) != hipSuccess) {
@@ -95,7 +96,7 @@ void bg_release(bg_ctx* c, void* p) {
   auto& L = c->live;
   auto it = L.find(p);
   if (it == L.end()) return;
-  c->free_list.push_back({p, it->second});
+  (c->defer_release ? c->deferred : c->free_list).push_back({p, it->second});
   L.erase(it);
 }
 
@@ -209,7 +210,9 @@ extern "C" void bg_close(bg_ctx* c) {
   if (c->ring_th.joinable()) c->ring_th.join();
   bg_pool_stop(c);
   hipStreamSynchronize(c->stream);
+  if (c->sstream) hipStreamSynchronize(c->sstream);
   for (auto& b : c->free_list) hipFree(b.p);
+  for (auto& b : c->deferred) hipFree(b.p);
   for (auto& kv : c->live) hipFree(kv.first);
   for (auto& m : c->marks) hipEventDestroy(m.second);
   for (auto& p : c->prof_pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
@@ -229,6 +232,9 @@ extern "C" void bg_close(bg_ctx* c) {
   for (auto e : c->copy_ev) hipEventDestroy(e);
   for (auto e : c->order_ev) hipEventDestroy(e);
   if (c->pstream) hipStreamDestroy(c->pstream);
+  if (c->sstream) hipStreamDestroy(c->sstream);
+  if (c->sfork) hipEventDestroy(c->sfork);
+  if (c->sjoin) hipEventDestroy(c->sjoin);
   hipStreamDestroy(c->stream);
   delete c;
 }

@@ -34,6 +34,8 @@
 // host over the keyed coordinates, and only when an operation can see an address tie (bg_map
 // decides). Not modelled: malloc_consolidate (heap growth while fast bins hold chunks), which
 // very large windows can trigger.
+#include <string.h>
+#include <algorithm>
 #include "bg_heap_replay.h"
 
 // per map row: id length and the remainder length the row's readline stores (restBuf):
@@ -67,22 +69,131 @@ __global__ void k_heap_lens(const char* __restrict__ text, const uint64_t* __res
 
 // rank of map row m's full_rest() among the rows of equal (start, end) around it (rows equal
 // in all three have equal ranks): the third key of CoordRestAddressCompare, in which
-// fixWindow's Add / Delete calls come. Runs of equal coordinates are short; a run of L rows
-// costs L^2 comparisons.
-__global__ void k_heap_rest_rank(const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
+// fixWindow's Add / Delete calls come. The runs come from their start flags (one compaction,
+// no per-row walk); a run of up to HEAP_RUN_DEV rows is ranked here, one thread per row and
+// one comparison per other row of its run; a longer run (PCR duplicates, placeholder rows: a
+// run of L rows would cost L^2) is listed for the host, which sorts it in O(L log L) as the
+// reference's std::set does (heap_long_ranks).
+#define HEAP_RUN_DEV 64
+__global__ void k_heap_run_flags(const int64_t* __restrict__ S, const int64_t* __restrict__ E, uint64_t n,
+                                 uint8_t* __restrict__ f) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < n) f[m] = m == 0 || S[m] != S[m - 1] || E[m] != E[m - 1];
+}
+__global__ void k_heap_rest_rank(const uint64_t* __restrict__ run0, uint64_t nrun, uint64_t n,
                                  const char* __restrict__ text, const uint64_t* __restrict__ rest_off,
-                                 const uint32_t* __restrict__ rest_len, int fields, uint32_t* __restrict__ rank) {
+                                 const uint32_t* __restrict__ rest_len, int fields, uint32_t* __restrict__ rank,
+                                 uint64_t* __restrict__ longs, unsigned long long* __restrict__ nlong) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
-  const int64_t s = S[m], e = E[m];
-  uint64_t lo = m, hi = m + 1;
-  while (lo > 0 && S[lo - 1] == s && E[lo - 1] == e) --lo;
-  while (hi < n && S[hi] == s && E[hi] == e) ++hi;
+  uint64_t a = 0, b = nrun;  // the last run starting at or before m
+  while (b - a > 1) {
+    const uint64_t mid = (a + b) >> 1;
+    if (run0[mid] <= m) a = mid;
+    else b = mid;
+  }
+  const uint64_t lo = run0[a], hi = a + 1 < nrun ? run0[a + 1] : n;
   uint32_t r = 0;
-  if (hi - lo > 1 && rest_off)
+  if (hi - lo > HEAP_RUN_DEV) {
+    if (m == lo) longs[atomicAdd(nlong, 1ULL)] = a;
+    r = 0;  // (the host's sort)
+  } else if (hi - lo > 1 && rest_off) {
     for (uint64_t j = lo; j < hi; ++j)
       if (j != m && bg_frest_cmp(text, rest_off, rest_len, fields, j, m) < 0) ++r;
+  }
   rank[m] = r;
+}
+// full_rest() lengths, then bytes, of the rows of listed runs (rows [row0[k], row0[k] + len[k]))
+__global__ void k_heap_rest_len(const uint64_t* __restrict__ rows, uint64_t nrows, const char* __restrict__ text,
+                                const uint64_t* __restrict__ rest_off, const uint32_t* __restrict__ rest_len,
+                                int fields, uint64_t* __restrict__ len) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const char *p1, *p2;
+  uint32_t l1, l2;
+  bg_frest(text, rest_off, rest_len, fields, rows[i], p1, l1, p2, l2);
+  len[i] = l1 + l2;
+}
+__global__ void k_heap_rest_copy(const uint64_t* __restrict__ rows, uint64_t nrows, const char* __restrict__ text,
+                                 const uint64_t* __restrict__ rest_off, const uint32_t* __restrict__ rest_len,
+                                 int fields, const uint64_t* __restrict__ off, char* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const char *p1, *p2;
+  uint32_t l1, l2;
+  bg_frest(text, rest_off, rest_len, fields, rows[i], p1, l1, p2, l2);
+  char* o = out + off[i];
+  for (uint32_t k = 0; k < l1; ++k) o[k] = p1[k];
+  for (uint32_t k = 0; k < l2; ++k) o[l1 + k] = p2[k];
+}
+
+// full_rest() of each listed map row to the host: row i's bytes are txt[off[i], off[i + 1])
+int bg_frest_gather(bg_ctx* c, const bg_table* M, int fields, const std::vector<uint64_t>& rows,
+                    std::vector<char>& txt, std::vector<uint64_t>& off) {
+  const uint64_t nr = rows.size();
+  off.assign(nr + 1, 0);
+  txt.clear();
+  if (!nr) return 0;
+  uint64_t* drows = (uint64_t*)bg_alloc(c, 8 * nr);
+  uint64_t* dlen = (uint64_t*)bg_alloc(c, 8 * (nr + 1));
+  if (!drows || !dlen) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(drows, rows.data(), 8 * nr, hipMemcpyHostToDevice, c->stream));
+  BG_LAUNCH(c, "k_heap_rest_len", k_heap_rest_len, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), drows, nr, M->text,
+            M->rest_off, M->rest_len, fields, dlen);
+  std::vector<uint64_t> len(nr);
+  BG_HIP(c, hipMemcpyAsync(len.data(), dlen, 8 * nr, hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  for (uint64_t i = 0; i < nr; ++i) off[i + 1] = off[i] + len[i];
+  char* dtxt = (char*)bg_alloc(c, off[nr] + 1);
+  if (!dtxt) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(dlen, off.data(), 8 * nr, hipMemcpyHostToDevice, c->stream));
+  BG_LAUNCH(c, "k_heap_rest_copy", k_heap_rest_copy, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), drows, nr, M->text,
+            M->rest_off, M->rest_len, fields, dlen, dtxt);
+  txt.resize(off[nr] + 1);
+  BG_HIP(c, hipMemcpyAsync(txt.data(), dtxt, off[nr], hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  bg_release(c, drows);
+  bg_release(c, dlen);
+  bg_release(c, dtxt);
+  return 0;
+}
+
+// the ranks of the runs longer than HEAP_RUN_DEV: their rows' full_rest() strings to the
+// host, each run sorted (strcmp order: bytes as unsigned, a prefix first), equal strings equal
+// ranks, written into hrank
+static int heap_long_ranks(bg_ctx* c, const bg_table* M, int fields, const uint64_t* d_run0, uint64_t nrun,
+                           const std::vector<uint64_t>& longs, std::vector<uint32_t>& hrank) {
+  const uint64_t nm = M->n;
+  std::vector<uint64_t> h0(nrun);
+  BG_HIP(c, hipMemcpyAsync(h0.data(), d_run0, 8 * nrun, hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> rows;
+  for (uint64_t a : longs) {
+    const uint64_t lo = h0[a], hi = a + 1 < nrun ? h0[a + 1] : nm;
+    for (uint64_t m = lo; m < hi; ++m) rows.push_back(m);
+  }
+  std::vector<char> txt;
+  std::vector<uint64_t> off;
+  int rc = bg_frest_gather(c, M, fields, rows, txt, off);
+  if (rc) return rc;
+  auto less = [&](uint64_t i, uint64_t j) {  // rows[i] vs rows[j] by full_rest()
+    return bg_bytes_less(txt.data() + off[i], off[i + 1] - off[i], txt.data() + off[j], off[j + 1] - off[j]);
+  };
+  uint64_t i0 = 0;
+  std::vector<uint64_t> ix;
+  for (uint64_t a : longs) {
+    const uint64_t n = (a + 1 < nrun ? h0[a + 1] : nm) - h0[a];
+    ix.resize(n);
+    for (uint64_t k = 0; k < n; ++k) ix[k] = i0 + k;
+    std::sort(ix.begin(), ix.end(), less);
+    uint32_t rk = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+      if (k > 0 && less(ix[k - 1], ix[k])) rk = (uint32_t)k;  // equal strings share a rank
+      hrank[rows[ix[k]]] = rk;
+    }
+    i0 += n;
+  }
+  return 0;
 }
 
 // does any map row equal its predecessor in (start, end) [and full_rest() when `rest`]?
@@ -121,13 +232,34 @@ int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, i
     BG_HIP(c, hipMemcpyAsync(hli.data(), dli, 4 * nm, hipMemcpyDeviceToHost, c->stream));
     BG_HIP(c, hipMemcpyAsync(hlr.data(), dlr, 4 * nm, hipMemcpyDeviceToHost, c->stream));
   }
+  uint64_t* run0 = nullptr;
+  uint64_t nrun = 0;
+  std::vector<uint64_t> longs;
   if (nm && M->rest_off && !spec->faster) {
     drk = (uint32_t*)bg_alloc(c, 4 * nm);
-    if (!drk) return BG_E_NOMEM;
-    BG_LAUNCH(c, "k_heap_rest_rank", k_heap_rest_rank, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), M->ks, M->ke, nm,
-              M->text, M->rest_off, M->rest_len, fields, drk);
+    uint8_t* f = (uint8_t*)bg_alloc(c, nm);
+    uint64_t* dl = (uint64_t*)bg_alloc(c, 8 * (nm + 1));  // long runs (count in the last slot)
+    if (!drk || !f || !dl) return BG_E_NOMEM;
+    BG_LAUNCH(c, "k_heap_run_flags", k_heap_run_flags, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), M->ks, M->ke, nm, f);
+    int rc = bg_compact_flags(c, f, nm, &run0, &nrun);
+    if (rc) return rc;
+    BG_HIP(c, hipMemsetAsync(dl + nm, 0, 8, c->stream));
+    BG_LAUNCH(c, "k_heap_rest_rank", k_heap_rest_rank, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), run0, nrun, nm,
+              M->text, M->rest_off, M->rest_len, fields, drk, dl, (unsigned long long*)(dl + nm));
     BG_HIP(c, hipGetLastError());
     BG_HIP(c, hipMemcpyAsync(hrank.data(), drk, 4 * nm, hipMemcpyDeviceToHost, c->stream));
+    uint64_t nl = 0;
+    if ((rc = bg_fetch_u64(c, dl + nm, &nl))) return rc;
+    if (nl) {
+      longs.resize(nl);
+      BG_HIP(c, hipMemcpyAsync(longs.data(), dl, 8 * nl, hipMemcpyDeviceToHost, c->stream));
+      BG_HIP(c, hipStreamSynchronize(c->stream));
+      std::sort(longs.begin(), longs.end());
+      if ((rc = heap_long_ranks(c, M, fields, run0, nrun, longs, hrank))) return rc;
+    }
+    bg_release(c, f);
+    bg_release(c, dl);
+    bg_release(c, run0);
   }
   if (nr && !single) {
     BG_HIP(c, hipMemcpyAsync(hRS.data(), R->ks, 8 * nr, hipMemcpyDeviceToHost, c->stream));

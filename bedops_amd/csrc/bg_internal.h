@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <mutex>
@@ -94,6 +95,12 @@ struct bg_ctx {
   std::mutex copy_mu;
   hipEvent_t cjoin = nullptr;     // its copies -> ctx's stream
   hipStream_t stream = nullptr;
+  // side stream: a set input's post-parse passes (bg_load.hip) run there beside the next
+  // input's parse; blocks released while it is in use wait in `deferred` until the join
+  hipStream_t sstream = nullptr;
+  hipEvent_t sfork = nullptr, sjoin = nullptr;
+  bool defer_release = false;
+  std::vector<bg_buf> deferred;
   std::string err;
   bg_dstatus* dstat = nullptr;  // device
   void* warm = nullptr;         // device scratch of the ring's warm-up copy
@@ -303,6 +310,14 @@ int bg_union_components(bg_ctx* c, bg_set* set, const int* files, int nf, Ivl& o
 bg_result* bg_new_ivl_result(bg_ctx* c, bg_set* set, Ivl& v);
 int bg_check_files(bg_ctx* c, bg_set* set, const int* files, int nf, int minf);
 int bg_compact_flags(bg_ctx* c, const uint8_t* flag, uint64_t n, uint64_t** rows, uint64_t* total);
+// full_rest() of each listed map row copied to the host: row i's bytes are txt[off[i], off[i+1])
+// (bg_heap.hip); strcmp order of two such byte strings
+int bg_frest_gather(bg_ctx* c, const bg_table* M, int fields, const std::vector<uint64_t>& rows,
+                    std::vector<char>& txt, std::vector<uint64_t>& off);
+static inline bool bg_bytes_less(const char* a, uint64_t la, const char* b, uint64_t lb) {
+  const int cmp = memcmp(a, b, la < lb ? la : lb);
+  return cmp ? cmp < 0 : la < lb;
+}
 // stable ascending radix sort of uint64 keys with an optional uint32 payload (bg_sort.hip)
 int bg_sort_u64(bg_ctx* c, uint64_t* keys, uint32_t* vals, uint64_t n);
 

@@ -2665,6 +2665,7 @@ struct LoadState {
   uint64_t* tcnt = nullptr;
   uint32_t* absorbed = nullptr;
   int64_t* tgb = nullptr;
+  uint32_t set_nt = 0;  // staging units of a BG_BED3_SET parse whose merge passes are pending
   // BED5: scores for k_score_big, (row, first byte) pairs
   uint64_t* big = nullptr;
   uint32_t bigcap = 0;
@@ -2937,6 +2938,18 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
     BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
               S.lcs, S.lce, TS, st);
   BG_HIP(c, hipGetLastError());
+  S.set_nt = nt;  // parse_set_merge follows
+  return 0;
+}
+
+// the passes after k_parse_set: the running max of earlier tiles, absorbed local components
+// and the final component columns. bg_load runs them on the side stream while the next
+// input parses (k_parse_set leaves HBM bandwidth to spare, k_set_write is bandwidth-bound)
+static int parse_set_merge(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
+  const uint32_t nt = S.set_nt;
+  S.set_nt = 0;
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
+  int rc;
   if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
   BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, BG_NT)), dim3(BG_NT), S.lcs, TS,
             S.mex, nt, S.tcnt, st);
@@ -2946,6 +2959,37 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
             S.lce, TS, S.mex, S.tcnt, nt, T->cs, T->ce);
   BG_HIP(c, hipGetLastError());
   return 0;
+}
+
+// parse_set_merge of input i on the side stream, forked from the ctx stream's current
+// position (BEDGPU_SET_SIDE=0: in line)
+static int set_merge_side(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
+  if (!c->sstream) {
+    if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sfork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sjoin, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return bg_fail(c, BG_E_HIP, "side stream creation failed");
+    }
+  }
+  BG_HIP(c, hipEventRecord(c->sfork, c->stream));
+  BG_HIP(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
+  c->defer_release = true;  // until set_merge_join: blocks the side stream may still use
+  hipStream_t main = c->stream;
+  c->stream = c->sstream;
+  const int rc = parse_set_merge(c, T, S, st);
+  c->stream = main;
+  if (rc) return rc;
+  BG_HIP(c, hipEventRecord(c->sjoin, c->sstream));
+  return 0;
+}
+static int set_merge_join(bg_ctx* c) {
+  if (!c->defer_release) return 0;
+  int rc = bg_hip_ok(c, hipStreamWaitEvent(c->stream, c->sjoin, 0));
+  c->defer_release = false;
+  for (auto& b : c->deferred) c->free_list.push_back(b);
+  c->deferred.clear();
+  return rc;
 }
 
 // after phase 3: per-input status, flags and the run -> row table
@@ -3107,9 +3151,20 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst, sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
   }
   HP("dict");
-  for (int i = 0; i < n && !rc; ++i)
+  static const bool side = [] {
+    const char* e = getenv("BEDGPU_SET_SIDE");
+    return !(e && atoi(e) == 0);
+  }();
+  for (int i = 0; i < n && !rc; ++i) {
     rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i)
                                        : parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
+    if (!rc && st[i].set_nt)
+      rc = (side && i + 1 < n) ? set_merge_side(c, s->t[i], st[i], dst + i) : parse_set_merge(c, s->t[i], st[i], dst + i);
+  }
+  {
+    const int rj = set_merge_join(c);  // (on errors too: the side stream's blocks return to the pool)
+    if (!rc) rc = rj;
+  }
   HP("parse_q");
   // round trip 3: statuses and run rows of every input (pageable copies block the host,
   // so they are issued only once all parses are queued)

@@ -566,8 +566,12 @@ __device__ __forceinline__ void ev_walk(const EvArgs& A, uint64_t a, uint64_t b,
 
 // A.ro: the rank of row t in its run of equal starts under CoordRestAddressCompare (a
 // strict total order: addresses are distinct), counted against the whole run — O(run) per
-// row, so O(run^2) once per map instead of per window
-__global__ void __launch_bounds__(BG_NT) k_ev_rank(EvArgs A, uint32_t* __restrict__ ro) {
+// row, so O(run^2) once per map instead of per window, for runs of up to EV_RUN_DEV rows;
+// longer runs (a pile of reads at one position) are listed in `longs` (count in *nlong) and
+// sorted on the host in O(run log run) (ev_long_order)
+#define EV_RUN_DEV 2048
+__global__ void __launch_bounds__(BG_NT) k_ev_rank(EvArgs A, uint32_t* __restrict__ ro, uint64_t* __restrict__ longs,
+                                                   unsigned long long* __restrict__ nlong) {
   const uint64_t t = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
   if (t >= A.nm) return;
   const int64_t s = A.MS[t];
@@ -577,6 +581,10 @@ __global__ void __launch_bounds__(BG_NT) k_ev_rank(EvArgs A, uint32_t* __restric
     return;
   }
   const uint64_t f0 = ev_run_lo(A.MS, t), f1 = ev_run_hi(A.MS, t, A.nm);
+  if (f1 - f0 > EV_RUN_DEV) {
+    if (t == f0) longs[atomicAdd(nlong, 1ULL)] = f0;
+    return;
+  }
   uint64_t r = 0;
   // (ME, prefix) decide almost every pair: independent loads, no byte walks
   const int64_t te = A.ME[t];
@@ -811,6 +819,65 @@ __global__ void k_mev_pick(const uint64_t* __restrict__ off, uint64_t nr, const 
   const uint64_t end = off[i + 1];
   dsum[i] = end ? SA[end - 1] : 0.0;
   if (dsq) dsq[i] = end ? QA[end - 1] : 0.0;
+}
+
+// A.ro for every run of equal map starts: k_ev_rank, then the long runs it listed sorted here
+// by (end, full_rest(), address) — CoordRestAddressCompare's order for rows of one start
+static int ev_order(bg_ctx* c, const EvArgs& E, const bg_table* M, int fields, uint32_t* ro) {
+  const uint64_t nm = E.nm;
+  uint64_t* dl = (uint64_t*)bg_alloc(c, 8 * (nm + 1));
+  if (!dl) return BG_E_NOMEM;
+  BG_HIP(c, hipMemsetAsync(dl + nm, 0, 8, c->stream));
+  BG_LAUNCH(c, "k_ev_rank", k_ev_rank, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), E, ro, dl,
+            (unsigned long long*)(dl + nm));
+  int rc = bg_hip_ok(c, hipGetLastError());
+  uint64_t nl = 0;
+  if (rc || (rc = bg_fetch_u64(c, dl + nm, &nl))) return rc;
+  if (nl) {
+    std::vector<uint64_t> f0(nl);
+    BG_HIP(c, hipMemcpyAsync(f0.data(), dl, 8 * nl, hipMemcpyDeviceToHost, c->stream));
+    std::vector<int64_t> ms(nm), me(nm), ad;
+    BG_HIP(c, hipMemcpyAsync(ms.data(), E.MS, 8 * nm, hipMemcpyDeviceToHost, c->stream));
+    BG_HIP(c, hipMemcpyAsync(me.data(), E.ME, 8 * nm, hipMemcpyDeviceToHost, c->stream));
+    if (E.addr) {
+      ad.resize(nm);
+      BG_HIP(c, hipMemcpyAsync(ad.data(), E.addr, 8 * nm, hipMemcpyDeviceToHost, c->stream));
+    }
+    BG_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> rows, run;  // run k: rows[run[k], run[k + 1])
+    for (uint64_t a : f0) {
+      run.push_back(rows.size());
+      for (uint64_t m = a; m < nm && ms[m] == ms[a]; ++m) rows.push_back(m);
+    }
+    run.push_back(rows.size());
+    std::vector<char> txt;
+    std::vector<uint64_t> off;
+    if (M->rest_off && (rc = bg_frest_gather(c, M, fields, rows, txt, off))) return rc;
+    auto less = [&](uint64_t i, uint64_t j) {  // rows[i] vs rows[j]
+      const uint64_t a = rows[i], b = rows[j];
+      if (me[a] != me[b]) return me[a] < me[b];
+      if (M->rest_off) {
+        const char *x = txt.data() + off[i], *y = txt.data() + off[j];
+        const uint64_t lx = off[i + 1] - off[i], ly = off[j + 1] - off[j];
+        if (bg_bytes_less(x, lx, y, ly)) return true;
+        if (bg_bytes_less(y, ly, x, lx)) return false;
+      }
+      return (E.addr ? ad[a] : (int64_t)a) < (E.addr ? ad[b] : (int64_t)b);
+    };
+    std::vector<uint64_t> ix;
+    std::vector<uint32_t> out;
+    for (uint64_t k = 0; k + 1 < run.size(); ++k) {
+      ix.resize(run[k + 1] - run[k]);
+      for (uint64_t i = 0; i < ix.size(); ++i) ix[i] = run[k] + i;
+      std::sort(ix.begin(), ix.end(), less);
+      out.resize(ix.size());
+      for (uint64_t i = 0; i < ix.size(); ++i) out[i] = (uint32_t)rows[ix[i]];
+      BG_HIP(c, hipMemcpyAsync(ro + rows[run[k]], out.data(), 4 * out.size(), hipMemcpyHostToDevice, c->stream));
+      BG_HIP(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  bg_release(c, dl);
+  return 0;
 }
 
 template <int CRIT>
@@ -1528,10 +1595,7 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
         rc = bg_hip_ok(c, hipGetLastError());
         E.P = pk;
         E.PL = pl;
-        if (!rc) {
-          BG_LAUNCH(c, "k_ev_rank", k_ev_rank, dim3(bg_blocks(M->n, BG_NT)), dim3(BG_NT), E, ro);
-          rc = bg_hip_ok(c, hipGetLastError());
-        }
+        if (!rc) rc = ev_order(c, E, M, mapfields, ro);
         E.ro = ro;
       }
     }

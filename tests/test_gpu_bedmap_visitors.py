@@ -233,3 +233,25 @@ def test_many_identical_map_rows_stay_fast(eng, oracle_bin):
                 gpu(eng, ["mean", "sum", "variance", "count"], rt, mt)
             times[identical] = time.perf_counter() - t0
     assert times[True] <= 3 * times[False] + 0.05, times
+
+
+def test_long_runs_of_equal_map_rows(eng, oracle_bin):
+    """a pile of 5000 map rows at one (start, end) and 3000 more at the same start with other
+    ends: the equal-coordinate runs (heap address ranks, bg_heap.hip) and the equal-start run
+    (running-sum set order, k_ev_rank) are longer than the device-ranked limits (64 and 2048
+    rows), so they are ordered on the host by sort; output equal to the oracle for echo-map
+    (address order), the running sums and tmean"""
+    rng = random.Random(5)
+    ref = [("chr1", s, s + 400) for s in range(0, 4000, 50)]
+    rt = randbed.text(ref).encode()
+    rows = [("chr1", 1000, 1600, f"id{rng.randint(0, 300)}") for _ in range(5000)]
+    rows += [("chr1", 1000, 1000 + rng.randint(1, 900), f"x{k}") for k in range(3000)]
+    rows += [("chr1", s, s + 100, f"y{s}") for s in range(0, 4000, 37)]
+    rows.sort(key=lambda r: (r[1], r[2]))
+    mt = "".join(f"{c}\t{s}\t{e}\t{i}\t{rng.randint(0, 9999) / 100}\n" for c, s, e, i in rows).encode()
+    with tempfile.TemporaryDirectory() as td:
+        for ops in (["echo-map", "count"], ["mean", "sum", "variance"], [("tmean", 0.1, 0.2), "echo-map-id"]):
+            want, err, rc = oracle(oracle_bin["bedmap"], argv(ops), [rt, mt], td)
+            assert rc == 0, err
+            got, _ = gpu(eng, ops, rt, mt)
+            assert got == want, ops
