@@ -490,8 +490,261 @@ __global__ void __launch_bounds__(BG_NT) k_closest_serial(ClArgs A) {
   }
 }
 
+// -------------------------------------------------------------------------------------
+// k_closest_wave (round 5, the default): ONE WAVE per chunk, the candidates of a ref row
+// taken 64 at a time, one per lane, in the reference's read order (the cache stack from
+// the top, then the file). The branch chain of cl_run is a left-to-right fold over the
+// candidates, but every piece of state it carries is a prefix function the wave computes
+// at once instead of one dependent candidate per iteration:
+//   brk      the first lane with d > 0 (or +inf): lanes after it are not read;
+//   ld       0 once a hangL / in_c was seen (the first inside-and-not-half lane before any
+//            hangL is the one in_c: ld != 0 only until then), otherwise the running max of
+//            the negative distances: newleft = d >= the exclusive prefix max (ties: >=);
+//   left     the last lane before this one setting it (newleft, hangL, in_c), else the
+//            incoming left — a ballot and a count of leading zeros; likewise right
+//            (firstR, hangR, in_a, in_d) and lc (the last lane changing it, and the value
+//            it set, which depends only on that lane's own case and hasL);
+//   rdist    0 after any hangR / in_a / in_d, else the incoming value (firstR only breaks);
+//   kept     each lane appends keepL, keepR, keepC in order at an exclusive prefix sum;
+//            the last reset (newleft, in_c) discards everything before it.
+// So a row costs one wave step per 64 candidates (the benchmark reads ~100 file rows and
+// pops ~26 cached rows per ref row: ~3 steps instead of ~126 dependent ones), and the file
+// rows come in coalesced. The stack and the kept list live in LDS (CW_LDS entries each per
+// wave); a chunk that outgrows them is left to k_closest_fix (cl_run, any depth) by a start
+// state no predecessor ends in, chunk 0 by a rerun of the pass with k_closest_chunks.
+#define CW_LDS 256
+#define CW_WAVES 4
+struct WaveCl {
+  int64_t ld, rdist, left, right, lce;
+  bool lc;
+  uint32_t nk;
+  bool ovf;
+};
+__device__ __forceinline__ int64_t wave_excl_max_i64(int64_t v, int64_t identity) {
+  const int lane = bg_lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v = u > v ? u : v;
+  }
+  const int64_t e = __shfl_up(v, 1, 64);
+  return lane ? (e > identity ? e : identity) : identity;
+}
+// the last lane below this one whose bit is set in m, or -1
+__device__ __forceinline__ int last_below(uint64_t m) {
+  const uint64_t b = m & ((1ull << bg_lane()) - 1);
+  return b ? 63 - __clzll(b) : -1;
+}
+__device__ __forceinline__ int last_set(uint64_t m) { return m ? 63 - __clzll(m) : -1; }
+
+// one window of up to 64 candidates (lane i: index c, keys cs/ce, valid = i < cnt) through
+// the chain for ref row (bs, be); returns the number consumed (through the breaking lane) and
+// sets brk
+__device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, uint32_t* kept, int64_t bs, int64_t be,
+                                              double cen, bool valid, uint32_t cnt, int64_t c, int64_t cs,
+                                              int64_t ce, bool& brk) {
+  const int lane = bg_lane();
+  const int64_t d = valid ? cl_dist(cs, ce, bs, be) : D_MINUS;
+  const bool live = valid && d != D_MINUS;  // (an earlier chromosome's row: no effect)
+  const bool plus0 = live && d == D_PLUS;
+  const bool pos0 = live && d > 0 && !plus0;
+  const uint64_t bm = __ballot(plus0 || pos0);
+  const int B = bm ? __ffsll((unsigned long long)bm) - 1 : 64;
+  const bool act = live && lane <= B;  // (the rows after the break are not read)
+  const bool plus = plus0 && act, pos = pos0 && act;
+  const bool neg = act && d < 0;
+  const bool ovl = act && d == 0 && A.overlaps;
+  const bool noov = act && d == 0 && !A.overlaps;
+  const bool hangL = ovl && cs <= bs;
+  const bool hangR = ovl && !hangL && be <= ce;
+  const bool inside = ovl && !hangL && !hangR;
+  bool half = false;
+  if (inside) {
+    const double cst = (double)(cs & BG_COORD_MASK);
+    const double prop =
+        cen < cst ? 0.0 : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
+    half = prop < 0.5;
+  }
+  // ld == 0 from the first hangL / (inside, !half) lane on (that lane itself still sees ld != 0)
+  const uint64_t zm = __ballot(hangL || (inside && !half));
+  const bool ld0z = W.ld == 0;
+  const int Z = ld0z ? -1 : (zm ? __ffsll((unsigned long long)zm) - 1 : 64);
+  const bool ldz = ld0z || lane > Z;
+  const bool in_c = inside && !half && !ldz;
+  const bool in_b = inside && !half && ldz;
+  const bool in_a = inside && half && ldz;
+  const bool in_d = inside && half && !ldz;
+  // (every wave-wide operation below runs on all lanes: no shuffle inside a select)
+  const int64_t pm = wave_excl_max_i64(neg ? d : D_MINUS, W.ld);
+  const int64_t ldi = ldz ? 0 : pm;
+  const bool newleft = neg && !ldz && d >= ldi;
+  const bool dropL = neg && !newleft;
+  const bool rz = last_below(__ballot(hangR || in_a || in_d)) >= 0;
+  const int64_t rdi = rz ? 0 : W.rdist;
+  const bool firstR = pos && d < rdi;
+  const bool farR = pos && !firstR;
+  const bool setleft = newleft || hangL || in_c;
+  const uint64_t lm = __ballot(setleft);
+  const int li = last_below(lm);
+  const int64_t lsc = __shfl(c, li < 0 ? 0 : li, 64), lse = __shfl(ce, li < 0 ? 0 : li, 64);
+  const int64_t lft = li >= 0 ? lsc : W.left;
+  const int64_t lce = li >= 0 ? lse : W.lce;
+  const bool hasL = lft >= 0;
+  const bool lc_zero = newleft || hangL || in_c;
+  const bool lc_one = dropL || in_a || in_b || (noov && hasL);
+  const bool lc_hasl = plus || firstR || farR || hangR || in_d;
+  const bool lc_ev = lc_zero || lc_one || lc_hasl;
+  const bool lc_after = lc_zero ? false : (lc_one ? true : hasL);
+  const uint64_t cm = __ballot(lc_ev);
+  const int ci = last_below(cm);
+  const int lcs = __shfl((int)lc_after, ci < 0 ? 0 : ci, 64);
+  const bool lci = ci >= 0 ? lcs != 0 : W.lc;
+  const bool setright = firstR || hangR || in_a || in_d;
+  const uint64_t rm = __ballot(setright);
+  const int ri = last_below(rm);
+  const int64_t rsc = __shfl(c, ri < 0 ? 0 : ri, 64);
+  const int64_t rgt = ri >= 0 ? rsc : W.right;
+  const bool hasR = rgt >= 0;
+  const bool keepL = act && hasL && !lci &&
+                     (plus || firstR || farR || hangR || in_d || noov || dropL || in_a || in_b ||
+                      (hangL && !(lce <= ce)));
+  const bool keepR = act && hasR && (plus || farR || hangR || in_a || in_d);
+  const bool keepC = plus || firstR || farR || in_b || noov;
+  const int R = last_set(__ballot(newleft || in_c));
+  const uint32_t e = lane >= R ? (uint32_t)keepL + (uint32_t)keepR + (uint32_t)keepC : 0u;
+  const uint32_t inc = wave_incl_scan(e, OpSum());
+  const uint32_t base = R >= 0 ? 0u : W.nk;
+  uint32_t p = base + inc - e;
+  if (e) {
+    if (keepL) { if (p < CW_LDS) kept[p] = (uint32_t)lft; ++p; }
+    if (keepR) { if (p < CW_LDS) kept[p] = (uint32_t)rgt; ++p; }
+    if (keepC) { if (p < CW_LDS) kept[p] = (uint32_t)c; }
+  }
+  // the state after the window (uniform)
+  W.nk = base + (uint32_t)__shfl((int)inc, 63, 64);
+  if (R >= 0) W.ovf = false;
+  if (W.nk > CW_LDS) W.ovf = true;
+  const int64_t dl63 = __shfl(neg ? d : D_MINUS, 63, 64);
+  const int64_t m63 = __shfl(pm, 63, 64);  // (lane 63's exclusive max: lanes 0..62 and the incoming ld)
+  if (ld0z || zm) W.ld = 0;
+  else W.ld = m63 > dl63 ? m63 : dl63;
+  if (lm) {
+    const int L = last_set(lm);
+    W.left = __shfl(c, L, 64);
+    W.lce = __shfl(ce, L, 64);
+  }
+  if (cm) W.lc = __shfl((int)lc_after, last_set(cm), 64) != 0;
+  if (rm) W.right = __shfl(c, last_set(rm), 64);
+  const int fB = __shfl((int)firstR, B < 64 ? B : 0, 64);
+  const int64_t dB = __shfl(d, B < 64 ? B : 0, 64);
+  if (B < 64 && fB) W.rdist = dB;
+  else if (__ballot(hangR || in_a || in_d)) W.rdist = 0;
+  brk = B < (int)cnt;
+  return brk ? (uint32_t)B + 1 : cnt;
+}
+
+// ref rows [b0, b1) from the wave's state (fp, stack stk[0, n) bottom first); false when
+// the stack or the kept list outgrew LDS
+__device__ bool cw_run(const ClArgs& A, uint64_t b0, uint64_t b1, uint64_t& fp, uint32_t& n, uint32_t* stk,
+                       uint32_t* kept, bool emit) {
+  const int lane = bg_lane();
+  for (uint64_t b = b0; b < b1; ++b) {
+    const int64_t bs = A.qs[b], be = A.qe[b];
+    const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
+    WaveCl W{D_MINUS, D_PLUS, -1, -1, 0, false, 0u, false};
+    bool brk = false;
+    while (n && !brk) {  // the cache, from the top
+      const uint32_t cnt = n < 64 ? n : 64u;
+      const bool v = (uint32_t)lane < cnt;
+      const int64_t c = v ? (int64_t)stk[n - 1 - lane] : 0;
+      const int64_t cs = v ? A.cs[c] : 0, ce = v ? A.ce[c] : 0;
+      n -= cw_window(A, W, kept, bs, be, cen, v, cnt, c, cs, ce, brk);
+    }
+    bool eof = false;
+    while (!brk) {  // the file
+      if (fp >= A.nc) {
+        eof = true;
+        break;
+      }
+      const uint64_t left_in_file = A.nc - fp;
+      const uint32_t cnt = left_in_file < 64 ? (uint32_t)left_in_file : 64u;
+      const bool v = (uint32_t)lane < cnt;
+      const int64_t c = (int64_t)fp + lane;
+      const int64_t cs = v ? A.cs[c] : 0, ce = v ? A.ce[c] : 0;
+      fp += cw_window(A, W, kept, bs, be, cen, v, cnt, c, cs, ce, brk);
+    }
+    if (eof) {
+      if (W.left >= 0 && !W.lc) {
+        if (lane == 0 && W.nk < CW_LDS) kept[W.nk] = (uint32_t)W.left;
+        ++W.nk;
+      }
+      if (W.right >= 0) {
+        if (lane == 0 && W.nk < CW_LDS) kept[W.nk] = (uint32_t)W.right;
+        ++W.nk;
+      }
+    }
+    if (W.ovf || W.nk > CW_LDS || n + W.nk > CW_LDS || n + W.nk > A.cap) return false;
+    __builtin_amdgcn_wave_barrier();
+    // BedReader::PushBack(list): the list comes back out in list order
+    for (uint32_t t = lane; t < W.nk; t += 64) stk[n + t] = kept[W.nk - 1 - t];
+    __builtin_amdgcn_wave_barrier();
+    n += W.nk;
+    if (emit && lane == 0) {
+      A.left[b] = W.left;
+      A.right[b] = W.right;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ void cw_store(const ClArgs& A, uint64_t slot, uint64_t fp, uint32_t n, const uint32_t* stk) {
+  uint32_t* g = cl_slot(A, slot);
+  for (uint32_t t = bg_lane(); t < n; t += 64) g[t] = stk[t];
+  if (bg_lane() == 0) {
+    A.st_fp[slot] = fp;
+    A.st_n[slot] = n;
+  }
+}
+
+__global__ void __launch_bounds__(64 * CW_WAVES) k_closest_wave(ClArgs A) {
+  __shared__ uint32_t lstk[CW_WAVES][CW_LDS], lkept[CW_WAVES][CW_LDS];
+  const uint32_t k = blockIdx.x * CW_WAVES + bg_wave();
+  if (k >= A.nchunks) return;
+  uint32_t* stk = lstk[bg_wave()];
+  uint32_t* kept = lkept[bg_wave()];
+  const uint64_t q0 = (uint64_t)k * A.cq, q1 = min(q0 + A.cq, A.nq);
+  uint64_t fp = 0;
+  uint32_t n = 0;
+  bool ok = true;
+  if (k > 0) {  // the speculative start of k_closest_chunks
+    const uint64_t qw = q0 - A.cw;
+    const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
+    const uint64_t f = lower_bound_i64(A.cs, A.nc, A.qs[qw] - A.lmax - 1);
+    fp = (p - f > CBACK) ? p - CBACK : f;
+    ok = cw_run(A, qw, q0, fp, n, stk, kept, false);
+  }
+  if (ok) {
+    cw_store(A, 2ull * k, fp, n, stk);  // the start state
+    ok = cw_run(A, q0, q1, fp, n, stk, kept, true);
+  }
+  if (!ok) {
+    if (k == 0) {
+      if (bg_lane() == 0) atomicOr(A.overflow, 2u);  // the pass is rerun by k_closest_chunks
+      return;
+    }
+    if (bg_lane() == 0) {  // left to k_closest_fix: a start no predecessor ends in
+      A.st_fp[2ull * k] = ~0ull;
+      A.st_n[2ull * k] = 0;
+      A.st_fp[2ull * k + 1] = ~0ull - 1;
+      A.st_n[2ull * k + 1] = 0;
+    }
+    return;
+  }
+  cw_store(A, 2ull * k + 1, fp, n, stk);
+}
+
 // one attempt at capacity A.cap; *ovf set if some state outgrew it
-static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf) {
+static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf, bool* wave) {
   *ovf = false;
   const uint64_t slots = 2ull * A.nchunks;
   A.st_fp = (uint64_t*)bg_alloc(c, 8 * slots);
@@ -504,7 +757,18 @@ static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf) {
   int rc = 0;
   if (!A.st_fp || !A.st_n || !A.st_c || !A.kl || !A.flag || !A.nflag) rc = BG_E_NOMEM;
   if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 8, c->stream));
-  if (!rc) {
+  if (!rc && *wave) {
+    BG_LAUNCH(c, "k_closest_chunks", k_closest_wave, dim3(bg_blocks(A.nchunks, CW_WAVES)), dim3(64 * CW_WAVES), A);
+    rc = bg_hip_ok(c, hipGetLastError());
+    uint32_t h2[2] = {0, 0};
+    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(h2, A.nflag, 8, hipMemcpyDeviceToHost, c->stream));
+    if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+    if (!rc && (h2[1] & 2u)) {  // chunk 0 outgrew the wave kernel's LDS state: the thread kernel
+      *wave = false;
+      rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 8, c->stream));
+    }
+  }
+  if (!rc && !*wave) {
     BG_LAUNCH(c, "k_closest_chunks", k_closest_chunks, dim3(bg_blocks(A.nchunks, BG_NT)),
               dim3(BG_NT), A);
     rc = bg_hip_ok(c, hipGetLastError());
@@ -583,9 +847,11 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
   int rc = 0;
   // the reader cache of the reference can hold many rows on nested inputs: grow the
   // per-chunk state capacity until it fits (bounded by device memory)
+  // BEDGPU_CLOSEST_WAVE=0: the thread-per-chunk kernel (k_closest_chunks) for every chunk
+  bool wave = !(getenv("BEDGPU_CLOSEST_WAVE") && atoi(getenv("BEDGPU_CLOSEST_WAVE")) == 0);
   for (A.cap = CAP0;; A.cap *= 4) {
     bool ovf = false;
-    rc = closest_pass(c, A, &ovf);
+    rc = closest_pass(c, A, &ovf, &wave);
     if (rc || !ovf) break;
     if (3ull * 4ull * A.cap * A.nchunks * 4 > (64ull << 30)) {
       rc = bg_fail(c, BG_E_UNSUPPORTED, "closest-features: reader cache too deep for device memory");
