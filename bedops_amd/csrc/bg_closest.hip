@@ -60,6 +60,7 @@ struct ClArgs {
   uint32_t cap;
   uint32_t cq, cw;  // rows per chunk, warm-up rows
   int64_t lmax;  // longest candidate: a row still cached can start at most lmax earlier
+  int apf;       // cl_run: load the cached rows' keys ahead (BEDGPU_CLOSEST_APF=1; measured neutral, off)
   uint32_t nchunks;
   uint32_t* flag;
   uint32_t* nflag;
@@ -97,6 +98,15 @@ __device__ __forceinline__ uint32_t cl_pop(ClState& S) {
     return S.l[(S.n & (CL_D - 1)) * BG_NT];
   }
   return S.c[S.n];
+}
+// entry i (from the bottom) without popping
+__device__ __forceinline__ uint32_t cl_peek(const ClState& S, uint32_t i) {
+  return i >= S.n - S.m ? S.l[(i & (CL_D - 1)) * BG_NT] : S.c[i];
+}
+// pop k entries
+__device__ __forceinline__ void cl_drop(ClState& S, uint32_t k) {
+  S.n -= k;
+  S.m = S.m > k ? S.m - k : 0;
 }
 // the whole stack in global memory (snapshots, comparisons)
 __device__ __forceinline__ void cl_flush(ClState& S) {
@@ -261,9 +271,40 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     //      ~70% of the rows read on the benchmark's inputs, at a compare and a select each;
     //   C: the rest of the file through the chain, up to the row that ends the scan.
     bool brk = false;
-    while (S.n && !brk) {  // A
-      const int64_t c = cl_pop(S);
-      brk = step(c, A.cs[c], A.ce[c]);
+    if (A.apf) {  // A, the next APF entries' keys loaded ahead (a pop's gather no longer waits)
+      constexpr int APF = 4;
+      int64_t pc[APF], ps[APF], pe[APF];
+      const uint32_t n0 = S.n;
+#pragma unroll
+      for (int i = 0; i < APF; ++i) {
+        pc[i] = (uint32_t)i < n0 ? (int64_t)cl_peek(S, n0 - 1 - i) : 0;
+        ps[i] = (uint32_t)i < n0 ? A.cs[pc[i]] : 0;
+        pe[i] = (uint32_t)i < n0 ? A.ce[pc[i]] : 0;
+      }
+      uint32_t k = 0;
+      while (k < n0 && !brk) {
+        const int64_t c = pc[0], cs = ps[0], ce = pe[0];
+#pragma unroll
+        for (int i = 0; i + 1 < APF; ++i) {
+          pc[i] = pc[i + 1];
+          ps[i] = ps[i + 1];
+          pe[i] = pe[i + 1];
+        }
+        const uint32_t nx = k + APF;
+        if (nx < n0) {
+          pc[APF - 1] = (int64_t)cl_peek(S, n0 - 1 - nx);
+          ps[APF - 1] = A.cs[pc[APF - 1]];
+          pe[APF - 1] = A.ce[pc[APF - 1]];
+        }
+        ++k;
+        brk = step(c, cs, ce);
+      }
+      cl_drop(S, k);
+    } else {
+      while (S.n && !brk) {  // A
+        const int64_t c = cl_pop(S);
+        brk = step(c, A.cs[c], A.ce[c]);
+      }
     }
 #ifndef BG_CL_CB
 #define BG_CL_CB 8
@@ -507,19 +548,37 @@ __global__ void __launch_bounds__(BG_NT) k_closest_serial(ClArgs A) {
 //   rdist    0 after any hangR / in_a / in_d, else the incoming value (firstR only breaks);
 //   kept     each lane appends keepL, keepR, keepC in order at an exclusive prefix sum;
 //            the last reset (newleft, in_c) discards everything before it.
-// So a row costs one wave step per 64 candidates (the benchmark reads ~100 file rows and
-// pops ~26 cached rows per ref row: ~3 steps instead of ~126 dependent ones), and the file
-// rows come in coalesced. The stack and the kept list live in LDS (CW_LDS entries each per
-// wave); a chunk that outgrows them is left to k_closest_fix (cl_run, any depth) by a start
-// state no predecessor ends in, chunk 0 by a rerun of the pass with k_closest_chunks.
-#define CW_LDS 256
+// A window takes the cache's entries first and fills its remaining lanes with file rows,
+// so a ref row usually costs two wave steps (the benchmark pops ~26 cached rows and reads
+// ~100 file rows per ref row) instead of ~126 dependent one-candidate steps. The latency is
+// hidden too: the cache's entries keep their keys beside them in LDS (no gather), and the
+// file rows come through two 64-row register blocks, the next block's coalesced load issued
+// as soon as the window leaves the first one (lanes pick their row with a bpermute). The
+// stack and the kept list live in LDS (CW_LDS entries each per wave); a chunk that outgrows
+// them is left to k_closest_fix (cl_run, any depth) by a start state no predecessor ends in,
+// chunk 0 by a rerun of the pass with k_closest_chunks.
+#define CW_LDS 192
 #define CW_WAVES 4
+struct CwKeys {  // one wave's LDS: an entry = candidate index + its keys
+  uint32_t i[CW_LDS];
+  int64_t s[CW_LDS], e[CW_LDS];
+};
 struct WaveCl {
-  int64_t ld, rdist, left, right, lce;
+  int64_t ld, rdist, left, right, lcs, lce, rcs, rce;
   bool lc;
   uint32_t nk;
   bool ovf;
 };
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t bperm64(int64_t v, int src) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)v);
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
 __device__ __forceinline__ int64_t wave_excl_max_i64(int64_t v, int64_t identity) {
   const int lane = bg_lane();
 #pragma unroll
@@ -540,7 +599,7 @@ __device__ __forceinline__ int last_set(uint64_t m) { return m ? 63 - __clzll(m)
 // one window of up to 64 candidates (lane i: index c, keys cs/ce, valid = i < cnt) through
 // the chain for ref row (bs, be); returns the number consumed (through the breaking lane) and
 // sets brk
-__device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, uint32_t* kept, int64_t bs, int64_t be,
+__device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, CwKeys& K, int64_t bs, int64_t be,
                                               double cen, bool valid, uint32_t cnt, int64_t c, int64_t cs,
                                               int64_t ce, bool& brk) {
   const int lane = bg_lane();
@@ -579,16 +638,17 @@ __device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, uint32
   const int64_t ldi = ldz ? 0 : pm;
   const bool newleft = neg && !ldz && d >= ldi;
   const bool dropL = neg && !newleft;
-  const bool rz = last_below(__ballot(hangR || in_a || in_d)) >= 0;
-  const int64_t rdi = rz ? 0 : W.rdist;
+  const uint64_t r0m = __ballot(hangR || in_a || in_d);
+  const int64_t rdi = last_below(r0m) >= 0 ? 0 : W.rdist;
   const bool firstR = pos && d < rdi;
   const bool farR = pos && !firstR;
   const bool setleft = newleft || hangL || in_c;
   const uint64_t lm = __ballot(setleft);
-  const int li = last_below(lm);
-  const int64_t lsc = __shfl(c, li < 0 ? 0 : li, 64), lse = __shfl(ce, li < 0 ? 0 : li, 64);
-  const int64_t lft = li >= 0 ? lsc : W.left;
-  const int64_t lce = li >= 0 ? lse : W.lce;
+  const int li = last_below(lm), lsrc = li < 0 ? 0 : li;
+  const int64_t xc = bperm64(c, lsrc), xs = bperm64(cs, lsrc), xe = bperm64(ce, lsrc);
+  const int64_t lft = li >= 0 ? xc : W.left;
+  const int64_t lcs = li >= 0 ? xs : W.lcs;
+  const int64_t lce = li >= 0 ? xe : W.lce;
   const bool hasL = lft >= 0;
   const bool lc_zero = newleft || hangL || in_c;
   const bool lc_one = dropL || in_a || in_b || (noov && hasL);
@@ -596,14 +656,16 @@ __device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, uint32
   const bool lc_ev = lc_zero || lc_one || lc_hasl;
   const bool lc_after = lc_zero ? false : (lc_one ? true : hasL);
   const uint64_t cm = __ballot(lc_ev);
+  const uint64_t lam = __ballot(lc_after);
   const int ci = last_below(cm);
-  const int lcs = __shfl((int)lc_after, ci < 0 ? 0 : ci, 64);
-  const bool lci = ci >= 0 ? lcs != 0 : W.lc;
+  const bool lci = ci >= 0 ? ((lam >> ci) & 1) != 0 : W.lc;
   const bool setright = firstR || hangR || in_a || in_d;
   const uint64_t rm = __ballot(setright);
-  const int ri = last_below(rm);
-  const int64_t rsc = __shfl(c, ri < 0 ? 0 : ri, 64);
-  const int64_t rgt = ri >= 0 ? rsc : W.right;
+  const int ri = last_below(rm), rsrc = ri < 0 ? 0 : ri;
+  const int64_t yc = bperm64(c, rsrc), ys = bperm64(cs, rsrc), ye = bperm64(ce, rsrc);
+  const int64_t rgt = ri >= 0 ? yc : W.right;
+  const int64_t rcs = ri >= 0 ? ys : W.rcs;
+  const int64_t rce = ri >= 0 ? ye : W.rce;
   const bool hasR = rgt >= 0;
   const bool keepL = act && hasL && !lci &&
                      (plus || firstR || farR || hangR || in_d || noov || dropL || in_a || in_b ||
@@ -616,77 +678,131 @@ __device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, uint32
   const uint32_t base = R >= 0 ? 0u : W.nk;
   uint32_t p = base + inc - e;
   if (e) {
-    if (keepL) { if (p < CW_LDS) kept[p] = (uint32_t)lft; ++p; }
-    if (keepR) { if (p < CW_LDS) kept[p] = (uint32_t)rgt; ++p; }
-    if (keepC) { if (p < CW_LDS) kept[p] = (uint32_t)c; }
+    if (keepL) { if (p < CW_LDS) { K.i[p] = (uint32_t)lft; K.s[p] = lcs; K.e[p] = lce; } ++p; }
+    if (keepR) { if (p < CW_LDS) { K.i[p] = (uint32_t)rgt; K.s[p] = rcs; K.e[p] = rce; } ++p; }
+    if (keepC) { if (p < CW_LDS) { K.i[p] = (uint32_t)c; K.s[p] = cs; K.e[p] = ce; } }
   }
-  // the state after the window (uniform)
-  W.nk = base + (uint32_t)__shfl((int)inc, 63, 64);
+  // the state after the window (uniform: lane reads)
+  W.nk = base + (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
   if (R >= 0) W.ovf = false;
   if (W.nk > CW_LDS) W.ovf = true;
-  const int64_t dl63 = __shfl(neg ? d : D_MINUS, 63, 64);
-  const int64_t m63 = __shfl(pm, 63, 64);  // (lane 63's exclusive max: lanes 0..62 and the incoming ld)
-  if (ld0z || zm) W.ld = 0;
-  else W.ld = m63 > dl63 ? m63 : dl63;
+  if (ld0z || zm) {
+    W.ld = 0;
+  } else {
+    const int64_t dl63 = rl64(neg ? d : D_MINUS, 63), m63 = rl64(pm, 63);
+    W.ld = m63 > dl63 ? m63 : dl63;
+  }
   if (lm) {
     const int L = last_set(lm);
-    W.left = __shfl(c, L, 64);
-    W.lce = __shfl(ce, L, 64);
+    W.left = rl64(c, L);
+    W.lcs = rl64(cs, L);
+    W.lce = rl64(ce, L);
   }
-  if (cm) W.lc = __shfl((int)lc_after, last_set(cm), 64) != 0;
-  if (rm) W.right = __shfl(c, last_set(rm), 64);
-  const int fB = __shfl((int)firstR, B < 64 ? B : 0, 64);
-  const int64_t dB = __shfl(d, B < 64 ? B : 0, 64);
-  if (B < 64 && fB) W.rdist = dB;
-  else if (__ballot(hangR || in_a || in_d)) W.rdist = 0;
+  if (cm) W.lc = ((lam >> last_set(cm)) & 1) != 0;
+  if (rm) {
+    const int L = last_set(rm);
+    W.right = rl64(c, L);
+    W.rcs = rl64(cs, L);
+    W.rce = rl64(ce, L);
+  }
+  if (B < 64 && (__ballot(firstR) >> B) & 1) W.rdist = rl64(d, B);
+  else if (r0m) W.rdist = 0;
   brk = B < (int)cnt;
   return brk ? (uint32_t)B + 1 : cnt;
 }
 
-// ref rows [b0, b1) from the wave's state (fp, stack stk[0, n) bottom first); false when
-// the stack or the kept list outgrew LDS
-__device__ bool cw_run(const ClArgs& A, uint64_t b0, uint64_t b1, uint64_t& fp, uint32_t& n, uint32_t* stk,
-                       uint32_t* kept, bool emit) {
+// the file rows [fa, fa + 128) in two register blocks (lane j: rows fa + j, fa + 64 + j)
+struct CwFile {
+  uint64_t fa;
+  int64_t s0, e0, s1, e1;
+};
+__device__ __forceinline__ void cw_load(const ClArgs& A, uint64_t r, int64_t& s, int64_t& e) {
+  s = r < A.nc ? A.cs[r] : LLONG_MAX;
+  e = r < A.nc ? A.ce[r] : LLONG_MAX;
+}
+__device__ __forceinline__ void cw_file_at(const ClArgs& A, CwFile& F, uint64_t fp) {
+  F.fa = fp;
+  cw_load(A, fp + bg_lane(), F.s0, F.e0);
+  cw_load(A, fp + 64 + bg_lane(), F.s1, F.e1);
+}
+// keep fp inside the first block: move on by whole blocks (the next block's load is issued
+// here, a window before it is read)
+__device__ __forceinline__ void cw_file_follow(const ClArgs& A, CwFile& F, uint64_t fp) {
+  if (fp >= F.fa + 128) {
+    cw_file_at(A, F, fp);
+  } else if (fp >= F.fa + 64) {
+    F.s0 = F.s1;
+    F.e0 = F.e1;
+    F.fa += 64;
+    cw_load(A, F.fa + 64 + bg_lane(), F.s1, F.e1);
+  }
+}
+
+// ref rows [b0, b1) from the wave's state (fp, stack K[0, n) bottom first, F at fp); false
+// when the stack or the kept list outgrew LDS
+__device__ bool cw_run(const ClArgs& A, uint64_t b0, uint64_t b1, uint64_t& fp, uint32_t& n, CwKeys& S,
+                       CwKeys& K, CwFile& F, bool emit) {
   const int lane = bg_lane();
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
     const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
-    WaveCl W{D_MINUS, D_PLUS, -1, -1, 0, false, 0u, false};
-    bool brk = false;
-    while (n && !brk) {  // the cache, from the top
-      const uint32_t cnt = n < 64 ? n : 64u;
-      const bool v = (uint32_t)lane < cnt;
-      const int64_t c = v ? (int64_t)stk[n - 1 - lane] : 0;
-      const int64_t cs = v ? A.cs[c] : 0, ce = v ? A.ce[c] : 0;
-      n -= cw_window(A, W, kept, bs, be, cen, v, cnt, c, cs, ce, brk);
-    }
-    bool eof = false;
-    while (!brk) {  // the file
-      if (fp >= A.nc) {
+    WaveCl W{D_MINUS, D_PLUS, -1, -1, 0, 0, 0, 0, false, 0u, false};
+    bool brk = false, eof = false;
+    while (!brk) {
+      // lanes [0, ns): the cache from the top; lanes [ns, cnt): the file from fp
+      const uint32_t ns = n < 64 ? n : 64u;
+      const uint64_t rem = fp < A.nc ? A.nc - fp : 0;
+      const uint32_t nf = ns < 64 ? (uint32_t)min<uint64_t>(64 - ns, rem) : 0u;
+      const uint32_t cnt = ns + nf;
+      if (cnt == 0) {
         eof = true;
         break;
       }
-      const uint64_t left_in_file = A.nc - fp;
-      const uint32_t cnt = left_in_file < 64 ? (uint32_t)left_in_file : 64u;
+      const bool fromstk = (uint32_t)lane < ns;
       const bool v = (uint32_t)lane < cnt;
-      const int64_t c = (int64_t)fp + lane;
-      const int64_t cs = v ? A.cs[c] : 0, ce = v ? A.ce[c] : 0;
-      fp += cw_window(A, W, kept, bs, be, cen, v, cnt, c, cs, ce, brk);
+      const uint32_t q = fromstk ? n - 1 - lane : 0;
+      const int j = (int)(fp - F.fa) + lane - (int)ns;  // the lane's row in the file blocks (< 128)
+      const int src = j & 63;
+      const int64_t fs0 = bperm64(F.s0, src), fe0 = bperm64(F.e0, src);
+      const int64_t fs1 = bperm64(F.s1, src), fe1 = bperm64(F.e1, src);
+      int64_t c, cs, ce;
+      if (fromstk) {
+        c = S.i[q];
+        cs = S.s[q];
+        ce = S.e[q];
+      } else {
+        c = (int64_t)(fp + (uint64_t)(lane - (int)ns));
+        cs = j < 64 ? fs0 : fs1;
+        ce = j < 64 ? fe0 : fe1;
+      }
+      const uint32_t used = cw_window(A, W, K, bs, be, cen, v, cnt, c, cs, ce, brk);
+      if (used <= ns) {
+        n -= used;
+      } else {
+        n -= ns;
+        fp += used - ns;
+        cw_file_follow(A, F, fp);
+      }
     }
     if (eof) {
       if (W.left >= 0 && !W.lc) {
-        if (lane == 0 && W.nk < CW_LDS) kept[W.nk] = (uint32_t)W.left;
+        if (lane == 0 && W.nk < CW_LDS) { K.i[W.nk] = (uint32_t)W.left; K.s[W.nk] = W.lcs; K.e[W.nk] = W.lce; }
         ++W.nk;
       }
       if (W.right >= 0) {
-        if (lane == 0 && W.nk < CW_LDS) kept[W.nk] = (uint32_t)W.right;
+        if (lane == 0 && W.nk < CW_LDS) { K.i[W.nk] = (uint32_t)W.right; K.s[W.nk] = W.rcs; K.e[W.nk] = W.rce; }
         ++W.nk;
       }
     }
     if (W.ovf || W.nk > CW_LDS || n + W.nk > CW_LDS || n + W.nk > A.cap) return false;
     __builtin_amdgcn_wave_barrier();
     // BedReader::PushBack(list): the list comes back out in list order
-    for (uint32_t t = lane; t < W.nk; t += 64) stk[n + t] = kept[W.nk - 1 - t];
+    for (uint32_t t = lane; t < W.nk; t += 64) {
+      const uint32_t f = W.nk - 1 - t;
+      S.i[n + t] = K.i[f];
+      S.s[n + t] = K.s[f];
+      S.e[n + t] = K.e[f];
+    }
     __builtin_amdgcn_wave_barrier();
     n += W.nk;
     if (emit && lane == 0) {
@@ -697,9 +813,9 @@ __device__ bool cw_run(const ClArgs& A, uint64_t b0, uint64_t b1, uint64_t& fp, 
   return true;
 }
 
-__device__ __forceinline__ void cw_store(const ClArgs& A, uint64_t slot, uint64_t fp, uint32_t n, const uint32_t* stk) {
+__device__ __forceinline__ void cw_store(const ClArgs& A, uint64_t slot, uint64_t fp, uint32_t n, const CwKeys& S) {
   uint32_t* g = cl_slot(A, slot);
-  for (uint32_t t = bg_lane(); t < n; t += 64) g[t] = stk[t];
+  for (uint32_t t = bg_lane(); t < n; t += 64) g[t] = S.i[t];
   if (bg_lane() == 0) {
     A.st_fp[slot] = fp;
     A.st_n[slot] = n;
@@ -707,11 +823,11 @@ __device__ __forceinline__ void cw_store(const ClArgs& A, uint64_t slot, uint64_
 }
 
 __global__ void __launch_bounds__(64 * CW_WAVES) k_closest_wave(ClArgs A) {
-  __shared__ uint32_t lstk[CW_WAVES][CW_LDS], lkept[CW_WAVES][CW_LDS];
+  __shared__ CwKeys lstk[CW_WAVES], lkept[CW_WAVES];
   const uint32_t k = blockIdx.x * CW_WAVES + bg_wave();
   if (k >= A.nchunks) return;
-  uint32_t* stk = lstk[bg_wave()];
-  uint32_t* kept = lkept[bg_wave()];
+  CwKeys& S = lstk[bg_wave()];
+  CwKeys& K = lkept[bg_wave()];
   const uint64_t q0 = (uint64_t)k * A.cq, q1 = min(q0 + A.cq, A.nq);
   uint64_t fp = 0;
   uint32_t n = 0;
@@ -721,11 +837,13 @@ __global__ void __launch_bounds__(64 * CW_WAVES) k_closest_wave(ClArgs A) {
     const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
     const uint64_t f = lower_bound_i64(A.cs, A.nc, A.qs[qw] - A.lmax - 1);
     fp = (p - f > CBACK) ? p - CBACK : f;
-    ok = cw_run(A, qw, q0, fp, n, stk, kept, false);
   }
+  CwFile F;
+  cw_file_at(A, F, fp);
+  if (k > 0) ok = cw_run(A, q0 - A.cw, q0, fp, n, S, K, F, false);
   if (ok) {
-    cw_store(A, 2ull * k, fp, n, stk);  // the start state
-    ok = cw_run(A, q0, q1, fp, n, stk, kept, true);
+    cw_store(A, 2ull * k, fp, n, S);  // the start state
+    ok = cw_run(A, q0, q1, fp, n, S, K, F, true);
   }
   if (!ok) {
     if (k == 0) {
@@ -740,7 +858,7 @@ __global__ void __launch_bounds__(64 * CW_WAVES) k_closest_wave(ClArgs A) {
     }
     return;
   }
-  cw_store(A, 2ull * k + 1, fp, n, stk);
+  cw_store(A, 2ull * k + 1, fp, n, S);
 }
 
 // one attempt at capacity A.cap; *ovf set if some state outgrew it
@@ -839,6 +957,7 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
   A.cs = C->ks; A.ce = C->ke; A.nc = C->n;
   A.overlaps = !o->no_overlaps;
   A.lmax = C->maxlen;
+  A.apf = getenv("BEDGPU_CLOSEST_APF") && atoi(getenv("BEDGPU_CLOSEST_APF")) == 1;
   A.left = r->left; A.right = r->right;
   A.cq = getenv("BEDGPU_CLOSEST_CQ") ? (uint32_t)atoi(getenv("BEDGPU_CLOSEST_CQ")) : CQ_DEF;
   A.cw = getenv("BEDGPU_CLOSEST_CW") ? (uint32_t)atoi(getenv("BEDGPU_CLOSEST_CW")) : CW_DEF;
@@ -847,8 +966,8 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
   int rc = 0;
   // the reader cache of the reference can hold many rows on nested inputs: grow the
   // per-chunk state capacity until it fits (bounded by device memory)
-  // BEDGPU_CLOSEST_WAVE=0: the thread-per-chunk kernel (k_closest_chunks) for every chunk
-  bool wave = !(getenv("BEDGPU_CLOSEST_WAVE") && atoi(getenv("BEDGPU_CLOSEST_WAVE")) == 0);
+  // BEDGPU_CLOSEST_WAVE=1: the wave-per-chunk kernel (k_closest_wave) first
+  bool wave = getenv("BEDGPU_CLOSEST_WAVE") && atoi(getenv("BEDGPU_CLOSEST_WAVE")) == 1;
   for (A.cap = CAP0;; A.cap *= 4) {
     bool ovf = false;
     rc = closest_pass(c, A, &ovf, &wave);

@@ -62,6 +62,7 @@ struct FmtArgs {
   const int64_t* zin;  // zero-length rows: sweep-window membership (bg_map_live)
   const int64_t* zout;
   const int64_t* maddr;  // map rows' heap addresses (bg_heap.hip), null: row order
+  const uint32_t* maord;  // each tie run of equal (start, end) by increasing address (after maddr)
   uint64_t n2;           // map rows
   int crit, mapfields, mdlen;
   int64_t ovr, range;
@@ -558,6 +559,17 @@ __device__ __forceinline__ void map_window_genomic(const FmtArgs& A, uint64_t k,
       uint64_t t = m + 1;
       while (t < tend && A.s2[t] == A.s2[m] && A.e2[t] == A.e2[m]) ++t;
       skip = t;
+      if (A.maord) {  // the whole run in address order (bg_heap_addr), its rows [m, t) taken
+        uint64_t r0 = m, r1 = t;
+        while (r0 > 0 && A.s2[r0 - 1] == A.s2[m] && A.e2[r0 - 1] == A.e2[m]) --r0;
+        while (r1 < A.n2 && A.s2[r1] == A.s2[m] && A.e2[r1] == A.e2[m]) ++r1;
+        for (uint64_t q = r0; q < r1; ++q) {
+          const uint64_t u = A.maord[q];
+          if (u < m || u >= t || !member(u)) continue;
+          if (!f(u)) return false;
+        }
+        return true;
+      }
       bool has = false;
       int64_t last = 0;
       for (;;) {  // the run's members by increasing address
@@ -1264,6 +1276,7 @@ static void fill_args(bg_result* r, FmtArgs& A) {
       A.zout = r->zout;
       A.maddr = r->maddr;
       A.n2 = M->n;
+      A.maord = r->maddr ? reinterpret_cast<const uint32_t*>(r->maddr + M->n) : nullptr;
       A.lrows = r->lrows;
       A.crit = r->mopts.faster ? BG_OVR_FAST : r->mopts.criterion;  // --faster: the deque is the window
       A.ovr = (int64_t)r->mopts.overlap_bp;

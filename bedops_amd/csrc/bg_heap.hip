@@ -303,9 +303,25 @@ int bg_heap_addr(bg_ctx* c, bg_set* set, const bg_table* R, const bg_table* M, i
   P.keyed.resize((size_t)spec->nops);
   if (single) P.run1();
   else P.run2();
-  int64_t* d = (int64_t*)bg_alloc(c, 8 * (nm ? nm : 1));
+  // after the nm addresses: each run of rows equal in (start, end) listed by increasing address
+  // (uint32 row indices, identity outside runs), so the formatter walks a tie run in
+  // GenomicAddressCompare order in O(run) instead of selecting the next address each time
+  std::vector<uint32_t> ord(nm);
+  for (uint64_t m = 0; m < nm;) {
+    uint64_t t = m + 1;
+    while (t < nm && hMS[t] == hMS[m] && hME[t] == hME[m]) ++t;
+    for (uint64_t u = m; u < t; ++u) ord[u] = (uint32_t)u;
+    if (t - m > 1)
+      std::sort(ord.begin() + (ptrdiff_t)m, ord.begin() + (ptrdiff_t)t,
+                [&](uint32_t a, uint32_t b) { return addr[a] < addr[b]; });
+    m = t;
+  }
+  int64_t* d = (int64_t*)bg_alloc(c, 8 * (nm ? nm : 1) + 4 * nm);
   if (!d) return BG_E_NOMEM;
-  if (nm) BG_HIP(c, hipMemcpyAsync(d, addr.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
+  if (nm) {
+    BG_HIP(c, hipMemcpyAsync(d, addr.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
+    BG_HIP(c, hipMemcpyAsync(d + nm, ord.data(), 4 * nm, hipMemcpyHostToDevice, c->stream));
+  }
   BG_HIP(c, hipStreamSynchronize(c->stream));
   *out = d;
   return 0;

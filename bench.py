@@ -54,9 +54,10 @@ REF_BEDMAP_R5M = {"rows": 4999998, "bytes": 54515904, "sha16": "899ec7973e166e2d
 # files (tools/pin_fullsize.py run in the build container -> tests/golden/ref_fullsize.json)
 try:
     with open(os.path.join(ROOT, "tests", "golden", "ref_fullsize.json")) as _f:
-        REF_FULL = {k: v["output"] for k, v in json.load(_f).items()}
+        REF_PINS = json.load(_f)
+    REF_FULL = {k: v["output"] for k, v in REF_PINS.items()}
 except OSError:
-    REF_FULL = {}
+    REF_PINS, REF_FULL = {}, {}
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
@@ -390,6 +391,21 @@ def cpu_single(W, paths, rows, td, runs):
                       f"median of {runs}"}
 
 
+def cpu_single_pinned(workload, rows):
+    """run (i) from the pin file: the genuine reference, one process on the same full inputs
+    (same generator, seeds and sizes), timed by tools/pin_fullsize.py in the BUILD container
+    (not on the GPU box: a 3-8 minute single-process run does not fit a box call)"""
+    pin = REF_PINS.get(workload)
+    if not pin or not pin.get("reference_seconds"):
+        return None
+    sec = float(pin["reference_seconds"])
+    return {"value": rows / sec, "unit": "intervals/s", "cores": 1, "kind": "reference",
+            "median_s": sec, "runs_s": [sec], "output_sha16": pin["output"]["sha16"],
+            "measured_in": "build container (tests/golden/ref_fullsize.json), not the GPU box",
+            "sample": f"full inputs ({rows} rows), one process: {pin.get('reference', '')}: "
+                      f"{pin.get('command', '')}"}
+
+
 def cpu_fanout_ref(L, W, paths, rows, td, workers, runs):
     """BASELINE.md run (ii), the reference's documented scale-out (bedops.rst:721-726): one
     `--chrom <c>` process per chromosome over the FULL input files (the reference's own
@@ -454,7 +470,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes of the CPU fan-out, run (ii) (default: min(nproc, 25))")
     ap.add_argument("--cpu-single-runs", type=int, default=1,
-                    help="runs of the one-process reference, run (i) (median; ~60 s each)")
+                    help="runs of the one-process reference, run (i) (median; ~60 s each); 0: take "
+                         "run (i) from tests/golden/ref_fullsize.json (timed in the build container)")
     ap.add_argument("--cpu-fanout-runs", type=int, default=3)
     ap.add_argument("--e2e-runs", type=int, default=3)
     ap.add_argument("--e2e-devices", default=None,
@@ -697,12 +714,13 @@ def main():
                           int(info["cgroup_cpu_quota"]) if info["cgroup_cpu_quota"] else workers)
                 fan = cpu_fanout_ref(L, W, paths, nrows, td, workers, args.cpu_fanout_runs) \
                     if _ref_exe(W) else None
-                single = cpu_single(W, paths, nrows, td, args.cpu_single_runs)
+                single = cpu_single(W, paths, nrows, td, args.cpu_single_runs) if args.cpu_single_runs > 0 \
+                    else cpu_single_pinned(args.workload, nrows)
                 top = fan or single
                 cpu = {"value": top["value"], "unit": "intervals/s",
                        "cores": eff if fan else top["cores"], "processes": top["cores"],
                        "kind": top["kind"], "sample": top["sample"], **info,
-                       "single": single, "fanout": fan}
+                       "single": single, "fanout": fan} if top else None
             for p in paths:
                 os.unlink(p)
 
@@ -730,7 +748,8 @@ def main():
         "e2e_sharded": e2e_sh,
         "e2e_sharded_intervals_per_s": round(e2e_sh["value"], 1) if e2e_sh else None,
         "gpu_vs_cpu": round(e2e["value"] / cpu["value"], 2) if (cpu and e2e) else None,
-        "gpu_vs_cpu_single": round(e2e["value"] / cpu["single"]["value"], 2) if (cpu and e2e) else None,
+        "gpu_vs_cpu_single": round(e2e["value"] / cpu["single"]["value"], 2)
+        if (cpu and e2e and cpu.get("single")) else None,
         "gpu_vs_cpu_back_to_back": round(e2e["back_to_back"]["value"] / cpu["value"], 2)
         if (cpu and e2e and "back_to_back" in e2e) else None,
         "gpu_vs_cpu_scope": ("file->file CLI (median of runs 0.5 s apart, the front process's "

@@ -212,20 +212,20 @@ def run_wave(Q, C, overlaps=True, W=64):
     stack, fp, out, caches = [], 0, [], []
     for b in Q:
         S = {"ld": MINUS, "rdist": PLUS, "left": -1, "right": -1, "lce": 0, "lc": False, "kept": []}
-        brk = False
-        while stack and not brk:
-            cnt = min(W, len(stack))
-            cands = [stack[len(stack) - 1 - i] for i in range(cnt)]
-            used, brk = _window(C, b, cands, S, overlaps)
-            del stack[len(stack) - used:]
-        eof = False
-        while not brk:
-            if fp >= len(C):
+        brk = eof = False
+        while not brk:  # a window: the cache from the top, then file rows in the lanes left
+            ns = min(W, len(stack))
+            nf = min(W - ns, len(C) - fp)
+            if ns + nf == 0:
                 eof = True
                 break
-            cnt = min(W, len(C) - fp)
-            used, brk = _window(C, b, list(range(fp, fp + cnt)), S, overlaps)
-            fp += used
+            cands = [stack[len(stack) - 1 - i] for i in range(ns)] + list(range(fp, fp + nf))
+            used, brk = _window(C, b, cands, S, overlaps)
+            if used <= ns:
+                del stack[len(stack) - used:]
+            else:
+                del stack[len(stack) - ns:]
+                fp += used - ns
         if eof and S["left"] >= 0 and not S["lc"]:
             S["kept"].append(S["left"])
         if eof and S["right"] >= 0:
