@@ -417,6 +417,9 @@ static void maybe_stats(bg_ctx* ctx) {
 #include <sys/prctl.h>
 #include <sys/wait.h>
 static int CLI_DETACH_FD = -1;
+/* a pipe fallback's ctx (cli_stream.h): its whole-file output must have passed the bytes the
+ * chromosome groups already sent (bg_set_output_skip), checked before the exit */
+static bg_ctx* CLI_SKIP_CTX = NULL;
 static pid_t CLI_WORKER = 0;
 /* the front process forwards termination signals to the worker (whose exit it mirrors) */
 static void cli_forward_signal(int sig) {
@@ -444,6 +447,7 @@ static inline void cli_detach(void) {
   if (pipe(p) != 0) return;
   fflush(stdout);
   fflush(stderr);
+  const pid_t front = getpid();
   const pid_t pid = fork();
   if (pid < 0) {
     close(p[0]);
@@ -456,7 +460,8 @@ static inline void cli_detach(void) {
     /* a front process killed outright (SIGKILL) takes the worker with it; cleared again in
      * fast_exit once the output is complete */
     prctl(PR_SET_PDEATHSIG, SIGKILL);
-    if (getppid() == 1) _exit(EXIT_FAILURE);
+    /* the front died before prctl: reparented (to init or to a subreaper, whatever its pid) */
+    if (getppid() != front) _exit(EXIT_FAILURE);
     return;
   }
   close(p[1]);
@@ -489,6 +494,12 @@ static inline void cli_detach(void) {
  * every HBM block, the pinned ring and the HIP runtime costs ~0.3 s; the kernel driver
  * reclaims a process's GPU resources at exit). Output went through write(2) only. */
 static inline void fast_exit(void) {
+  if (CLI_SKIP_CTX) {
+    uint64_t left = 0;
+    if (bg_output_skip_left(CLI_SKIP_CTX, &left) != 0 || left != 0)
+      die_msg("bedgpu", "the whole-file output is shorter than the part already sent down the pipe");
+    CLI_SKIP_CTX = NULL;
+  }
   fflush(stdout);
   fflush(stderr);
   cli_mark("exit");

@@ -212,9 +212,21 @@ static void* shard_writer(void* p) {
   sh_write_job_t* W = (sh_write_job_t*)p;
   shard_job_t* J = W->J;
   W->rc = bg_bind(J->ctx);
-  for (int g = 0; g < W->ngc && !W->rc; ++g)
-    if (W->owner[g] == J->dev && J->len[g])
-      W->rc = bg_pwrite_device(J->ctx, J->text + J->off[g], J->len[g], 1, (int64_t)(W->off0 + (off_t)W->pos[g]));
+  /* chromosomes adjacent both in this device's text and in the output go out as one range
+   * (one ring pass instead of one per contig: assemblies with thousands of scaffolds) */
+  uint64_t rt = 0, ro = 0, rl = 0;
+  for (int g = 0; g < W->ngc && !W->rc; ++g) {
+    if (W->owner[g] != J->dev || !J->len[g]) continue;
+    if (rl && J->off[g] == rt + rl && W->pos[g] == ro + rl) {
+      rl += J->len[g];
+      continue;
+    }
+    if (rl) W->rc = bg_pwrite_device(J->ctx, J->text + rt, rl, 1, (int64_t)(W->off0 + (off_t)ro));
+    rt = J->off[g];
+    ro = W->pos[g];
+    rl = J->len[g];
+  }
+  if (rl && !W->rc) W->rc = bg_pwrite_device(J->ctx, J->text + rt, rl, 1, (int64_t)(W->off0 + (off_t)ro));
   return NULL;
 }
 

@@ -375,6 +375,7 @@ static int stream_run(bg_ctx* ctx, const bg_input* proto, shard_op_fn op, void* 
       /* the groups written so far are the whole-file output's first `sent` bytes (every
        * covered operation is chromosome-local): the whole-file path continues after them */
       if (pushed && bg_set_output_skip(ctx, sent) != 0) die_ctx(CLI_PROG, ctx, rc);
+      if (pushed) CLI_SKIP_CTX = ctx;  /* fast_exit checks the rerun passed `sent` */
       return 1;
     }
     /* never write the whole-file output after leftover group output */

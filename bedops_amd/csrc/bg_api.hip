@@ -40,7 +40,13 @@ static void pool_start(bg_ctx* c, int n);
 void bg_pool_stop(bg_ctx* c);
 
 int bg_fail(bg_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
+  if (!c) return code;
+  if (std::this_thread::get_id() != c->owner) {
+    std::lock_guard<std::mutex> g(c->copy_mu);
+    c->err_async = msg;
+    return code;
+  }
+  c->err = msg;
   return code;
 }
 
@@ -181,6 +187,7 @@ extern "C" int bg_open(bg_ctx** out, int device) {
   if (!out) return BG_E_ARG;
   *out = nullptr;
   bg_ctx* c = new bg_ctx();
+  c->owner = std::this_thread::get_id();
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -279,7 +286,18 @@ uint32_t bg_resident_blocks(bg_ctx* c, const void* kern) {
   return n;
 }
 
-extern "C" const char* bg_last_error(const bg_ctx* c) { return c ? c->err.c_str() : "no context"; }
+extern "C" const char* bg_last_error(const bg_ctx* c) {
+  if (!c) return "no context";
+  bg_ctx* m = const_cast<bg_ctx*>(c);
+  {
+    std::lock_guard<std::mutex> g(m->copy_mu);
+    if (!m->err_async.empty()) {
+      m->err = m->err_async;
+      m->err_async.clear();
+    }
+  }
+  return m->err.c_str();
+}
 
 extern "C" int bg_sync(bg_ctx* c) {
   BG_HIP(c, hipStreamSynchronize(c->stream));
@@ -1047,6 +1065,12 @@ static int write_device_ring(bg_ctx* c, const void* d, uint64_t n, int fd, off_t
 extern "C" int bg_set_output_skip(bg_ctx* c, uint64_t n) {
   if (!c) return BG_E_ARG;
   c->out_skip = n;
+  return 0;
+}
+
+extern "C" int bg_output_skip_left(const bg_ctx* c, uint64_t* n) {
+  if (!c || !n) return BG_E_ARG;
+  *n = c->out_skip;
   return 0;
 }
 

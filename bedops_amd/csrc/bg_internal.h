@@ -92,7 +92,12 @@ struct bg_ctx {
   std::vector<hipEvent_t> copy_ev;  // bg_file_image_copy slots
   std::vector<hipEvent_t> order_ev;  // bg_copy_order: ctx's stream position a slot's copies wait for
   std::vector<char> order_set;
-  std::mutex copy_mu;
+  std::mutex copy_mu;  // (also guards err_async)
+  // errors raised on another host thread (the read-ahead copier, bg_file_image_copy) land in
+  // err_async under copy_mu and move to err when bg_last_error is read on the owner's side;
+  // only the thread that launches work may call bg_alloc / bg_release
+  std::thread::id owner;
+  std::string err_async;
   hipEvent_t cjoin = nullptr;     // its copies -> ctx's stream
   hipStream_t stream = nullptr;
   // side stream: a set input's post-parse passes (bg_load.hip) run there beside the next

@@ -248,6 +248,8 @@ int bg_pwrite_device(bg_ctx* ctx, const void* dptr, uint64_t n, int fd, int64_t 
  * across calls): a run whose first part already went down a pipe (the drop-ins' chromosome
  * groups, cli_stream.h) redoes the whole file and continues the output after that part */
 int bg_set_output_skip(bg_ctx* ctx, uint64_t n);
+/* the part of a bg_set_output_skip not yet dropped (0 once the output has passed it) */
+int bg_output_skip_left(const bg_ctx* ctx, uint64_t* n);
 /* read a regular file into a new device buffer of ctx's device (its host image DMA'd to HBM,
  * see bg_file_image below); load it with bg_input.on_device = 1, free with bg_device_free.
  * Replaces the reader side of allocate_iterator_starch_bed for plain BED files
