@@ -54,7 +54,7 @@ SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_l
            "bg_group_size", "bg_group_ctx", "bg_group_close", "bg_group_gather", "bg_device_free",
            "bg_device_gather_host", "bg_read_file_device", "bg_sortbed", "bg_starch_is",
            "bg_starch_decode", "bg_file_image_open", "bg_file_image_register", "bg_file_image_to_device",
-           "bg_file_image_close", "bg_pwrite_device", "bg_device_release", "bg_set_output_skip",
+           "bg_file_image_close", "bg_pwrite_device", "bg_device_release", "bg_set_output_skip", "bg_output_skip_left",
            "bg_device_alloc", "bg_file_image_copy", "bg_copy_order", "bg_copy_fence"]
 UID_BYTES = 128
 
