@@ -43,6 +43,7 @@ struct bg_dstatus {
   unsigned long long stop_row;   // bedmap: first row where the reference throws (~0: none)
   unsigned long long pad[2];
   unsigned long long nbig;       // BED5 scores left to the exact big-number conversion (k_score_big)
+  unsigned long long nrows;      // k_parse_n without a scout pass: the input's lines (its last tile's prefix)
 };
 
 // bedmap: map rows longer than thr, by length class (see bg_map_cands below)
@@ -72,6 +73,7 @@ struct bg_buf {
 struct bg_ctx {
   int device = 0;
   bool row_wide = false;  // bg_load: rows parsed by k_parse (a redo after BG_ROW_OVERFLOW)
+  bool row_scout = false;  // bg_load: row offsets from the k_scout pass (a redo after BG_ROW_LOOKBACK)
   uint64_t out_skip = 0;  // bytes write_device_ring still drops (bg_set_output_skip)
   int ncu = 256;  // compute units
   std::vector<std::pair<const void*, uint32_t>> resident;  // kernel -> resident BG_NT blocks

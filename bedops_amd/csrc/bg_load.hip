@@ -175,6 +175,29 @@ __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt
   }
 }
 
+// newlines of `ns` tiles spread evenly over the input (sample k of ntiles: tile k * ntiles / ns),
+// summed into *cnt: the row loaders without a scout pass size their columns from it
+__global__ void __launch_bounds__(BG_NT) k_sample_nl(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
+                                                     uint32_t ns, unsigned long long* __restrict__ cnt) {
+  __shared__ uint32_t sh[BG_NT / 64];
+  const uint64_t t = (uint64_t)blockIdx.x * ntiles / ns;
+  const int64_t b = (int64_t)t * TT + (int64_t)threadIdx.x * 32;
+  const uint4 a = load16(txt, b, nb), v = load16(txt, b + 16, nb);
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, v.x, v.y, v.z, v.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c += __popc(nl_mask4(w[k]));
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if (bg_lane() == 0) sh[bg_wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int q = 0; q < BG_NT / 64; ++q) s += sh[q];
+    atomicAdd(cnt, (unsigned long long)s);
+  }
+}
+
 // line_token's hash of the line at ls from three aligned 16-byte loads, when the line
 // starts with its token (no leading whitespace) of at most 16 bytes ending within 32
 // bytes; false: the caller takes the byte loop
@@ -1048,9 +1071,10 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
 
 // sort order across tile boundaries: the first rows of each tile vs their predecessors
 __global__ void k_check_bounds(const int64_t* __restrict__ KS, const uint64_t* __restrict__ row0,
-                               uint32_t ntiles, uint64_t nrows, bg_dstatus* st) {
+                               uint32_t ntiles, uint64_t nrows, bg_dstatus* st, int from_status) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
+  if (from_status) nrows = min(nrows, (uint64_t)st->nrows);  // (k_parse_n counted them)
   const uint64_t r = row0[t];
   for (uint64_t q = r; q < r + 2 && q < nrows; ++q)
     if (q > 0 && KS[q] < KS[q - 1]) bg_report(st, q, ERR_UNSORTED);
@@ -1177,6 +1201,7 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 #define SCAP 512
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
 #define BG_ROW_OVERFLOW 16ULL  // k_parse_n: a tile of more than LCAP_WS lines
+#define BG_ROW_LOOKBACK 128ULL  // k_parse_n without a scout pass: rows past the estimated capacity, or a look-back that timed out
 
 __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
   v = max(v, dpp32<0x111, 0xF, true>(v));
@@ -1535,16 +1560,72 @@ __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const ui
 // 8 KiB tile, the tile classified for whitespace only (tile_prologue_n<NT, true>), fields and
 // digits checked in parse_line_fast_ws / parse_score_fast_ws. Lines the fast path refuses
 // take parse_line_slow in the same loop. Same outputs and error reports as k_parse.
+// The row offsets without a scout pass: a decoupled look-back over the tiles' newline counts.
+// Tile t publishes its count c_t (newlines in [t0, t0 + TT)) as an aggregate as soon as its
+// prologue has found its lines, then walks back over the tiles before it, 64 at a time (one
+// per lane, agent-scope atomic loads: the words are the only data exchanged, flag and value in
+// one 64-bit word), summing aggregates until it reaches a tile that has published its
+// inclusive prefix; then it publishes its own inclusive prefix. Tiles only wait on lower
+// tiles, which were dispatched before them; a wait that outlasts LB_SPIN polls (never seen)
+// publishes anyway and flags BG_ROW_LOOKBACK, and bg_load redoes the load with k_scout.
+#define LB_AGG (1ull << 62)
+#define LB_INC (2ull << 62)
+#define LB_VAL ((1ull << 62) - 1)
+#define LB_SPIN (1u << 22)
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave 0 of tile t: the exclusive prefix of the counts (all lanes return it)
+__device__ uint64_t lb_prefix(uint64_t* __restrict__ words, uint32_t t, uint64_t c, bg_dstatus* st) {
+  const int lane = bg_lane();
+  if (t == 0) {
+    if (lane == 0) lb_store(&words[0], LB_INC | c);
+    return 0;
+  }
+  if (lane == 0) lb_store(&words[t], LB_AGG | c);
+  uint64_t excl = 0;
+  int64_t u = (int64_t)t - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t idx = u - lane;
+    const uint64_t w = idx >= 0 ? lb_load(&words[idx]) : LB_INC;  // before tile 0: 0
+    const uint32_t f = (uint32_t)(w >> 62);
+    const uint64_t pm = __ballot(f == 2), zm = __ballot(f == 0);
+    const int fp = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
+    const uint64_t below = fp == 64 ? ~0ull : ((2ull << fp) - 1);  // lanes 0..fp
+    if (zm & below) {  // a tile before the nearest inclusive one has not published yet
+      if (++spins > LB_SPIN) {
+        if (lane == 0) atomicOr(&st->flags, BG_ROW_LOOKBACK);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    uint64_t v = (uint64_t)lane <= (uint64_t)fp ? (w & LB_VAL) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    excl += v;
+    if (fp < 64) break;
+    u -= 64;
+  }
+  if (lane == 0) lb_store(&words[t], LB_INC | (excl + c));
+  return excl;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_n(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
+    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, uint64_t* __restrict__ row0,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
-    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap) {
+    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap, uint64_t* __restrict__ lbw) {
   __shared__ ParseLdsWs S;
   constexpr uint32_t NR = LCAP_WS / NT;  // rounds of NT lines at most
   __shared__ int64_t kfirst[NR][NT / 64], klast[NR][NT / 64];  // keys at the waves' edges
+  __shared__ uint64_t s_row0;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   int64_t last_end = -1;
   uint32_t L;
@@ -1555,7 +1636,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
   }
   const auto& B = S.b[0];
   const bool has0 = (t0 == 0) || B.buf[HB - 1] == '\n';
-  const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1);  // row of the first owned line
+  uint64_t rt;  // newlines before the tile
+  if (lbw) {  // no scout pass: the look-back (nrows = the columns' capacity)
+    if (threadIdx.x < 64) {
+      // L = newlines in [t0, t0 + TT - 1) + has0: the tile's own count adds its last byte
+      const uint64_t c = (uint64_t)L - (has0 ? 1u : 0u) + (B.buf[HB + TT - 1] == '\n' ? 1u : 0u);
+      const uint64_t ex = lb_prefix(lbw, blockIdx.x, c, st);
+      if (threadIdx.x == 0) {
+        s_row0 = ex;
+        row0[blockIdx.x] = ex;
+        if (blockIdx.x + 1 == gridDim.x) st->nrows = ex + c;
+      }
+    }
+    __syncthreads();
+    rt = s_row0;
+  } else {
+    rt = row0[blockIdx.x];
+  }
+  const uint64_t r0 = rt + (has0 ? 0 : 1);  // row of the first owned line
   if (L > LCAP_WS) return;  // (BG_ROW_OVERFLOW: the load is redone with k_parse)
   const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];
   const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
@@ -1569,7 +1667,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8)))
     const int64_t ls = k < L ? t0 + S.lst[k] : 0;
     const uint64_t r = r0 + k;
     const int64_t le = k >= L ? -1 : (k + 1 < L) ? t0 + S.lst[k + 1] - 1 : last_end;
-    if (k < L && r < nrows && le >= 0) {  // r >= nrows: the unterminated last line (dropped)
+    if (lbw && k < L && le >= 0 && r >= nrows) atomicOr(&st->flags, BG_ROW_LOOKBACK);  // past the capacity
+    if (k < L && r < nrows && le >= 0) {  // le < 0 / r >= nrows: the unterminated last line (dropped)
       Fast F;
       const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
       const RunInfo& I = R.info[run];
@@ -2666,6 +2765,9 @@ struct LoadState {
   uint32_t* absorbed = nullptr;
   int64_t* tgb = nullptr;
   uint32_t set_nt = 0;  // staging units of a BG_BED3_SET parse whose merge passes are pending
+  // row loads without a scout pass (k_parse_n's look-back): tile words, sampled tiles
+  uint64_t* lbw = nullptr;
+  uint32_t nsamp = 0;
   // BED5: scores for k_score_big, (row, first byte) pairs
   uint64_t* big = nullptr;
   uint32_t bigcap = 0;
@@ -2677,7 +2779,7 @@ static void release_state(bg_ctx* c, LoadState& S) {
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
                   (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed,
-                  (void*)S.tgb, (void*)S.big})
+                  (void*)S.tgb, (void*)S.big, (void*)S.lbw})
     bg_release(c, p);
   S = LoadState();
 }
@@ -2707,11 +2809,34 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   // a boundary tile records at most one entry per line (+1)
   S.rc = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
   const bool set = in.kind == BG_BED3_SET;  // no row numbers: no scout pass
+  // row loads: the scout pass counts every tile's lines first (k_scout, a streaming read at
+  // ~6 TB/s). BEDGPU_ROW_LOOKBACK=1 drops it: k_parse_n finds the row offsets by a decoupled
+  // look-back and the columns are sized from a sample of the tiles' newline counts — exact
+  // (the GPU suite passes with it) but measured slower: bedmap 50M x 500M k_parse 11.4 ->
+  // 20.7 ms against the 3.3 ms k_scout it saves (waves spinning on their predecessors' words
+  // hold the slots the parse needs), so it stays off
+  static const bool scout_env = [] {
+    const char* e = getenv("BEDGPU_ROW_LOOKBACK");
+    const char* p = getenv("BEDGPU_ROW_PARSE");  // (0: k_parse, which takes the scout's offsets)
+    return !(e && atoi(e) == 1) || (p && atoi(p) == 0);
+  }();
+  const bool scout = !set && (scout_env || c->row_scout || c->row_wide);
   if (!set) {
-    S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
     S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
+    if (!S.row0) return BG_E_NOMEM;
+  }
+  if (scout) {
+    S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
     S.fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
-    if (!S.cnt || !S.row0 || !S.fnl) return BG_E_NOMEM;
+    if (!S.cnt || !S.fnl) return BG_E_NOMEM;
+  } else if (!set) {
+    S.lbw = (uint64_t*)bg_alloc(c, 8ull * nt);
+    if (!S.lbw) return BG_E_NOMEM;
+    BG_HIP(c, hipMemsetAsync(S.lbw, 0, 8ull * nt, c->stream));
+    S.nsamp = std::min<uint32_t>(nt, 4096);
+    BG_LAUNCH(c, "k_sample_nl", k_sample_nl, dim3(S.nsamp), dim3(BG_NT), txt, S.nb, nt, S.nsamp,
+              (unsigned long long*)&ctr[0]);
+    BG_HIP(c, hipGetLastError());
   }
   S.fls = (int64_t*)bg_alloc(c, 8ull * nt);
   S.fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
@@ -2719,7 +2844,7 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   S.recs = (RunRec*)bg_alloc(c, sizeof(RunRec) * (size_t)S.rc);
   if (!S.fls || !S.fhash || !S.blist || !S.recs)
     return BG_E_NOMEM;
-  if (!set) {
+  if (scout) {
     BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
               S.cnt, S.fnl);
     BG_HIP(c, hipGetLastError());
@@ -2727,7 +2852,7 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, S.fnl,
             S.fls, S.fhash);
   BG_HIP(c, hipGetLastError());
-  if (!set) {
+  if (scout) {
     int rc = bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
     if (rc) return rc;
   }
@@ -2847,17 +2972,17 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     S.big = (uint64_t*)bg_alloc(c, 16ull * (S.bigcap ? S.bigcap : 1));
     if (!S.big) return BG_E_NOMEM;
   }
-  if (row_n && !c->row_wide)
+  if (S.lbw || (row_n && !c->row_wide))
     BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
               S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
-              S.big, S.bigcap);
+              S.big, S.bigcap, S.lbw);
   else
     BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
               S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
               S.big, S.bigcap);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
-            S.row0, S.ntiles, T->n, st);
+            S.row0, S.ntiles, T->n, st, S.lbw ? 1 : 0);
   BG_HIP(c, hipGetLastError());
   S.nrows_run = nr;  // copied back after every input's parse is queued
   return 0;
@@ -3008,6 +3133,7 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
     T->run_name.clear();
     return 0;
   }
+  if (S.lbw) T->n = std::min<uint64_t>(T->n, h.nrows);  // (the look-back's count; capacity checked)
   int rc = report_status(c, idx, h);
   if (rc) return rc;
   if (h.nbig) {  // scores past the fast paths: exact big-number conversion (bg_strtod.h)
@@ -3122,6 +3248,11 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   for (int i = 0; i < n && !rc; ++i) {
     LoadState& S = st[i];
     s->t[i]->n = S.ntiles ? hctr[8ull * i] : 0;
+    if (S.lbw && S.nsamp) {  // sampled newlines -> the columns' capacity (+12.5% + 4096; overflow: redo)
+      const double est = (double)hctr[8ull * i] * (double)S.ntiles / (double)S.nsamp;
+      const uint64_t cap = (uint64_t)(est * 1.125) + 4096;
+      s->t[i]->n = std::min<uint64_t>(cap, S.nb + 1);
+    }
     const uint32_t nr = (uint32_t)hctr[8ull * i + 2];
     if (nr > S.rc) { rc = bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input"); break; }
     S.nrec = nr;
@@ -3189,6 +3320,10 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   // a row input with a tile of more lines than k_parse_n holds: redone with k_parse
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && (hst[i].flags & BG_ROW_OVERFLOW)) redo = wide = true;
+  // a row input past its estimated capacity (or a look-back that timed out): redone with k_scout
+  bool scoutredo = false;
+  for (int i = 0; i < n && !rc; ++i)
+    if (inputs[i].kind != BG_BED3_SET && st[i].lbw && (hst[i].flags & BG_ROW_LOOKBACK)) redo = scoutredo = true;
   for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
   if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies use the pinned staging
   for (auto& S : st) release_state(c, S);
@@ -3200,10 +3335,12 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     std::vector<bg_input> rows(inputs, inputs + n);
     for (auto& in : rows)
       if (in.kind == BG_BED3_SET) in.kind = BG_BED3;
-    const bool w0 = c->row_wide;
+    const bool w0 = c->row_wide, s0 = c->row_scout;
     if (wide) c->row_wide = true;
+    if (scoutredo) c->row_scout = true;
     const int rc2 = bg_load(c, n, rows.data(), out);
     c->row_wide = w0;
+    c->row_scout = s0;
     return rc2;
   }
   for (bg_table* T : s->t)  // keep every column non-null for empty inputs
