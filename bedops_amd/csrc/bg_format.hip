@@ -1120,6 +1120,75 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_ivl_write(FmtArgs A, const uint64
     *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
 }
 
+// RES_ROWS rows (the input line re-rendered: "%s\t%lu\t%lu" + its rest + "\n", bedops
+// --element-of / --not-element-of): k_fmt_ivl_write's layout — thread t renders rows 2t and
+// 2t+1 of the tile (their row indices, keys and rest spans loaded up front), one block scan of
+// the per-thread byte counts places them, LDS staging, 16-byte stores — instead of
+// k_fmt_write<RES_ROWS>'s two renders per row (a counting one for the stripe scan, then the
+// real one)
+__device__ __forceinline__ void rows_put(const FmtArgs& A, char* p, uint64_t r, int64_t s, int64_t e) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  const uint32_t nl = A.name_len[g];
+  const char* nm = A.names + A.name_off[g];
+  for (uint32_t q = 0; q < nl; ++q) p[q] = nm[q];
+  p += nl;
+  *p++ = '\t';
+  const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
+  const int l1 = dec_len_u64(cs), l2 = dec_len_u64(ce);
+  put_u64_lds(p, cs, l1);
+  p += l1;
+  *p++ = '\t';
+  put_u64_lds(p, ce, l2);
+  p += l2;
+  const uint32_t rl = A.rest_len[r];
+  const char* rp = A.text + A.rest_off[r];
+  for (uint32_t q = 0; q < rl; ++q) p[q] = rp[q];
+  p[rl] = '\n';
+}
+__global__ void __launch_bounds__(BG_NT) k_fmt_rows_write(FmtArgs A, const uint64_t* __restrict__ toff,
+                                                          char* __restrict__ out) {
+  __shared__ uint32_t sh[BG_NT / 64 + 1];
+  __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
+  static_assert(FT_ROWS == 2, "two rows per thread");
+  const uint64_t k0 = (uint64_t)blockIdx.x * FT_TILE + 2ull * threadIdx.x;
+  const bool v0 = k0 < A.n, v1 = k0 + 1 < A.n;
+  uint64_t r0 = 0, r1 = 0;
+  if (v1) {
+    const ulonglong2 R = reinterpret_cast<const ulonglong2*>(A.rows)[k0 >> 1];
+    r0 = R.x;
+    r1 = R.y;
+  } else if (v0) {
+    r0 = A.rows[k0];
+  }
+  const int64_t s0 = v0 ? A.s[r0] : 0, e0 = v0 ? A.e[r0] : 0;
+  const int64_t s1 = v1 ? A.s[r1] : 0, e1 = v1 ? A.e[r1] : 0;
+  const uint32_t l0 = v0 ? bg_ivl_len(A.name_len, s0, e0) + A.rest_len[r0] : 0u;
+  const uint32_t l1 = v1 ? bg_ivl_len(A.name_len, s1, e1) + A.rest_len[r1] : 0u;
+  uint32_t tot;
+  const uint32_t my = block_excl_scan(l0 + l1, OpSum(), 0u, sh, &tot);
+  const uint64_t dst0 = toff[blockIdx.x];
+  if (tot > FT_LDS) {  // oversized tile (long names / rests): render straight to HBM
+    if (v0) rows_put(A, out + dst0 + my, r0, s0, e0);
+    if (v1) rows_put(A, out + dst0 + my + l0, r1, s1, e1);
+    return;
+  }
+  const uint32_t skew = (uint32_t)(dst0 & 15);
+  if (v0) rows_put(A, buf + skew + my, r0, s0, e0);
+  if (v1) rows_put(A, buf + skew + my + l0, r1, s1, e1);
+  __syncthreads();
+  const uint64_t a0 = dst0, a1 = dst0 + tot;
+  const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;
+  const char* bb = buf + skew;
+  if (al0 >= al1) {
+    for (uint64_t p = a0 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+    return;
+  }
+  for (uint64_t p = a0 + threadIdx.x; p < al0; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al1 + threadIdx.x; p < a1; p += BG_NT) out[p] = bb[p - a0];
+  for (uint64_t p = al0 + 16ull * threadIdx.x; p < al1; p += 16ull * BG_NT)
+    *reinterpret_cast<uint4*>(out + p) = *reinterpret_cast<const uint4*>(bb + (p - a0));
+}
+
 // a segmented RES_IVL (bg_result::nseg, straight from k_mp_tile): one workgroup per segment,
 // its byte offset and printed size already scanned (seg_boff), so there is no count pass.
 // The segment's pieces (up to BG_SEG_CAP, ~660 for 100M x 100M --intersect) go in rounds of
@@ -1425,10 +1494,17 @@ count_again:
     if (!d_stop) return BG_E_NOMEM;
     A.stop_out = d_stop;
   }
+  static const bool rows_fast = [] {  // BEDGPU_FMT_ROWS=0: k_fmt_write<RES_ROWS> (A/B)
+    const char* e = getenv("BEDGPU_FMT_ROWS");
+    return !(e && atoi(e) == 0);
+  }();
   if (nb) {
     switch (A.kind) {
       case RES_IVL: BG_LAUNCH(c, "k_fmt_write", k_fmt_ivl_write, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
-      case RES_ROWS: BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text); break;
+      case RES_ROWS:
+        if (rows_fast) BG_LAUNCH(c, "k_fmt_write", k_fmt_rows_write, dim3(nb), dim3(BG_NT), A, tb, r->text);
+        else BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_ROWS>, dim3(nb), dim3(BG_NT), A, tb, r->text);
+        break;
       case RES_MAP:
         if (simple) BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAPS>, dim3(nb), dim3(BG_NT), A, tb, r->text);
         else BG_LAUNCH(c, "k_fmt_write", k_fmt_write<RES_MAP>, dim3(nb), dim3(BG_NT), A, tb, r->text);

@@ -332,15 +332,24 @@ __device__ __forceinline__ uint32_t lds_upper(const int64_t* X, uint32_t lo, uin
   }
   return lo;
 }
+// the first component of each k_element_flags block (one thread per block: every search in
+// flight at once, instead of one search per resident 256-thread block while its other threads
+// wait); the block finds the end of its range by a gallop from there (usually a few steps)
+__global__ void __launch_bounds__(BG_NT) k_element_lo(const int64_t* __restrict__ RS,
+                                                    const int64_t* __restrict__ OE_, uint64_t no,
+                                                    uint64_t nblk, uint64_t* __restrict__ blo) {
+  const uint64_t b = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
+  if (b < nblk) blo[b] = upper_bound_i64(OE_, no, RS[b * BG_NT]);  // rows start at >= RS[b * BG_NT]
+}
 __global__ void __launch_bounds__(BG_NT) k_element_flags(
     const int64_t* __restrict__ RS, const int64_t* __restrict__ RE, uint64_t nr,
     const int64_t* __restrict__ OS_, const int64_t* __restrict__ OE_, uint64_t no,
     const uint64_t* __restrict__ P, double thres, int use_pct, int invert,
-    uint8_t* __restrict__ flag, const uint32_t* __restrict__ name_len = nullptr,
-    const uint32_t* __restrict__ rest_len = nullptr, uint16_t* __restrict__ blen = nullptr,
-    unsigned int* __restrict__ blen_ovf = nullptr) {
+    uint8_t* __restrict__ flag, const uint32_t* __restrict__ name_len,
+    const uint32_t* __restrict__ rest_len, uint16_t* __restrict__ blen,
+    unsigned int* __restrict__ blen_ovf, const uint64_t* __restrict__ blo_) {
   __shared__ int64_t wmax[BG_NT / 64];
-  __shared__ uint64_t bnd[2];
+  __shared__ uint64_t bnd1;
   __shared__ int64_t xs[EF_SLICE], xe[EF_SLICE];
   const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
   const uint64_t r = r0 + threadIdx.x;
@@ -348,15 +357,26 @@ __global__ void __launch_bounds__(BG_NT) k_element_flags(
   const int64_t s = live ? RS[r] : LLONG_MAX, e = live ? RE[r] : LLONG_MIN;
   const int64_t em = wave_max_all(e);
   if (bg_lane() == 0) wmax[bg_wave()] = em;
+  const uint64_t blo = blo_[blockIdx.x];
   __syncthreads();
-  if (threadIdx.x == 0) bnd[0] = upper_bound_i64(OE_, no, RS[r0]);  // rows start at >= RS[r0]
-  if (threadIdx.x == 64) {
+  if (threadIdx.x == 0) {  // first component starting at/after the block's largest end: a gallop
     int64_t m = wmax[0];
     for (int w = 1; w < BG_NT / 64; ++w) m = max(m, wmax[w]);
-    bnd[1] = lower_bound_i64(OS_, no, m);  // no row ends after m
+    uint64_t lo = blo, step = 1;  // OS_[k] < m for every k < lo
+    while (lo < no && OS_[lo] < m) {
+      const uint64_t nx = lo + step;
+      if (nx >= no || OS_[nx] >= m) {
+        bnd1 = lower_bound_in(OS_, lo + 1, nx < no ? nx : no, m);
+        lo = ~0ull;
+        break;
+      }
+      lo = nx + 1;
+      step <<= 1;
+    }
+    if (lo != ~0ull) bnd1 = lo < no ? lo : no;
   }
   __syncthreads();
-  const uint64_t blo = bnd[0], bhi = max(bnd[0], bnd[1]);
+  const uint64_t bhi = max(blo, bnd1);
   const bool staged = bhi - blo <= EF_SLICE;  // block-uniform
   if (staged) {
     for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) {
@@ -1033,10 +1053,16 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
   }
   if ((rc = bg_scan_sum_u64(c, P, P, o.n, P + o.n))) return rc;
   if (R->n) {
-    BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3(bg_blocks(R->n, BG_NT)), dim3(BG_NT),
+    const uint64_t nblk = bg_blocks(R->n, BG_NT);
+    uint64_t* bnd = (uint64_t*)bg_alloc(c, 8 * nblk);
+    if (!bnd) return BG_E_NOMEM;
+    BG_LAUNCH(c, "k_element_lo", k_element_lo, dim3(bg_blocks(nblk, BG_NT)), dim3(BG_NT), R->ks, o.e, o.n, nblk,
+              bnd);
+    BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3((unsigned)nblk), dim3(BG_NT),
               R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag, set->d_name_len, R->rest_len,
-              blen, ovf);
+              blen, ovf, (const uint64_t*)bnd);
     BG_HIP(c, hipGetLastError());
+    bg_release(c, bnd);
   }
   uint64_t total = 0;
   uint64_t* rows = nullptr;
