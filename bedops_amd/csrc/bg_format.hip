@@ -1201,30 +1201,71 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_rows_write(FmtArgs A, const uint6
 // 512-row tiles located through per-piece byte prefixes: 0.50-0.55 ms with the prefixes
 // making k_mp_tile 0.38-0.39 ms; four pieces per thread in one 32 KiB round: 0.69 ms; two
 // per thread in rounds of 512: 0.56 ms.)
+// (round 5) every round's keys are loaded up front (a segment holds at most BG_SEG_CAP =
+// 4 rounds), so only the first round waits on HBM; and the chromosome name of the segment's
+// first piece is staged in LDS — pieces of that chromosome (nearly all) copy it from there
+// instead of byte loads from the global name table
+#define SEG_R (BG_SEG_CAP / BG_NT)
+__device__ __forceinline__ void ivl_put_nm(const FmtArgs& A, char* p, int64_t s, int64_t e, uint32_t g0,
+                                           const char* nm0, uint32_t nl0) {
+  const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
+  if (g == g0) {
+    for (uint32_t q = 0; q < nl0; ++q) p[q] = nm0[q];
+    p += nl0;
+  } else {
+    const uint32_t nl = A.name_len[g];
+    const char* nm = A.names + A.name_off[g];
+    for (uint32_t q = 0; q < nl; ++q) p[q] = nm[q];
+    p += nl;
+  }
+  *p++ = '\t';
+  const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
+  const int l1 = dec_len_u64(cs), l2 = dec_len_u64(ce);
+  put_u64_lds(p, cs, l1);
+  p += l1;
+  *p++ = '\t';
+  put_u64_lds(p, ce, l2);
+  p[l2] = '\n';
+}
 __global__ void __launch_bounds__(BG_NT) k_fmt_ivl_seg(FmtArgs A, const uint64_t* __restrict__ seg_off,
                                                        const uint64_t* __restrict__ seg_boff,
                                                        char* __restrict__ out, uint64_t* __restrict__ toff) {
+  static_assert(SEG_R * BG_NT == BG_SEG_CAP, "segment rounds");
   __shared__ uint32_t sh[BG_NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
+  __shared__ char nm0[BG_CHR_MAX + 1];
   const uint64_t t = blockIdx.x;
   const uint64_t c0 = seg_off[t];
   const uint32_t n = (uint32_t)(seg_off[t + 1] - c0);
   const int64_t* S = A.s + t * BG_SEG_CAP;
   const int64_t* E = A.e + t * BG_SEG_CAP;
+  int64_t ks[SEG_R], ke[SEG_R];
+#pragma unroll
+  for (int q = 0; q < SEG_R; ++q) {
+    const uint32_t j = q * BG_NT + threadIdx.x;
+    ks[q] = j < n ? S[j] : 0;
+    ke[q] = j < n ? E[j] : 0;
+  }
+  const uint32_t g0 = n ? (uint32_t)(S[0] >> BG_KEY_SHIFT) : ~0u;
+  const uint32_t nl0 = n ? A.name_len[g0] : 0u;
+  if (threadIdx.x < nl0) nm0[threadIdx.x] = A.names[A.name_off[g0] + threadIdx.x];
   uint64_t dst0 = seg_boff[t];
-  for (uint32_t r0 = 0; r0 < n; r0 += BG_NT) {  // block-uniform trip count
+#pragma unroll
+  for (int q = 0; q < SEG_R; ++q) {
+    const uint32_t r0 = q * BG_NT;
+    if (r0 >= n) break;  // (block-uniform)
     const uint32_t j = r0 + threadIdx.x;
     const bool v = j < n;
-    const int64_t s = v ? S[j] : 0, e = v ? E[j] : 0;
+    const int64_t s = ks[q], e = ke[q];
     const uint32_t l = v ? ivl_len(A, s, e) : 0u;
     uint32_t tot;
-    const uint32_t my = block_excl_scan(l, OpSum(), 0u, sh, &tot);
+    const uint32_t my = block_excl_scan(l, OpSum(), 0u, sh, &tot);  // (its barrier also publishes nm0)
     if (v && (c0 + j) % FT_TILE == 0) toff[(c0 + j) / FT_TILE] = dst0 + my;
     if (tot > FT_LDS) {  // oversized round (long names): render straight to HBM
       if (v) ivl_put(A, out + dst0 + my, s, e);
     } else {
       const uint32_t skew = (uint32_t)(dst0 & 15);
-      if (v) ivl_put(A, buf + skew + my, s, e);
+      if (v) ivl_put_nm(A, buf + skew + my, s, e, g0, nm0, nl0);
       __syncthreads();
       const uint64_t a0 = dst0, a1 = dst0 + tot;
       const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;

@@ -10,7 +10,7 @@ for s in ${SIDE_SETS-1 0 1 0}; do
   BEDGPU_SET_SIDE=$s timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $O/b_$s.json 2> $O/b_$s.err || exit 1
   python3 -c "import json; d=json.load(open('$O/b_$s.json')); print('side=$s', d['ms_per_step'], d['parity'], d['roofline']['avg_ms'])"
 done
-for w in ${CL_SETS:-BEDGPU_CLOSEST_WAVE=1 BEDGPU_CLOSEST_WAVE=0}; do
+for w in ${CL_SETS-BEDGPU_CLOSEST_WAVE=1 BEDGPU_CLOSEST_WAVE=0}; do
   N=$(echo "$w" | tr '=,' '__')
   env $(echo "$w" | tr ',' ' ') timeout -k 10 400 python3 bench.py --workload closest --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --profile-all > $O/c_$N.json 2> $O/c_$N.err || exit 1
   python3 -c "import json; d=json.load(open('$O/c_$N.json')); print('$w', d['ms_per_step'], d['parity'], list(d['kernels_ms_per_step'].items())[:4])"
