@@ -1126,12 +1126,18 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_ivl_write(FmtArgs A, const uint64
 // the per-thread byte counts places them, LDS staging, 16-byte stores — instead of
 // k_fmt_write<RES_ROWS>'s two renders per row (a counting one for the stripe scan, then the
 // real one)
-__device__ __forceinline__ void rows_put(const FmtArgs& A, char* p, uint64_t r, int64_t s, int64_t e) {
+__device__ __forceinline__ void rows_put(const FmtArgs& A, char* p, uint64_t r, int64_t s, int64_t e,
+                                         uint32_t g0 = ~0u, const char* nm0 = nullptr, uint32_t nl0 = 0) {
   const uint32_t g = (uint32_t)(s >> BG_KEY_SHIFT);
-  const uint32_t nl = A.name_len[g];
-  const char* nm = A.names + A.name_off[g];
-  for (uint32_t q = 0; q < nl; ++q) p[q] = nm[q];
-  p += nl;
+  if (g == g0) {  // the tile's first chromosome, staged in LDS
+    for (uint32_t q = 0; q < nl0; ++q) p[q] = nm0[q];
+    p += nl0;
+  } else {
+    const uint32_t nl = A.name_len[g];
+    const char* nm = A.names + A.name_off[g];
+    for (uint32_t q = 0; q < nl; ++q) p[q] = nm[q];
+    p += nl;
+  }
   *p++ = '\t';
   const uint64_t cs = (uint64_t)(s & BG_COORD_MASK), ce = (uint64_t)(e & BG_COORD_MASK);
   const int l1 = dec_len_u64(cs), l2 = dec_len_u64(ce);
@@ -1149,9 +1155,17 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_rows_write(FmtArgs A, const uint6
                                                           char* __restrict__ out) {
   __shared__ uint32_t sh[BG_NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) char buf[FT_LDS + 16];
+  __shared__ char nm0[BG_CHR_MAX + 1];
   static_assert(FT_ROWS == 2, "two rows per thread");
   const uint64_t k0 = (uint64_t)blockIdx.x * FT_TILE + 2ull * threadIdx.x;
   const bool v0 = k0 < A.n, v1 = k0 + 1 < A.n;
+  {  // the tile's first row's chromosome name -> LDS (published by the scan's barrier)
+    const uint64_t f = (uint64_t)blockIdx.x * FT_TILE;
+    const uint32_t g = (uint32_t)(A.s[A.rows[f]] >> BG_KEY_SHIFT);
+    if (threadIdx.x < A.name_len[g]) nm0[threadIdx.x] = A.names[A.name_off[g] + threadIdx.x];
+  }
+  const uint32_t g0 = (uint32_t)(A.s[A.rows[(uint64_t)blockIdx.x * FT_TILE]] >> BG_KEY_SHIFT);
+  const uint32_t nl0 = A.name_len[g0];
   uint64_t r0 = 0, r1 = 0;
   if (v1) {
     const ulonglong2 R = reinterpret_cast<const ulonglong2*>(A.rows)[k0 >> 1];
@@ -1173,8 +1187,8 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_rows_write(FmtArgs A, const uint6
     return;
   }
   const uint32_t skew = (uint32_t)(dst0 & 15);
-  if (v0) rows_put(A, buf + skew + my, r0, s0, e0);
-  if (v1) rows_put(A, buf + skew + my + l0, r1, s1, e1);
+  if (v0) rows_put(A, buf + skew + my, r0, s0, e0, g0, nm0, nl0);
+  if (v1) rows_put(A, buf + skew + my + l0, r1, s1, e1, g0, nm0, nl0);
   __syncthreads();
   const uint64_t a0 = dst0, a1 = dst0 + tot;
   const uint64_t al0 = (a0 + 15) & ~15ULL, al1 = a1 & ~15ULL;

@@ -2204,12 +2204,14 @@ __device__ __forceinline__ uint4 ldsu128(const void* p) {
 #ifndef BG_EXP_V
 #define BG_EXP_V 0
 #endif
-// BG_GTXT (default 1): an interior sub-tile is not staged in LDS; its lines' token and
-// numbers are read from the text through the vector memory path (the unaligned LDS reads
-// were the LDS pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave), 3% faster on
-// MI355X; 0 stages every sub-tile (A/B)
+// BG_GTXT=1: an interior sub-tile is not staged in LDS; its lines' token and numbers are
+// read from the text through the vector memory path (the unaligned LDS reads were the LDS
+// pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave). Timed within +-3% of staging on
+// two boxes (one each way), but those per-line reads go to L2 a second time and miss it often:
+// PMC 4.21 GB per launch against 2.95 GB staged (2.81 algorithmic, gpurun_out/r05_abp) — so
+// 0 (stage every sub-tile) is the default
 #ifndef BG_GTXT
-#define BG_GTXT 1
+#define BG_GTXT 0
 #endif
 // the value of a number of L (1..9) digits whose last digit is the high byte of D.z (the 12
 // bytes D end at the number's end); ok cleared when one of its bytes is not a digit
