@@ -2552,17 +2552,18 @@ __global__ void __launch_bounds__(64) k_parse_set_v(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st, uint32_t pfd,
-    uint32_t* __restrict__ pf_sink) {
+    uint32_t* __restrict__ pf_sink, uint32_t u0) {
   __shared__ ParseLdsV S;
   SubRegs V;
-  load_sub(txt, nb, (int64_t)blockIdx.x * TW, V);
+  const uint32_t u = u0 + blockIdx.x;  // (u0: the launch covers sub-tiles [u0, u0 + gridDim.x))
+  load_sub(txt, nb, (int64_t)u * TW, V);
   uint32_t pf = 0;
   if (pfd) {
-    const uint64_t a = ((uint64_t)blockIdx.x + pfd) * TW + 128u * threadIdx.x;
+    const uint64_t a = ((uint64_t)u + pfd) * TW + 128u * threadIdx.x;
     if (threadIdx.x < (TW + HA_V + 32 + 127) / 128 && a + 4 <= nb)
       pf = *reinterpret_cast<const uint32_t*>(txt + a);
   }
-  parse_sub_v(txt, nb, blockIdx.x, V, S, runlo, runhi, R, LCS, LCE, TS, st);
+  parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
   if (pf_sink) pf_sink[threadIdx.x] = pf;
 }
 
@@ -2598,9 +2599,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8)))
 __global__ void __launch_bounds__(BG_NT) k_set_count(const int64_t* __restrict__ LCS, SetTiles TS,
                                                      const int64_t* __restrict__ mex,
                                                      uint32_t ntiles, uint64_t* __restrict__ cnt,
-                                                     bg_dstatus* st) {
+                                                     bg_dstatus* st, uint32_t u0) {
   __shared__ unsigned long long srows[BG_NT / 64];
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = u0 + blockIdx.x * blockDim.x + threadIdx.x;  // (tiles [u0, ntiles))
   uint64_t rows = 0;
   if (t < ntiles) {
     const uint64_t b = TS.base[t], n = TS.nloc[t];
@@ -2646,12 +2647,17 @@ __global__ void __launch_bounds__(BG_NT) k_set_count(const int64_t* __restrict__
 // running max just before component g+1 opens, written by the tile holding that opening
 // (the last one by the last tile).
 #define SW_TILES 64  // tiles per k_set_write workgroup
+// (a range [u0, ntiles) of a file's tiles: off[] holds the range's exclusive offsets and
+// *carry the components of the tiles before u0; the file's last tile is nlast - 1, whose
+// workgroup also writes the file's component count to *total)
 __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__ LCS,
                                                      const int64_t* __restrict__ LCE, SetTiles TS,
                                                      const int64_t* __restrict__ mex,
                                                      const uint64_t* __restrict__ off,
                                                      uint32_t ntiles, int64_t* __restrict__ CS,
-                                                     int64_t* __restrict__ CE) {
+                                                     int64_t* __restrict__ CE, uint32_t u0, uint32_t nlast,
+                                                     const uint64_t* __restrict__ carry,
+                                                     unsigned long long* __restrict__ total_out) {
   // SW_TILES tiles per workgroup, their surviving components flattened over all threads
   // (element e -> its tile by a search of the LDS prefix of counts): every load of a
   // workgroup is independent, instead of a wave waiting on one tile's descriptor first
@@ -2660,8 +2666,9 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
   __shared__ uint32_t sab[SW_TILES];       // absorbed local components (the first survivor's index)
   __shared__ int64_t sgb[SW_TILES];        // staging form (SetTiles::gb)
   __shared__ int64_t first_end[SW_TILES];  // CE value before the tile's first global component
-  const uint32_t t0 = blockIdx.x * SW_TILES;
+  const uint32_t t0 = u0 + blockIdx.x * SW_TILES;
   const uint32_t nt = min((uint32_t)SW_TILES, ntiles - t0);
+  const uint64_t cy = carry ? *carry : 0;
   uint32_t c = 0;
   if (threadIdx.x < nt) {
     const uint32_t t = t0 + threadIdx.x;
@@ -2671,11 +2678,12 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
     src[threadIdx.x] = b;
     sab[threadIdx.x] = (uint32_t)a;
     sgb[threadIdx.x] = gb;
-    dst[threadIdx.x] = off[t];
+    dst[threadIdx.x] = cy + off[t];
     first_end[threadIdx.x] = (c > 0) ? max(M, a > 0 ? set_key(LCE, b, gb, a - 1) : LLONG_MIN) : 0;
-    if (t + 1 == ntiles) {  // the last component ends at the running max of everything
-      const uint64_t total = off[t] + c;
+    if (t + 1 == nlast) {  // the last component ends at the running max of everything
+      const uint64_t total = cy + off[t] + c;
       if (total > 0) CE[total - 1] = max(M, TS.tmax[t]);
+      if (total_out) *total_out = total;
     }
   }
   // exclusive scan of c over the first wave (SW_TILES == 64)
@@ -2767,6 +2775,9 @@ struct LoadState {
   uint32_t* absorbed = nullptr;
   int64_t* tgb = nullptr;
   uint32_t set_nt = 0;  // staging units of a BG_BED3_SET parse whose merge passes are pending
+  uint32_t set_split = 0;  // > 0: only sub-tiles [0, set_split) are parsed yet (set_split_finish)
+  int64_t* mex2 = nullptr;
+  uint64_t* dtot = nullptr;
   // row loads without a scout pass (k_parse_n's look-back): tile words, sampled tiles
   uint64_t* lbw = nullptr;
   uint32_t nsamp = 0;
@@ -2781,7 +2792,7 @@ static void release_state(bg_ctx* c, LoadState& S) {
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
                   (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed,
-                  (void*)S.tgb, (void*)S.big, (void*)S.lbw})
+                  (void*)S.tgb, (void*)S.big, (void*)S.lbw, (void*)S.mex2, (void*)S.dtot})
     bg_release(c, p);
   S = LoadState();
 }
@@ -2994,7 +3005,7 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
 // (T->cs/T->ce, capacity = rows; the count lands in st->pad[0] and comes back with the
 // statuses)
 static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
-                         const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
+                         const std::map<std::string, int32_t>& gid, bg_dstatus* st, bool split = false) {
   T->is_set = true;
   const uint32_t nr = (uint32_t)S.run_pos.size();
   static const int set_nt = [] {  // BEDGPU_SET_NT=64|128|256: the wave / 8 KiB-tile kernels (A/B)
@@ -3049,8 +3060,21 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
       const char* e = getenv("BEDGPU_SET_PF");
       return e ? (uint32_t)atoi(e) : 0u;
     }();
-    BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st, pfd, (uint32_t*)nullptr);
+    // split (the last input): the first half now, set_split_finish queues the second half
+    // after the first half's merge passes have gone to the side stream
+    // (BEDGPU_SET_SPLIT_MIN: the smallest input split, in 4 KiB sub-tiles; read per call so a
+    // test can force small splits)
+    const char* sm = getenv("BEDGPU_SET_SPLIT_MIN");
+    const uint32_t smin = sm ? (uint32_t)std::max(2, atoi(sm)) : 8192u;
+    const uint32_t h = (split && nt >= smin) ? nt / 2 : 0;
+    if (h) {
+      S.mex2 = (int64_t*)bg_alloc(c, 8ull * nt);
+      S.dtot = (uint64_t*)bg_alloc(c, 16);
+      if (!S.mex2 || !S.dtot) return BG_E_NOMEM;
+      S.set_split = h;
+    }
+    BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(h ? h : nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+              S.lcs, S.lce, TS, st, pfd, (uint32_t*)nullptr, 0u);
   }
   else if (wave)
     BG_LAUNCH(c, "k_parse_set", k_parse_set_w, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
@@ -3072,24 +3096,70 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
 // the passes after k_parse_set: the running max of earlier tiles, absorbed local components
 // and the final component columns. bg_load runs them on the side stream while the next
 // input parses (k_parse_set leaves HBM bandwidth to spare, k_set_write is bandwidth-bound)
+// the merge passes over tiles [u0, u1) of nt: the running max over [0, u1) into mex, the
+// range's counts scanned in place (its total to *scan_total), the components written after
+// *carry earlier ones; total_out: the file's component count (from the file's last tile)
+static int set_merge_range(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st, uint32_t u0, uint32_t u1,
+                           uint32_t nt, int64_t* mex, uint64_t* scan_total, const uint64_t* carry,
+                           unsigned long long* total_out, hipEvent_t wait_before_write = nullptr) {
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
+  int rc;
+  if ((rc = bg_scan_max_i64(c, S.tmax, mex, u1, LLONG_MIN))) return rc;
+  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(u1 - u0, BG_NT)), dim3(BG_NT), S.lcs, TS,
+            (const int64_t*)mex, u1, S.tcnt, st, u0);
+  BG_HIP(c, hipGetLastError());
+  if ((rc = bg_scan_sum_u64(c, S.tcnt + u0, S.tcnt + u0, u1 - u0, scan_total))) return rc;
+  if (wait_before_write) BG_HIP(c, hipStreamWaitEvent(c->stream, wait_before_write, 0));
+  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(u1 - u0, SW_TILES)), dim3(BG_NT), S.lcs,
+            S.lce, TS, (const int64_t*)mex, (const uint64_t*)S.tcnt, u1, T->cs, T->ce, u0, nt, carry, total_out);
+  BG_HIP(c, hipGetLastError());
+  return 0;
+}
 static int parse_set_merge(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
   const uint32_t nt = S.set_nt;
   S.set_nt = 0;
-  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  int rc;
-  if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
-  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, BG_NT)), dim3(BG_NT), S.lcs, TS,
-            S.mex, nt, S.tcnt, st);
-  BG_HIP(c, hipGetLastError());
-  if ((rc = bg_scan_sum_u64(c, S.tcnt, S.tcnt, nt, (uint64_t*)&st->pad[0]))) return rc;
-  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, SW_TILES)), dim3(BG_NT), S.lcs,
-            S.lce, TS, S.mex, S.tcnt, nt, T->cs, T->ce);
-  BG_HIP(c, hipGetLastError());
-  return 0;
+  return set_merge_range(c, T, S, st, 0, nt, nt, S.mex, (uint64_t*)&st->pad[0], nullptr, nullptr);
 }
 
 // parse_set_merge of input i on the side stream, forked from the ctx stream's current
 // position (BEDGPU_SET_SIDE=0: in line)
+static int side_open(bg_ctx* c) {
+  if (!c->sstream) {
+    if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sfork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sjoin, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return bg_fail(c, BG_E_HIP, "side stream creation failed");
+    }
+  }
+  return 0;
+}
+// the last input, split: its first half's merge passes on the side stream while the second
+// half parses on the ctx stream, then the second half's passes (their write waits for the
+// first half's component count)
+static int set_split_finish(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st,
+                            const std::map<std::string, int32_t>& gid) {
+  const uint32_t nt = S.set_nt, h = S.set_split;
+  S.set_nt = 0;
+  S.set_split = 0;
+  int rc = side_open(c);
+  if (rc) return rc;
+  BG_HIP(c, hipEventRecord(c->sfork, c->stream));
+  BG_HIP(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
+  c->defer_release = true;
+  hipStream_t main = c->stream;
+  c->stream = c->sstream;
+  rc = set_merge_range(c, T, S, st, 0, h, nt, S.mex, S.dtot, nullptr, nullptr);
+  c->stream = main;
+  if (rc) return rc;
+  BG_HIP(c, hipEventRecord(c->sjoin, c->sstream));
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
+  const RunTable R{S.d_info, S.d_row, (uint32_t)S.run_pos.size()};
+  BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt - h), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+            S.lcs, S.lce, TS, st, 0u, (uint32_t*)nullptr, h);
+  BG_HIP(c, hipGetLastError());
+  return set_merge_range(c, T, S, st, h, nt, nt, S.mex2, S.dtot + 1, S.dtot, &st->pad[0], c->sjoin);
+}
 static int set_merge_side(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
   if (!c->sstream) {
     if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
@@ -3288,10 +3358,20 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     const char* e = getenv("BEDGPU_SET_SIDE");
     return !(e && atoi(e) == 0);
   }();
+  // BEDGPU_SET_SPLIT=1: the last set input parsed in two halves around its first half's merge
+  // passes (set_split_finish). Exact (tests/test_gpu_setload.py forces it on small inputs) but
+  // measured slower on 100M x 100M --intersect (3.48 vs 3.46 ms: the second launch's ramp and
+  // tail cost more than the ~0.1 ms of passes it hides), so off by default
+  static const bool split_last = [] {
+    const char* e = getenv("BEDGPU_SET_SPLIT");
+    return e && atoi(e) == 1;
+  }();
   for (int i = 0; i < n && !rc; ++i) {
-    rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i)
+    const bool split = side && (split_last || getenv("BEDGPU_SET_SPLIT_MIN")) && i > 0 && i + 1 == n;
+    rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i, split)
                                        : parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
-    if (!rc && st[i].set_nt)
+    if (!rc && st[i].set_nt && st[i].set_split) rc = set_split_finish(c, s->t[i], st[i], dst + i, gid);
+    else if (!rc && st[i].set_nt)
       rc = (side && i + 1 < n) ? set_merge_side(c, s->t[i], st[i], dst + i) : parse_set_merge(c, s->t[i], st[i], dst + i);
   }
   {

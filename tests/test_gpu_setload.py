@@ -221,3 +221,22 @@ def test_set_load_every_byte(eng, where):
                 "after_end": c + b"\t" + s + b"\t" + e + x + b"rest"}[where]
         text = head + line + b"\n" + tail
         assert _outcome(eng, [text], True) == _outcome(eng, [text], False), (where, b)
+
+
+@pytest.mark.parametrize("mode,extra", MODES)
+def test_split_last_input_equals_oracle(eng, oracle_bin, monkeypatch, mode, extra):
+    """the last set input parsed in two halves with the first half's merge passes on the side
+    stream (set_split_finish), forced on small inputs (BEDGPU_SET_SPLIT_MIN=4 sub-tiles): long
+    rows of the last file reach across the split point, so the second half's first tiles are
+    absorbed by the first half's running max, and its components continue the first half's"""
+    monkeypatch.setenv("BEDGPU_SET_SPLIT_MIN", "4")
+    rng = random.Random(zlib.crc32(repr(("split", mode)).encode()))
+    n = 20000
+    texts = _texts(rng, 2 if mode != "-s" else 3, n, 200, 300_000)
+    long_rows = randbed.rows(rng, n, chroms=["chr1", "chr2"], span=2_000_000, maxlen=30000)
+    long_rows.append(("chr1", 10, 1_500_000))  # one row over half the last file's chr1
+    long_rows.sort(key=lambda r: (r[0], r[1], r[2]))
+    texts[-1] = randbed.text(long_rows).encode()
+    with tempfile.TemporaryDirectory() as td:
+        want = run_oracle(oracle_bin["bedops"], [mode] + extra, texts, td)
+    assert _run(eng, mode, extra, texts, True) == want
