@@ -254,20 +254,32 @@ def _phases(stderr):
     return {"host_ms": host, "stage_ms": stage}
 
 
-def _run_pipe(argv, env):
+def _run_pipe(argv, env, cap=None):
     """one CLI run with stdout to a pipe drained by this process; (seconds, sha16, bytes, rc,
     stderr). The clock stops when the process has exited and the pipe is drained; the consumer
     only collects the bytes (a hash while reading would make it the slowest stage, ~1.5 GB/s):
-    the output is hashed after the clock stops."""
+    the output is hashed after the clock stops. cap (the output size of the file run): the
+    consumer reads into one buffer allocated and touched before the clock starts, as a C
+    reader (`cat`, `gzip`) reads into its own reused buffer — a new 1 MiB bytes object per
+    read() made the consumer, not the pipe, the slow end (~4.6 GB/s)."""
+    import threading
+    buf = bytearray(cap + (1 << 22)) if cap else None
+    mv = memoryview(buf) if buf is not None else None
     chunks = []
+    off = 0
     t0 = time.perf_counter()
     p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, bufsize=0)
-    import threading
     err = []
     th = threading.Thread(target=lambda: err.append(p.stderr.read()))
     th.start()
     fd = p.stdout.fileno()
     while True:
+        if mv is not None and off + (1 << 22) <= len(buf):
+            k = os.readv(fd, [mv[off:off + (1 << 22)]])
+            if k == 0:
+                break
+            off += k
+            continue
         b = os.read(fd, 1 << 22)
         if not b:
             break
@@ -276,14 +288,16 @@ def _run_pipe(argv, env):
     th.join()
     dt = time.perf_counter() - t0
     h = hashlib.sha256()
-    n = 0
+    if mv is not None:
+        h.update(mv[:off])
+    n = off
     for b in chunks:
         h.update(b)
         n += len(b)
     return dt, h.hexdigest()[:16], n, rc, b"".join(err)
 
 
-def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", extra_env=None):
+def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", extra_env=None, pipe_cap=None):
     """the drop-in CLI, file -> file: `bedops_amd/bin/<tool> <args> <files> > out`, input files
     in the page cache, process start + HIP init + reads + device work + output write all
     inside the wall clock. Median of `runs`, with the BEDGPU_STATS phase
@@ -308,7 +322,7 @@ def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", 
         if i and spacing:
             time.sleep(spacing)
         if sink == "pipe":
-            dt, sha, nbytes, rc, err = _run_pipe([exe, *args, *paths], env)
+            dt, sha, nbytes, rc, err = _run_pipe([exe, *args, *paths], env, pipe_cap)
         else:
             with open(out, "wb") as fo:
                 t0 = time.perf_counter()
@@ -331,6 +345,8 @@ def e2e_cli(W, paths, rows, td, runs=3, devices=None, spacing=0.5, sink="file", 
                       f"bedops_amd/bin/{W['cli']} {' '.join(args)} <files> "
                       f"{'| reader' if sink == 'pipe' else '> out'}",
            "output_sha16": sha, "output_bytes": nbytes,
+           "consumer": (("readv into one preallocated buffer" if pipe_cap else "os.read 4 MiB chunks")
+                        if sink == "pipe" else None),
            "phases": _phases(logs[times.index(med)]),
            # the staging ring's own report of the median run (copy issue / drain times, and
            # how long its threads waited on DMA vs copied on the CPU)
@@ -693,10 +709,10 @@ def main():
                 # process lifetime (BEDGPU_DETACH=0), and with stdout to a pipe
                 variants = {"back_to_back": {"spacing": 0},
                             "no_detach": {"extra_env": {"BEDGPU_DETACH": "0"}},
-                            "pipe": {"sink": "pipe"}}
+                            "pipe": {"sink": "pipe", "pipe_cap": e2e["output_bytes"]}}
                 for name, kw in variants.items():
                     v = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs, **kw)
-                    e2e[name] = {k: v[k] for k in ("median_s", "runs_s", "command", "output_sha16")}
+                    e2e[name] = {k: v[k] for k in ("median_s", "runs_s", "command", "output_sha16", "consumer")}
                     e2e[name]["value"] = round(v["value"], 1)
                 if W["ref"]:
                     e2e["matches_reference"] = all(x == W["ref"]["sha16"] for x in
