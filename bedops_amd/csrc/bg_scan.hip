@@ -3,18 +3,21 @@
 // inter-workgroup hand-off inside a launch).
 #include "bg_internal.h"
 
-#define SCAN_ITEMS 16
+#ifndef SCAN_ITEMS
+#define SCAN_ITEMS 4  // (16 -> 4: 4x the workgroups on the ~0.6M-entry tile arrays of the loaders)
+#endif
 #define SCAN_TILE (BG_NT * SCAN_ITEMS)
 
+// (the reduction's order does not matter: striped, coalesced loads)
 template <typename T, typename Op>
 __global__ void __launch_bounds__(BG_NT) k_tile_reduce(const T* __restrict__ in, uint64_t n,
                                                        T* __restrict__ part, Op op, T identity) {
   __shared__ T sh[BG_NT / 64 + 1];
-  uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x;
   T acc = identity;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k)
-    if (base + k < n) acc = op(acc, in[base + k]);
+    if (base + (uint64_t)k * BG_NT < n) acc = op(acc, in[base + (uint64_t)k * BG_NT]);
   T tot;
   (void)block_excl_scan(acc, op, identity, sh, &tot);
   if (threadIdx.x == 0) part[blockIdx.x] = tot;

@@ -28,10 +28,24 @@ def oracle_bin():
             "sortbed": os.path.join(ROOT, "oracle", "build", "sortbed_oracle")}
 
 
+def _lib_fresh():
+    """the in-tree libbedgpu.so is newer than every source it is built from (the objects are
+    not shipped to the GPU box: make would rebuild the whole library there, ~100 s)"""
+    import glob
+    lib = os.path.join(ROOT, "bedops_amd", "lib", "libbedgpu.so")
+    if not os.path.exists(lib):
+        return False
+    srcs = glob.glob(os.path.join(ROOT, "bedops_amd", "csrc", "*")) + [os.path.join(ROOT, "include", "bedgpu.h")]
+    return os.path.getmtime(lib) >= max(os.path.getmtime(f) for f in srcs)
+
+
 @pytest.fixture(scope="session")
 def gpu_bin():
     """The drop-in front-ends (C, linked to libbedgpu.so)."""
-    _make("lib", "cli")
+    if _lib_fresh():
+        _make("-o", "bedops_amd/lib/libbedgpu.so", "cli")  # (-o: take the library as built)
+    else:
+        _make("lib", "cli")
     return {"bedops": os.path.join(ROOT, "bedops_amd", "bin", "bedops"),
             "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap"),
             "closest": os.path.join(ROOT, "bedops_amd", "bin", "closest-features"),
