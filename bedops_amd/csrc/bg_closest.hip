@@ -210,7 +210,14 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
       const bool hangR = ovl && !hangL && be <= ce;
       const bool inside = ovl && !hangL && !hangR;
       bool half = false;
-      if (inside) {  // rare: the double division is skipped by every wave without such a row
+#ifndef BG_CL_IHALF
+#define BG_CL_IHALF 1
+#endif
+      if (BG_CL_IHALF) {  // the reference's double test in exact integers (see cw_window)
+        const int64_t bsc = bs & BG_COORD_MASK, bec = be & BG_COORD_MASK;
+        const int64_t csc = cs & BG_COORD_MASK, cec = ce & BG_COORD_MASK;
+        half = inside && (2 * csc > bsc + bec - 1 || bsc + bec + 1 - 2 * csc < cec - csc);
+      } else if (inside) {  // rare: the double division is skipped by every wave without such a row
         const double cst = (double)(cs & BG_COORD_MASK);
         const double prop =
             cen < cst ? 0.0
@@ -579,6 +586,16 @@ __device__ __forceinline__ int64_t bperm64(int64_t v, int src) {
   const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)((uint64_t)v >> 32));
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+__device__ __forceinline__ int32_t wave_excl_max_i32(int32_t v, int32_t identity) {
+  const int lane = bg_lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v = u > v ? u : v;
+  }
+  const int32_t e = __shfl_up(v, 1, 64);
+  return lane ? (e > identity ? e : identity) : identity;
+}
 __device__ __forceinline__ int64_t wave_excl_max_i64(int64_t v, int64_t identity) {
   const int lane = bg_lane();
 #pragma unroll
@@ -617,13 +634,15 @@ __device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, CwKeys
   const bool hangL = ovl && cs <= bs;
   const bool hangR = ovl && !hangL && be <= ce;
   const bool inside = ovl && !hangL && !hangR;
-  bool half = false;
-  if (inside) {
-    const double cst = (double)(cs & BG_COORD_MASK);
-    const double prop =
-        cen < cst ? 0.0 : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
-    half = prop < 0.5;
-  }
+  // the centroid proportion test in integers: prop < 0.5 of the reference's doubles
+  // (ClosestFeature.cpp:227-239, cen = (be - 1 + bs) / 2, prop = cen < cs ? 0 : (cen + 1 - cs)
+  // / (ce - cs)) holds iff 2cs > bs + be - 1, or N = bs + be + 1 - 2cs < L = ce - cs: the
+  // quotient N / 2L is exact up to one rounding, and N < L keeps it at least 1/(2L) > 2^-41
+  // below 0.5, far beyond that rounding (2^-54) — no double division per window
+  const int64_t bsc = bs & BG_COORD_MASK, bec = be & BG_COORD_MASK;
+  const int64_t csc = cs & BG_COORD_MASK, cec = ce & BG_COORD_MASK;
+  const bool half = inside && (2 * csc > bsc + bec - 1 || bsc + bec + 1 - 2 * csc < cec - csc);
+  (void)cen;
   // ld == 0 from the first hangL / (inside, !half) lane on (that lane itself still sees ld != 0)
   const uint64_t zm = __ballot(hangL || (inside && !half));
   const bool ld0z = W.ld == 0;
@@ -634,7 +653,14 @@ __device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, CwKeys
   const bool in_a = inside && half && ldz;
   const bool in_d = inside && half && !ldz;
   // (every wave-wide operation below runs on all lanes: no shuffle inside a select)
-  const int64_t pm = wave_excl_max_i64(neg ? d : D_MINUS, W.ld);
+  int64_t pm;
+  if (__ballot(neg && d <= (int64_t)INT_MIN)) {  // gaps past 2^31: the 64-bit scan
+    pm = wave_excl_max_i64(neg ? d : D_MINUS, W.ld);
+  } else {  // every negative distance fits in int32 (INT_MIN: none / the incoming ld below all)
+    const int32_t id = W.ld <= (int64_t)INT_MIN ? INT_MIN : (int32_t)W.ld;
+    pm = (int64_t)wave_excl_max_i32(neg ? (int32_t)d : INT_MIN, id);
+    if (pm == (int64_t)INT_MIN) pm = W.ld <= (int64_t)INT_MIN ? W.ld : pm;
+  }
   const int64_t ldi = ldz ? 0 : pm;
   const bool newleft = neg && !ldz && d >= ldi;
   const bool dropL = neg && !newleft;

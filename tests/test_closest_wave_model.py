@@ -65,3 +65,38 @@ def test_sequential_form_matches_oracle(oracle_bin, tmp_path):
                          for x in (left, right)]
                 want.append("|".join(parts))
             assert out == want, (seed, overlaps)
+
+
+def _half_double(bs, be, cs, ce):
+    cen = (be - 1.0 + bs) / 2.0  # ClosestFeature.cpp:227-239 in doubles
+    prop = 0.0 if cen < cs else (cen + 1 - cs) / float(ce - cs)
+    return prop < 0.5
+
+
+def _half_int(bs, be, cs, ce):  # bg_closest.hip: cl_run / cw_window
+    return 2 * cs > bs + be - 1 or bs + be + 1 - 2 * cs < ce - cs
+
+
+def test_integer_centroid_test_equals_double():
+    """the kernels' integer form of the centroid proportion test equals the reference's
+    double computation: random rows, rows at the proportion's boundary (N = L - 1, L, L + 1),
+    and coordinates near 2^40 (the key space's limit)"""
+    rng = random.Random(11)
+    cases = []
+    for _ in range(200000):
+        top = rng.choice([100, 10**4, 10**9, 1 << 40])
+        bs = rng.randrange(top)
+        be = bs + rng.randint(1, min(top, 10**6))
+        cs = rng.randint(bs, be)  # an "inside" candidate starts inside the ref row
+        ce = cs + rng.randint(1, min(top, 10**6))
+        cases.append((bs, be, cs, ce))
+    for _ in range(50000):  # at the boundary: N = bs + be + 1 - 2cs vs L = ce - cs
+        bs = rng.randrange(1 << 40)
+        be = bs + rng.randint(1, 10**6)
+        cs = rng.randint(bs, be)
+        n = bs + be + 1 - 2 * cs
+        for L in (n - 1, n, n + 1):
+            if L >= 1:
+                cases.append((bs, be, cs, cs + L))
+    for bs, be, cs, ce in cases:
+        assert _half_int(bs, be, cs, ce) == _half_double(bs, be, cs, ce), (bs, be, cs, ce)
