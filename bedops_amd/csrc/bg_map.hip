@@ -138,11 +138,15 @@ __global__ void __launch_bounds__(BG_NT) k_map_bounds(MapArgs A, int crit, uint6
 // CRIT == BG_OVR_FAST (bedmap --faster, bg_faster.hip): the window [wlo, whi) of every row
 // is an input, its members are the rows that joined the sweep's deque (zin), and no criterion
 // is re-tested
-template <int CRIT, bool ZM, bool LONG>
+// SA: the candidates' ends and scores are staged beside their starts (72 KiB of LDS, 2
+// workgroups per CU), so the per-row candidate loop reads only LDS
+template <int CRIT, bool ZM, bool LONG, bool SA = false>
 __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
   __shared__ int64_t xs[MAP_SLICE];  // the workgroup's candidate starts, when they fit
+  __shared__ int64_t xe[SA ? MAP_SLICE : 1];
+  __shared__ double xc[SA ? MAP_SLICE : 1];
   constexpr bool FAST = CRIT == BG_OVR_FAST;
   const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
   const uint64_t r = r0 + threadIdx.x;
@@ -176,7 +180,13 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   // level then costs an LDS read instead of an L2 round trip)
   const bool staged = !FAST && bhi - blo <= MAP_SLICE;
   if (staged) {
-    for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) xs[i] = A.MS[blo + i];
+    for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) {
+      xs[i] = A.MS[blo + i];
+      if (SA) {
+        xe[i] = A.ME[blo + i];
+        if (A.need & (NEED_SUM | NEED_EXT)) xc[i] = A.SC[blo + i];
+      }
+    }
     __syncthreads();
   }
   if (!live) return;
@@ -247,8 +257,8 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
     for (int j = 0; j < MU; ++j) {
       const uint64_t m = min(m0 + j, hi - 1);
       ms[j] = staged ? xs[m - blo] : A.MS[m];
-      me[j] = A.ME[m];
-      sc[j] = (A.need & (NEED_SUM | NEED_EXT)) ? A.SC[m] : 0.0;
+      me[j] = (SA && staged) ? xe[m - blo] : A.ME[m];
+      sc[j] = (A.need & (NEED_SUM | NEED_EXT)) ? ((SA && staged) ? xc[m - blo] : A.SC[m]) : 0.0;
       live_m[j] = !ZM || bg_map_live(A.zin, A.zout, r, m);
     }
 #pragma unroll
@@ -1553,6 +1563,10 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
               (const int64_t*)bmx, bnd);
     A.bnd = bnd;
   }
+  static const bool stage_all = [] {  // BEDGPU_MAP_STAGE=1: ends and scores staged too (A/B)
+    const char* e = getenv("BEDGPU_MAP_STAGE");
+    return e && atoi(e) == 1;
+  }();
   if (R->n) {
     const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);
 #define BG_MAP_LAUNCH(K)                                                                   \
@@ -1560,6 +1574,9 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
     if (A.lrows.ncls) {                                                                    \
       if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, true>), g, b, A);           \
       else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, true>), g, b, A);                \
+    } else if (stage_all) {                                                                \
+      if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, false, true>), g, b, A);    \
+      else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false, true>), g, b, A);         \
     } else {                                                                               \
       if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, false>), g, b, A);          \
       else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false>), g, b, A);               \
