@@ -1615,8 +1615,11 @@ __device__ uint64_t lb_prefix(uint64_t* __restrict__ words, uint32_t t, uint64_t
   return excl;
 }
 
+#ifndef BG_PN_WAVES
+#define BG_PN_WAVES 6  // k_parse_n's minimum waves per SIMD (6: <= 80 VGPRs)
+#endif
 template <int NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_n(
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_WAVES, 8))) k_parse_n(
     const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, uint64_t* __restrict__ row0,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
