@@ -3300,9 +3300,33 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   HP("alloc");
   if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(ctr, 0, 64ull * n, c->stream));
   HP("memset");
+  // BEDGPU_SCOUT_SIDE=1: odd inputs' first-phase kernels (token hashes, boundaries, run
+  // records: latency-bound launches of a few thousand waves) on the side stream beside the
+  // even ones' — exact, but measured 0.07 ms slower per intersect step (the fork/join events
+  // cost more than the overlap), so off
+  static const bool scout_side = [] {
+    const char* e = getenv("BEDGPU_SCOUT_SIDE");
+    return e && atoi(e) == 1;
+  }();
   for (int i = 0; i < n && !rc; ++i) {
     s->t.push_back(new bg_table());
-    rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
+    if (scout_side && (i & 1) && !(rc = side_open(c))) {
+      rc = bg_hip_ok(c, hipEventRecord(c->sfork, c->stream));
+      if (!rc) rc = bg_hip_ok(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
+      if (rc) break;
+      c->defer_release = true;
+      hipStream_t main = c->stream;
+      c->stream = c->sstream;
+      rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
+      c->stream = main;
+      if (!rc) rc = bg_hip_ok(c, hipEventRecord(c->sjoin, c->sstream));
+    } else if (!rc) {
+      rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
+    }
+  }
+  {
+    const int rj = set_merge_join(c);  // the side stream's first-phase work before round trip 1
+    if (!rc) rc = rj;
   }
   HP("scout");
   // round trip 1: rows and record counts of every input, with the first REC_SPEC records
