@@ -2145,16 +2145,18 @@ __device__ __forceinline__ void classify16(const uint4 a, uint32_t& ws, uint32_t
 struct LdsU3 {
   uint32_t x, y, z;
 };
-// unaligned LDS reads (any byte address); BG_LDS_ALIGNED=1: aligned dwords + alignbyte
+// BG_LDS_ALIGNED=1 (default): aligned dwords + alignbyte (one extra ds_read per window, no
+// LDS_UNALIGNED_STALL: k_parse_set_v 0.99 -> 0.92 ms, round 5); 0: unaligned LDS reads
 #ifndef BG_LDS_ALIGNED
-#define BG_LDS_ALIGNED 0
+#define BG_LDS_ALIGNED 1
 #endif
 #if BG_LDS_ALIGNED
 template <int N>
 __device__ __forceinline__ void lds_words(const void* p, uint32_t* o) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t* d = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
+  // (the aligned address by pointer arithmetic on p, not an integer round trip: the compiler
+  // keeps p's LDS address space and emits ds_read, not flat loads)
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(p) - sh);
   uint32_t w[N + 1];
 #pragma unroll
   for (int i = 0; i <= N; ++i) w[i] = d[i];
