@@ -24,9 +24,22 @@ $(OBJ)/%.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/bedgpu.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(HIPOBJS)
+# bg_build_hash(): content hash of the sources, Makefile and flags (tools/src_hash.py), checked
+# by tests/conftest.py against the tree; the file is rewritten only when the hash changes
+BUILD_FLAGS = $(HIPFLAGS) ARCH=$(ARCH)
+$(OBJ)/bg_buildhash.c: FORCE
+	@mkdir -p $(OBJ)
+	@python3 tools/src_hash.py --flags "$(BUILD_FLAGS)" --write $@ > /dev/null
+
+$(OBJ)/bg_buildhash.o: $(OBJ)/bg_buildhash.c
+	$(CC) -O2 -fPIC -c $< -o $@
+
+$(LIB): $(HIPOBJS) $(OBJ)/bg_buildhash.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lz -ldl -Wl,-rpath,/opt/rocm/lib
+
+print-hash:
+	@python3 tools/src_hash.py --flags "$(BUILD_FLAGS)"
 
 $(BIN)/%: bedops_amd/cli/%.c bedops_amd/cli/cli_common.h bedops_amd/cli/cli_shard.h bedops_amd/cli/cli_stream.h include/bedgpu.h $(LIB)
 	@mkdir -p $(BIN)
@@ -60,4 +73,5 @@ clean:
 	rm -rf build bedops_amd/lib bedops_amd/bin tools/build
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib cli tools oracle clean
+.PHONY: all lib cli tools oracle clean print-hash FORCE
+FORCE:

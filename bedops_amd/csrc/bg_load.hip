@@ -2715,8 +2715,148 @@ __global__ void __launch_bounds__(BG_NT) k_set_write(const int64_t* __restrict__
 }
 
 // -------------------------------------------------------------------------------------
+// blank lines. The reference reads rows with fscanf("%s\t%lu\t%lu...") + fgetc
+// (Bed.hpp:244-255): after a row's '\n' the next %s skips every whitespace byte, so lines of
+// only whitespace (and a line's leading whitespace) are never seen. The loaders split on '\n',
+// so a load that meets a blank line (ERR_BLANK) is redone on the text with those bytes removed:
+// byte p goes iff it is whitespace or '\n' and the last '\n' before p comes after the last
+// other byte before p (at the start of the text: both "before" values are below every
+// position, the '\n' one higher). One wave per 4 KiB tile, 64 bytes per lane.
+// -------------------------------------------------------------------------------------
+constexpr uint32_t BK_T = 4096;
+
+// per tile: its last '\n' (-1: none) and its last byte that is neither '\n' nor whitespace
+// (-2: none), the identities of the exclusive max-scans that follow
+__global__ void __launch_bounds__(BG_NT) k_blank_marks(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                       uint32_t nt, int64_t* __restrict__ tnl,
+                                                       int64_t* __restrict__ tns) {
+  const uint32_t lane = threadIdx.x & 63, t = blockIdx.x * (BG_NT / 64) + (threadIdx.x >> 6);
+  if (t >= nt) return;
+  const uint64_t b0 = (uint64_t)t * BK_T + 64ull * lane;
+  int64_t lnl = -1, lns = -2;
+  for (uint32_t k = 0; k < 64 && b0 + k < nb; ++k) {
+    const uint8_t ch = txt[b0 + k];
+    if (ch == '\n') lnl = (int64_t)(b0 + k);
+    else if (!bg_isws(ch)) lns = (int64_t)(b0 + k);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    lnl = max(lnl, (int64_t)__shfl_xor(lnl, d, 64));
+    lns = max(lns, (int64_t)__shfl_xor(lns, d, 64));
+  }
+  if (lane == 0) {
+    tnl[t] = lnl;
+    tns[t] = lns;
+  }
+}
+
+// count pass (out == nullptr: kept bytes per tile into cnt) or write pass (kept bytes to
+// out + off[t]); xnl/xns: the exclusive max-scans of k_blank_marks' values
+__global__ void __launch_bounds__(BG_NT) k_blank_pack(const uint8_t* __restrict__ txt, uint64_t nb,
+                                                      uint32_t nt, const int64_t* __restrict__ xnl,
+                                                      const int64_t* __restrict__ xns,
+                                                      uint64_t* __restrict__ cnt,
+                                                      const uint64_t* __restrict__ off,
+                                                      uint8_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63, t = blockIdx.x * (BG_NT / 64) + (threadIdx.x >> 6);
+  if (t >= nt) return;
+  const uint64_t b0 = (uint64_t)t * BK_T + 64ull * lane;
+  int64_t lnl = -1, lns = -2;  // this lane's own marks, then the lanes before it
+  for (uint32_t k = 0; k < 64 && b0 + k < nb; ++k) {
+    const uint8_t ch = txt[b0 + k];
+    if (ch == '\n') lnl = (int64_t)(b0 + k);
+    else if (!bg_isws(ch)) lns = (int64_t)(b0 + k);
+  }
+  for (int d = 1; d < 64; d <<= 1) {  // inclusive max-scan over the lanes
+    const int64_t a = __shfl_up(lnl, d, 64), b = __shfl_up(lns, d, 64);
+    if (lane >= (uint32_t)d) {
+      lnl = max(lnl, a);
+      lns = max(lns, b);
+    }
+  }
+  int64_t cnl = __shfl_up(lnl, 1, 64), cns = __shfl_up(lns, 1, 64);
+  if (lane == 0) cnl = -1, cns = -2;
+  cnl = max(cnl, xnl[t]);
+  cns = max(cns, xns[t]);
+  const int64_t snl = cnl, sns = cns;
+  uint32_t keep = 0;
+  for (uint32_t k = 0; k < 64 && b0 + k < nb; ++k) {
+    const uint8_t ch = txt[b0 + k];
+    const bool sp = ch == '\n' || bg_isws(ch);
+    keep += !(sp && cnl > cns);
+    if (ch == '\n') cnl = (int64_t)(b0 + k);
+    else if (!sp) cns = (int64_t)(b0 + k);
+  }
+  uint32_t pre = keep;  // inclusive sum over the lanes
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = __shfl_up(pre, d, 64);
+    if (lane >= (uint32_t)d) pre += a;
+  }
+  if (!out) {
+    if (lane == 63) cnt[t] = pre;
+    return;
+  }
+  uint64_t o = off[t] + pre - keep;
+  cnl = snl;
+  cns = sns;
+  for (uint32_t k = 0; k < 64 && b0 + k < nb; ++k) {
+    const uint8_t ch = txt[b0 + k];
+    const bool sp = ch == '\n' || bg_isws(ch);
+    if (!(sp && cnl > cns)) out[o++] = ch;
+    if (ch == '\n') cnl = (int64_t)(b0 + k);
+    else if (!sp) cns = (int64_t)(b0 + k);
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // host side
 // -------------------------------------------------------------------------------------
+
+// the device text txt[0, nb) without its blank lines (k_blank_*): *out (bg_alloc'ed, nbytes
+// + 16), *nout bytes
+static int strip_blank_lines(bg_ctx* c, const uint8_t* txt, uint64_t nb, char** out, uint64_t* nout) {
+  *out = nullptr;
+  *nout = 0;
+  const uint32_t nt = (uint32_t)bg_blocks(nb, BK_T);
+  char* o = (char*)bg_alloc(c, nb + 16);
+  int64_t* w = (int64_t*)bg_alloc(c, 32ull * (nt ? nt : 1) + 16);
+  if (!o || !w) {
+    bg_release(c, o);
+    bg_release(c, w);
+    return BG_E_NOMEM;
+  }
+  int64_t *tnl = w, *tns = w + nt, *xnl = w + 2ull * nt, *xns = w + 3ull * nt;
+  uint64_t* cnt = (uint64_t*)tnl;  // (tnl is dead once scanned)
+  uint64_t* tot = (uint64_t*)(w + 4ull * nt);
+  int rc = 0;
+  if (nt) {
+    const dim3 g(bg_blocks(nt, BG_NT / 64));
+    hipLaunchKernelGGL(k_blank_marks, g, dim3(BG_NT), 0, c->stream, txt, nb, nt, tnl, tns);
+    rc = bg_hip_ok(c, hipGetLastError());
+    if (!rc) rc = bg_scan_max_i64(c, tnl, xnl, nt, -1);
+    if (!rc) rc = bg_scan_max_i64(c, tns, xns, nt, -2);
+    if (!rc) {
+      hipLaunchKernelGGL(k_blank_pack, g, dim3(BG_NT), 0, c->stream, txt, nb, nt, (const int64_t*)xnl,
+                         (const int64_t*)xns, cnt, (const uint64_t*)nullptr, (uint8_t*)nullptr);
+      rc = bg_hip_ok(c, hipGetLastError());
+    }
+    if (!rc) rc = bg_scan_sum_u64(c, cnt, cnt, nt, tot);
+    if (!rc) {
+      hipLaunchKernelGGL(k_blank_pack, g, dim3(BG_NT), 0, c->stream, txt, nb, nt, (const int64_t*)xnl,
+                         (const int64_t*)xns, (uint64_t*)nullptr, (const uint64_t*)cnt, (uint8_t*)o);
+      rc = bg_hip_ok(c, hipGetLastError());
+    }
+    if (!rc) rc = bg_fetch_u64(c, tot, nout);
+  }
+  bg_release(c, w);
+  if (rc) {
+    bg_release(c, o);
+    *nout = 0;
+    return rc;
+  }
+  *out = o;
+  return 0;
+}
+
 static const char* kind_name(int k) {
   return (k == BG_BED5 || k == BG_BED5_REST) ? "BED5" : (k == BG_BED3_REST ? "BED3+rest" : "BED3");
 }
@@ -3436,10 +3576,43 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].lbw && (hst[i].flags & BG_ROW_LOOKBACK)) redo = scoutredo = true;
   for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
+  // blank lines (k_blank_*): the load is redone on the texts without them, which then belong
+  // to the new set
+  std::vector<char*> stripped;
+  std::vector<bg_input> unblank;
+  if (rc == BG_E_BLANK) {
+    rc = 0;
+    bool changed = false;
+    stripped.assign(n, nullptr);
+    unblank.assign(inputs, inputs + n);
+    for (int i = 0; i < n && !rc; ++i) {
+      if (!st[i].ntiles || (!hst[i].nblank && (hst[i].first_bad == ~0ULL || (hst[i].first_bad & 0xff) != ERR_BLANK)))
+        continue;
+      uint64_t nb2 = 0;
+      rc = strip_blank_lines(c, st[i].txt, st[i].nb, &stripped[i], &nb2);
+      if (!rc) unblank[i] = bg_input{stripped[i], nb2, 1, inputs[i].kind};
+      if (!rc && nb2 != st[i].nb) changed = true;
+    }
+    if (!rc && !changed) rc = BG_E_BLANK;  // (cannot happen: a stripped text has no blank line)
+    if (rc) {
+      for (char* p : stripped) bg_release(c, p);
+      unblank.clear();
+    }
+  }
   if (rc) (void)hipStreamSynchronize(c->stream);  // pending copies use the pinned staging
   for (auto& S : st) release_state(c, S);
   bg_release(c, ctr);
   bg_release(c, dst);
+  if (!rc && !unblank.empty()) {
+    bg_set_free(s);
+    const int rc2 = bg_load(c, n, unblank.data(), out);
+    for (int i = 0; i < n; ++i) {
+      if (!stripped[i]) continue;
+      if (rc2 == 0) (*out)->t[i]->own_text = stripped[i];
+      else bg_release(c, stripped[i]);
+    }
+    return rc2;
+  }
   if (rc || redo) {
     bg_set_free(s);
     if (rc) return rc;

@@ -240,6 +240,161 @@ __global__ void k_sd_out(EvView v, const uint64_t* __restrict__ U, const uint64_
   oe[k] = v.key(U[C[k]]);
 }
 
+// --symmdiff over inputs with zero-length rows. A zero-length piece survives or not depending
+// on which file heads are pending when nextSymmetricDiffLine meets it, so the coverage form
+// above does not apply; the stream is replayed instead. Each file is read only through
+// getNextFileMergedCoords (Bedops.cpp:792-814), so its stream is its list of touching-merged
+// components. One thread per segment = component of the union of all inputs: no file head,
+// piece or doSymmetricDifference join (mergeOverlap, Bedops.cpp:697-747) crosses the gap
+// between two segments, and a head beyond the segment never changes a case's outcome (its
+// start exceeds every end inside the segment, so "minSecond > nextFirst" is false, which is
+// what the cases without a next do). Within a segment the replay follows
+// nextSymmetricDiffLine (Bedops.cpp:1343-1467) call by call: every head merged and pushed
+// back, the minimum start's files (allMins) and the next start (allNext), then cases 1-4 on
+// the push-back stacks (depth <= 2: a merged head over one read-ahead row).
+struct SdFile {
+  const int64_t* s;
+  const int64_t* e;
+  uint64_t n;
+};
+struct SdRd {
+  uint64_t pos, hi;
+  int sp;
+  int64_t ss[3], se[3];
+};
+__device__ __forceinline__ bool sd_has(const SdRd& r) { return r.sp > 0 || r.pos < r.hi; }
+__device__ __forceinline__ void sd_read(SdRd& r, const SdFile& F, int64_t& s, int64_t& e) {
+  if (r.sp > 0) {
+    --r.sp;
+    s = r.ss[r.sp];
+    e = r.se[r.sp];
+  } else {
+    s = F.s[r.pos];
+    e = F.e[r.pos];
+    ++r.pos;
+  }
+}
+__device__ __forceinline__ void sd_push(SdRd& r, int64_t s, int64_t e, int* err) {
+  if (r.sp >= 3) {
+    *err = 1;
+    return;
+  }
+  r.ss[r.sp] = s;
+  r.se[r.sp] = e;
+  ++r.sp;
+}
+// mergeOverlap(p1, p2) within one chromosome: the union when they overlap or touch
+__device__ __forceinline__ bool sd_merge(int64_t s1, int64_t e1, int64_t s2, int64_t e2, int64_t& s,
+                                         int64_t& e) {
+  if (s1 < s2) {
+    if (e1 < s2) return false;
+    s = s1;
+  } else if (s1 > s2) {
+    if (e2 < s1) return false;
+    s = s2;
+  } else {
+    s = s1;
+  }
+  e = e1 > e2 ? e1 : e2;
+  return true;
+}
+
+template <bool WRITE>
+__global__ void k_sd_replay(const SdFile* __restrict__ F, int nf, const int64_t* __restrict__ US,
+                            const int64_t* __restrict__ UE, uint64_t nseg, SdRd* __restrict__ scr,
+                            uint64_t nthr, uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                            int64_t* __restrict__ os, int64_t* __restrict__ oe, int* __restrict__ err) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= nthr) return;
+  SdRd* rd = scr + tid * (uint64_t)nf;
+  for (uint64_t g = tid; g < nseg; g += nthr) {
+    for (int f = 0; f < nf; ++f) {
+      SdRd& r = rd[f];
+      r.pos = lower_bound_i64(F[f].s, F[f].n, US[g]);
+      r.hi = upper_bound_in(F[f].s, r.pos, F[f].n, UE[g]);
+      r.sp = 0;
+    }
+    uint64_t k = 0, o = WRITE ? off[g] : 0;
+    bool have = false;
+    int64_t ts = 0, te = 0;
+    auto emit = [&](int64_t s, int64_t e) {
+      int64_t ms, me;
+      if (!have) {
+        ts = s, te = e, have = true;
+      } else if (sd_merge(s, e, ts, te, ms, me)) {
+        ts = ms, te = me;
+      } else {
+        if (WRITE) os[o + k] = ts, oe[o + k] = te;
+        ++k;
+        ts = s, te = e;
+      }
+    };
+    for (;;) {
+      int64_t mn = LLONG_MAX;
+      for (int f = 0; f < nf; ++f) {  // getNextFileMergedCoords of every file, pushed back
+        SdRd& r = rd[f];
+        if (!sd_has(r)) continue;
+        int64_t s, e, ns, ne, ms, me;
+        sd_read(r, F[f], s, e);
+        while (sd_has(r)) {
+          sd_read(r, F[f], ns, ne);
+          if (sd_merge(ns, ne, s, e, ms, me)) {
+            s = ms, e = me;
+          } else {
+            sd_push(r, ns, ne, err);
+            break;
+          }
+        }
+        sd_push(r, s, e, err);
+        mn = s < mn ? s : mn;
+      }
+      if (mn == LLONG_MAX) break;
+      int nm = 0, last_min = 0;
+      int64_t min_second = LLONG_MAX, next_first = LLONG_MAX;
+      for (int f = 0; f < nf; ++f) {
+        const SdRd& r = rd[f];
+        if (r.sp == 0) continue;
+        const int64_t hs = r.ss[r.sp - 1], he = r.se[r.sp - 1];
+        if (hs == mn) {
+          ++nm;
+          last_min = f;
+          min_second = he < min_second ? he : min_second;
+        } else if (hs < next_first) {
+          next_first = hs;
+        }
+      }
+      const bool has_next = next_first != LLONG_MAX;
+      int64_t s, e;
+      if (nm == 1 && !has_next) {  // case 1
+        sd_read(rd[last_min], F[last_min], s, e);
+        emit(s, e);
+      } else if (nm == 1) {  // case 3
+        sd_read(rd[last_min], F[last_min], s, e);
+        if (min_second > next_first) {
+          emit(s, next_first);
+          sd_push(rd[last_min], next_first, e, err);
+        } else {
+          emit(s, e);
+        }
+      } else {  // cases 2 and 4: the shared prefix is cut off every minimum file's head
+        const bool cut_next = has_next && min_second > next_first;
+        for (int f = 0; f < nf; ++f) {
+          SdRd& r = rd[f];
+          if (r.sp == 0 || r.ss[r.sp - 1] != mn) continue;
+          sd_read(r, F[f], s, e);
+          if (cut_next) sd_push(r, next_first, e, err);
+          else if (e != min_second) sd_push(r, min_second, e, err);
+        }
+      }
+    }
+    if (have) {
+      if (WRITE) os[o + k] = ts, oe[o + k] = te;
+      ++k;
+    }
+    if (!WRITE) cnt[g] = k;
+  }
+}
+
 // ------------------------------- --everything ---------------------------------------
 // accumulated merge: coordinates + a pointer to each row's verbatim remainder
 struct Multi {
@@ -506,18 +661,68 @@ extern "C" int bg_partition(bg_ctx* c, bg_set* set, const int* files, int nf, bg
   return 0;
 }
 
+// --symmdiff when an input has zero-length rows: k_sd_replay per union component (count pass,
+// scan, write pass)
+static int symmdiff_replay(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
+  int rc;
+  std::vector<Ivl> comps(nf);
+  for (int k = 0; k < nf; ++k)
+    if ((rc = bg_table_components(c, set->t[files[k]], comps[k]))) return rc;
+  Ivl u;
+  if ((rc = bg_union_components(c, set, files, nf, u))) return rc;
+  std::vector<SdFile> hf(nf);
+  for (int k = 0; k < nf; ++k) hf[k] = SdFile{comps[k].s, comps[k].e, comps[k].n};
+  const uint64_t nseg = u.n;
+  // threads: one per segment, capped so the per-thread reader states stay within 64 MiB
+  const uint64_t cap = std::max<uint64_t>(256, (64ull << 20) / (sizeof(SdRd) * (uint64_t)nf));
+  const uint64_t nthr = std::min<uint64_t>(nseg, cap);
+  SdFile* df = (SdFile*)bg_alloc(c, sizeof(SdFile) * nf);
+  SdRd* scr = (SdRd*)bg_alloc(c, sizeof(SdRd) * (nthr ? nthr : 1) * nf);
+  uint64_t* off = (uint64_t*)bg_alloc(c, 8 * (nseg + 1));
+  int* err = (int*)bg_alloc(c, 8);
+  if (!df || !scr || !off || !err) return BG_E_NOMEM;
+  BG_HIP(c, hipMemcpyAsync(df, hf.data(), sizeof(SdFile) * nf, hipMemcpyHostToDevice, c->stream));
+  BG_HIP(c, hipMemsetAsync(err, 0, 8, c->stream));
+  if (nthr) {
+    BG_LAUNCH(c, "k_sd_replay", k_sd_replay<false>, dim3(bg_blocks(nthr, 64)), dim3(64), df, nf,
+              (const int64_t*)u.s, (const int64_t*)u.e, nseg, scr, nthr, off, (const uint64_t*)nullptr,
+              (int64_t*)nullptr, (int64_t*)nullptr, err);
+    BG_HIP(c, hipGetLastError());
+  }
+  rc = bg_scan_sum_u64(c, off, off, nseg, off + nseg);
+  uint64_t total = 0;
+  if (!rc) rc = bg_fetch_u64(c, off + nseg, &total);
+  Ivl g;
+  if (!rc) rc = ivl_alloc(c, g, total);
+  if (rc) return rc;
+  if (nthr) {
+    BG_LAUNCH(c, "k_sd_replay", k_sd_replay<true>, dim3(bg_blocks(nthr, 64)), dim3(64), df, nf,
+              (const int64_t*)u.s, (const int64_t*)u.e, nseg, scr, nthr, (uint64_t*)nullptr,
+              (const uint64_t*)off, g.s, g.e, err);
+    BG_HIP(c, hipGetLastError());
+  }
+  int herr = 0;
+  BG_HIP(c, hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  BG_HIP(c, hipStreamSynchronize(c->stream));
+  for (Ivl& v : comps) ivl_free(c, v);
+  ivl_free(c, u);
+  for (void* p : {(void*)df, (void*)scr, (void*)off, (void*)err}) bg_release(c, p);
+  if (herr) {
+    ivl_free(c, g);
+    return bg_fail(c, BG_E_HIP, "symmdiff replay: push-back stack overflow");
+  }
+  *out = bg_new_ivl_result(c, set, g);
+  bg_mark(c, "symmdiff");
+  return 0;
+}
+
 extern "C" int bg_symmdiff(bg_ctx* c, bg_set* set, const int* files, int nf, bg_result** out) {
   int rc = bg_check_files(c, set, files, nf, 2);
   if (rc || !out) return rc ? rc : BG_E_ARG;
-  // Zero-length rows (rejected by the reference's own --ec checker,
-  // BedCheckIterator.hpp:619-620) survive nextSymmetricDiffLine depending on which file
-  // heads are pending at that moment; that stream state is not reproduced here.
+  // zero-length rows (rejected by the reference's own --ec checker,
+  // BedCheckIterator.hpp:619-620, but read without it): the stream replay (k_sd_replay)
   for (int k = 0; k < nf; ++k)
-    if (set->t[files[k]]->has_zero_len)
-      return bg_fail(c, BG_E_UNSUPPORTED,
-                     "zero-length elements (end == start) are not supported by --symmdiff on "
-                     "the GPU path (BEDOPS --ec rejects them: End coordinates must be greater "
-                     "than start coordinates)");
+    if (set->t[files[k]]->has_zero_len) return symmdiff_replay(c, set, files, nf, out);
   std::vector<Ivl> comps(nf);
   for (int k = 0; k < nf; ++k)
     if ((rc = bg_table_components(c, set->t[files[k]], comps[k]))) return rc;

@@ -42,7 +42,7 @@ ERRORS = {-11: "INTERNAL", -1: "HIP", -2: "PARSE", -3: "UNSORTED", -4: "RANGE", 
 BG_E_VISITOR = -12
 
 # exported symbols of include/bedgpu.h (checked by tests/test_abi.py)
-SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_load",
+SYMBOLS = ["bg_open", "bg_close", "bg_last_error", "bg_sync", "bg_stream", "bg_build_hash", "bg_load",
            "bg_set_rows", "bg_set_restrict_chrom", "bg_set_free", "bg_merge", "bg_intersect",
            "bg_difference", "bg_element_of", "bg_map", "bg_result_rows", "bg_result_format",
            "bg_result_text_device", "bg_result_copy_text", "bg_result_write", "bg_result_free",

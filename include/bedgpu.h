@@ -170,6 +170,9 @@ void bg_close(bg_ctx* ctx);
 const char* bg_last_error(const bg_ctx* ctx);
 int bg_sync(bg_ctx* ctx);
 void* bg_stream(bg_ctx* ctx); /* the hipStream_t all work of this context runs on */
+/* content hash of the sources, Makefile and flags this library was built from
+   (tools/src_hash.py); the test harness refuses a library whose hash differs from the tree */
+const char* bg_build_hash(void);
 
 /* loading: parse N BED texts into device-resident keyed SoA columns */
 int bg_load(bg_ctx* ctx, int n, const bg_input* inputs, bg_set** out);

@@ -28,15 +28,32 @@ def oracle_bin():
             "sortbed": os.path.join(ROOT, "oracle", "build", "sortbed_oracle")}
 
 
-def _lib_fresh():
-    """the in-tree libbedgpu.so is newer than every source it is built from (the objects are
-    not shipped to the GPU box: make would rebuild the whole library there, ~100 s)"""
-    import glob
+def tree_build_hash():
+    """the content hash the Makefile would embed for this tree and its flags"""
+    r = subprocess.run(["make", "-s", "print-hash"], cwd=ROOT, check=True, stdout=subprocess.PIPE)
+    return r.stdout.decode().strip()
+
+
+def lib_build_hash():
+    """bg_build_hash() of the in-tree libbedgpu.so (None when it is missing)"""
+    import ctypes
     lib = os.path.join(ROOT, "bedops_amd", "lib", "libbedgpu.so")
     if not os.path.exists(lib):
+        return None
+    L = ctypes.CDLL(lib)
+    L.bg_build_hash.restype = ctypes.c_char_p
+    return L.bg_build_hash().decode()
+
+
+def _lib_fresh():
+    """the in-tree libbedgpu.so was built from exactly this tree's sources, Makefile and flags
+    (content hash, not mtimes: a checkout or the copy to the GPU box resets those). Objects are
+    not shipped to the GPU box, so a fresh library is taken as built there (no ~100 s rebuild)."""
+    try:
+        have = lib_build_hash()
+    except (OSError, AttributeError):
         return False
-    srcs = glob.glob(os.path.join(ROOT, "bedops_amd", "csrc", "*")) + [os.path.join(ROOT, "include", "bedgpu.h")]
-    return os.path.getmtime(lib) >= max(os.path.getmtime(f) for f in srcs)
+    return have is not None and have == tree_build_hash()
 
 
 @pytest.fixture(scope="session")
@@ -45,7 +62,9 @@ def gpu_bin():
     if _lib_fresh():
         _make("-o", "bedops_amd/lib/libbedgpu.so", "cli")  # (-o: take the library as built)
     else:
+        sys.stderr.write("conftest: libbedgpu.so is missing or was built from other sources; rebuilding\n")
         _make("lib", "cli")
+        assert _lib_fresh(), "libbedgpu.so does not carry this tree's build hash after a rebuild"
     return {"bedops": os.path.join(ROOT, "bedops_amd", "bin", "bedops"),
             "bedmap": os.path.join(ROOT, "bedops_amd", "bin", "bedmap"),
             "closest": os.path.join(ROOT, "bedops_amd", "bin", "closest-features"),

@@ -82,16 +82,11 @@ MODES = [
 @pytest.mark.parametrize("mode,extra,nfiles,kw", MODES,
                          ids=lambda v: "_".join(v) if isinstance(v, list) else str(v))
 def test_random_modes_vs_oracle(eng, oracle_bin, mode, extra, nfiles, kw, zero_frac):
-    from bedops_amd import BedgpuError
     rng = random.Random(zlib.crc32(repr((mode, extra, nfiles, zero_frac)).encode()))
     with tempfile.TemporaryDirectory() as td:
         for trial in range(10):
             texts = gen(rng, nfiles, zero_frac, rest=(mode == "-u"))
-            if mode == "-s" and has_zero(texts):  # refused loudly, never approximated
-                with pytest.raises(BedgpuError) as ei:
-                    eng.bedops(mode, texts, **kw)
-                assert ei.value.code == -8
-                continue
+            # (--symmdiff over zero-length rows: the stream replay, k_sd_replay)
             want = run_oracle(oracle_bin["bedops"], [mode] + extra, texts, td)
             got = eng.bedops(mode, texts, **kw)
             assert got == want, (mode, extra, trial)
@@ -162,3 +157,19 @@ def test_modes_large_vs_oracle(eng, oracle_bin, mode, nfiles):
     with tempfile.TemporaryDirectory() as td:
         want = run_oracle(oracle_bin["bedops"], [mode] + extra, texts, td)
     assert eng.bedops(mode, texts, **kw) == want
+
+
+@pytest.mark.parametrize("nfiles", [2, 3, 5])
+def test_symmdiff_zero_length_replay_vs_oracle(eng, oracle_bin, nfiles):
+    """--symmdiff over zero-length rows: the per-segment stream replay (k_sd_replay) against the
+    oracle's nextSymmetricDiffLine (Bedops.cpp:1343-1467), dense zero-length, nested and
+    duplicated rows near base 0"""
+    rng = random.Random(zlib.crc32(repr(("sd-zero", nfiles)).encode()))
+    seen = 0
+    with tempfile.TemporaryDirectory() as td:
+        for trial in range(25):
+            texts = gen(rng, nfiles, rng.choice([0.1, 0.3, 0.6]), near_zero=rng.random() < 0.5)
+            seen += has_zero(texts)
+            want = run_oracle(oracle_bin["bedops"], ["-s"], texts, td)
+            assert eng.bedops("-s", texts) == want, (nfiles, trial)
+    assert seen >= 10
