@@ -74,6 +74,7 @@ struct bg_ctx {
   int device = 0;
   bool row_wide = false;  // bg_load: rows parsed by k_parse (a redo after BG_ROW_OVERFLOW)
   bool row_scout = false;  // bg_load: row offsets from the k_scout pass (a redo after BG_ROW_LOOKBACK)
+  uint64_t big_need = 0;   // bg_load: capacity of the k_score_big list (a redo after it overflowed)
   uint64_t out_skip = 0;  // bytes write_device_ring still drops (bg_set_output_skip)
   int ncu = 256;  // compute units
   std::vector<std::pair<const void*, uint32_t>> resident;  // kernel -> resident BG_NT blocks

@@ -2209,6 +2209,9 @@ __device__ __forceinline__ uint4 ldsu128(const void* p) {
 #ifndef BG_EXP_V
 #define BG_EXP_V 0
 #endif
+#ifndef BG_WSM_AL
+#define BG_WSM_AL 0
+#endif
 // BG_GTXT=1: an interior sub-tile is not staged in LDS; its lines' token and numbers are
 // read from the text through the vector memory path (the unaligned LDS reads were the LDS
 // pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave). Timed within +-3% of staging on
@@ -2403,7 +2406,12 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     const uint32_t len = qn - q - 1;  // bytes before the line's '\n'
     uint32_t WS;
     {
+#if BG_WSM_AL  // (wsm is dword-aligned: two plain reads, no alignbyte funnel)
+      const uint32_t* wp = &S.wsm[q >> 5];
+      const uint2 two = make_uint2(wp[0], wp[1]);
+#else
       const uint2 two = ldsu64(&S.wsm[q >> 5]);
+#endif
       WS = __builtin_amdgcn_alignbit(two.y, two.x, q & 31u);
     }
     WS |= len < 32u ? (~0u << (len & 31u)) : 0u;  // bytes past the line end act as whitespace
@@ -2553,7 +2561,15 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
 // (SQ: 2830 of a wave's 5465 quad-cycles were waits, 2029 of them before the first byte in
 // a loads-only variant). The touched dwords are consumed (pf_sink, null at run time) so the
 // loads are real; they are waited for only at the end, long after they landed.
-__global__ void __launch_bounds__(64) k_parse_set_v(
+#ifndef BG_PSV_SGPR
+#define BG_PSV_SGPR 0
+#endif
+#if BG_PSV_SGPR
+#define BG_PSV_ATTR __attribute__((amdgpu_num_sgpr(BG_PSV_SGPR)))
+#else
+#define BG_PSV_ATTR
+#endif
+__global__ void __launch_bounds__(64) BG_PSV_ATTR k_parse_set_v(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st, uint32_t pfd,
@@ -3124,9 +3140,15 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     const char* e = getenv("BEDGPU_ROW_PARSE");
     return !(e && atoi(e) == 0);
   }();
-  // scores past the loader's fast paths (parse_score: isint -1) go to k_score_big (finish_one)
+  // scores past the loader's fast paths (parse_score: isint -1) go to k_score_big (finish_one);
+  // the list holds 2^20 (BEDGPU_BIGCAP) unless a load that overflowed it is being redone with
+  // the count it found (c->big_need)
   if (T->score) {
-    S.bigcap = (uint32_t)std::min<uint64_t>(T->n, 1u << 20);
+    static const uint64_t cap0 = [] {
+      const char* e = getenv("BEDGPU_BIGCAP");
+      return e ? (uint64_t)std::max(1, atoi(e)) : (uint64_t)(1u << 20);
+    }();
+    S.bigcap = (uint32_t)std::min<uint64_t>(T->n, std::max<uint64_t>(cap0, c->big_need));
     S.big = (uint64_t*)bg_alloc(c, 16ull * (S.bigcap ? S.bigcap : 1));
     if (!S.big) return BG_E_NOMEM;
   }
@@ -3354,7 +3376,7 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
   int rc = report_status(c, idx, h);
   if (rc) return rc;
   if (h.nbig) {  // scores past the fast paths: exact big-number conversion (bg_strtod.h)
-    if (h.nbig > S.bigcap || !T->score)
+    if (h.nbig > S.bigcap || !T->score)  // (bg_load redoes a load whose list overflowed)
       return bg_fail(c, BG_E_UNSUPPORTED, "too many scores needing the exact big-number conversion");
     BG_LAUNCH(c, "k_score_big", k_score_big, dim3(bg_blocks(h.nbig, 64)), dim3(64), S.txt, S.nb, S.big, h.nbig,
               T->score);
@@ -3563,11 +3585,11 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   HP("rt3");
   // a BG_BED3_SET input with an error (its exact line is not known) or a staging overflow:
   // the whole load is redone with that input's row columns (BG_BED3)
-  bool redo = false, wide = false;
+  bool redo = false, wide = false, setredo = false;
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind == BG_BED3_SET && st[i].ntiles &&
         (hst[i].first_bad != ~0ULL || (hst[i].flags & BG_SET_OVERFLOW)))
-      redo = true;
+      redo = setredo = true;
   // a row input with a tile of more lines than k_parse_n holds: redone with k_parse
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && (hst[i].flags & BG_ROW_OVERFLOW)) redo = wide = true;
@@ -3575,6 +3597,12 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   bool scoutredo = false;
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].lbw && (hst[i].flags & BG_ROW_LOOKBACK)) redo = scoutredo = true;
+  // a row input with more long scores than its k_score_big list holds: redone with room for all
+  uint64_t bigneed = 0;
+  for (int i = 0; i < n && !rc; ++i)
+    if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && hst[i].first_bad == ~0ULL && hst[i].nbig > st[i].bigcap)
+      bigneed = std::max<uint64_t>(bigneed, hst[i].nbig);
+  if (bigneed) redo = true;
   for (int i = 0; i < n && !rc && !redo; ++i) rc = finish_one(c, i, inputs[i], s->t[i], st[i], hst[i]);
   // blank lines (k_blank_*): the load is redone on the texts without them, which then belong
   // to the new set
@@ -3618,13 +3646,16 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     if (rc) return rc;
     std::vector<bg_input> rows(inputs, inputs + n);
     for (auto& in : rows)
-      if (in.kind == BG_BED3_SET) in.kind = BG_BED3;
+      if (setredo && in.kind == BG_BED3_SET) in.kind = BG_BED3;
     const bool w0 = c->row_wide, s0 = c->row_scout;
+    const uint64_t b0 = c->big_need;
     if (wide) c->row_wide = true;
     if (scoutredo) c->row_scout = true;
+    if (bigneed) c->big_need = std::max(b0, bigneed);
     const int rc2 = bg_load(c, n, rows.data(), out);
     c->row_wide = w0;
     c->row_scout = s0;
+    c->big_need = b0;
     return rc2;
   }
   for (bg_table* T : s->t)  // keep every column non-null for empty inputs

@@ -10,7 +10,8 @@
 //                  (doPartitions / nextPartitionGroup, Bedops.cpp:614-686, :1249-1337)
 //   bg_symmdiff    touching-merged components of the coordinates covered by exactly one
 //                  file (doSymmetricDifference / nextSymmetricDiffLine, Bedops.cpp:697-747,
-//                  :1343-1467; inputs with zero-length rows are refused)
+//                  :1343-1467; inputs with zero-length rows: the stream replayed per union
+//                  component, k_sd_replay)
 //   bg_everything  k-way merge of every row of every file, ties on (start, end) broken by
 //                  strcmp of the remainder, then by file order (doUnionAll /
 //                  nextUnionAllLine, Bedops.cpp:752-786, :1472-1518)
@@ -555,7 +556,10 @@ __global__ void k_pad_eval(const int64_t* __restrict__ KS, const int64_t* __rest
   }
   keep[i] = k ? 1 : 0;
   clamp[i] = (k && cl) ? 1 : 0;
-  if (k && (ns > BG_MAX_COORD || ne > BG_MAX_COORD)) bg_report(st, i, ERR_RANGE);
+  // coordinates past 999999999999 are printed by the reference and kept here while they fit
+  // the key (< 2^40 - 1); an end that wraps below zero in the reference's uint64 arithmetic
+  // (getFirst's break row, :212) prints as ~1.8e19 and is refused
+  if (k && (ns >= BG_KEY_COORD_MAX || ne >= BG_KEY_COORD_MAX)) bg_report(st, i, ERR_RANGE);
   NS[i] = ck | (int64_t)(ns & BG_COORD_MASK);
   NE[i] = ck | (int64_t)(ne & BG_COORD_MASK);
 }
@@ -855,8 +859,8 @@ extern "C" int bg_set_pad(bg_ctx* c, bg_set* set, int file, int lpad, int rpad) 
   BG_HIP(c, hipStreamSynchronize(c->stream));
   if (c->hstat->first_bad != ~0ULL)
     return bg_fail(c, BG_E_UNSUPPORTED,
-                   "--range moves a coordinate outside 0..999999999999 (not supported on the GPU "
-                   "path)");
+                   "--range moves a coordinate past 2^40 - 2 (an end that wraps below zero in the "
+                   "reference's unsigned arithmetic): not supported on the GPU path");
   // compact every column by the kept rows
   auto gather = [&](auto* src, auto*& dst) -> int {
     using T0 = std::remove_reference_t<decltype(*src)>;

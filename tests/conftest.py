@@ -35,24 +35,22 @@ def tree_build_hash():
 
 
 def lib_build_hash():
-    """bg_build_hash() of the in-tree libbedgpu.so (None when it is missing)"""
-    import ctypes
+    """the build hash embedded in the in-tree libbedgpu.so (None when it is missing), read from
+    the file: a library dlopen'ed once stays loaded, so a rebuilt one would not be seen"""
+    import re
     lib = os.path.join(ROOT, "bedops_amd", "lib", "libbedgpu.so")
     if not os.path.exists(lib):
         return None
-    L = ctypes.CDLL(lib)
-    L.bg_build_hash.restype = ctypes.c_char_p
-    return L.bg_build_hash().decode()
+    with open(lib, "rb") as f:
+        m = re.search(rb"bedgpu-build-hash:([0-9a-f]{32})", f.read())
+    return m.group(1).decode() if m else None
 
 
 def _lib_fresh():
     """the in-tree libbedgpu.so was built from exactly this tree's sources, Makefile and flags
     (content hash, not mtimes: a checkout or the copy to the GPU box resets those). Objects are
     not shipped to the GPU box, so a fresh library is taken as built there (no ~100 s rebuild)."""
-    try:
-        have = lib_build_hash()
-    except (OSError, AttributeError):
-        return False
+    have = lib_build_hash()
     return have is not None and have == tree_build_hash()
 
 

@@ -19,6 +19,8 @@ Suites (VERDICT r02 "Next round" item 5):
   ec       --ec messages of bedops / bedmap / closest-features on malformed inputs
   faster   bedmap --faster (the sweep's own window) under its four criteria
   f2       round 5: window sums past 2^53, --prec past 17, huge/tiny values in %lf and %e
+  r6       round 6: blank lines without --ec, --symmdiff over zero-length rows, --range past
+           999999999999, more long scores than the loader's first big-number list
 The *-rand element operations are excluded: the reference seeds std::random_shuffle with
 time(NULL) (ExtremeVisitor.hpp:47-72), so it has no single answer.
 """
@@ -466,7 +468,78 @@ def f2():
     s.save()
 
 
+# ------------------------------------------------------------------------------- r6
+def _blanks(rng, text):
+    """the same rows with whitespace-only lines (and a few leading-whitespace rows) inserted:
+    before the first row, between rows, after the last one"""
+    out = []
+    for ln in text.splitlines(keepends=True):
+        if rng.random() < 0.15:
+            out.append(rng.choice(["\n", "\n\n", " \n", "\t\n", "\r\n", " \t \n"]))
+        if rng.random() < 0.03:
+            ln = rng.choice([" ", "\t", "  "]) + ln
+        out.append(ln)
+    if rng.random() < 0.7:
+        out.append(rng.choice(["\n", "\n\n\n", "  \n", "\n \t"]))
+    return "".join(out)
+
+
+def r6():
+    """round 6 (VERDICT r05 "Next round" item 1): blank lines without --ec (skipped by the
+    reference's fscanf), --symmdiff over zero-length rows, --range coordinates past
+    999999999999, more long scores than the loader's first big-number list holds (the GPU test
+    runs this suite with BEDGPU_BIGCAP=16)"""
+    s = Suite("r6")
+    rng = random.Random(6006)
+    modes = [["--merge"], ["--intersect"], ["--difference"], ["--everything"], ["--element-of", "1"],
+             ["--not-element-of", "1"], ["--complement"], ["--symmdiff"], ["--partition"], ["--chop", "7"]]
+    for trial in range(6):
+        a = randbed.text(randbed.rows(rng, rng.choice([5, 60, 300]), span=rng.choice([300, 3000]), maxlen=60))
+        b = randbed.text(randbed.rows(rng, rng.choice([5, 60, 300]), span=rng.choice([300, 3000]), maxlen=60))
+        g = s.group(_blanks(rng, a), _blanks(rng, b) if trial % 2 else b)
+        for m in modes:
+            s.run("bedops", m, g, files=[0] if m[0] in ("--merge", "--complement", "--chop") else None)
+        mp = _int_map(rng, randbed.rows(rng, 400, span=3000, maxlen=80))
+        g2 = s.group(_blanks(rng, a), _blanks(rng, mp))
+        s.run("bedmap", ["--echo", "--count", "--mean", "--echo-map-id"], g2)
+        s.run("bedmap", ["--echo", "--max", "--bases"], g2, files=[1])
+        s.run("closest", ["--dist"], g)
+        s.run("closest", ["--closest"], g)
+    # blank lines only / at the very start / a file of only whitespace
+    for t in ["\n", "\n\n", "chr1\t5\t10\n\nchr1\t20\t30\n", "\nchr1\t5\t10\n",
+              "chr1\t5\t10\nchr1\t20\t30\n\n\n", " \n\t\nchr1\t1\t2\n", "chr1\t5\t10\n\nchr1\t20\t30"]:
+        g = s.group(t, "chr1\t0\t100\n")
+        s.run("bedops", ["--merge"], g, files=[0])
+        s.run("bedops", ["--intersect"], g)
+        s.run("bedmap", ["--echo", "--count"], g)
+    # --symmdiff over zero-length rows, 2-5 files
+    for trial in range(30):
+        nf = rng.choice([2, 2, 3, 5])
+        texts = [randbed.text(randbed.rows(rng, rng.choice([0, 3, 40, 200]), span=rng.choice([40, 300, 2000]),
+                                           maxlen=rng.choice([4, 30]), zero_frac=rng.choice([0.1, 0.3, 0.7])))
+                 for _ in range(nf)]
+        s.run("bedops", ["--symmdiff"], s.group(*texts))
+    # --range past 999999999999 (the reference prints such coordinates)
+    top = "".join(f"chr{c}\t{999999999000 + k * 100}\t{999999999000 + k * 100 + 50 + k}\n"
+                  for c in (1, 2) for k in range(9))
+    g = s.group(top, top.replace("\t5", "\t6"))
+    for pad in ("0:100", "100:100", "1000:2000", "-40:500"):
+        for m in (["--merge"], ["--everything"], ["--intersect"], ["--complement"], ["--partition"]):
+            s.run("bedops", ["--range", pad] + m, g, files=[0] if m[0] in ("--merge", "--complement") else None)
+    # more long scores (> 19 significant digits or exponents past the 128-bit path) than 16
+    ref = randbed.rows(rng, 120, span=2000, maxlen=60)
+    mp = randbed.rows(rng, 500, span=2000, maxlen=80)
+    longs = ["0.1234567890123456789012345", "1.00000000000000000000000001e-30", "7e-330",
+             "123456789012345678901234567890", "2.5e-310", "0.30000000000000000000000000001", "5"]
+    lm = "".join(f"{c}\t{a}\t{b}\tid{i}\t{rng.choice(longs)}\n" for i, (c, a, b) in enumerate(mp))
+    g = s.group(randbed.text(ref), lm)
+    for args in (["--count", "--sum", "--prec", "30"], ["--min", "--max", "--sci"], ["--echo-map-score", "--prec", "20"],
+                 ["--mean", "--median"]):
+        s.run("bedmap", args, g)
+    s.save()
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec", "faster", "f2"]
+    which = sys.argv[1:] or ["closest", "bedmap", "decimal", "sortbed", "ec", "faster", "f2", "r6"]
     for w in which:
         globals()[w]()

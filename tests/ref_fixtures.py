@@ -9,7 +9,7 @@ import subprocess
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SUITES = ["closest", "bedmap", "decimal", "sortbed", "ec", "faster", "f2"]
+SUITES = ["closest", "bedmap", "decimal", "sortbed", "ec", "faster", "f2", "r6"]
 
 
 def load(suite):

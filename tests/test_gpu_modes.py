@@ -108,8 +108,8 @@ def test_range_padding_vs_oracle(eng, oracle_bin, mode, nfiles, pad):
         for trial in range(8):
             texts = gen(rng, nfiles, 0.05, rest=(mode in ("-u", "-e")), near_zero=True)
             # A uint64 wrap of an end inside the reference's getFirst (BedPadReader.hpp:212)
-            # yields ends beyond 999999999999 (the reference then prints them, or loops for
-            # ~2^64 steps in --chop): such inputs are refused on the GPU path. The oracle's
+            # yields ends near 2^64 (the reference then prints them, or loops for ~2^64 steps
+            # in --chop): such inputs are refused on the GPU path (past the 2^40 key range). The oracle's
             # --everything prints each padded input to detect them.
             huge = False
             for i in range(nfiles):
@@ -117,7 +117,7 @@ def test_range_padding_vs_oracle(eng, oracle_bin, mode, nfiles, pad):
                     continue
                 out = run_oracle(oracle_bin["bedops"], ["--range", f"{pad[0]}:{pad[1]}", "-u"],
                                  [texts[i]], td)
-                huge |= any(int(x) > 999999999999 for ln in out.decode().splitlines()
+                huge |= any(int(x) >= 2 ** 40 - 1 for ln in out.decode().splitlines()
                             for x in ln.split("\t")[1:3])
             if huge:
                 with pytest.raises(BedgpuError) as ei:

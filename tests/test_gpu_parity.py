@@ -497,9 +497,35 @@ def test_unsorted_input_is_an_error(eng):
 
 def test_malformed_line_is_an_error(eng):
     from bedops_amd import BedgpuError
-    for bad in (b"chr1\t5\n", b"chr1\tx\t10\n", b"chr1\t5\t2\n", b"chr1\t1\t2\n\nchr1\t3\t4\n"):
+    for bad in (b"chr1\t5\n", b"chr1\tx\t10\n", b"chr1\t5\t2\n"):
         with pytest.raises(BedgpuError):
             eng.bedops("-m", [bad])
+
+
+BLANKS = [b"chr1\t1\t2\n\nchr1\t3\t4\n", b"\nchr1\t1\t2\n", b"chr1\t1\t2\nchr1\t3\t4\n\n\n",
+          b" \n\t\n\r\nchr1\t1\t2\n \nchr2\t3\t4\n", b"\n", b"\n\n \n", b"chr1\t1\t2\n\nchr1\t3\t4",
+          b"chr1\t1\t2\n  chr1\t3\t9\n\t\n"]
+
+
+@pytest.mark.parametrize("mode", ["-m", "-i", "-d", "-u", "-e", "-n", "-c", "-s", "-p"])
+def test_blank_lines_are_skipped_like_fscanf(eng, oracle_bin, mode):
+    """whitespace-only lines without --ec: the reference's fscanf (Bed.hpp:244-255) skips them
+    (its --ec rejects them: "Empty line found."); the loader strips them and reloads
+    (k_blank_*), in short files and in files of many 4 KiB tiles"""
+    rng = random.Random(zlib.crc32(repr(("blank", mode)).encode()))
+    big = randbed.text(randbed.rows(rng, 3000)).encode()
+    lines = big.splitlines(keepends=True)
+    for k in range(0, len(lines), 37):
+        lines[k] = rng.choice([b"\n", b" \n", b"\t\t\n", b"\r\n"]) * rng.randint(1, 3) + lines[k]
+    big_blank = b"".join(lines) + b"\n \n"
+    b = b"chr1\t0\t3\nchr1\t3\t40\nchr2\t0\t5\n"
+    cases = [[t] if mode in ("-m", "-c") else [t, b] for t in BLANKS]
+    cases += [[big_blank] if mode in ("-m", "-c") else [big_blank, big]]
+    spec = "1" if mode in ("-e", "-n") else None
+    with tempfile.TemporaryDirectory() as td:
+        for texts in cases:
+            want = run_oracle(oracle_bin["bedops"], [mode] + ([spec] if spec else []), texts, td)
+            assert eng.bedops(mode, texts, spec=spec) == want, (mode, texts[0][:60])
 
 
 def test_chrom_restriction(eng, oracle_bin):

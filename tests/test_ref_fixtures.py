@@ -26,7 +26,7 @@ def _bin(oracle_bin, tool):
                        "sortbed": "sortbed"}[tool]]
 
 
-@pytest.mark.parametrize("suite", ["closest", "bedmap", "decimal", "sortbed", "faster"])
+@pytest.mark.parametrize("suite", ["closest", "bedmap", "decimal", "sortbed", "faster", "f2", "r6"])
 def test_oracle_reproduces_reference(oracle_bin, suite):
     fx = R.load(suite)
     bad = []
