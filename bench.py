@@ -9,9 +9,12 @@ load both files (k_scout, k_tokhash, run/dictionary kernels, k_parse_set) -> per
 components -> intersect (k_mp_partition, k_mp_tile) -> render the sorted BED text back into
 HBM (k_fmt_*). With N GPUs (one process per GPU; `--gpus N` starts them itself, or
 torch.distributed.run does) the chromosomes are assigned to ranks by
-bedops_amd.shard.assign (LPT), every rank runs the step on its chromosomes only, and the
-per-chromosome texts are reassembled on rank 0 in strcmp order by bg_group_gather
-(bedops_amd/csrc/bg_group.hip: grouped ncclSend/ncclRecv over xGMI) inside the step.
+bedops_amd.shard.assign (LPT), every rank runs the step on its chromosomes only and the
+ranks exchange their per-chromosome byte counts, which places each rank's text at its
+offset of the sorted output (the sharded drop-in then writes it in place, cli_shard.h);
+the same steps with the whole text reassembled on rank 0 in strcmp order by
+bg_group_gather (bedops_amd/csrc/bg_group.hip: grouped ncclSend/ncclRecv over xGMI) are
+timed beside them (`multi_gpu`: placement vs with-gather step time, the gather's cost).
 Strong scaling by default: the dataset is the fixed 100M x 100M at every N (`--weak`: N x
 100M rows per file). After the timed steps rank 0 hashes the reassembled output against the
 reference binary's hash at every N.
@@ -496,6 +499,9 @@ def main():
                     help="time the loader stage alone (text in HBM -> keyed columns)")
     ap.add_argument("--profile-all", action="store_true",
                     help="time every kernel during the timed steps (default: only the dominant one)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="(rehearsal of N > 1 on a one-GPU box) every rank on cuda:0, no RCCL "
+                         "between ranks: the placement steps only, no gather, no parity hash")
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
@@ -508,7 +514,7 @@ def main():
             f"{world}-GPU run as {args.gpus} GPUs")
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     from bedops_amd.engine import Group, group_uid
@@ -527,7 +533,8 @@ def main():
         uid = bytes(128)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    grp = Group(device=local, uid=uid, nranks=world, rank=rank)
+    grp = Group(device=local, uid=bytes(128), nranks=1, rank=0) if args.share_device else \
+        Group(device=local, uid=uid, nranks=world, rank=rank)
     eng = grp.engines[0]
 
     L = bedgen_lib()
@@ -551,7 +558,12 @@ def main():
     state = {}
     inputs = [((t.data_ptr(), nb), k) for t, nb, k in zip(bufs, texts, W["kinds"])]
 
-    def step():
+    def step(gather=False):
+        """one pass of the hot path. N > 1: each rank loads, operates and formats its
+        chromosomes (the text stays in its HBM, as at N = 1) and the ranks exchange their
+        per-chromosome byte counts, which places every rank's spans in the sorted output (what
+        the sharded drop-in writes in place with per-device pwrite, cli_shard.h); gather=True
+        also reassembles the whole text on rank 0 over RCCL (bg_group_gather)"""
         s = eng.load(inputs)
         if args.load_only:
             state["out_rows"] = state["out_bytes"] = 0
@@ -561,16 +573,24 @@ def main():
         nbytes = r.format()
         state["out_rows"] = r.rows()
         state["out_bytes"] = nbytes
-        if world > 1:  # the path's one exchange: per-chromosome text -> rank 0 (RCCL)
+        if world > 1:
             names = s.chroms()
-            dptr, _ = r.device_text()
             offs, lens = member_spans(names, r.chrom_spans(len(names)), gnames)
-            out, n = grp.gather(len(gnames), [(dptr, offs, lens)])
-            if rank == 0:
-                if "keep" in state:
-                    state["text"] = read_device(out, n)
-                    del state["keep"]
-                eng.device_free(out)
+            if gather or "keep" in state:  # the path's one data exchange: text -> rank 0 (RCCL)
+                dptr, _ = r.device_text()
+                out, n = grp.gather(len(gnames), [(dptr, offs, lens)])
+                if rank == 0:
+                    if "keep" in state:
+                        state["text"] = read_device(out, n)
+                        del state["keep"]
+                    eng.device_free(out)
+            else:  # placement: every chromosome's byte count from every rank (host, gloo)
+                cnt = torch.tensor(lens, dtype=torch.int64)
+                allc = [torch.empty_like(cnt) for _ in range(world)]
+                dist.all_gather(allc, cnt)
+                tot = torch.stack(allc).sum(0)
+                before = torch.cumsum(tot, 0) - tot  # output offset of each chromosome
+                state["place"] = int(before[[i for i, ln in enumerate(lens) if ln][0]]) if any(lens) else 0
         elif "keep" in state:
             state["text"] = r.text()
             del state["keep"]
@@ -628,10 +648,35 @@ def main():
         dist.all_reduce(rt)
         total_rows = int(rt.item())
     prof = eng.prof_read()
+    # N > 1: the same steps with the whole text reassembled on rank 0 (the RCCL gather the
+    # drop-in's pipe output needs), timed the same way, reported beside the placement steps
+    multi = None
+    if dist and not args.load_only and not args.share_device:
+        barrier()
+        g0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(gather=True)
+        eng.sync()
+        torch.cuda.synchronize(dev)
+        g1 = time.perf_counter()
+        dist.barrier()
+        gt = torch.tensor([g1 - g0], dtype=torch.float64)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gms = float(gt.item()) / args.steps * 1e3
+        ob = torch.tensor([state["out_bytes"]], dtype=torch.int64)
+        dist.all_reduce(ob)
+        multi = {"step_ms_placement": round(elapsed / args.steps * 1e3, 3),
+                 "step_ms_with_gather": round(gms, 3),
+                 "gather_ms": round(gms - elapsed / args.steps * 1e3, 3),
+                 "output_bytes": int(ob.item()),
+                 "value_with_gather": round(total_rows / (gms / 1e3), 1),
+                 "rank_rows": rows, "note": "max over ranks; value = placement steps (text left "
+                 "in each rank's HBM at its output offset), value_with_gather = every step also "
+                 "gathers the text to rank 0 over RCCL"}
 
     # parity after timing: the reassembled output against the reference hash, at every N
     verify = None
-    if not args.no_verify and not args.load_only and args.scale == 1.0 and not args.weak:
+    if not args.no_verify and not args.load_only and args.scale == 1.0 and not args.weak and not args.share_device:
         if rank == 0:
             state["keep"] = True
         step()
@@ -689,7 +734,8 @@ def main():
         grp.close()
         grp = None
         dist.barrier()
-        if not args.no_e2e and args.scale == 1.0 and not args.load_only and not args.weak:
+        if not args.no_e2e and args.scale == 1.0 and not args.load_only and not args.weak \
+                and not args.share_device:
             with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR")) as td:
                 paths, nrows = write_inputs(L, W, td)
                 e2e_sh = e2e_cli(W, paths, nrows, td, runs=args.e2e_runs,
@@ -755,8 +801,9 @@ def main():
                    "rows_per_input": [r * (world if args.weak else 1) for r in
                                       [int(x * args.scale) for x in W["rows"]]],
                    "parallelism": "single GPU" if world == 1 else
-                   f"{world} GPUs (one process each), chromosome shards (LPT) + RCCL gather "
-                   "to rank 0 inside every step",
+                   f"{world} GPUs (one process each), chromosome shards (LPT); each step places "
+                   "every rank's spans in the output by a byte-count exchange, the text stays in "
+                   "its rank's HBM (the RCCL gather to rank 0 is timed beside it: multi_gpu)",
                    "output_rows": state["out_rows"] if world == 1 else None},
         "roofline": roof, "cpu_baseline": cpu,
         "e2e_intervals_per_s": round(e2e["value"], 1) if e2e else None,
@@ -775,6 +822,7 @@ def main():
                              "e2e.no_detach includes the GPU teardown, e2e.pipe writes to a pipe")
         if (cpu and e2e) else None,
         "parity": verify,
+        "multi_gpu": multi,
         "kernels_first_step_ms": {k: round(v[1], 4) for k, v in
                                   sorted(first.items(), key=lambda kv: -kv[1][1])},
         "kernels_warm_step_ms": {k: round(v[1], 4) for k, v in

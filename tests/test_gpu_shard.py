@@ -375,3 +375,18 @@ def test_sharded_cli_writes_each_device_part_at_its_offset(gpu_bin, oracle_bin, 
     r = subprocess.run([gpu_bin["bedops"], "-i", a, b], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
                        timeout=120)
     assert r.returncode == 0 and r.stdout == want, r.stderr
+
+
+def test_bench_multi_rank_placement_step_on_one_gpu():
+    """bench.py --gpus 2 (two rank processes, gloo coordination) with both ranks on cuda:0:
+    the N > 1 placement step (per-chromosome byte counts exchanged, text left in each rank's
+    HBM) runs and reports one line for 2 GPUs; the RCCL gather needs distinct devices"""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
+                        "--scale", "0.002", "--steps", "2", "--warmup", "1", "--no-e2e",
+                        "--no-cpu-baseline"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    line = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert "byte-count exchange" in line["config"]["parallelism"]
