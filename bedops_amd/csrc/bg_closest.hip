@@ -539,7 +539,8 @@ __global__ void __launch_bounds__(BG_NT) k_closest_serial(ClArgs A) {
 }
 
 // -------------------------------------------------------------------------------------
-// k_closest_wave (round 5, the default): ONE WAVE per chunk, the candidates of a ref row
+// k_closest_wave (round 5, opt-in with BEDGPU_CLOSEST_WAVE=1: measured slower than the
+// lane-per-chunk k_closest_chunks, 20.5-23.1 vs 18 ms): ONE WAVE per chunk, the candidates of a ref row
 // taken 64 at a time, one per lane, in the reference's read order (the cache stack from
 // the top, then the file). The branch chain of cl_run is a left-to-right fold over the
 // candidates, but every piece of state it carries is a prefix function the wave computes

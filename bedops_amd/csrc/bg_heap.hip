@@ -134,8 +134,9 @@ int bg_frest_gather(bg_ctx* c, const bg_table* M, int fields, const std::vector<
   off.assign(nr + 1, 0);
   txt.clear();
   if (!nr) return 0;
-  uint64_t* drows = (uint64_t*)bg_alloc(c, 8 * nr);
-  uint64_t* dlen = (uint64_t*)bg_alloc(c, 8 * (nr + 1));
+  BgHold hold(c);
+  uint64_t* drows = hold((uint64_t*)bg_alloc(c, 8 * nr));
+  uint64_t* dlen = hold((uint64_t*)bg_alloc(c, 8 * (nr + 1)));
   if (!drows || !dlen) return BG_E_NOMEM;
   BG_HIP(c, hipMemcpyAsync(drows, rows.data(), 8 * nr, hipMemcpyHostToDevice, c->stream));
   BG_LAUNCH(c, "k_heap_rest_len", k_heap_rest_len, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), drows, nr, M->text,
@@ -144,7 +145,7 @@ int bg_frest_gather(bg_ctx* c, const bg_table* M, int fields, const std::vector<
   BG_HIP(c, hipMemcpyAsync(len.data(), dlen, 8 * nr, hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
   for (uint64_t i = 0; i < nr; ++i) off[i + 1] = off[i] + len[i];
-  char* dtxt = (char*)bg_alloc(c, off[nr] + 1);
+  char* dtxt = hold((char*)bg_alloc(c, off[nr] + 1));
   if (!dtxt) return BG_E_NOMEM;
   BG_HIP(c, hipMemcpyAsync(dlen, off.data(), 8 * nr, hipMemcpyHostToDevice, c->stream));
   BG_LAUNCH(c, "k_heap_rest_copy", k_heap_rest_copy, dim3(bg_blocks(nr, BG_NT)), dim3(BG_NT), drows, nr, M->text,
@@ -152,9 +153,6 @@ int bg_frest_gather(bg_ctx* c, const bg_table* M, int fields, const std::vector<
   txt.resize(off[nr] + 1);
   BG_HIP(c, hipMemcpyAsync(txt.data(), dtxt, off[nr], hipMemcpyDeviceToHost, c->stream));
   BG_HIP(c, hipStreamSynchronize(c->stream));
-  bg_release(c, drows);
-  bg_release(c, dlen);
-  bg_release(c, dtxt);
   return 0;
 }
 

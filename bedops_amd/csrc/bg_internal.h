@@ -255,6 +255,20 @@ void* bg_pin_take(bg_ctx* c, size_t bytes);
 // allocator / error helpers (bg_api.cpp)
 void* bg_alloc(bg_ctx* c, size_t bytes);
 void bg_release(bg_ctx* c, void* p);
+// device blocks released to the context's pool on every exit path of a host function
+struct BgHold {
+  bg_ctx* c;
+  std::vector<void*> p;
+  explicit BgHold(bg_ctx* cc) : c(cc) {}
+  template <class T>
+  T* operator()(T* q) {
+    p.push_back((void*)q);
+    return q;
+  }
+  ~BgHold() {
+    for (void* q : p) bg_release(c, q);
+  }
+};
 int bg_fail(bg_ctx* c, int code, const std::string& msg);
 int bg_hip_fail(bg_ctx* c, hipError_t e, const char* what);
 void bg_mark(bg_ctx* c, const char* name);

@@ -2209,9 +2209,6 @@ __device__ __forceinline__ uint4 ldsu128(const void* p) {
 #ifndef BG_EXP_V
 #define BG_EXP_V 0
 #endif
-#ifndef BG_WSM_AL
-#define BG_WSM_AL 0
-#endif
 // BG_GTXT=1: an interior sub-tile is not staged in LDS; its lines' token and numbers are
 // read from the text through the vector memory path (the unaligned LDS reads were the LDS
 // pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave). Timed within +-3% of staging on
@@ -2406,12 +2403,7 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     const uint32_t len = qn - q - 1;  // bytes before the line's '\n'
     uint32_t WS;
     {
-#if BG_WSM_AL  // (wsm is dword-aligned: two plain reads, no alignbyte funnel)
-      const uint32_t* wp = &S.wsm[q >> 5];
-      const uint2 two = make_uint2(wp[0], wp[1]);
-#else
       const uint2 two = ldsu64(&S.wsm[q >> 5]);
-#endif
       WS = __builtin_amdgcn_alignbit(two.y, two.x, q & 31u);
     }
     WS |= len < 32u ? (~0u << (len & 31u)) : 0u;  // bytes past the line end act as whitespace
@@ -2561,15 +2553,9 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
 // (SQ: 2830 of a wave's 5465 quad-cycles were waits, 2029 of them before the first byte in
 // a loads-only variant). The touched dwords are consumed (pf_sink, null at run time) so the
 // loads are real; they are waited for only at the end, long after they landed.
-#ifndef BG_PSV_SGPR
-#define BG_PSV_SGPR 0
-#endif
-#if BG_PSV_SGPR
-#define BG_PSV_ATTR __attribute__((amdgpu_num_sgpr(BG_PSV_SGPR)))
-#else
-#define BG_PSV_ATTR
-#endif
-__global__ void __launch_bounds__(64) BG_PSV_ATTR k_parse_set_v(
+// (106 SGPRs: 6 waves per SIMD by SGPRs, 7 by LDS. Caps of 96 or 80 SGPRs, 7 waves, measured
+// the same 0.92-0.93 ms, round 6: occupancy is not what bounds it)
+__global__ void __launch_bounds__(64) k_parse_set_v(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st, uint32_t pfd,
@@ -2945,6 +2931,7 @@ struct LoadState {
   // BED5: scores for k_score_big, (row, first byte) pairs
   uint64_t* big = nullptr;
   uint32_t bigcap = 0;
+  bool blank = false;  // a run record of a whitespace-only line (runs_one)
 };
 
 static void release_state(bg_ctx* c, LoadState& S) {
@@ -3056,6 +3043,10 @@ static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSta
   for (uint32_t k : ord) {  // runs: records by position, consecutive duplicates removed
     if (!S.run_pos.empty() && (last_pos == H[k].pos || last_hash == H[k].hash)) continue;
     if (H[k].len > BG_CHR_MAX) return bg_fail(c, BG_E_CHROM, "chromosome name longer than 127 characters");
+    if (H[k].len == 0) {  // a whitespace-only line opens a tile: bg_load strips such lines
+      S.blank = true;
+      return bg_fail(c, BG_E_BLANK, "blank line");
+    }
     last_pos = H[k].pos;
     last_hash = H[k].hash;
     S.run_pos.push_back(H[k].pos);
@@ -3582,6 +3573,7 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   // (the status init above was read by the device before this copy overwrites it: stream order)
   if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(hst, dst, sizeof(bg_dstatus) * n, hipMemcpyDeviceToHost, c->stream));
   if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
+  const bool hst_valid = rc == 0;
   HP("rt3");
   // a BG_BED3_SET input with an error (its exact line is not known) or a staging overflow:
   // the whole load is redone with that input's row columns (BG_BED3)
@@ -3614,8 +3606,9 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     stripped.assign(n, nullptr);
     unblank.assign(inputs, inputs + n);
     for (int i = 0; i < n && !rc; ++i) {
-      if (!st[i].ntiles || (!hst[i].nblank && (hst[i].first_bad == ~0ULL || (hst[i].first_bad & 0xff) != ERR_BLANK)))
-        continue;
+      const bool b = st[i].blank || (hst_valid && (hst[i].nblank || (hst[i].first_bad != ~0ULL &&
+                                                                    (hst[i].first_bad & 0xff) == ERR_BLANK)));
+      if (!st[i].ntiles || !b) continue;
       uint64_t nb2 = 0;
       rc = strip_blank_lines(c, st[i].txt, st[i].nb, &stripped[i], &nb2);
       if (!rc) unblank[i] = bg_input{stripped[i], nb2, 1, inputs[i].kind};

@@ -875,7 +875,8 @@ __global__ void k_mev_pick(const uint64_t* __restrict__ off, uint64_t nr, const 
 // by (end, full_rest(), address) — CoordRestAddressCompare's order for rows of one start
 static int ev_order(bg_ctx* c, const EvArgs& E, const bg_table* M, int fields, uint32_t* ro) {
   const uint64_t nm = E.nm;
-  uint64_t* dl = (uint64_t*)bg_alloc(c, 8 * (nm + 1));
+  BgHold hold(c);
+  uint64_t* dl = hold((uint64_t*)bg_alloc(c, 8 * (nm + 1)));
   if (!dl) return BG_E_NOMEM;
   BG_HIP(c, hipMemsetAsync(dl + nm, 0, 8, c->stream));
   BG_LAUNCH(c, "k_ev_rank", k_ev_rank, dim3(bg_blocks(nm, BG_NT)), dim3(BG_NT), E, ro, dl,
@@ -926,7 +927,6 @@ static int ev_order(bg_ctx* c, const EvArgs& E, const bg_table* M, int fields, u
       BG_HIP(c, hipStreamSynchronize(c->stream));
     }
   }
-  bg_release(c, dl);
   return 0;
 }
 

@@ -1058,6 +1058,7 @@ extern "C" int bg_element_of(bg_ctx* c, bg_set* set, int ref, const int* others,
     if (!bnd) return BG_E_NOMEM;
     BG_LAUNCH(c, "k_element_lo", k_element_lo, dim3(bg_blocks(nblk, BG_NT)), dim3(BG_NT), R->ks, o.e, o.n, nblk,
               bnd);
+    BG_HIP(c, hipGetLastError());
     BG_LAUNCH(c, "k_element_flags", k_element_flags, dim3((unsigned)nblk), dim3(BG_NT),
               R->ks, R->ke, R->n, o.s, o.e, o.n, P, thres, use_pct, invert, flag, set->d_name_len, R->rest_len,
               blen, ovf, (const uint64_t*)bnd);
