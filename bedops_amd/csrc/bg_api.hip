@@ -233,8 +233,6 @@ extern "C" void bg_close(bg_ctx* c) {
   for (size_t k = c->ring_base ? BG_RING_SLOTS : 0; k < c->ring.size(); ++k)
     if (c->ring[k]) hipHostFree(c->ring[k]);
   if (c->ring_base) hipHostFree(c->ring_base);
-  if (c->cjoin) hipEventDestroy(c->cjoin);
-  if (c->cstream) hipStreamDestroy(c->cstream);
   if (c->pstream) hipStreamSynchronize(c->pstream);
   for (auto e : c->copy_ev) hipEventDestroy(e);
   for (auto e : c->order_ev) hipEventDestroy(e);
@@ -483,7 +481,6 @@ static double now_ms() {
 }
 // pins the ring's slots, one thread each (bg_open runs this on a thread of its own, so the
 // pinning overlaps whatever the caller does next)
-static int copy_streams();
 // slot events wait by sleeping (hipEventBlockingSync) instead of polling, leaving the
 // box's CPU quota (16 CPUs) to the copying threads and the output writer; the copies are
 // DMA-bound either way (profiles/r03_e2e/var_i5_summary.txt). BEDGPU_EVENT_BLOCK=0: poll
@@ -544,11 +541,6 @@ static int ring_alloc(bg_ctx* c) {
   c->ring = ring;
   c->ring_ev = ev;
   pool_start(c, ring_threads() - 1);
-  if (copy_streams() == 2 && (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
-                              hipEventCreateWithFlags(&c->cjoin, hipEventDisableTiming) != hipSuccess)) {
-    (void)hipGetLastError();
-    c->cstream = nullptr;  // one copy stream
-  }
   if (c->stats)
     fprintf(stderr, "bedgpu ring   %d x %llu MiB pinned in %.3f ms\n", (int)(BG_RING_SLOTS + BG_WR_SLOTS),
             (unsigned long long)(BG_RING_CH >> 20), now_ms() - t0);
@@ -581,32 +573,8 @@ static int ring_threads() {
   }();
   return t;
 }
-// BEDGPU_COPY_STREAMS: 1 or 2 streams carry the ring's H2D copies (2: chunks alternate
-// between ctx's stream and a second one, so two DMA engines pull from the slots)
-static int copy_streams() {
-  static const int v = [] {
-    const char* s = getenv("BEDGPU_COPY_STREAMS");
-    return (s && atoi(s) == 2) ? 2 : 1;
-  }();
-  return v;
-}
-static int copy_kernel() {
-  static const int v = [] {
-    const char* s = getenv("BEDGPU_COPY_KERNEL");
-    return s ? atoi(s) : 0;
-  }();
-  return v;
-}
-// one chunk of pinned host memory -> device, read by the CUs over the link (16-byte loads;
-// len and both pointers are 16-byte aligned except the chunk's tail)
-__global__ void k_pull(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len) {
-  const uint64_t n16 = len / 16;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  const uint64_t t = n16 * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < len && blockIdx.x == 0) dst[t] = src[t];
-}
+// (Measured and removed in round 6: a second copy stream, and kernels pulling the pinned
+// slots over the link instead of the DMA engine — the same 38-44 GB/s)
 // The ring's copy threads: started once with the ring (bg_open's thread), parked on a
 // condition variable between calls. (Spawning them per call cost 4-7 ms the first time:
 // thread stacks mapped while HIP was mapping its own memory.)
@@ -755,7 +723,7 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = 
   if (!n) return 0;
   int rc = ring_get(c);
   if (rc) return rc;
-  if (c->ring_base && copy_kernel() == 0 && !c->cstream)
+  if (c->ring_base)
     return ring_h2d_grouped(c, dst, src, n, fd, foff, ring_group(), c->stream);
   const uint64_t nch = (n + BG_RING_CH - 1) / BG_RING_CH;
   const int TT_ = ring_threads();
@@ -792,18 +760,9 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = 
         t_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(a1 - a0).count();
         t_copy += std::chrono::duration_cast<std::chrono::nanoseconds>(a2 - a1).count();
       }
-      hipStream_t cs = (c->cstream && (k & 1)) ? c->cstream : c->stream;
-      // BEDGPU_COPY_KERNEL: 1 = every chunk pulled by a kernel reading the pinned slot over
-      // the link, 2 = chunks on the second stream by kernel, the others by the DMA engine
-      const int ck = copy_kernel();
-      const bool by_kernel = ck == 1 || (ck == 2 && cs != c->stream);
       std::lock_guard<std::mutex> g(mu);
-      if (by_kernel) {
-        const unsigned nb = (unsigned)std::min<uint64_t>(1024, (len + 16 * 256 - 1) / (16 * 256));
-        hipLaunchKernelGGL(k_pull, dim3(nb), dim3(256), 0, cs, (uint8_t*)(dst + off), (const uint8_t*)c->ring[sl], len);
-      }
-      if ((!by_kernel && hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, cs) != hipSuccess) ||
-          hipEventRecord(c->ring_ev[sl], cs) != hipSuccess) {
+      if (hipMemcpyAsync(dst + off, c->ring[sl], len, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+          hipEventRecord(c->ring_ev[sl], c->stream) != hipSuccess) {
         bad = 1;
         return;
       }
@@ -815,9 +774,6 @@ static int ring_h2d(bg_ctx* c, char* dst, const char* src, uint64_t n, int fd = 
   };
   pool_run(c, job);  // the pool's threads take t = 1..; this thread t = 0
   const double t_spawn = now_ms();
-  if (c->cstream && nch > 1 &&  // later work on ctx's stream waits for the second stream's copies
-      (hipEventRecord(c->cjoin, c->cstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->cjoin, 0) != hipSuccess))
-    bad = 1;
   if (c->stats) {  // the last copies drained (stats runs only: this waits)
     const double t1 = now_ms();
     hipStreamSynchronize(c->stream);
@@ -913,7 +869,7 @@ extern "C" int bg_file_image_copy(bg_ctx* c, const bg_file_image* m, uint64_t of
   int rc = 0;
   if (len) {
     if ((rc = ring_get(c))) return rc;
-    if (c->ring_base && copy_kernel() == 0) {
+    if (c->ring_base) {
       const int fd = rd_pread() ? image_fd(m) : -1;
       rc = ring_h2d_grouped(c, (char*)dst, m->data + off, len, fd, off, ring_group(), ps);
     } else if (hipMemcpyAsync(dst, m->data + off, (size_t)len, hipMemcpyHostToDevice, ps) != hipSuccess) {

@@ -36,7 +36,7 @@
 #include "bg_internal.h"
 
 #define CQ_DEF 24  // ref rows per chunk (10M x 1B sweep: 16-64 rows, 3-8 warm-up rows, profiles/r04_closest_cq.txt)
-#define CW_DEF 4   // speculative warm-up rows before a chunk (BEDGPU_CLOSEST_CQ/_CW override)
+#define CW_DEF 4   // speculative warm-up rows before a chunk
 #define CBACK 4096 // at most this many candidates before the warm-up row are re-read
 #define CAP0 256   // initial capacity of the cache stack / kept list (x4 on overflow)
 #define FIX_ROUNDS 8
@@ -60,7 +60,6 @@ struct ClArgs {
   uint32_t cap;
   uint32_t cq, cw;  // rows per chunk, warm-up rows
   int64_t lmax;  // longest candidate: a row still cached can start at most lmax earlier
-  int apf;       // cl_run: load the cached rows' keys ahead (BEDGPU_CLOSEST_APF=1; measured neutral, off)
   uint32_t nchunks;
   uint32_t* flag;
   uint32_t* nflag;
@@ -164,13 +163,7 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
   // the next CPF file candidates, loaded ahead: the scan's loads are independent of its
   // decisions, so the file stream is software-pipelined (one candidate at a time each
   // lane waited an L2 round trip per candidate; lanes read disjoint regions)
-#ifndef BG_CPF
-#define BG_CPF 4
-#endif
-  constexpr int CPF = BG_CPF;
-#ifndef BG_CL_FAST
-#define BG_CL_FAST true
-#endif
+  constexpr int CPF = 4;
   int64_t pcs[CPF], pce[CPF];
   const uint64_t nc1 = A.nc ? A.nc - 1 : 0;
 #pragma unroll
@@ -181,7 +174,6 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
   }
   for (uint64_t b = b0; b < b1; ++b) {
     const int64_t bs = A.qs[b], be = A.qe[b];
-    const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
     int64_t ld = D_MINUS, rdist = D_PLUS;
     int64_t left = -1, right = -1, lce = 0;  // lce = ce[left]
     bool lc = false;  // leftCached
@@ -210,19 +202,12 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
       const bool hangR = ovl && !hangL && be <= ce;
       const bool inside = ovl && !hangL && !hangR;
       bool half = false;
-#ifndef BG_CL_IHALF
-#define BG_CL_IHALF 1
-#endif
-      if (BG_CL_IHALF) {  // the reference's double test in exact integers (see cw_window)
+      {  // the reference's centroid test (ClosestFeature.cpp: prop = (cen + 1 - cs) / (ce - cs),
+         // cen = (be - 1 + bs) / 2 as doubles, prop < 0.5) in exact integers (round 5; checked
+         // against the double form, boundary cases included, tests/test_closest_model.py)
         const int64_t bsc = bs & BG_COORD_MASK, bec = be & BG_COORD_MASK;
         const int64_t csc = cs & BG_COORD_MASK, cec = ce & BG_COORD_MASK;
         half = inside && (2 * csc > bsc + bec - 1 || bsc + bec + 1 - 2 * csc < cec - csc);
-      } else if (inside) {  // rare: the double division is skipped by every wave without such a row
-        const double cst = (double)(cs & BG_COORD_MASK);
-        const double prop =
-            cen < cst ? 0.0
-                      : (cen + 1 - cst) / (double)((uint64_t)(ce & BG_COORD_MASK) - (uint64_t)(cs & BG_COORD_MASK));
-        half = prop < 0.5;
       }
       const bool in_a = inside && ld == 0 && half;    // keepL(!lc), lc = 1, keepR, right = c
       const bool in_b = inside && ld == 0 && !half;   // keepL(!lc), lc = 1, keepC
@@ -278,72 +263,20 @@ __device__ bool cl_run(const ClArgs& A, uint64_t b0, uint64_t b1, ClState& S, co
     //      ~70% of the rows read on the benchmark's inputs, at a compare and a select each;
     //   C: the rest of the file through the chain, up to the row that ends the scan.
     bool brk = false;
-    if (A.apf) {  // A, the next APF entries' keys loaded ahead (a pop's gather no longer waits)
-      constexpr int APF = 4;
-      int64_t pc[APF], ps[APF], pe[APF];
-      const uint32_t n0 = S.n;
-#pragma unroll
-      for (int i = 0; i < APF; ++i) {
-        pc[i] = (uint32_t)i < n0 ? (int64_t)cl_peek(S, n0 - 1 - i) : 0;
-        ps[i] = (uint32_t)i < n0 ? A.cs[pc[i]] : 0;
-        pe[i] = (uint32_t)i < n0 ? A.ce[pc[i]] : 0;
-      }
-      uint32_t k = 0;
-      while (k < n0 && !brk) {
-        const int64_t c = pc[0], cs = ps[0], ce = pe[0];
-#pragma unroll
-        for (int i = 0; i + 1 < APF; ++i) {
-          pc[i] = pc[i + 1];
-          ps[i] = ps[i + 1];
-          pe[i] = pe[i + 1];
-        }
-        const uint32_t nx = k + APF;
-        if (nx < n0) {
-          pc[APF - 1] = (int64_t)cl_peek(S, n0 - 1 - nx);
-          ps[APF - 1] = A.cs[pc[APF - 1]];
-          pe[APF - 1] = A.ce[pc[APF - 1]];
-        }
-        ++k;
-        brk = step(c, cs, ce);
-      }
-      cl_drop(S, k);
-    } else {
-      while (S.n && !brk) {  // A
-        const int64_t c = cl_pop(S);
-        brk = step(c, A.cs[c], A.ce[c]);
-      }
+    while (S.n && !brk) {  // A
+      const int64_t c = cl_pop(S);
+      brk = step(c, A.cs[c], A.ce[c]);
     }
-#ifndef BG_CL_CB
-#define BG_CL_CB 8
-#endif
-    if (BG_CL_FAST && BG_CL_CB == 0 && !brk) {  // B, one row at a time
-      const int64_t gb = bs >> BG_KEY_SHIFT;
-      while (S.fp < A.nc && pce[0] <= bs) {
-        const int64_t ce0 = pce[0];
-        const uint64_t c0 = S.fp++;
-        advance();
-        if ((ce0 >> BG_KEY_SHIFT) != gb) continue;  // earlier chromosome: dropped
-        const int64_t d = -((bs - ce0) + 1);
-        if (d >= ld) {
-          nk = 0;
-          ovf = false;
-          left = (int64_t)c0;
-          lce = ce0;
-          ld = d;
-          lc = false;
-        } else {
-          if (left >= 0 && !lc) KEEP(left);
-          lc = true;
-        }
-      }
-    } else if (BG_CL_FAST && !brk) {  // B in closed form, the file's ends CB at a time
+    if (!brk) {  // B in closed form, the file's ends CB at a time
       // Over the run, the chain's effect is: every row whose end is >= the running maximum
       // (and >= the current left's, d >= ld) is a new left (reset), every other row a
       // dropL. So the left afterwards is the LAST row holding the run's largest end M when
       // M beats the current left, the kept list is reset there, and a row after it keeps
       // it (lc); otherwise the first row keeps the current left (unless cached) and lc = 1.
-      // Only the ends are needed: CB of them per load, all in flight together.
-      constexpr int CB = BG_CL_CB > 0 ? BG_CL_CB : 2;
+      // Only the ends are needed: CB of them per load, all in flight together (one row at a
+      // time through the chain, round 3, waited an L2 round trip per row: 28.1 -> 19.0 ms;
+      // CB = 16, 18.7 ms, costs registers)
+      constexpr int CB = 8;
       const int64_t gb = bs >> BG_KEY_SHIFT;
       uint64_t j = S.fp, jend = A.nc;
       int64_t M = LLONG_MIN;
@@ -538,358 +471,8 @@ __global__ void __launch_bounds__(BG_NT) k_closest_serial(ClArgs A) {
   }
 }
 
-// -------------------------------------------------------------------------------------
-// k_closest_wave (round 5, opt-in with BEDGPU_CLOSEST_WAVE=1: measured slower than the
-// lane-per-chunk k_closest_chunks, 20.5-23.1 vs 18 ms): ONE WAVE per chunk, the candidates of a ref row
-// taken 64 at a time, one per lane, in the reference's read order (the cache stack from
-// the top, then the file). The branch chain of cl_run is a left-to-right fold over the
-// candidates, but every piece of state it carries is a prefix function the wave computes
-// at once instead of one dependent candidate per iteration:
-//   brk      the first lane with d > 0 (or +inf): lanes after it are not read;
-//   ld       0 once a hangL / in_c was seen (the first inside-and-not-half lane before any
-//            hangL is the one in_c: ld != 0 only until then), otherwise the running max of
-//            the negative distances: newleft = d >= the exclusive prefix max (ties: >=);
-//   left     the last lane before this one setting it (newleft, hangL, in_c), else the
-//            incoming left — a ballot and a count of leading zeros; likewise right
-//            (firstR, hangR, in_a, in_d) and lc (the last lane changing it, and the value
-//            it set, which depends only on that lane's own case and hasL);
-//   rdist    0 after any hangR / in_a / in_d, else the incoming value (firstR only breaks);
-//   kept     each lane appends keepL, keepR, keepC in order at an exclusive prefix sum;
-//            the last reset (newleft, in_c) discards everything before it.
-// A window takes the cache's entries first and fills its remaining lanes with file rows,
-// so a ref row usually costs two wave steps (the benchmark pops ~26 cached rows and reads
-// ~100 file rows per ref row) instead of ~126 dependent one-candidate steps. The latency is
-// hidden too: the cache's entries keep their keys beside them in LDS (no gather), and the
-// file rows come through two 64-row register blocks, the next block's coalesced load issued
-// as soon as the window leaves the first one (lanes pick their row with a bpermute). The
-// stack and the kept list live in LDS (CW_LDS entries each per wave); a chunk that outgrows
-// them is left to k_closest_fix (cl_run, any depth) by a start state no predecessor ends in,
-// chunk 0 by a rerun of the pass with k_closest_chunks.
-#define CW_LDS 192
-#define CW_WAVES 4
-struct CwKeys {  // one wave's LDS: an entry = candidate index + its keys
-  uint32_t i[CW_LDS];
-  int64_t s[CW_LDS], e[CW_LDS];
-};
-struct WaveCl {
-  int64_t ld, rdist, left, right, lcs, lce, rcs, rce;
-  bool lc;
-  uint32_t nk;
-  bool ovf;
-};
-__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ int64_t bperm64(int64_t v, int src) {
-  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)v);
-  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)((uint64_t)v >> 32));
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-__device__ __forceinline__ int32_t wave_excl_max_i32(int32_t v, int32_t identity) {
-  const int lane = bg_lane();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t u = __shfl_up(v, d, 64);
-    if (lane >= d) v = u > v ? u : v;
-  }
-  const int32_t e = __shfl_up(v, 1, 64);
-  return lane ? (e > identity ? e : identity) : identity;
-}
-__device__ __forceinline__ int64_t wave_excl_max_i64(int64_t v, int64_t identity) {
-  const int lane = bg_lane();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t u = __shfl_up(v, d, 64);
-    if (lane >= d) v = u > v ? u : v;
-  }
-  const int64_t e = __shfl_up(v, 1, 64);
-  return lane ? (e > identity ? e : identity) : identity;
-}
-// the last lane below this one whose bit is set in m, or -1
-__device__ __forceinline__ int last_below(uint64_t m) {
-  const uint64_t b = m & ((1ull << bg_lane()) - 1);
-  return b ? 63 - __clzll(b) : -1;
-}
-__device__ __forceinline__ int last_set(uint64_t m) { return m ? 63 - __clzll(m) : -1; }
-
-// one window of up to 64 candidates (lane i: index c, keys cs/ce, valid = i < cnt) through
-// the chain for ref row (bs, be); returns the number consumed (through the breaking lane) and
-// sets brk
-__device__ __forceinline__ uint32_t cw_window(const ClArgs& A, WaveCl& W, CwKeys& K, int64_t bs, int64_t be,
-                                              double cen, bool valid, uint32_t cnt, int64_t c, int64_t cs,
-                                              int64_t ce, bool& brk) {
-  const int lane = bg_lane();
-  const int64_t d = valid ? cl_dist(cs, ce, bs, be) : D_MINUS;
-  const bool live = valid && d != D_MINUS;  // (an earlier chromosome's row: no effect)
-  const bool plus0 = live && d == D_PLUS;
-  const bool pos0 = live && d > 0 && !plus0;
-  const uint64_t bm = __ballot(plus0 || pos0);
-  const int B = bm ? __ffsll((unsigned long long)bm) - 1 : 64;
-  const bool act = live && lane <= B;  // (the rows after the break are not read)
-  const bool plus = plus0 && act, pos = pos0 && act;
-  const bool neg = act && d < 0;
-  const bool ovl = act && d == 0 && A.overlaps;
-  const bool noov = act && d == 0 && !A.overlaps;
-  const bool hangL = ovl && cs <= bs;
-  const bool hangR = ovl && !hangL && be <= ce;
-  const bool inside = ovl && !hangL && !hangR;
-  // the centroid proportion test in integers: prop < 0.5 of the reference's doubles
-  // (ClosestFeature.cpp:227-239, cen = (be - 1 + bs) / 2, prop = cen < cs ? 0 : (cen + 1 - cs)
-  // / (ce - cs)) holds iff 2cs > bs + be - 1, or N = bs + be + 1 - 2cs < L = ce - cs: the
-  // quotient N / 2L is exact up to one rounding, and N < L keeps it at least 1/(2L) > 2^-41
-  // below 0.5, far beyond that rounding (2^-54) — no double division per window
-  const int64_t bsc = bs & BG_COORD_MASK, bec = be & BG_COORD_MASK;
-  const int64_t csc = cs & BG_COORD_MASK, cec = ce & BG_COORD_MASK;
-  const bool half = inside && (2 * csc > bsc + bec - 1 || bsc + bec + 1 - 2 * csc < cec - csc);
-  (void)cen;
-  // ld == 0 from the first hangL / (inside, !half) lane on (that lane itself still sees ld != 0)
-  const uint64_t zm = __ballot(hangL || (inside && !half));
-  const bool ld0z = W.ld == 0;
-  const int Z = ld0z ? -1 : (zm ? __ffsll((unsigned long long)zm) - 1 : 64);
-  const bool ldz = ld0z || lane > Z;
-  const bool in_c = inside && !half && !ldz;
-  const bool in_b = inside && !half && ldz;
-  const bool in_a = inside && half && ldz;
-  const bool in_d = inside && half && !ldz;
-  // (every wave-wide operation below runs on all lanes: no shuffle inside a select)
-  int64_t pm;
-  if (__ballot(neg && d <= (int64_t)INT_MIN)) {  // gaps past 2^31: the 64-bit scan
-    pm = wave_excl_max_i64(neg ? d : D_MINUS, W.ld);
-  } else {  // every negative distance fits in int32 (INT_MIN: none / the incoming ld below all)
-    const int32_t id = W.ld <= (int64_t)INT_MIN ? INT_MIN : (int32_t)W.ld;
-    pm = (int64_t)wave_excl_max_i32(neg ? (int32_t)d : INT_MIN, id);
-    if (pm == (int64_t)INT_MIN) pm = W.ld <= (int64_t)INT_MIN ? W.ld : pm;
-  }
-  const int64_t ldi = ldz ? 0 : pm;
-  const bool newleft = neg && !ldz && d >= ldi;
-  const bool dropL = neg && !newleft;
-  const uint64_t r0m = __ballot(hangR || in_a || in_d);
-  const int64_t rdi = last_below(r0m) >= 0 ? 0 : W.rdist;
-  const bool firstR = pos && d < rdi;
-  const bool farR = pos && !firstR;
-  const bool setleft = newleft || hangL || in_c;
-  const uint64_t lm = __ballot(setleft);
-  const int li = last_below(lm), lsrc = li < 0 ? 0 : li;
-  const int64_t xc = bperm64(c, lsrc), xs = bperm64(cs, lsrc), xe = bperm64(ce, lsrc);
-  const int64_t lft = li >= 0 ? xc : W.left;
-  const int64_t lcs = li >= 0 ? xs : W.lcs;
-  const int64_t lce = li >= 0 ? xe : W.lce;
-  const bool hasL = lft >= 0;
-  const bool lc_zero = newleft || hangL || in_c;
-  const bool lc_one = dropL || in_a || in_b || (noov && hasL);
-  const bool lc_hasl = plus || firstR || farR || hangR || in_d;
-  const bool lc_ev = lc_zero || lc_one || lc_hasl;
-  const bool lc_after = lc_zero ? false : (lc_one ? true : hasL);
-  const uint64_t cm = __ballot(lc_ev);
-  const uint64_t lam = __ballot(lc_after);
-  const int ci = last_below(cm);
-  const bool lci = ci >= 0 ? ((lam >> ci) & 1) != 0 : W.lc;
-  const bool setright = firstR || hangR || in_a || in_d;
-  const uint64_t rm = __ballot(setright);
-  const int ri = last_below(rm), rsrc = ri < 0 ? 0 : ri;
-  const int64_t yc = bperm64(c, rsrc), ys = bperm64(cs, rsrc), ye = bperm64(ce, rsrc);
-  const int64_t rgt = ri >= 0 ? yc : W.right;
-  const int64_t rcs = ri >= 0 ? ys : W.rcs;
-  const int64_t rce = ri >= 0 ? ye : W.rce;
-  const bool hasR = rgt >= 0;
-  const bool keepL = act && hasL && !lci &&
-                     (plus || firstR || farR || hangR || in_d || noov || dropL || in_a || in_b ||
-                      (hangL && !(lce <= ce)));
-  const bool keepR = act && hasR && (plus || farR || hangR || in_a || in_d);
-  const bool keepC = plus || firstR || farR || in_b || noov;
-  const int R = last_set(__ballot(newleft || in_c));
-  const uint32_t e = lane >= R ? (uint32_t)keepL + (uint32_t)keepR + (uint32_t)keepC : 0u;
-  const uint32_t inc = wave_incl_scan(e, OpSum());
-  const uint32_t base = R >= 0 ? 0u : W.nk;
-  uint32_t p = base + inc - e;
-  if (e) {
-    if (keepL) { if (p < CW_LDS) { K.i[p] = (uint32_t)lft; K.s[p] = lcs; K.e[p] = lce; } ++p; }
-    if (keepR) { if (p < CW_LDS) { K.i[p] = (uint32_t)rgt; K.s[p] = rcs; K.e[p] = rce; } ++p; }
-    if (keepC) { if (p < CW_LDS) { K.i[p] = (uint32_t)c; K.s[p] = cs; K.e[p] = ce; } }
-  }
-  // the state after the window (uniform: lane reads)
-  W.nk = base + (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-  if (R >= 0) W.ovf = false;
-  if (W.nk > CW_LDS) W.ovf = true;
-  if (ld0z || zm) {
-    W.ld = 0;
-  } else {
-    const int64_t dl63 = rl64(neg ? d : D_MINUS, 63), m63 = rl64(pm, 63);
-    W.ld = m63 > dl63 ? m63 : dl63;
-  }
-  if (lm) {
-    const int L = last_set(lm);
-    W.left = rl64(c, L);
-    W.lcs = rl64(cs, L);
-    W.lce = rl64(ce, L);
-  }
-  if (cm) W.lc = ((lam >> last_set(cm)) & 1) != 0;
-  if (rm) {
-    const int L = last_set(rm);
-    W.right = rl64(c, L);
-    W.rcs = rl64(cs, L);
-    W.rce = rl64(ce, L);
-  }
-  if (B < 64 && (__ballot(firstR) >> B) & 1) W.rdist = rl64(d, B);
-  else if (r0m) W.rdist = 0;
-  brk = B < (int)cnt;
-  return brk ? (uint32_t)B + 1 : cnt;
-}
-
-// the file rows [fa, fa + 128) in two register blocks (lane j: rows fa + j, fa + 64 + j)
-struct CwFile {
-  uint64_t fa;
-  int64_t s0, e0, s1, e1;
-};
-__device__ __forceinline__ void cw_load(const ClArgs& A, uint64_t r, int64_t& s, int64_t& e) {
-  s = r < A.nc ? A.cs[r] : LLONG_MAX;
-  e = r < A.nc ? A.ce[r] : LLONG_MAX;
-}
-__device__ __forceinline__ void cw_file_at(const ClArgs& A, CwFile& F, uint64_t fp) {
-  F.fa = fp;
-  cw_load(A, fp + bg_lane(), F.s0, F.e0);
-  cw_load(A, fp + 64 + bg_lane(), F.s1, F.e1);
-}
-// keep fp inside the first block: move on by whole blocks (the next block's load is issued
-// here, a window before it is read)
-__device__ __forceinline__ void cw_file_follow(const ClArgs& A, CwFile& F, uint64_t fp) {
-  if (fp >= F.fa + 128) {
-    cw_file_at(A, F, fp);
-  } else if (fp >= F.fa + 64) {
-    F.s0 = F.s1;
-    F.e0 = F.e1;
-    F.fa += 64;
-    cw_load(A, F.fa + 64 + bg_lane(), F.s1, F.e1);
-  }
-}
-
-// ref rows [b0, b1) from the wave's state (fp, stack K[0, n) bottom first, F at fp); false
-// when the stack or the kept list outgrew LDS
-__device__ bool cw_run(const ClArgs& A, uint64_t b0, uint64_t b1, uint64_t& fp, uint32_t& n, CwKeys& S,
-                       CwKeys& K, CwFile& F, bool emit) {
-  const int lane = bg_lane();
-  for (uint64_t b = b0; b < b1; ++b) {
-    const int64_t bs = A.qs[b], be = A.qe[b];
-    const double cen = ((double)(be & BG_COORD_MASK) - 1.0 + (double)(bs & BG_COORD_MASK)) / 2.0;
-    WaveCl W{D_MINUS, D_PLUS, -1, -1, 0, 0, 0, 0, false, 0u, false};
-    bool brk = false, eof = false;
-    while (!brk) {
-      // lanes [0, ns): the cache from the top; lanes [ns, cnt): the file from fp
-      const uint32_t ns = n < 64 ? n : 64u;
-      const uint64_t rem = fp < A.nc ? A.nc - fp : 0;
-      const uint32_t nf = ns < 64 ? (uint32_t)min<uint64_t>(64 - ns, rem) : 0u;
-      const uint32_t cnt = ns + nf;
-      if (cnt == 0) {
-        eof = true;
-        break;
-      }
-      const bool fromstk = (uint32_t)lane < ns;
-      const bool v = (uint32_t)lane < cnt;
-      const uint32_t q = fromstk ? n - 1 - lane : 0;
-      const int j = (int)(fp - F.fa) + lane - (int)ns;  // the lane's row in the file blocks (< 128)
-      const int src = j & 63;
-      const int64_t fs0 = bperm64(F.s0, src), fe0 = bperm64(F.e0, src);
-      const int64_t fs1 = bperm64(F.s1, src), fe1 = bperm64(F.e1, src);
-      int64_t c, cs, ce;
-      if (fromstk) {
-        c = S.i[q];
-        cs = S.s[q];
-        ce = S.e[q];
-      } else {
-        c = (int64_t)(fp + (uint64_t)(lane - (int)ns));
-        cs = j < 64 ? fs0 : fs1;
-        ce = j < 64 ? fe0 : fe1;
-      }
-      const uint32_t used = cw_window(A, W, K, bs, be, cen, v, cnt, c, cs, ce, brk);
-      if (used <= ns) {
-        n -= used;
-      } else {
-        n -= ns;
-        fp += used - ns;
-        cw_file_follow(A, F, fp);
-      }
-    }
-    if (eof) {
-      if (W.left >= 0 && !W.lc) {
-        if (lane == 0 && W.nk < CW_LDS) { K.i[W.nk] = (uint32_t)W.left; K.s[W.nk] = W.lcs; K.e[W.nk] = W.lce; }
-        ++W.nk;
-      }
-      if (W.right >= 0) {
-        if (lane == 0 && W.nk < CW_LDS) { K.i[W.nk] = (uint32_t)W.right; K.s[W.nk] = W.rcs; K.e[W.nk] = W.rce; }
-        ++W.nk;
-      }
-    }
-    if (W.ovf || W.nk > CW_LDS || n + W.nk > CW_LDS || n + W.nk > A.cap) return false;
-    __builtin_amdgcn_wave_barrier();
-    // BedReader::PushBack(list): the list comes back out in list order
-    for (uint32_t t = lane; t < W.nk; t += 64) {
-      const uint32_t f = W.nk - 1 - t;
-      S.i[n + t] = K.i[f];
-      S.s[n + t] = K.s[f];
-      S.e[n + t] = K.e[f];
-    }
-    __builtin_amdgcn_wave_barrier();
-    n += W.nk;
-    if (emit && lane == 0) {
-      A.left[b] = W.left;
-      A.right[b] = W.right;
-    }
-  }
-  return true;
-}
-
-__device__ __forceinline__ void cw_store(const ClArgs& A, uint64_t slot, uint64_t fp, uint32_t n, const CwKeys& S) {
-  uint32_t* g = cl_slot(A, slot);
-  for (uint32_t t = bg_lane(); t < n; t += 64) g[t] = S.i[t];
-  if (bg_lane() == 0) {
-    A.st_fp[slot] = fp;
-    A.st_n[slot] = n;
-  }
-}
-
-__global__ void __launch_bounds__(64 * CW_WAVES) k_closest_wave(ClArgs A) {
-  __shared__ CwKeys lstk[CW_WAVES], lkept[CW_WAVES];
-  const uint32_t k = blockIdx.x * CW_WAVES + bg_wave();
-  if (k >= A.nchunks) return;
-  CwKeys& S = lstk[bg_wave()];
-  CwKeys& K = lkept[bg_wave()];
-  const uint64_t q0 = (uint64_t)k * A.cq, q1 = min(q0 + A.cq, A.nq);
-  uint64_t fp = 0;
-  uint32_t n = 0;
-  bool ok = true;
-  if (k > 0) {  // the speculative start of k_closest_chunks
-    const uint64_t qw = q0 - A.cw;
-    const uint64_t p = lower_bound_i64(A.cs, A.nc, A.qs[qw]);
-    const uint64_t f = lower_bound_i64(A.cs, A.nc, A.qs[qw] - A.lmax - 1);
-    fp = (p - f > CBACK) ? p - CBACK : f;
-  }
-  CwFile F;
-  cw_file_at(A, F, fp);
-  if (k > 0) ok = cw_run(A, q0 - A.cw, q0, fp, n, S, K, F, false);
-  if (ok) {
-    cw_store(A, 2ull * k, fp, n, S);  // the start state
-    ok = cw_run(A, q0, q1, fp, n, S, K, F, true);
-  }
-  if (!ok) {
-    if (k == 0) {
-      if (bg_lane() == 0) atomicOr(A.overflow, 2u);  // the pass is rerun by k_closest_chunks
-      return;
-    }
-    if (bg_lane() == 0) {  // left to k_closest_fix: a start no predecessor ends in
-      A.st_fp[2ull * k] = ~0ull;
-      A.st_n[2ull * k] = 0;
-      A.st_fp[2ull * k + 1] = ~0ull - 1;
-      A.st_n[2ull * k + 1] = 0;
-    }
-    return;
-  }
-  cw_store(A, 2ull * k + 1, fp, n, S);
-}
-
 // one attempt at capacity A.cap; *ovf set if some state outgrew it
-static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf, bool* wave) {
+static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf) {
   *ovf = false;
   const uint64_t slots = 2ull * A.nchunks;
   A.st_fp = (uint64_t*)bg_alloc(c, 8 * slots);
@@ -902,18 +485,7 @@ static int closest_pass(bg_ctx* c, ClArgs& A, bool* ovf, bool* wave) {
   int rc = 0;
   if (!A.st_fp || !A.st_n || !A.st_c || !A.kl || !A.flag || !A.nflag) rc = BG_E_NOMEM;
   if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 8, c->stream));
-  if (!rc && *wave) {
-    BG_LAUNCH(c, "k_closest_chunks", k_closest_wave, dim3(bg_blocks(A.nchunks, CW_WAVES)), dim3(64 * CW_WAVES), A);
-    rc = bg_hip_ok(c, hipGetLastError());
-    uint32_t h2[2] = {0, 0};
-    if (!rc) rc = bg_hip_ok(c, hipMemcpyAsync(h2, A.nflag, 8, hipMemcpyDeviceToHost, c->stream));
-    if (!rc) rc = bg_hip_ok(c, hipStreamSynchronize(c->stream));
-    if (!rc && (h2[1] & 2u)) {  // chunk 0 outgrew the wave kernel's LDS state: the thread kernel
-      *wave = false;
-      rc = bg_hip_ok(c, hipMemsetAsync(A.nflag, 0, 8, c->stream));
-    }
-  }
-  if (!rc && !*wave) {
+  if (!rc) {
     BG_LAUNCH(c, "k_closest_chunks", k_closest_chunks, dim3(bg_blocks(A.nchunks, BG_NT)),
               dim3(BG_NT), A);
     rc = bg_hip_ok(c, hipGetLastError());
@@ -984,20 +556,16 @@ extern "C" int bg_closest(bg_ctx* c, bg_set* set, int ref, int query, const bg_c
   A.cs = C->ks; A.ce = C->ke; A.nc = C->n;
   A.overlaps = !o->no_overlaps;
   A.lmax = C->maxlen;
-  A.apf = getenv("BEDGPU_CLOSEST_APF") && atoi(getenv("BEDGPU_CLOSEST_APF")) == 1;
   A.left = r->left; A.right = r->right;
-  A.cq = getenv("BEDGPU_CLOSEST_CQ") ? (uint32_t)atoi(getenv("BEDGPU_CLOSEST_CQ")) : CQ_DEF;
-  A.cw = getenv("BEDGPU_CLOSEST_CW") ? (uint32_t)atoi(getenv("BEDGPU_CLOSEST_CW")) : CW_DEF;
-  if (A.cw > A.cq) A.cw = A.cq;
+  A.cq = CQ_DEF;
+  A.cw = CW_DEF;
   A.nchunks = (uint32_t)((Q->n + A.cq - 1) / A.cq);
   int rc = 0;
   // the reader cache of the reference can hold many rows on nested inputs: grow the
   // per-chunk state capacity until it fits (bounded by device memory)
-  // BEDGPU_CLOSEST_WAVE=1: the wave-per-chunk kernel (k_closest_wave) first
-  bool wave = getenv("BEDGPU_CLOSEST_WAVE") && atoi(getenv("BEDGPU_CLOSEST_WAVE")) == 1;
   for (A.cap = CAP0;; A.cap *= 4) {
     bool ovf = false;
-    rc = closest_pass(c, A, &ovf, &wave);
+    rc = closest_pass(c, A, &ovf);
     if (rc || !ovf) break;
     if (3ull * 4ull * A.cap * A.nchunks * 4 > (64ull << 30)) {
       rc = bg_fail(c, BG_E_UNSUPPORTED, "closest-features: reader cache too deep for device memory");

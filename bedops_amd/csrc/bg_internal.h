@@ -73,7 +73,6 @@ struct bg_buf {
 struct bg_ctx {
   int device = 0;
   bool row_wide = false;  // bg_load: rows parsed by k_parse (a redo after BG_ROW_OVERFLOW)
-  bool row_scout = false;  // bg_load: row offsets from the k_scout pass (a redo after BG_ROW_LOOKBACK)
   uint64_t big_need = 0;   // bg_load: capacity of the k_score_big list (a redo after it overflowed)
   uint64_t out_skip = 0;  // bytes write_device_ring still drops (bg_set_output_skip)
   int ncu = 256;  // compute units
@@ -90,7 +89,6 @@ struct bg_ctx {
   std::thread ring_th;  // bg_open starts pinning the ring; its first use joins
   int ring_rc = 0;
   struct bg_pool* pool = nullptr;  // the ring's copy threads (bg_api.hip)
-  hipStream_t cstream = nullptr;  // second H2D copy stream of the ring (BEDGPU_COPY_STREAMS=2)
   hipStream_t pstream = nullptr;  // prefetch copies (bg_file_image_copy), fenced by slot events
   std::vector<hipEvent_t> copy_ev;  // bg_file_image_copy slots
   std::vector<hipEvent_t> order_ev;  // bg_copy_order: ctx's stream position a slot's copies wait for
@@ -101,7 +99,6 @@ struct bg_ctx {
   // only the thread that launches work may call bg_alloc / bg_release
   std::thread::id owner;
   std::string err_async;
-  hipEvent_t cjoin = nullptr;     // its copies -> ctx's stream
   hipStream_t stream = nullptr;
   // side stream: a set input's post-parse passes (bg_load.hip) run there beside the next
   // input's parse; blocks released while it is in use wait in `deferred` until the join

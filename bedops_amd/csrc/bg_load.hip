@@ -175,28 +175,6 @@ __global__ void __launch_bounds__(BG_NT) k_scout(const uint8_t* __restrict__ txt
   }
 }
 
-// newlines of `ns` tiles spread evenly over the input (sample k of ntiles: tile k * ntiles / ns),
-// summed into *cnt: the row loaders without a scout pass size their columns from it
-__global__ void __launch_bounds__(BG_NT) k_sample_nl(const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
-                                                     uint32_t ns, unsigned long long* __restrict__ cnt) {
-  __shared__ uint32_t sh[BG_NT / 64];
-  const uint64_t t = (uint64_t)blockIdx.x * ntiles / ns;
-  const int64_t b = (int64_t)t * TT + (int64_t)threadIdx.x * 32;
-  const uint4 a = load16(txt, b, nb), v = load16(txt, b + 16, nb);
-  const uint32_t w[8] = {a.x, a.y, a.z, a.w, v.x, v.y, v.z, v.w};
-  uint32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) c += __popc(nl_mask4(w[k]));
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-  if (bg_lane() == 0) sh[bg_wave()] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (int q = 0; q < BG_NT / 64; ++q) s += sh[q];
-    atomicAdd(cnt, (unsigned long long)s);
-  }
-}
 
 // line_token's hash of the line at ls from three aligned 16-byte loads, when the line
 // starts with its token (no leading whitespace) of at most 16 bytes ending within 32
@@ -771,7 +749,7 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   return true;
 }
 
-// parse_line_fast from the whitespace mask alone (k_parse_set_n: the tile is classified for
+// parse_line_fast from the whitespace mask alone (k_parse_n: the tile is classified for
 // whitespace only, half the prologue's work): numbers end at whitespace and their bytes are
 // checked to be digits while they are converted (bgp_fields_ws / bgp_digits_rc); a line this
 // refuses takes the byte path, as in parse_line_fast
@@ -888,7 +866,7 @@ struct ParseLdsT {
   uint32_t shs[BG_NT / 64 + 1];
 };
 
-// k_parse_set_n's whitespace-only layout: no digit bitmap, and line starts for up to
+// k_parse_n's whitespace-only layout: no digit bitmap, and line starts for up to
 // LCAP_WS lines (8 KiB of lines averaging >= 8 bytes; a tile of shorter lines reports a
 // parse error and the load is redone with row columns, as any set-path refusal): 2.1 KiB
 // less LDS per workgroup, 13 instead of 11 workgroups per CU
@@ -1071,10 +1049,9 @@ __global__ void __launch_bounds__(BG_NT) k_parse(
 
 // sort order across tile boundaries: the first rows of each tile vs their predecessors
 __global__ void k_check_bounds(const int64_t* __restrict__ KS, const uint64_t* __restrict__ row0,
-                               uint32_t ntiles, uint64_t nrows, bg_dstatus* st, int from_status) {
+                               uint32_t ntiles, uint64_t nrows, bg_dstatus* st) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
-  if (from_status) nrows = min(nrows, (uint64_t)st->nrows);  // (k_parse_n counted them)
   const uint64_t r = row0[t];
   for (uint64_t q = r; q < r + 2 && q < nrows; ++q)
     if (q > 0 && KS[q] < KS[q - 1]) bg_report(st, q, ERR_UNSORTED);
@@ -1085,8 +1062,8 @@ __global__ void k_check_bounds(const int64_t* __restrict__ KS, const uint64_t* _
 //
 // The file's components are what every set operation reads (mergeOverlap /
 // getNextFileMergedCoords, Bedops.cpp:792-814,865-886): row i opens a component iff
-// ks[i] > max(ke[0..i-1]). k_parse_set parses a tile (one line per thread per round of
-// BG_NT lines, in line order), and with block max-scans finds the tile's LOCAL
+// ks[i] > max(ke[0..i-1]). k_parse_set_v parses a 4 KiB sub-tile (one line per lane per round
+// of 64 lines, in line order), and with wave max-scans finds the sub-tile's LOCAL
 // components (running max started at -inf), written to a staging area at the tile's
 // first row index (a tile has at least as many rows as local components). k_set_count /
 // k_set_write then apply the running max M of all earlier tiles: local components that
@@ -1117,9 +1094,6 @@ __device__ __forceinline__ int64_t set_key(const int64_t* X, uint64_t b, int64_t
 // bg_load re-reads the input with its row columns to report the exact line.
 // ONE: the tile lies inside one chromosome run (rl == rh), so the run and its token are
 // workgroup-uniform (scalar loads, no per-lane run search)
-#ifndef BG_EXP_SET
-#define BG_EXP_SET 0
-#endif
 template <bool ONE = false, bool WSO = false, typename BufT = ParseBuf>
 __device__ __forceinline__ bool set_row(const BufT& B, const uint16_t* lst, const TileText& T,
                                         const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
@@ -1128,13 +1102,6 @@ __device__ __forceinline__ bool set_row(const BufT& B, const uint16_t* lst, cons
   const int64_t ls = t0 + lst[k];
   const int64_t le = (k + 1 < L) ? t0 + lst[k + 1] - 1 : last_end;
   if (le < 0) return false;  // the unterminated last line (dropped, Bed.hpp:244-255 + feof)
-#if BG_EXP_SET == 2
-  {  // experiment: no field parsing (round machinery only)
-    ks = ls;
-    ke = ls + 1;
-    return true;
-  }
-#endif
   const uint32_t run = ONE ? rl : ((rl == rh) ? rl : run_of(R, ls, rl, rh));
   const RunInfo& I = R.info[run];
   uint64_t start, end;
@@ -1189,19 +1156,11 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 
 // Keys inside the round loop are shifted by one, K = ks + 1 and E = ke + 1 (valid keys are
 // >= 0), so 0 means "no row" and is the identity of every max below.
-// BG_BED3_SET staging: local components of tile t go to slots [t * SCAP, t * SCAP + SCAP).
-// A tile with more (8 KiB of rows shorter than 16 bytes, almost all disjoint) sets
-// BG_SET_OVERFLOW and bg_load re-reads that input with its row columns (BG_BED3).
-// 256-thread workgroups are admitted 8 per CU only with <= 80 SGPRs (MI355X_MICROARCH.md,
-// residency): capping the set kernel's SGPRs (a few spill to VGPR lanes) takes it from 6 to
-// 8 workgroups per CU, 1.73 -> 1.54 ms per 100M-row file
-#ifndef BG_SGPR_CAP
-#define BG_SGPR_CAP __attribute__((amdgpu_num_sgpr(80)))
-#endif
-#define SCAP 512
+// BG_BED3_SET staging: local components of sub-tile t go to slots [t * SCAP_W, (t + 1) * SCAP_W).
+// A sub-tile with more than SCAP_W (4 KiB of rows shorter than 16 bytes, almost all
+// disjoint) sets BG_SET_OVERFLOW and bg_load re-reads that input with its row columns (BG_BED3).
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
 #define BG_ROW_OVERFLOW 16ULL  // k_parse_n: a tile of more than LCAP_WS lines
-#define BG_ROW_LOOKBACK 128ULL  // k_parse_n without a scout pass: rows past the estimated capacity, or a look-back that timed out
 
 __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
   v = max(v, dpp32<0x111, 0xF, true>(v));
@@ -1217,156 +1176,10 @@ __device__ __forceinline__ uint64_t wave_incl_max_v(uint64_t v) { return wave_in
 __device__ __forceinline__ uint32_t wave_shr1_v(uint32_t v) { return dpp32<0x138, 0xF, true>(v); }
 __device__ __forceinline__ uint64_t wave_shr1_v(uint64_t v) { return wave_shr1_u64(v); }
 
-// LDS of the set kernel's rounds
-struct SetLds {
-  uint64_t xe[2][BG_NT / 64], xk[2][BG_NT / 64];  // wave max E / last K, by round parity
-  uint32_t xc[2][BG_NT / 64];                     // wave component counts
-  uint64_t klast[2];  // K of the tile's last and second-to-last lines (0: not a row)
-};
 
-// The rounds of one tile: BG_NT lines per round, one per thread, in line order. V is the
-// scan type: uint32_t for a tile inside one chromosome run (K = start + 1, E = end + 1 on
-// the coordinates; the key prefix gbase is uniform), uint64_t otherwise (K, E on the
-// keys, gbase = 0). 0 means "no row" and is the identity of every max. A coordinate
-// >= 2^32 - 2 in a one-run tile sets BG_SET_OVERFLOW (the input is re-read with rows).
-template <typename V>
-__device__ __forceinline__ void set_rounds(const ParseBuf& B, const uint16_t* lst, const TileText& T,
-                                           const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
-                                           uint32_t L, int64_t last_end, int64_t gbase,
-                                           uint64_t base, int64_t* __restrict__ LCS,
-                                           int64_t* __restrict__ LCE, SetLds& X, uint64_t& nc,
-                                           V& carry_e, bg_dstatus* st) {
-  constexpr bool NARROW = sizeof(V) == 4;
-  const int lane = bg_lane(), w = bg_wave();
-  const uint64_t lt = (1ULL << lane) - 1;
-  V carry_k = 0;  // K of the previous round's last line
-  const uint32_t rounds = (L + BG_NT - 1) / BG_NT;
-  for (uint32_t j = 0; j < rounds; ++j) {  // block-uniform trip count (barriers inside)
-    const uint32_t k = j * BG_NT + threadIdx.x;
-    int64_t ks = 0, ke = 0;
-    const bool valid = k < L && set_row(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
-    V K = 0, E = 0;
-    if (valid) {
-      if (NARROW) {
-        const uint64_t ce = (uint64_t)(ke & BG_COORD_MASK) + 1;
-        if (ce >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
-        K = (V)((uint64_t)(ks & BG_COORD_MASK) + 1);
-        E = (V)ce;
-      } else {
-        K = (V)ks + 1;
-        E = (V)ke + 1;
-      }
-    }
-    const V ie = wave_incl_max_v(E);
-    const V pk = wave_shr1_v(K);  // previous line's K (lane 0: from LDS below)
-    const int p = j & 1;
-    if (lane == 63) { X.xe[p][w] = ie; X.xk[p][w] = K; }
-    __syncthreads();
-    V pe = carry_e, te = carry_e;
-#pragma unroll
-    for (int q = 0; q < BG_NT / 64; ++q) {
-      const V x = (V)X.xe[p][q];
-      if (q < w) pe = max(pe, x);
-      te = max(te, x);
-    }
-    const V prevK = lane ? pk : (w ? (V)X.xk[p][w - 1] : carry_k);
-    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
-    const V ex_e = max(pe, wave_shr1_v(ie));
-    const bool open = valid && K > ex_e;
-    const uint64_t bal = __ballot(open);
-    if (lane == 0) X.xc[p][w] = (uint32_t)__popcll(bal);
-    // the tile's largest K (sorted rows): its last line's, or the one before when the last
-    // line is the file's dropped unterminated tail (any other non-row is an error)
-    if (k + 2 >= L && k < L) X.klast[L - 1 - k] = K;
-    __syncthreads();
-    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
-#pragma unroll
-    for (int q = 0; q < BG_NT / 64; ++q) {
-      if (q < w) pos += X.xc[p][q];
-      tot += X.xc[p][q];
-    }
-    if (open && pos < SCAP) {
-      LCS[base + pos] = ks;
-      if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);  // previous local component ends here
-    }
-    carry_e = te;
-    carry_k = (V)X.xk[p][BG_NT / 64 - 1];
-    nc += tot;
-  }
-}
-
-// one tile per workgroup, 8 waves per SIMD (<= 64 VGPRs). (Measured on MI355X and dropped:
-// two lines per thread with one scan pass per tile instead of one per 256 lines — 1.53 ms
-// either way once held to 64 VGPRs, 1.59 at 67; a persistent grid streaming the
-// next tile into a second LDS buffer by LDS-DMA while parsing this one — 2.3-2.4 vs 1.83 ms
-// per 100M-row file: this kernel is VALU-issue bound, not load-latency bound.)
-#ifndef BG_SET_WAVES
-#define BG_SET_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
-#endif
-__global__ void __launch_bounds__(BG_NT) BG_SGPR_CAP BG_SET_WAVES k_parse_set(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
-    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
-    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
-  __shared__ ParseLdsT<1> S;
-  __shared__ SetLds X;
-  const uint32_t tile = blockIdx.x;
-  const int64_t t0 = (int64_t)tile * TT;
-  const uint64_t base = (uint64_t)tile * SCAP;
-  if (threadIdx.x == 0) X.klast[0] = X.klast[1] = 0;
-  int64_t last_end;
-  uint32_t L;
-  {
-    TileRegs TR;
-    load_tile(txt, nb, t0, TR);
-    uint64_t r0_unused;
-    L = tile_prologue(txt, nb, nullptr, t0, tile, S, S.b[0], TR, r0_unused, last_end, st);
-  }
-  if (L > LCAP) {  // error reported; leave an empty tile for the fix-up kernels
-    if (threadIdx.x == 0) {
-      TS.tmax[tile] = TS.tlast[tile] = LLONG_MIN;
-      TS.base[tile] = base;
-      TS.nloc[tile] = 0;
-      TS.nrow[tile] = 0;
-      TS.gb[tile] = -1;
-    }
-    return;
-  }
-  const ParseBuf& B = S.b[0];
-  const uint32_t rl = runlo[tile], rh = runhi[tile];
-  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
-  uint64_t nc = 0;  // local components
-  uint64_t cmax = 0;  // max E (+1; 0 = no row): coordinates for one-run tiles, keys otherwise
-  int64_t gbase = 0;
-  if (rl == rh) {  // one chromosome run: 32-bit scans on the coordinates
-    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
-    uint32_t ce = 0;
-    set_rounds<uint32_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
-    cmax = ce;
-  } else {
-    set_rounds<uint64_t>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
-  }
-  __syncthreads();  // klast complete (also when the tile has no lines)
-  if (threadIdx.x == 0) {
-    if (nc > SCAP) {
-      atomicOr(&st->flags, BG_SET_OVERFLOW);
-      nc = 0;
-    }
-    if (nc > 0) LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
-    TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
-    const uint64_t kmax = X.klast[0] ? X.klast[0] : X.klast[1];
-    TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
-    TS.base[tile] = base;
-    TS.nloc[tile] = nc;
-    TS.gb[tile] = -1;
-    TS.nrow[tile] = L - ((L > 0 && last_end < 0) ? 1 : 0);  // (errors fail the load anyway)
-  }
-}
-
-// ---- k_parse_set with NT-thread workgroups --------------------------------------------
-// The same tile (8 KiB), staging and outputs as k_parse_set, run by NT = 128 threads: each
-// thread stages and classifies 64 tile bytes, and the ~340 lines of a tile (24-byte rows)
-// go in rounds of 128 (3 rounds, 89% of the lanes busy) instead of 256 (2 rounds, 67%).
-// The kernel is VALU-issue bound, so lanes idle in a partial round are time lost.
+// ---- the row parse's tile front end: NT-thread workgroups over 8 KiB tiles -----------------
+// each thread stages and classifies TT / NT tile bytes (k_parse_n: NT = 128, the ~340 lines of
+// a tile in rounds of 128)
 template <int NT>
 struct TileRegsN {
   uint4 v[TT / NT / 16];  // this thread's TT / NT tile bytes
@@ -1556,65 +1369,11 @@ __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const ui
   return true;
 }
 
-// Row parse (keys, rest spans, scores) with k_parse_set_n's tile front end: NT threads per
-// 8 KiB tile, the tile classified for whitespace only (tile_prologue_n<NT, true>), fields and
-// digits checked in parse_line_fast_ws / parse_score_fast_ws. Lines the fast path refuses
-// take parse_line_slow in the same loop. Same outputs and error reports as k_parse.
-// The row offsets without a scout pass: a decoupled look-back over the tiles' newline counts.
-// Tile t publishes its count c_t (newlines in [t0, t0 + TT)) as an aggregate as soon as its
-// prologue has found its lines, then walks back over the tiles before it, 64 at a time (one
-// per lane, agent-scope atomic loads: the words are the only data exchanged, flag and value in
-// one 64-bit word), summing aggregates until it reaches a tile that has published its
-// inclusive prefix; then it publishes its own inclusive prefix. Tiles only wait on lower
-// tiles, which were dispatched before them; a wait that outlasts LB_SPIN polls (never seen)
-// publishes anyway and flags BG_ROW_LOOKBACK, and bg_load redoes the load with k_scout.
-#define LB_AGG (1ull << 62)
-#define LB_INC (2ull << 62)
-#define LB_VAL ((1ull << 62) - 1)
-#define LB_SPIN (1u << 22)
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// wave 0 of tile t: the exclusive prefix of the counts (all lanes return it)
-__device__ uint64_t lb_prefix(uint64_t* __restrict__ words, uint32_t t, uint64_t c, bg_dstatus* st) {
-  const int lane = bg_lane();
-  if (t == 0) {
-    if (lane == 0) lb_store(&words[0], LB_INC | c);
-    return 0;
-  }
-  if (lane == 0) lb_store(&words[t], LB_AGG | c);
-  uint64_t excl = 0;
-  int64_t u = (int64_t)t - 1;
-  uint32_t spins = 0;
-  for (;;) {
-    const int64_t idx = u - lane;
-    const uint64_t w = idx >= 0 ? lb_load(&words[idx]) : LB_INC;  // before tile 0: 0
-    const uint32_t f = (uint32_t)(w >> 62);
-    const uint64_t pm = __ballot(f == 2), zm = __ballot(f == 0);
-    const int fp = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
-    const uint64_t below = fp == 64 ? ~0ull : ((2ull << fp) - 1);  // lanes 0..fp
-    if (zm & below) {  // a tile before the nearest inclusive one has not published yet
-      if (++spins > LB_SPIN) {
-        if (lane == 0) atomicOr(&st->flags, BG_ROW_LOOKBACK);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    uint64_t v = (uint64_t)lane <= (uint64_t)fp ? (w & LB_VAL) : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    excl += v;
-    if (fp < 64) break;
-    u -= 64;
-  }
-  if (lane == 0) lb_store(&words[t], LB_INC | (excl + c));
-  return excl;
-}
-
+// Row parse (keys, rest spans, scores): NT threads per 8 KiB tile, the tile classified for
+// whitespace only (tile_prologue_n<NT, true>), fields and digits checked in
+// parse_line_fast_ws / parse_score_fast_ws. Lines the fast path refuses take parse_line_slow
+// in the same loop. Same outputs and error reports as k_parse. The tiles' first rows come
+// from the scout pass (row0).
 #ifndef BG_PN_WAVES
 #define BG_PN_WAVES 6  // k_parse_n's minimum waves per SIMD (6: <= 80 VGPRs)
 #endif
@@ -1624,11 +1383,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_W
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
     int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
     uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
-    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap, uint64_t* __restrict__ lbw) {
+    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap) {
   __shared__ ParseLdsWs S;
   constexpr uint32_t NR = LCAP_WS / NT;  // rounds of NT lines at most
   __shared__ int64_t kfirst[NR][NT / 64], klast[NR][NT / 64];  // keys at the waves' edges
-  __shared__ uint64_t s_row0;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   int64_t last_end = -1;
   uint32_t L;
@@ -1639,23 +1397,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_W
   }
   const auto& B = S.b[0];
   const bool has0 = (t0 == 0) || B.buf[HB - 1] == '\n';
-  uint64_t rt;  // newlines before the tile
-  if (lbw) {  // no scout pass: the look-back (nrows = the columns' capacity)
-    if (threadIdx.x < 64) {
-      // L = newlines in [t0, t0 + TT - 1) + has0: the tile's own count adds its last byte
-      const uint64_t c = (uint64_t)L - (has0 ? 1u : 0u) + (B.buf[HB + TT - 1] == '\n' ? 1u : 0u);
-      const uint64_t ex = lb_prefix(lbw, blockIdx.x, c, st);
-      if (threadIdx.x == 0) {
-        s_row0 = ex;
-        row0[blockIdx.x] = ex;
-        if (blockIdx.x + 1 == gridDim.x) st->nrows = ex + c;
-      }
-    }
-    __syncthreads();
-    rt = s_row0;
-  } else {
-    rt = row0[blockIdx.x];
-  }
+  const uint64_t rt = row0[blockIdx.x];  // newlines before the tile
   const uint64_t r0 = rt + (has0 ? 0 : 1);  // row of the first owned line
   if (L > LCAP_WS) return;  // (BG_ROW_OVERFLOW: the load is redone with k_parse)
   const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];
@@ -1670,7 +1412,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_W
     const int64_t ls = k < L ? t0 + S.lst[k] : 0;
     const uint64_t r = r0 + k;
     const int64_t le = k >= L ? -1 : (k + 1 < L) ? t0 + S.lst[k + 1] - 1 : last_end;
-    if (lbw && k < L && le >= 0 && r >= nrows) atomicOr(&st->flags, BG_ROW_LOOKBACK);  // past the capacity
     if (k < L && r < nrows && le >= 0) {  // le < 0 / r >= nrows: the unterminated last line (dropped)
       Fast F;
       const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
@@ -1732,169 +1473,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_W
   }
 }
 
-template <int NT>
-struct SetLdsN {
-  uint64_t xe[2][NT / 64], xk[2][NT / 64];
-  uint32_t xc[2][NT / 64];
-  uint64_t klast[2];
-};
-
-// set_rounds with NT lines per round
-template <int NT, typename V, bool WSO, typename BufT>
-__device__ __forceinline__ void set_rounds_n(const BufT& B, const uint16_t* lst, const TileText& T,
-                                             const RunTable& R, uint32_t rl, uint32_t rh, int64_t t0,
-                                             uint32_t L, int64_t last_end, int64_t gbase,
-                                             uint64_t base, int64_t* __restrict__ LCS,
-                                             int64_t* __restrict__ LCE, SetLdsN<NT>& X, uint64_t& nc,
-                                             V& carry_e, bg_dstatus* st) {
-  constexpr bool NARROW = sizeof(V) == 4;
-  const int lane = bg_lane(), w = bg_wave();
-  const uint64_t lt = (1ULL << lane) - 1;
-  V carry_k = 0;
-  const uint32_t rounds = (L + NT - 1) / NT;
-  for (uint32_t j = 0; j < rounds; ++j) {
-    const uint32_t k = j * NT + threadIdx.x;
-    int64_t ks = 0, ke = 0;
-    const bool valid = k < L && set_row<NARROW, WSO>(B, lst, T, R, rl, rh, t0, k, L, last_end, ks, ke, st);
-    V K = 0, E = 0;
-    if (valid) {
-      if (NARROW) {
-        const uint64_t ce = (uint64_t)(ke & BG_COORD_MASK) + 1;
-        if (ce >= 0xFFFFFFFFull) atomicOr(&st->flags, BG_SET_OVERFLOW);
-        K = (V)((uint64_t)(ks & BG_COORD_MASK) + 1);
-        E = (V)ce;
-      } else {
-        K = (V)ks + 1;
-        E = (V)ke + 1;
-      }
-    }
-    const V ie = wave_incl_max_v(E);
-    const V pk = wave_shr1_v(K);
-    const int p = j & 1;
-    if (lane == 63) { X.xe[p][w] = ie; X.xk[p][w] = K; }
-    __syncthreads();
-    V pe = carry_e, te = carry_e;
-#pragma unroll
-    for (int q = 0; q < NT / 64; ++q) {
-      const V x = (V)X.xe[p][q];
-      if (q < w) pe = max(pe, x);
-      te = max(te, x);
-    }
-    const V prevK = lane ? pk : (w ? (V)X.xk[p][w - 1] : carry_k);
-    if (valid && prevK && K < prevK) bg_report(st, 0, ERR_UNSORTED);
-    const V ex_e = max(pe, wave_shr1_v(ie));
-    const bool open = valid && K > ex_e;
-    const uint64_t bal = __ballot(open);
-    if (lane == 0) X.xc[p][w] = (uint32_t)__popcll(bal);
-    if (k + 2 >= L && k < L) X.klast[L - 1 - k] = K;
-    __syncthreads();
-    uint64_t pos = nc + __popcll(bal & lt), tot = 0;
-#pragma unroll
-    for (int q = 0; q < NT / 64; ++q) {
-      if (q < w) pos += X.xc[p][q];
-      tot += X.xc[p][q];
-    }
-    if (open && pos < SCAP) {
-      if (NARROW) {  // 32-bit coordinates (SetTiles::gb)
-        reinterpret_cast<uint32_t*>(LCS + base)[pos] = (uint32_t)(K - 1);
-        if (pos > 0) reinterpret_cast<uint32_t*>(LCE + base)[pos - 1] = (uint32_t)(ex_e - 1);
-      } else {
-        LCS[base + pos] = ks;
-        if (pos > 0) LCE[base + pos - 1] = gbase | (int64_t)(ex_e - 1);
-      }
-    }
-    carry_e = te;
-    carry_k = (V)X.xk[p][NT / 64 - 1];
-    nc += tot;
-  }
-}
-
-// (LDS holds 11 of these workgroups per CU: 5-6 waves per SIMD)
-template <int NT, bool WSO = true>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_set_n(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t ntiles,
-    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
-    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
-  using LdsT = std::conditional_t<WSO, ParseLdsWs, ParseLdsT<1>>;
-  constexpr uint32_t CAP = WSO ? LCAP_WS : LCAP;
-  __shared__ LdsT S;
-  __shared__ SetLdsN<NT> X;
-  const uint32_t tile = blockIdx.x;
-  const int64_t t0 = (int64_t)tile * TT;
-  const uint64_t base = (uint64_t)tile * SCAP;
-  if (threadIdx.x == 0) X.klast[0] = X.klast[1] = 0;
-  int64_t last_end = -1;
-  uint32_t L;
-  {
-    TileRegsN<NT> TR;
-    load_tile_n<NT>(txt, nb, t0, TR);
-    L = tile_prologue_n<NT, WSO>(txt, nb, t0, S, TR, last_end, st);
-  }
-  if (L > CAP) {
-    if (threadIdx.x == 0) {
-      TS.tmax[tile] = TS.tlast[tile] = LLONG_MIN;
-      TS.base[tile] = base;
-      TS.nloc[tile] = 0;
-      TS.nrow[tile] = 0;
-      TS.gb[tile] = -1;
-    }
-    return;
-  }
-  const auto& B = S.b[0];
-  const uint32_t rl = runlo[tile], rh = runhi[tile];
-  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
-  uint64_t nc = 0;
-  uint64_t cmax = 0;
-  int64_t gbase = 0;
-#if BG_EXP_SET == 1
-  if (true) {  // experiment: prologue only
-  } else
-#endif
-  if (rl == rh) {
-    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
-    uint32_t ce = 0;
-    set_rounds_n<NT, uint32_t, WSO>(B, S.lst, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, X, nc, ce, st);
-    cmax = ce;
-  } else {
-    set_rounds_n<NT, uint64_t, WSO>(B, S.lst, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, X, nc, cmax, st);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (nc > SCAP) {
-      atomicOr(&st->flags, BG_SET_OVERFLOW);
-      nc = 0;
-    }
-    if (nc > 0) {
-      if (rl == rh) reinterpret_cast<uint32_t*>(LCE + base)[nc - 1] = (uint32_t)(cmax - 1);
-      else LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
-    }
-    TS.gb[tile] = (rl == rh) ? gbase : -1;
-    TS.tmax[tile] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
-    const uint64_t kmax = X.klast[0] ? X.klast[0] : X.klast[1];
-    TS.tlast[tile] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
-    TS.base[tile] = base;
-    TS.nloc[tile] = nc;
-    TS.nrow[tile] = L - ((L > 0 && last_end < 0) ? 1 : 0);
-  }
-}
-
-// ---- k_parse_set_w: one wavefront per 4 KiB sub-tile -----------------------------------
-// The same parse and staging as k_parse_set_n, with the tile cut to TW = 4 KiB and owned by
-// ONE wave (64 lanes x 64 bytes): every exchange of the 2-wave kernel (line-start counts, the
-// per-round max of ends, the last key, the opening counts) becomes a DPP step or a readlane
-// into a scalar register, and the workgroup barriers compile to nothing (the workgroup is
-// one wave). The halo mask words and the halo's first '\n' come from the lanes that loaded
-// the halo (a lane pair per mask word, a ballot for the '\n'), without LDS atomics. Sub-tile
-// u stages its local components in slots [u * SCAP_W, u * SCAP_W + SCAP_W) and has its own
-// SetTiles entry: k_set_count / k_set_write treat sub-tiles as tiles.
+// ---- BG_BED3_SET: one wavefront per 4 KiB sub-tile -------------------------------------
+// A tile of TW = 4 KiB owned by ONE wave (64 lanes x 64 bytes): every exchange between lines
+// (line-start counts, the per-round max of ends, the last key, the opening counts) is a DPP
+// step or a readlane into a scalar register, and the workgroup barriers compile to nothing
+// (the workgroup is one wave). Sub-tile u stages its local components in slots
+// [u * SCAP_W, u * SCAP_W + SCAP_W) and has its own SetTiles entry: k_set_count /
+// k_set_write treat sub-tiles as tiles. (Rounds 2-4 kernels with 8 KiB tiles of 128/256
+// threads and the round-4 wave kernel measured 1.51 / 1.23 / 1.19 ms per file against 0.92
+// for k_parse_set_v and were removed in round 6.)
 #define TW 4096
 #define SCAP_W 256
 #define LCAP_W 512  // lines per sub-tile (4 KiB of lines averaging >= 8 bytes; more: refused)
-struct ParseLdsW {
-  __attribute__((aligned(16))) uint8_t buf[HB + TW + HA + 32];
-  uint32_t wsm[TW / 32 + (HA + 32) / 32 + 1];
-  uint16_t lst[LCAP_W + 1];
-};
 
 __device__ __forceinline__ uint32_t wave_readlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -1903,70 +1493,9 @@ __device__ __forceinline__ uint64_t wave_readlane(uint64_t v, int l) {
   return ((uint64_t)wave_readlane((uint32_t)(v >> 32), l) << 32) | wave_readlane((uint32_t)v, l);
 }
 
-// 4 dwords -> '\n' flags of their 16 bytes (bit j = byte j)
-__device__ __forceinline__ uint32_t nl16(const uint4 a) {
-  return bgp_group4(nl_mask4(a.x)) | (bgp_group4(nl_mask4(a.y)) << 4) | (bgp_group4(nl_mask4(a.z)) << 8) |
-         (bgp_group4(nl_mask4(a.w)) << 12);
-}
-__device__ __forceinline__ uint32_t ws16(const uint4 a) { return bgp_ws8(a.x, a.y) | (bgp_ws8(a.z, a.w) << 8); }
-
-// prologue of sub-tile t0: LDS staging, whitespace masks, line starts (S.lst). Returns the
-// number of owned lines (> LCAP_W: error reported); last_end as tile_prologue_n.
-__device__ __forceinline__ uint32_t prologue_w(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
-                                               ParseLdsW& S, int64_t& last_end, bg_dstatus* st) {
-  constexpr int HL = (HA + 32) / 16;  // lanes holding 16 halo bytes after the sub-tile
-  static_assert(HL % 2 == 0 && HL < 63, "halo lanes");
-  const int lane = threadIdx.x;
-  uint4 v[4];
-  const int64_t b = t0 + 64 * lane;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = load16(txt, b + 16 * i, nb);
-  uint4 vh = make_uint4(0, 0, 0, 0);
-  if (lane < HL) vh = load16(txt, t0 + TW + 16 * lane, nb);
-  else if (lane == 63) vh = load16(txt, t0 - HB, nb);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
-  if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
-  else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
-  S.wsm[2 * lane] = ws16(v[0]) | (ws16(v[1]) << 16);
-  S.wsm[2 * lane + 1] = ws16(v[2]) | (ws16(v[3]) << 16);
-  {  // halo: lane pairs make its mask words; its first '\n' by ballot
-    const uint32_t h = ws16(vh);
-    const uint32_t hn = __shfl_down(h, 1, 64);
-    if (lane < HL && !(lane & 1)) S.wsm[TW / 32 + lane / 2] = h | (hn << 16);
-    if (lane == HL) S.wsm[TW / 32 + HL / 2] = 0;  // read past the halo by mask_window
-  }
-  const uint32_t hm = lane < HL ? nl16(vh) : 0u;
-  const uint64_t hb = __ballot(hm != 0);
-  int64_t hnl = -1;
-  if (hb) {
-    const int f = __builtin_ctzll(hb);
-    hnl = TW + 16 * f + __builtin_ctz(wave_readlane(hm, f));
-  }
-  const bool has0 = t0 == 0 || (wave_readlane(vh.w, 63) >> 24) == '\n';
-  const bool endnl = (wave_readlane(v[3].w, 63) >> 24) == '\n';
-  uint32_t n0 = nl16(v[0]) | (nl16(v[1]) << 16), n1 = nl16(v[2]) | (nl16(v[3]) << 16);
-  if (lane == 63) n1 &= 0x7FFFFFFFu;  // a '\n' in the last byte starts the next sub-tile's line
-  const uint32_t cnt = (uint32_t)(__popc(n0) + __popc(n1));
-  const uint32_t inc = wave_incl_scan(cnt, OpSum());
-  const uint32_t L = wave_readlane(inc, 63) + (has0 ? 1u : 0u);
-  if (L > LCAP_W) {
-    if (lane == 0) bg_report(st, 0, ERR_PARSE);
-    return L;
-  }
-  uint32_t o = inc - cnt + (has0 ? 1u : 0u);
-  if (lane == 0 && has0) S.lst[0] = 0;
-  for (uint32_t m = n0; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + bgp_ctz(m) + 1);
-  for (uint32_t m = n1; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + 32 + bgp_ctz(m) + 1);
-  __syncthreads();  // (one wave: orders the LDS writes above before the reads below)
-  TileText T{txt, S.buf, t0 - HB, t0 + TW + HA, nb};
-  last_end = L == 0 ? -1 : endnl ? t0 + TW - 1 : (hnl >= 0 ? t0 + hnl : find_nl(T, t0 + TW + HA + 32));
-  return L;
-}
-
 // the rounds of one sub-tile: 64 lines per round, one per lane, in line order (V as
-// set_rounds_n). kl: K (+1 form) of the sub-tile's largest row key.
-template <typename V, typename LdsT = ParseLdsW>
+// k_parse_n's rows). kl: K (+1 form) of the sub-tile's largest row key.
+template <typename V, typename LdsT>
 __device__ __forceinline__ void set_rounds_w(const LdsT& S, const TileText& T, const RunTable& R,
                                              uint32_t rl, uint32_t rh, int64_t t0, uint32_t L,
                                              int64_t last_end, int64_t gbase, uint64_t base,
@@ -2022,62 +1551,12 @@ __device__ __forceinline__ void set_rounds_w(const LdsT& S, const TileText& T, c
   }
 }
 
-__global__ void __launch_bounds__(64) k_parse_set_w(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
-    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
-    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
-  __shared__ ParseLdsW S;
-  const uint32_t u = blockIdx.x;
-  const int64_t t0 = (int64_t)u * TW;
-  const uint64_t base = (uint64_t)u * SCAP_W;
-  int64_t last_end = -1;
-  const uint32_t L = prologue_w(txt, nb, t0, S, last_end, st);
-  if (L > LCAP_W) {
-    if (threadIdx.x == 0) {
-      TS.tmax[u] = TS.tlast[u] = LLONG_MIN;
-      TS.base[u] = base;
-      TS.nloc[u] = 0;
-      TS.nrow[u] = 0;
-      TS.gb[u] = -1;
-    }
-    return;
-  }
-  const uint32_t rl = runlo[u], rh = runhi[u];
-  const TileText T{txt, S.buf, t0 - HB, t0 + TW + HA, nb};
-  uint64_t nc = 0, cmax = 0, kmax = 0;
-  int64_t gbase = 0;
-  if (rl == rh) {
-    gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
-    uint32_t ce = 0, kl = 0;
-    set_rounds_w<uint32_t>(S, T, R, rl, rh, t0, L, last_end, gbase, base, LCS, LCE, nc, ce, kl, st);
-    cmax = ce;
-    kmax = kl;
-  } else {
-    set_rounds_w<uint64_t>(S, T, R, rl, rh, t0, L, last_end, 0, base, LCS, LCE, nc, cmax, kmax, st);
-  }
-  if (threadIdx.x == 0) {
-    if (nc > SCAP_W) {
-      atomicOr(&st->flags, BG_SET_OVERFLOW);
-      nc = 0;
-    }
-    if (nc > 0) {
-      if (rl == rh) reinterpret_cast<uint32_t*>(LCE + base)[nc - 1] = (uint32_t)(cmax - 1);
-      else LCE[base + nc - 1] = gbase | (int64_t)(cmax - 1);
-    }
-    TS.gb[u] = (rl == rh) ? gbase : -1;
-    TS.tmax[u] = cmax ? (gbase | (int64_t)(cmax - 1)) : LLONG_MIN;
-    TS.tlast[u] = kmax ? (gbase | (int64_t)(kmax - 1)) : LLONG_MIN;
-    TS.base[u] = base;
-    TS.nloc[u] = nc;
-    TS.nrow[u] = L - ((L > 0 && last_end < 0) ? 1 : 0);
-  }
-}
 
-// ---- k_parse_set_v (round 5, the default): k_parse_set_w with a lean common path -------
-// Same sub-tiles, LDS layout, staging and SetTiles entries as k_parse_set_w. The SQ counters
-// of k_parse_set_w (profiles/r04_sq_k_parse_set_w.txt: 1294 VALU + 504 SALU per 4 KiB wave)
-// and its ISA (64-bit address arithmetic, compares and masks, guarded byte-loop loads, funnel
-// shifts for every unaligned LDS word) set what this kernel removes. On the common path — a
+// ---- k_parse_set_v (round 5): the set parse with a lean common path ---------------------
+// The SQ counters of round 4's wave kernel (profiles/r04_sq_k_parse_set_w.txt: 1294 VALU + 504
+// SALU per 4 KiB wave) and its ISA (64-bit address arithmetic, compares and masks, guarded
+// byte-loop loads, funnel shifts for every unaligned LDS word) set what this kernel removes.
+// On the common path — a
 // sub-tile inside one chromosome run (rl == rh) whose lines are "<token> <start> <end>[...]"
 // within their first 32 bytes, the token the run's, both numbers of at most 9 digits —
 // every step is 32-bit:
@@ -2088,8 +1567,8 @@ __global__ void __launch_bounds__(64) k_parse_set_w(
 //    32-bit LDS read of lst[k], lst[k+1];
 //  - fields from the transitions of the line's whitespace window (starts = non-ws after ws,
 //    ends = ws after non-ws: three ffbl + clear-lowest each) instead of a chain of masks;
-//  - unaligned LDS reads (ds_read_b64/b96; gfx950 DS takes any byte address) for the window,
-//    the token and each number's last 12 bytes: no alignbyte funnels;
+//  - the window, the token and each number's last 12 bytes read from LDS as aligned dwords
+//    funnelled by alignbyte (ldsu*: unaligned ds_reads stalled the LDS pipe);
 //  - a number of <= 9 digits converts with two byte dot products per dword and 24-bit
 //    multiply-adds (< 10^9 < 2^32);
 //  - the token compared under the run's length mask (uniform).
@@ -2145,12 +1624,8 @@ __device__ __forceinline__ void classify16(const uint4 a, uint32_t& ws, uint32_t
 struct LdsU3 {
   uint32_t x, y, z;
 };
-// BG_LDS_ALIGNED=1 (default): aligned dwords + alignbyte (one extra ds_read per window, no
-// LDS_UNALIGNED_STALL: k_parse_set_v 0.99 -> 0.92 ms, round 5); 0: unaligned LDS reads
-#ifndef BG_LDS_ALIGNED
-#define BG_LDS_ALIGNED 1
-#endif
-#if BG_LDS_ALIGNED
+// unaligned LDS reads as aligned dwords + alignbyte (one extra ds_read per window, no
+// LDS_UNALIGNED_STALL: k_parse_set_v 0.99 -> 0.92 ms, round 5, against unaligned ds_reads)
 template <int N>
 __device__ __forceinline__ void lds_words(const void* p, uint32_t* o) {
   // (the aligned address by pointer arithmetic on p, not an integer round trip: the compiler
@@ -2183,41 +1658,9 @@ __device__ __forceinline__ uint4 ldsu128(const void* p) {
   lds_words<4>(p, o);
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
-#else
-__device__ __forceinline__ uint32_t ldsu32(const void* p) {
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-}
-__device__ __forceinline__ uint2 ldsu64(const void* p) {
-  uint2 v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-}
-__device__ __forceinline__ LdsU3 ldsu96(const void* p) {
-  LdsU3 v;
-  __builtin_memcpy(&v, p, 12);
-  return v;
-}
-__device__ __forceinline__ uint4 ldsu128(const void* p) {
-  uint4 v;
-  __builtin_memcpy(&v, p, 16);
-  return v;
-}
-#endif
 
-#ifndef BG_EXP_V
-#define BG_EXP_V 0
-#endif
-// BG_GTXT=1: an interior sub-tile is not staged in LDS; its lines' token and numbers are
-// read from the text through the vector memory path (the unaligned LDS reads were the LDS
-// pipe's largest load: SQ_LDS_UNALIGNED_STALL 707 per wave). Timed within +-3% of staging on
-// two boxes (one each way), but those per-line reads go to L2 a second time and miss it often:
-// PMC 4.21 GB per launch against 2.95 GB staged (2.81 algorithmic, gpurun_out/r05_abp) — so
-// 0 (stage every sub-tile) is the default
-#ifndef BG_GTXT
-#define BG_GTXT 0
-#endif
+// (every sub-tile is staged in LDS: reading interior sub-tiles' line bytes from the text
+// itself was timed within +-3% but read 4.21 GB per launch against 2.95 GB staged, round 5)
 // the value of a number of L (1..9) digits whose last digit is the high byte of D.z (the 12
 // bytes D end at the number's end); ok cleared when one of its bytes is not a digit
 __device__ __forceinline__ uint32_t digits9(const LdsU3 D, uint32_t L, bool& ok) {
@@ -2272,9 +1715,8 @@ __device__ __forceinline__ int64_t find_nl_wave(const uint8_t* __restrict__ txt,
 __device__ __forceinline__ bool sub_inb(int64_t t0, uint64_t nb) {
   return t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb;
 }
-// what set_row / set_rounds_w read a sub-tile's lines through: its bytes from offset t0 - HB
-// (the LDS copy, or the text itself for an interior sub-tile under BG_GTXT), whitespace
-// masks and line starts (LDS)
+// what set_row / set_rounds_w read a sub-tile's lines through: its bytes from offset t0 - HB,
+// whitespace masks and line starts (LDS)
 struct SubView {
   const uint8_t* buf;
   const uint32_t* wsm;
@@ -2320,12 +1762,10 @@ __device__ __forceinline__ uint32_t prologue_v(const uint8_t* __restrict__ txt, 
   const int lane = threadIdx.x;
   const uint4* const v = R.v;
   const uint4 vh = R.vh;
-  if (!sub_inb(t0, nb) || !BG_GTXT) {  // interior sub-tiles are read from the text itself
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
-    if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
-    else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
-  }
+  for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&S.buf[HB + 64 * lane + 16 * i]) = v[i];
+  if (lane < HL) *reinterpret_cast<uint4*>(&S.buf[HB + TW + 16 * lane]) = vh;
+  else if (lane == 63) *reinterpret_cast<uint4*>(&S.buf[0]) = vh;
   uint32_t w0, w1, n0, n1, hw, hm;
   classify32(v[0], v[1], w0, n0);
   classify32(v[2], v[3], w1, n1);
@@ -2371,7 +1811,7 @@ __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return (uint32_t)__builti
 
 // the rounds of a one-run sub-tile (32-bit coordinates under the key prefix, set_rounds_w's
 // staging); TOK16: the run's token is 9..16 bytes
-template <bool TOK16, bool GTXT>
+template <bool TOK16>
 __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, const ParseLdsV& S,
                                              const SubView& SV, const TileText& T, const RunTable& R,
                                              uint32_t rl, int64_t t0, uint32_t L, int64_t last_end,
@@ -2422,9 +1862,7 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     // the third field ends inside the window (so do the others); short numbers; the token's
     // length; the line has an end (lst[L] != 0xFFFF)
     bool ok = act && e1 <= 31u && qn != 0xFFFFu && (a1 - a0) == tlen && (s1 - s0) <= 9u && (e1 - e0) <= 9u;
-    // the line's bytes: LDS, or (GTXT) the text itself through the vector memory path,
-    // which the LDS pipe's unaligned reads do not share
-    const uint8_t* lb = GTXT ? txt + (t0 + q) : &SV.buf[HB + q];
+    const uint8_t* lb = &SV.buf[HB + q];  // the line's bytes (LDS)
     {
       uint32_t dif;
       if (TOK16) {
@@ -2436,12 +1874,8 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
       }
       ok = ok && dif == 0;
     }
-#if BG_EXP_V == 2  // experiment: no number conversion
-    uint32_t start = (uint32_t)((t0 + q) >> 1), end = start + 1 + (e1 & 1);
-#else
     uint32_t start = digits9(ldsu96(lb + (s1 & 31u) - 12), (s1 - s0) & 15u, ok);
     uint32_t end = digits9(ldsu96(lb + (e1 & 31u) - 12), (e1 - e0) & 15u, ok);
-#endif
     bool valid = ok;
     if (act && !ok) {  // the full grammar (and its errors), this lane only
       int64_t ks = 0, ke = 0;
@@ -2500,29 +1934,18 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
     return;
   }
   const uint32_t rl = runlo[u], rh = runhi[u];
-  const bool direct = BG_GTXT && sub_inb(t0, nb);  // line bytes from the text (not staged)
-  const SubView SV{direct ? txt + (t0 - HB) : S.buf, S.wsm, S.lst};
+  const SubView SV{S.buf, S.wsm, S.lst};
   const TileText T{txt, SV.buf, t0 - HB, t0 + TW + HA_V, nb};
   uint64_t nc = 0, cmax = 0, kmax = 0;
   int64_t gbase = 0;
-#if BG_EXP_V == 1
-  if (true) {  // experiment: prologue only
-  } else
-#endif
   if (rl == rh) {
     gbase = (int64_t)R.info[rl].gid << BG_KEY_SHIFT;
     uint32_t ce = 0, kl = 0;
     const bool tok16 = R.info[rl].tlen > 8;
-#if BG_GTXT
-    if (direct) {  // every read inside the text
-      if (tok16) set_rounds_v<true, true>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
-      else set_rounds_v<false, true>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
-    } else
-#endif
     if (tok16)
-      set_rounds_v<true, false>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      set_rounds_v<true>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
     else
-      set_rounds_v<false, false>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
+      set_rounds_v<false>(txt, S, SV, T, R, rl, t0, L, last_end, base, LCS, LCE, nc, ce, kl, st);
     cmax = ce;
     kmax = kl;
   } else {
@@ -2547,56 +1970,20 @@ __device__ __forceinline__ void parse_sub_v(const uint8_t* __restrict__ txt, uin
 }
 
 // one wave per sub-tile
-// pfd > 0: after its own loads, the wave touches every 128-byte line of sub-tile u + pfd
-// (one dword per line, 35 lanes), which a wave starting about one wave lifetime later
-// will parse: its loads then hit L2 / the Infinity Cache instead of waiting out HBM latency
-// (SQ: 2830 of a wave's 5465 quad-cycles were waits, 2029 of them before the first byte in
-// a loads-only variant). The touched dwords are consumed (pf_sink, null at run time) so the
-// loads are real; they are waited for only at the end, long after they landed.
 // (106 SGPRs: 6 waves per SIMD by SGPRs, 7 by LDS. Caps of 96 or 80 SGPRs, 7 waves, measured
-// the same 0.92-0.93 ms, round 6: occupancy is not what bounds it)
+// the same 0.92-0.93 ms, round 6: occupancy is not what bounds it; an L2 prefetch of a later
+// sub-tile, round 5, measured neutral)
 __global__ void __launch_bounds__(64) k_parse_set_v(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
-    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
-    int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st, uint32_t pfd,
-    uint32_t* __restrict__ pf_sink, uint32_t u0) {
-  __shared__ ParseLdsV S;
-  SubRegs V;
-  const uint32_t u = u0 + blockIdx.x;  // (u0: the launch covers sub-tiles [u0, u0 + gridDim.x))
-  load_sub(txt, nb, (int64_t)u * TW, V);
-  uint32_t pf = 0;
-  if (pfd) {
-    const uint64_t a = ((uint64_t)u + pfd) * TW + 128u * threadIdx.x;
-    if (threadIdx.x < (TW + HA_V + 32 + 127) / 128 && a + 4 <= nb)
-      pf = *reinterpret_cast<const uint32_t*>(txt + a);
-  }
-  parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
-  if (pf_sink) pf_sink[threadIdx.x] = pf;
-}
-
-// persistent waves (grid-strided over the sub-tiles): the next sub-tile's bytes are loaded
-// into registers while this one is parsed, so every wave keeps a load in flight through its
-// compute instead of waiting for its own bytes first
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_set_p(
     const uint8_t* __restrict__ txt, uint64_t nb, uint32_t nsub,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ LCS, int64_t* __restrict__ LCE, SetTiles TS, bg_dstatus* st) {
   __shared__ ParseLdsV S;
-  uint32_t u = blockIdx.x;
-  if (u >= nsub) return;
   SubRegs V;
+  const uint32_t u = blockIdx.x;
   load_sub(txt, nb, (int64_t)u * TW, V);
-  for (;;) {
-    const uint32_t un = u + gridDim.x;
-    SubRegs N;
-    if (un < nsub) load_sub(txt, nb, (int64_t)un * TW, N);
-    __syncthreads();  // (one wave: the previous sub-tile's LDS reads before this one's writes)
-    parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
-    if (un >= nsub) break;
-    V = N;
-    u = un;
-  }
+  parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
 }
+
 
 // per tile: sort check against the nearest earlier tile with rows (every tile is sorted
 // inside, or has reported it), how many local components the running max M of the
@@ -2922,12 +2309,6 @@ struct LoadState {
   uint32_t* absorbed = nullptr;
   int64_t* tgb = nullptr;
   uint32_t set_nt = 0;  // staging units of a BG_BED3_SET parse whose merge passes are pending
-  uint32_t set_split = 0;  // > 0: only sub-tiles [0, set_split) are parsed yet (set_split_finish)
-  int64_t* mex2 = nullptr;
-  uint64_t* dtot = nullptr;
-  // row loads without a scout pass (k_parse_n's look-back): tile words, sampled tiles
-  uint64_t* lbw = nullptr;
-  uint32_t nsamp = 0;
   // BED5: scores for k_score_big, (row, first byte) pairs
   uint64_t* big = nullptr;
   uint32_t bigcap = 0;
@@ -2940,7 +2321,7 @@ static void release_state(bg_ctx* c, LoadState& S) {
                   (void*)S.d_info, (void*)S.d_row, (void*)S.rlo, (void*)S.rhi, (void*)S.lcs,
                   (void*)S.lce, (void*)S.tmax, (void*)S.tlast, (void*)S.mex, (void*)S.sex,
                   (void*)S.tbase, (void*)S.nloc, (void*)S.tcnt, (void*)S.absorbed,
-                  (void*)S.tgb, (void*)S.big, (void*)S.lbw, (void*)S.mex2, (void*)S.dtot})
+                  (void*)S.tgb, (void*)S.big})
     bg_release(c, p);
   S = LoadState();
 }
@@ -2971,33 +2352,14 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   S.rc = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
   const bool set = in.kind == BG_BED3_SET;  // no row numbers: no scout pass
   // row loads: the scout pass counts every tile's lines first (k_scout, a streaming read at
-  // ~6 TB/s). BEDGPU_ROW_LOOKBACK=1 drops it: k_parse_n finds the row offsets by a decoupled
-  // look-back and the columns are sized from a sample of the tiles' newline counts — exact
-  // (the GPU suite passes with it) but measured slower: bedmap 50M x 500M k_parse 11.4 ->
-  // 20.7 ms against the 3.3 ms k_scout it saves (waves spinning on their predecessors' words
-  // hold the slots the parse needs), so it stays off
-  static const bool scout_env = [] {
-    const char* e = getenv("BEDGPU_ROW_LOOKBACK");
-    const char* p = getenv("BEDGPU_ROW_PARSE");  // (0: k_parse, which takes the scout's offsets)
-    return !(e && atoi(e) == 1) || (p && atoi(p) == 0);
-  }();
-  const bool scout = !set && (scout_env || c->row_scout || c->row_wide);
-  if (!set) {
-    S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
-    if (!S.row0) return BG_E_NOMEM;
-  }
+  // ~6 TB/s) for the rows' numbers (a decoupled look-back inside k_parse_n instead measured
+  // 2x slower in round 5: bedmap 50M x 500M k_parse 11.4 -> 20.7 ms)
+  const bool scout = !set;
   if (scout) {
+    S.row0 = (uint64_t*)bg_alloc(c, 8ull * nt);
     S.cnt = (uint64_t*)bg_alloc(c, 8ull * nt);
     S.fnl = (uint32_t*)bg_alloc(c, 4ull * nt);
-    if (!S.cnt || !S.fnl) return BG_E_NOMEM;
-  } else if (!set) {
-    S.lbw = (uint64_t*)bg_alloc(c, 8ull * nt);
-    if (!S.lbw) return BG_E_NOMEM;
-    BG_HIP(c, hipMemsetAsync(S.lbw, 0, 8ull * nt, c->stream));
-    S.nsamp = std::min<uint32_t>(nt, 4096);
-    BG_LAUNCH(c, "k_sample_nl", k_sample_nl, dim3(S.nsamp), dim3(BG_NT), txt, S.nb, nt, S.nsamp,
-              (unsigned long long*)&ctr[0]);
-    BG_HIP(c, hipGetLastError());
+    if (!S.row0 || !S.cnt || !S.fnl) return BG_E_NOMEM;
   }
   S.fls = (int64_t*)bg_alloc(c, 8ull * nt);
   S.fhash = (uint64_t*)bg_alloc(c, 8ull * nt);
@@ -3066,7 +2428,7 @@ static int runs_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadSta
 }
 
 // run table of one input on the device (+ the runs each tile can hold)
-// (tb: the tile size the per-tile run ranges are for; TW for k_parse_set_w's sub-tiles)
+// (tb: the tile size the per-tile run ranges are for; TW for k_parse_set_v's sub-tiles)
 static int upload_runs(bg_ctx* c, bg_table* T, LoadState& S,
                        const std::map<std::string, int32_t>& gid, RunTable& R, int tb = TT) {
   const uint32_t ntr = tb == TT ? S.ntiles : (uint32_t)bg_blocks(S.nb, (uint64_t)tb);
@@ -3126,11 +2488,7 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   int rc = upload_runs(c, T, S, gid, R);
   if (rc) return rc;
   // k_parse_n (whitespace-only tile front end, 128 threads) unless a load found a tile of very
-  // short lines (BG_ROW_OVERFLOW) and is being redone, or BEDGPU_ROW_PARSE=0
-  static const bool row_n = [] {
-    const char* e = getenv("BEDGPU_ROW_PARSE");
-    return !(e && atoi(e) == 0);
-  }();
+  // short lines (BG_ROW_OVERFLOW) and is being redone with k_parse
   // scores past the loader's fast paths (parse_score: isint -1) go to k_score_big (finish_one);
   // the list holds 2^20 (BEDGPU_BIGCAP) unless a load that overflowed it is being redone with
   // the count it found (c->big_need)
@@ -3143,17 +2501,17 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     S.big = (uint64_t*)bg_alloc(c, 16ull * (S.bigcap ? S.bigcap : 1));
     if (!S.big) return BG_E_NOMEM;
   }
-  if (S.lbw || (row_n && !c->row_wide))
+  if (!c->row_wide)
     BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
               S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
-              S.big, S.bigcap, S.lbw);
+              S.big, S.bigcap);
   else
     BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
               S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
               S.big, S.bigcap);
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
-            S.row0, S.ntiles, T->n, st, S.lbw ? 1 : 0);
+            S.row0, S.ntiles, T->n, st);
   BG_HIP(c, hipGetLastError());
   S.nrows_run = nr;  // copied back after every input's parse is queued
   return 0;
@@ -3163,32 +2521,17 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
 // (T->cs/T->ce, capacity = rows; the count lands in st->pad[0] and comes back with the
 // statuses)
 static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
-                         const std::map<std::string, int32_t>& gid, bg_dstatus* st, bool split = false) {
+                         const std::map<std::string, int32_t>& gid, bg_dstatus* st) {
   T->is_set = true;
   const uint32_t nr = (uint32_t)S.run_pos.size();
-  static const int set_nt = [] {  // BEDGPU_SET_NT=64|128|256: the wave / 8 KiB-tile kernels (A/B)
-    const char* e = getenv("BEDGPU_SET_NT");
-    return e ? atoi(e) : 64;
-  }();
-  static const bool set_ws = [] {  // BEDGPU_SET_WS=0: whitespace + digit classes (A/B)
-    const char* e = getenv("BEDGPU_SET_WS");
-    return !(e && atoi(e) == 0);
-  }();
-  static const int set_lean = [] {  // BEDGPU_SET_V=0: k_parse_set_w (round 4); 2: persistent
-    const char* e = getenv("BEDGPU_SET_V");
-    return e ? atoi(e) : 1;
-  }();
-  const bool wave = set_nt == 64;
-  // staging units: 4 KiB sub-tiles (k_parse_set_w) or 8 KiB tiles
-  const uint32_t nt = wave ? (uint32_t)bg_blocks(S.nb, (uint64_t)TW) : S.ntiles;
-  const uint64_t scap = wave ? SCAP_W : SCAP;
-  const uint64_t cap = nt ? (uint64_t)nt * scap : 1;  // components <= staged slots
+  const uint32_t nt = (uint32_t)bg_blocks(S.nb, (uint64_t)TW);  // staging units: 4 KiB sub-tiles
+  const uint64_t cap = nt ? (uint64_t)nt * SCAP_W : 1;  // components <= staged slots
   T->cs = (int64_t*)bg_alloc(c, 8 * cap);
   T->ce = (int64_t*)bg_alloc(c, 8 * cap);
   if (!T->cs || !T->ce) return BG_E_NOMEM;
   if (nt == 0 || nr == 0) return 0;
   RunTable R;
-  int rc = upload_runs(c, T, S, gid, R, wave ? TW : TT);
+  int rc = upload_runs(c, T, S, gid, R, TW);
   if (rc) return rc;
   S.lcs = (int64_t*)bg_alloc(c, 8 * cap);
   S.lce = (int64_t*)bg_alloc(c, 8 * cap);
@@ -3205,119 +2548,35 @@ static int parse_set_one(bg_ctx* c, bg_table* T, LoadState& S,
       !S.tcnt || !S.absorbed || !S.cnt || !S.tgb)
     return BG_E_NOMEM;
   SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  if (wave && set_lean == 2) {  // persistent: BEDGPU_SET_GRID waves per CU (256 CUs)
-    static const uint32_t per_cu = [] {
-      const char* e = getenv("BEDGPU_SET_GRID");
-      return e ? (uint32_t)atoi(e) : 24u;
-    }();
-    const uint32_t g = std::min<uint32_t>(nt, 256u * std::max<uint32_t>(per_cu, 1u));
-    BG_LAUNCH(c, "k_parse_set", k_parse_set_p, dim3(g), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st);
-  } else if (wave && set_lean) {
-    static const uint32_t pfd = [] {  // BEDGPU_SET_PF: prefetch distance in sub-tiles (0: off)
-      const char* e = getenv("BEDGPU_SET_PF");
-      return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    // split (the last input): the first half now, set_split_finish queues the second half
-    // after the first half's merge passes have gone to the side stream
-    // (BEDGPU_SET_SPLIT_MIN: the smallest input split, in 4 KiB sub-tiles; read per call so a
-    // test can force small splits)
-    const char* sm = getenv("BEDGPU_SET_SPLIT_MIN");
-    const uint32_t smin = sm ? (uint32_t)std::max(2, atoi(sm)) : 8192u;
-    const uint32_t h = (split && nt >= smin) ? nt / 2 : 0;
-    if (h) {
-      S.mex2 = (int64_t*)bg_alloc(c, 8ull * nt);
-      S.dtot = (uint64_t*)bg_alloc(c, 16);
-      if (!S.mex2 || !S.dtot) return BG_E_NOMEM;
-      S.set_split = h;
-    }
-    BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(h ? h : nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st, pfd, (uint32_t*)nullptr, 0u);
-  }
-  else if (wave)
-    BG_LAUNCH(c, "k_parse_set", k_parse_set_w, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st);
-  else if (set_nt == 128 && set_ws)
-    BG_LAUNCH(c, "k_parse_set", (k_parse_set_n<128, true>), dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi,
-              R, S.lcs, S.lce, TS, st);
-  else if (set_nt == 128)
-    BG_LAUNCH(c, "k_parse_set", (k_parse_set_n<128, false>), dim3(nt), dim3(128), S.txt, S.nb, nt, S.rlo, S.rhi,
-              R, S.lcs, S.lce, TS, st);
-  else
-    BG_LAUNCH(c, "k_parse_set", k_parse_set, dim3(nt), dim3(BG_NT), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-              S.lcs, S.lce, TS, st);
+  BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
+            S.lcs, S.lce, TS, st);
   BG_HIP(c, hipGetLastError());
   S.set_nt = nt;  // parse_set_merge follows
   return 0;
 }
 
-// the passes after k_parse_set: the running max of earlier tiles, absorbed local components
-// and the final component columns. bg_load runs them on the side stream while the next
-// input parses (k_parse_set leaves HBM bandwidth to spare, k_set_write is bandwidth-bound)
-// the merge passes over tiles [u0, u1) of nt: the running max over [0, u1) into mex, the
-// range's counts scanned in place (its total to *scan_total), the components written after
-// *carry earlier ones; total_out: the file's component count (from the file's last tile)
-static int set_merge_range(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st, uint32_t u0, uint32_t u1,
-                           uint32_t nt, int64_t* mex, uint64_t* scan_total, const uint64_t* carry,
-                           unsigned long long* total_out, hipEvent_t wait_before_write = nullptr) {
-  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  int rc;
-  if ((rc = bg_scan_max_i64(c, S.tmax, mex, u1, LLONG_MIN))) return rc;
-  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(u1 - u0, BG_NT)), dim3(BG_NT), S.lcs, TS,
-            (const int64_t*)mex, u1, S.tcnt, st, u0);
-  BG_HIP(c, hipGetLastError());
-  if ((rc = bg_scan_sum_u64(c, S.tcnt + u0, S.tcnt + u0, u1 - u0, scan_total))) return rc;
-  if (wait_before_write) BG_HIP(c, hipStreamWaitEvent(c->stream, wait_before_write, 0));
-  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(u1 - u0, SW_TILES)), dim3(BG_NT), S.lcs,
-            S.lce, TS, (const int64_t*)mex, (const uint64_t*)S.tcnt, u1, T->cs, T->ce, u0, nt, carry, total_out);
-  BG_HIP(c, hipGetLastError());
-  return 0;
-}
+// the passes after k_parse_set: the running max of earlier tiles (mex), the absorbed local
+// components and each tile's count (k_set_count), their offsets (scanned in place; the total
+// to st->pad[0]) and the final component columns (k_set_write). bg_load runs them on the
+// side stream while the next input parses (k_parse_set leaves HBM bandwidth to spare,
+// k_set_write is bandwidth-bound)
 static int parse_set_merge(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
   const uint32_t nt = S.set_nt;
   S.set_nt = 0;
-  return set_merge_range(c, T, S, st, 0, nt, nt, S.mex, (uint64_t*)&st->pad[0], nullptr, nullptr);
-}
-
-// parse_set_merge of input i on the side stream, forked from the ctx stream's current
-// position (BEDGPU_SET_SIDE=0: in line)
-static int side_open(bg_ctx* c) {
-  if (!c->sstream) {
-    if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sfork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sjoin, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      return bg_fail(c, BG_E_HIP, "side stream creation failed");
-    }
-  }
+  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
+  int rc;
+  if ((rc = bg_scan_max_i64(c, S.tmax, S.mex, nt, LLONG_MIN))) return rc;
+  BG_LAUNCH(c, "k_set_count", k_set_count, dim3(bg_blocks(nt, BG_NT)), dim3(BG_NT), S.lcs, TS,
+            (const int64_t*)S.mex, nt, S.tcnt, st, 0u);
+  BG_HIP(c, hipGetLastError());
+  if ((rc = bg_scan_sum_u64(c, S.tcnt, S.tcnt, nt, (uint64_t*)&st->pad[0]))) return rc;
+  BG_LAUNCH(c, "k_set_write", k_set_write, dim3(bg_blocks(nt, SW_TILES)), dim3(BG_NT), S.lcs,
+            S.lce, TS, (const int64_t*)S.mex, (const uint64_t*)S.tcnt, nt, T->cs, T->ce, 0u, nt,
+            (const uint64_t*)nullptr, (unsigned long long*)nullptr);
+  BG_HIP(c, hipGetLastError());
   return 0;
 }
-// the last input, split: its first half's merge passes on the side stream while the second
-// half parses on the ctx stream, then the second half's passes (their write waits for the
-// first half's component count)
-static int set_split_finish(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st,
-                            const std::map<std::string, int32_t>& gid) {
-  const uint32_t nt = S.set_nt, h = S.set_split;
-  S.set_nt = 0;
-  S.set_split = 0;
-  int rc = side_open(c);
-  if (rc) return rc;
-  BG_HIP(c, hipEventRecord(c->sfork, c->stream));
-  BG_HIP(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
-  c->defer_release = true;
-  hipStream_t main = c->stream;
-  c->stream = c->sstream;
-  rc = set_merge_range(c, T, S, st, 0, h, nt, S.mex, S.dtot, nullptr, nullptr);
-  c->stream = main;
-  if (rc) return rc;
-  BG_HIP(c, hipEventRecord(c->sjoin, c->sstream));
-  SetTiles TS{S.tmax, S.tlast, S.tbase, S.nloc, S.absorbed, S.cnt, S.tgb};
-  const RunTable R{S.d_info, S.d_row, (uint32_t)S.run_pos.size()};
-  BG_LAUNCH(c, "k_parse_set", k_parse_set_v, dim3(nt - h), dim3(64), S.txt, S.nb, nt, S.rlo, S.rhi, R,
-            S.lcs, S.lce, TS, st, 0u, (uint32_t*)nullptr, h);
-  BG_HIP(c, hipGetLastError());
-  return set_merge_range(c, T, S, st, h, nt, nt, S.mex2, S.dtot + 1, S.dtot, &st->pad[0], c->sjoin);
-}
+
 static int set_merge_side(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st) {
   if (!c->sstream) {
     if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
@@ -3363,7 +2622,6 @@ static int finish_one(bg_ctx* c, int idx, const bg_input& in, bg_table* T, LoadS
     T->run_name.clear();
     return 0;
   }
-  if (S.lbw) T->n = std::min<uint64_t>(T->n, h.nrows);  // (the look-back's count; capacity checked)
   int rc = report_status(c, idx, h);
   if (rc) return rc;
   if (h.nbig) {  // scores past the fast paths: exact big-number conversion (bg_strtod.h)
@@ -3455,33 +2713,9 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   HP("alloc");
   if (!rc) rc = bg_hip_ok(c, hipMemsetAsync(ctr, 0, 64ull * n, c->stream));
   HP("memset");
-  // BEDGPU_SCOUT_SIDE=1: odd inputs' first-phase kernels (token hashes, boundaries, run
-  // records: latency-bound launches of a few thousand waves) on the side stream beside the
-  // even ones' — exact, but measured 0.07 ms slower per intersect step (the fork/join events
-  // cost more than the overlap), so off
-  static const bool scout_side = [] {
-    const char* e = getenv("BEDGPU_SCOUT_SIDE");
-    return e && atoi(e) == 1;
-  }();
   for (int i = 0; i < n && !rc; ++i) {
     s->t.push_back(new bg_table());
-    if (scout_side && (i & 1) && !(rc = side_open(c))) {
-      rc = bg_hip_ok(c, hipEventRecord(c->sfork, c->stream));
-      if (!rc) rc = bg_hip_ok(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
-      if (rc) break;
-      c->defer_release = true;
-      hipStream_t main = c->stream;
-      c->stream = c->sstream;
-      rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
-      c->stream = main;
-      if (!rc) rc = bg_hip_ok(c, hipEventRecord(c->sjoin, c->sstream));
-    } else if (!rc) {
-      rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
-    }
-  }
-  {
-    const int rj = set_merge_join(c);  // the side stream's first-phase work before round trip 1
-    if (!rc) rc = rj;
+    rc = scout_one(c, inputs[i], s->t[i], st[i], ctr + 8ull * i);
   }
   HP("scout");
   // round trip 1: rows and record counts of every input, with the first REC_SPEC records
@@ -3502,11 +2736,6 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   for (int i = 0; i < n && !rc; ++i) {
     LoadState& S = st[i];
     s->t[i]->n = S.ntiles ? hctr[8ull * i] : 0;
-    if (S.lbw && S.nsamp) {  // sampled newlines -> the columns' capacity (+12.5% + 4096; overflow: redo)
-      const double est = (double)hctr[8ull * i] * (double)S.ntiles / (double)S.nsamp;
-      const uint64_t cap = (uint64_t)(est * 1.125) + 4096;
-      s->t[i]->n = std::min<uint64_t>(cap, S.nb + 1);
-    }
     const uint32_t nr = (uint32_t)hctr[8ull * i + 2];
     if (nr > S.rc) { rc = bg_fail(c, BG_E_UNSUPPORTED, "too many chromosome changes in one input"); break; }
     S.nrec = nr;
@@ -3536,25 +2765,13 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     rc = bg_hip_ok(c, hipMemcpyAsync(dst, hst, sizeof(bg_dstatus) * n, hipMemcpyHostToDevice, c->stream));
   }
   HP("dict");
-  static const bool side = [] {
-    const char* e = getenv("BEDGPU_SET_SIDE");
-    return !(e && atoi(e) == 0);
-  }();
-  // BEDGPU_SET_SPLIT=1: the last set input parsed in two halves around its first half's merge
-  // passes (set_split_finish). Exact (tests/test_gpu_setload.py forces it on small inputs) but
-  // measured slower on 100M x 100M --intersect (3.48 vs 3.46 ms: the second launch's ramp and
-  // tail cost more than the ~0.1 ms of passes it hides), so off by default
-  static const bool split_last = [] {
-    const char* e = getenv("BEDGPU_SET_SPLIT");
-    return e && atoi(e) == 1;
-  }();
+  // each set input's merge passes on the side stream beside the next input's parse (the
+  // last input's in line)
   for (int i = 0; i < n && !rc; ++i) {
-    const bool split = side && (split_last || getenv("BEDGPU_SET_SPLIT_MIN")) && i > 0 && i + 1 == n;
-    rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i, split)
+    rc = inputs[i].kind == BG_BED3_SET ? parse_set_one(c, s->t[i], st[i], gid, dst + i)
                                        : parse_one(c, inputs[i], s->t[i], st[i], gid, dst + i);
-    if (!rc && st[i].set_nt && st[i].set_split) rc = set_split_finish(c, s->t[i], st[i], dst + i, gid);
-    else if (!rc && st[i].set_nt)
-      rc = (side && i + 1 < n) ? set_merge_side(c, s->t[i], st[i], dst + i) : parse_set_merge(c, s->t[i], st[i], dst + i);
+    if (!rc && st[i].set_nt)
+      rc = i + 1 < n ? set_merge_side(c, s->t[i], st[i], dst + i) : parse_set_merge(c, s->t[i], st[i], dst + i);
   }
   {
     const int rj = set_merge_join(c);  // (on errors too: the side stream's blocks return to the pool)
@@ -3585,10 +2802,6 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   // a row input with a tile of more lines than k_parse_n holds: redone with k_parse
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && (hst[i].flags & BG_ROW_OVERFLOW)) redo = wide = true;
-  // a row input past its estimated capacity (or a look-back that timed out): redone with k_scout
-  bool scoutredo = false;
-  for (int i = 0; i < n && !rc; ++i)
-    if (inputs[i].kind != BG_BED3_SET && st[i].lbw && (hst[i].flags & BG_ROW_LOOKBACK)) redo = scoutredo = true;
   // a row input with more long scores than its k_score_big list holds: redone with room for all
   uint64_t bigneed = 0;
   for (int i = 0; i < n && !rc; ++i)
@@ -3640,14 +2853,12 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     std::vector<bg_input> rows(inputs, inputs + n);
     for (auto& in : rows)
       if (setredo && in.kind == BG_BED3_SET) in.kind = BG_BED3;
-    const bool w0 = c->row_wide, s0 = c->row_scout;
+    const bool w0 = c->row_wide;
     const uint64_t b0 = c->big_need;
     if (wide) c->row_wide = true;
-    if (scoutredo) c->row_scout = true;
     if (bigneed) c->big_need = std::max(b0, bigneed);
     const int rc2 = bg_load(c, n, rows.data(), out);
     c->row_wide = w0;
-    c->row_scout = s0;
     c->big_need = b0;
     return rc2;
   }

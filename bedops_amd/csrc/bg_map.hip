@@ -70,7 +70,6 @@ struct MapArgs {
   const int64_t* zout;
   int64_t touch;       // 1: rows that only touch the reference row can be in S(r) (tiny fractions)
   bg_dstatus* st;
-  const uint64_t* bnd;  // each workgroup's candidate range (k_map_bounds), null: searched in k_map_ops
 };
 
 __device__ __forceinline__ int64_t wmax64(int64_t v) {
@@ -99,54 +98,17 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const int64_t* X, uint32_t l
 
 #define MAP_SLICE 3072  // map starts staged per workgroup (24 KiB of LDS)
 
-// the candidate range of every k_map_ops workgroup before it starts: the largest candidate
-// bound khi of its rows (one wave per workgroup, coalesced), then both searches with one
-// thread per workgroup, every search in flight at once (inside k_map_ops they took two threads
-// of each resident workgroup while its other 254 waited: ~27 dependent loads per workgroup)
-__device__ __forceinline__ int64_t map_klo(int crit, const MapArgs& A, int64_t s) {
-  const int64_t g = s & ~BG_COORD_MASK;
-  const int64_t pad = crit == BG_OVR_RANGE ? A.range : 0;
-  return max(g, s - pad - A.L + 1 - A.touch);
-}
-__device__ __forceinline__ int64_t map_khi(int crit, const MapArgs& A, int64_t s, int64_t e) {
-  const int64_t g = s & ~BG_COORD_MASK;
-  const int64_t pad = crit == BG_OVR_RANGE ? A.range : 0;
-  return min(g + (1LL << BG_KEY_SHIFT), e + pad + (crit == BG_OVR_EXACT ? 1 : A.touch));
-}
-__global__ void __launch_bounds__(BG_NT) k_map_bmax(MapArgs A, int crit, uint64_t nblk, int64_t* __restrict__ bm) {
-  const uint64_t b = (uint64_t)blockIdx.x * (BG_NT / 64) + bg_wave();
-  if (b >= nblk) return;
-  int64_t m = LLONG_MIN;
-#pragma unroll
-  for (int k = 0; k < BG_NT / 64; ++k) {
-    const uint64_t r = b * BG_NT + (uint64_t)k * 64 + bg_lane();
-    if (r < A.nr) m = max(m, map_khi(crit, A, A.RS[r], A.RE[r]));
-  }
-  m = wmax64(m);
-  if (bg_lane() == 0) bm[b] = m;
-}
-__global__ void __launch_bounds__(BG_NT) k_map_bounds(MapArgs A, int crit, uint64_t nblk,
-                                                    const int64_t* __restrict__ bm, uint64_t* __restrict__ bnd) {
-  const uint64_t b = (uint64_t)blockIdx.x * BG_NT + threadIdx.x;
-  if (b >= nblk) return;
-  const uint64_t lo = lower_bound_i64(A.MS, A.nm, map_klo(crit, A, A.RS[b * BG_NT]));  // klo: non-decreasing
-  const uint64_t hi = lower_bound_i64(A.MS, A.nm, bm[b]);
-  bnd[2 * b] = lo;
-  bnd[2 * b + 1] = max(lo, hi);
-}
-
 // CRIT == BG_OVR_FAST (bedmap --faster, bg_faster.hip): the window [wlo, whi) of every row
 // is an input, its members are the rows that joined the sweep's deque (zin), and no criterion
 // is re-tested
-// SA: the candidates' ends and scores are staged beside their starts (72 KiB of LDS, 2
-// workgroups per CU), so the per-row candidate loop reads only LDS
-template <int CRIT, bool ZM, bool LONG, bool SA = false>
+// (staging the candidates' ends and scores beside their starts, 72 KiB of LDS, measured 6.5 ->
+// 12.0 ms on 50M x 500M, round 5: 2 workgroups per CU; the workgroups' candidate ranges from
+// separate pre-kernels measured 6.62 -> 6.93 ms)
+template <int CRIT, bool ZM, bool LONG>
 __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   __shared__ int64_t wmax[BG_NT / 64];
   __shared__ uint64_t bnd[2];
   __shared__ int64_t xs[MAP_SLICE];  // the workgroup's candidate starts, when they fit
-  __shared__ int64_t xe[SA ? MAP_SLICE : 1];
-  __shared__ double xc[SA ? MAP_SLICE : 1];
   constexpr bool FAST = CRIT == BG_OVR_FAST;
   const uint64_t r0 = (uint64_t)blockIdx.x * BG_NT;
   const uint64_t r = r0 + threadIdx.x;
@@ -159,10 +121,7 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   // tiny fractions: rows touching either end)
   const int64_t khi = min(g + (1LL << BG_KEY_SHIFT), e + pad + (CRIT == BG_OVR_EXACT ? 1 : A.touch));
   uint64_t blo = 0, bhi = 0;
-  if (!FAST && A.bnd) {
-    blo = A.bnd[2 * blockIdx.x];
-    bhi = A.bnd[2 * blockIdx.x + 1];
-  } else if (!FAST) {
+  if (!FAST) {
     const int64_t hm = wmax64(live ? khi : LLONG_MIN);
     if (bg_lane() == 0) wmax[bg_wave()] = hm;
     __syncthreads();
@@ -182,10 +141,6 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
   if (staged) {
     for (uint32_t i = threadIdx.x; i < bhi - blo; i += BG_NT) {
       xs[i] = A.MS[blo + i];
-      if (SA) {
-        xe[i] = A.ME[blo + i];
-        if (A.need & (NEED_SUM | NEED_EXT)) xc[i] = A.SC[blo + i];
-      }
     }
     __syncthreads();
   }
@@ -257,8 +212,8 @@ __global__ void __launch_bounds__(BG_NT) k_map_ops(MapArgs A) {
     for (int j = 0; j < MU; ++j) {
       const uint64_t m = min(m0 + j, hi - 1);
       ms[j] = staged ? xs[m - blo] : A.MS[m];
-      me[j] = (SA && staged) ? xe[m - blo] : A.ME[m];
-      sc[j] = (A.need & (NEED_SUM | NEED_EXT)) ? ((SA && staged) ? xc[m - blo] : A.SC[m]) : 0.0;
+      me[j] = A.ME[m];
+      sc[j] = (A.need & (NEED_SUM | NEED_EXT)) ? A.SC[m] : 0.0;
       live_m[j] = !ZM || bg_map_live(A.zin, A.zout, r, m);
     }
 #pragma unroll
@@ -1543,32 +1498,6 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
   A.zin = res->zin;
   A.zout = res->zout;
   A.st = c->dstat;
-  A.bnd = nullptr;
-  uint64_t* bnd = nullptr;
-  int64_t* bmx = nullptr;
-  // BEDGPU_MAP_BOUNDS=1: the workgroups' candidate ranges from k_map_bmax + k_map_bounds
-  // (measured on bedmap 50M x 500M: k_map_ops 6.62 -> 6.93 ms, the in-kernel searches are not
-  // what bounds it), so off by default
-  static const bool pre_bounds = [] {
-    const char* e = getenv("BEDGPU_MAP_BOUNDS");
-    return e && atoi(e) == 1;
-  }();
-  if (R->n && !faster && pre_bounds) {
-    const uint64_t nblk = bg_blocks(R->n, BG_NT);
-    bnd = (uint64_t*)bg_alloc(c, 16 * nblk);
-    bmx = (int64_t*)bg_alloc(c, 8 * nblk);
-    if (!bnd || !bmx) return BG_E_NOMEM;
-    BG_LAUNCH(c, "k_map_bmax", k_map_bmax, dim3(bg_blocks(nblk, BG_NT / 64)), dim3(BG_NT), A, crit, nblk, bmx);
-    BG_LAUNCH(c, "k_map_bounds", k_map_bounds, dim3(bg_blocks(nblk, BG_NT)), dim3(BG_NT), A, crit, nblk,
-              (const int64_t*)bmx, bnd);
-    A.bnd = bnd;
-  }
-  // BEDGPU_MAP_STAGE=1: ends and scores staged too — exact (bedmap GPU tests pass with it) but
-  // k_map_ops 6.5 -> 12.0 ms on 50M x 500M: 72 KiB of LDS leaves 2 workgroups per CU
-  static const bool stage_all = [] {
-    const char* e = getenv("BEDGPU_MAP_STAGE");
-    return e && atoi(e) == 1;
-  }();
   if (R->n) {
     const dim3 g(bg_blocks(R->n, BG_NT)), b(BG_NT);
 #define BG_MAP_LAUNCH(K)                                                                   \
@@ -1576,9 +1505,6 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
     if (A.lrows.ncls) {                                                                    \
       if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, true>), g, b, A);           \
       else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, true>), g, b, A);                \
-    } else if (stage_all) {                                                                \
-      if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, false, true>), g, b, A);    \
-      else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false, true>), g, b, A);         \
     } else {                                                                               \
       if (A.zin) BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, true, false>), g, b, A);          \
       else BG_LAUNCH(c, "k_map_ops", (k_map_ops<K, false, false>), g, b, A);               \
@@ -1596,8 +1522,6 @@ static int map_impl(bg_ctx* c, bg_set* set, int ref, int map, const bg_map_opts*
     }
 #undef BG_MAP_LAUNCH
   }
-  bg_release(c, bnd);
-  bg_release(c, bmx);
   int rc = bg_hip_ok(c, hipGetLastError());
   // equal map rows are ordered by the reference's heap addresses (bg_heap.hip): replay them
   // when an operation can see such a tie (both modes: one file replays sweep overload 1)

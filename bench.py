@@ -64,12 +64,7 @@ except OSError:
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
-            "k_parse_set": ("k_parse_set" if os.environ.get("BEDGPU_SET_NT") == "256" else
-                            ("k_parse_set_w" if os.environ.get("BEDGPU_SET_V") == "0" else
-                             "k_parse_set_p" if os.environ.get("BEDGPU_SET_V") == "2" else "k_parse_set_v")
-                            if os.environ.get("BEDGPU_SET_NT", "64") == "64" else
-                            "k_parse_set_n<128, false>" if os.environ.get("BEDGPU_SET_WS") == "0" else
-                            "k_parse_set_n<128, true>"),
+            "k_parse_set": "k_parse_set_v",
             "k_intersect_count": "k_mp_tile<0, false>", "k_intersect_write": "k_mp_tile<0, true, true>"}
 
 

@@ -1,12 +1,11 @@
-"""The wave form of closest-features' scan (k_closest_wave, bedops_amd/csrc/bg_closest.hip)
-against the one-candidate-at-a-time form (cl_run): same left/right and the same reader cache
-after every ref row, on random nested inputs, windows of 64 and of a few candidates (so every
-piece of carried state crosses window edges); and the sequential form against the
-control-flow oracle (oracle/closest_oracle.c) through its printed output."""
+"""The one-candidate-at-a-time form of closest-features' scan (cl_run in
+bedops_amd/csrc/bg_closest.hip, modelled in tests/model_closest_seq.py) against the
+control-flow oracle (oracle/closest_oracle.c) through its printed output, on random nested
+inputs; and the kernel's integer centroid test against the reference's double form."""
 import random
 import subprocess
 
-import model_closest_wave as M
+import model_closest_seq as M
 
 
 def rand_rows(rng, n, chroms, span, maxlen, nested=0.0):
@@ -27,19 +26,6 @@ CASES = [  # (seed, query rows, candidate rows, chroms, span, maxlen, nested)
     (4, 120, 200, 3, 5000, 200, 0.2),
     (5, 40, 900, 1, 2500, 15, 0.05),
 ]
-
-
-def test_wave_form_equals_sequential_form():
-    for seed, nq, nc, chroms, span, maxlen, nested in CASES:
-        rng = random.Random(seed)
-        Q = rand_rows(rng, nq, chroms, span, maxlen, nested)
-        C = rand_rows(rng, nc, chroms, span, maxlen, nested)
-        for overlaps in (True, False):
-            want = M.run_seq(Q, C, overlaps)
-            for W in (64, 5, 3, 1):
-                got = M.run_wave(Q, C, overlaps, W)
-                assert got[0] == want[0], (seed, overlaps, W)
-                assert got[1] == want[1], (seed, overlaps, W)
 
 
 def _bed(rows, tag):
@@ -73,7 +59,7 @@ def _half_double(bs, be, cs, ce):
     return prop < 0.5
 
 
-def _half_int(bs, be, cs, ce):  # bg_closest.hip: cl_run / cw_window
+def _half_int(bs, be, cs, ce):  # bg_closest.hip: cl_run
     return 2 * cs > bs + be - 1 or bs + be + 1 - 2 * cs < ce - cs
 
 

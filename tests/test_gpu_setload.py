@@ -225,12 +225,10 @@ def test_set_load_every_byte(eng, where):
 
 
 @pytest.mark.parametrize("mode,extra", MODES)
-def test_split_last_input_equals_oracle(eng, oracle_bin, monkeypatch, mode, extra):
-    """the last set input parsed in two halves with the first half's merge passes on the side
-    stream (set_split_finish), forced on small inputs (BEDGPU_SET_SPLIT_MIN=4 sub-tiles): long
-    rows of the last file reach across the split point, so the second half's first tiles are
-    absorbed by the first half's running max, and its components continue the first half's"""
-    monkeypatch.setenv("BEDGPU_SET_SPLIT_MIN", "4")
+def test_long_rows_across_subtiles_equal_oracle(eng, oracle_bin, mode, extra):
+    """long rows of the last file reach across hundreds of 4 KiB sub-tiles, so whole sub-tiles
+    are absorbed by the running max of earlier ones (k_set_count) and components continue
+    across them (k_set_write), with the earlier inputs' merge passes on the side stream"""
     rng = random.Random(zlib.crc32(repr(("split", mode)).encode()))
     n = 20000
     texts = _texts(rng, 2 if mode != "-s" else 3, n, 200, 300_000)
