@@ -1697,7 +1697,7 @@ struct ParseLdsV {
 
 // first '\n' at or after `from` (-1: none before the end of the text), one wave, 1 KiB a step
 __device__ __forceinline__ int64_t find_nl_wave(const uint8_t* __restrict__ txt, uint64_t nb, int64_t from) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   for (int64_t b = from; b >= 0 && (uint64_t)b < nb; b += 1024) {
     const uint4 x = load16(txt, b + 16 * lane, nb);  // bytes past the text read as 0
     const uint32_t m = (gather8x128(nl80_v(x.x), nl80_v(x.y)) >> 7) | (gather8x128(nl80_v(x.z), nl80_v(x.w)) << 1);
@@ -1710,11 +1710,6 @@ __device__ __forceinline__ int64_t find_nl_wave(const uint8_t* __restrict__ txt,
   return -1;
 }
 
-// the sub-tile and its halos lie inside the text (wave-uniform): unguarded loads, and every
-// read of the line bytes may go to the text itself
-__device__ __forceinline__ bool sub_inb(int64_t t0, uint64_t nb) {
-  return t0 >= HB && (uint64_t)t0 + TW + HA_V + 32 <= nb;
-}
 // what set_row / set_rounds_w read a sub-tile's lines through: its bytes from offset t0 - HB,
 // whitespace masks and line starts (LDS)
 struct SubView {
@@ -1731,14 +1726,16 @@ struct SubRegs {
   uint4 v[4];
   uint4 vh;
 };
+// (HAX: the staged halo after the sub-tile, + 32 bytes; k_parse_rv stages more than HA_V)
+template <int HAX = HA_V>
 __device__ __forceinline__ void load_sub(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0, SubRegs& R) {
-  constexpr int HL = HL_W;
+  constexpr int HL = (HAX + 32) / 16;
   static_assert(HL % 2 == 0 && HL < 63, "halo lanes");
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   uint4* const v = R.v;
   uint4& vh = R.vh;
   vh = make_uint4(0, 0, 0, 0);
-  if (sub_inb(t0, nb)) {  // wave-uniform: no guards
+  if (t0 >= HB && (uint64_t)t0 + TW + HAX + 32 <= nb) {  // wave-uniform: no guards
     const uint4* p = reinterpret_cast<const uint4*>(txt + t0) + 4 * lane;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = p[i];
@@ -1753,13 +1750,24 @@ __device__ __forceinline__ void load_sub(const uint8_t* __restrict__ txt, uint64
   }
 }
 
+// LDS order inside one wave (k_parse_rv: two waves per workgroup, each with its own LDS
+// block): the wave's LDS operations complete in order, so a code-motion barrier suffices
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // prologue of k_parse_set_v: prologue_w from the registers of load_sub, with the cheaper
-// '\n' classes and lst[L] = the last line's end + 1 (0xFFFF: none or out of reach)
+// '\n' classes and lst[L] = the last line's end + 1 (0xFFFF: none or out of reach).
+// ROWS (k_parse_rv): more than CAP lines set BG_ROW_OVERFLOW (the load is redone with
+// k_parse) instead of ERR_PARSE, and the waves of the workgroup do not wait for each other
+template <typename LdsT = ParseLdsV, uint32_t CAP = LCAP_V, bool ROWS = false, int HAX = HA_V>
 __device__ __forceinline__ uint32_t prologue_v(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
-                                               const SubRegs& R, ParseLdsV& S, int64_t& last_end,
+                                               const SubRegs& R, LdsT& S, int64_t& last_end,
                                                bg_dstatus* st) {
-  constexpr int HL = HL_W;
-  const int lane = threadIdx.x;
+  constexpr int HL = (HAX + 32) / 16;
+  const int lane = threadIdx.x & 63;
   const uint4* const v = R.v;
   const uint4 vh = R.vh;
 #pragma unroll
@@ -1789,21 +1797,26 @@ __device__ __forceinline__ uint32_t prologue_v(const uint8_t* __restrict__ txt, 
   const uint32_t cnt = (uint32_t)(__popc(n0) + __popc(n1));
   const uint32_t inc = wave_incl_scan(cnt, OpSum());
   const uint32_t L = wave_readlane(inc, 63) + (has0 ? 1u : 0u);
-  if (L > LCAP_V) {
-    if (lane == 0) bg_report(st, 0, ERR_PARSE);
+  if (L > CAP) {
+    if (lane == 0) {
+      if (ROWS) atomicOr(&st->flags, BG_ROW_OVERFLOW);
+      else bg_report(st, 0, ERR_PARSE);
+    }
     return L;
   }
   uint32_t o = inc - cnt + (has0 ? 1u : 0u);
   if (lane == 0 && has0) S.lst[0] = 0;
   for (uint32_t m = n0; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + bgp_ctz(m) + 1);
   for (uint32_t m = n1; m; m &= m - 1) S.lst[o++] = (uint16_t)(64 * lane + 32 + bgp_ctz(m) + 1);
-  __syncthreads();  // (one wave: orders the LDS writes above before the reads below)
-  last_end = L == 0 ? -1 : endnl ? t0 + TW - 1 : (hnl >= 0 ? t0 + hnl : find_nl_wave(txt, nb, t0 + TW + HA_V + 32));
+  if (ROWS) wave_lds_sync();
+  else __syncthreads();  // (one wave: orders the LDS writes above before the reads below)
+  last_end = L == 0 ? -1 : endnl ? t0 + TW - 1 : (hnl >= 0 ? t0 + hnl : find_nl_wave(txt, nb, t0 + TW + HAX + 32));
   if (lane == 0) {
     const int64_t d = last_end - t0 + 1;
     S.lst[L] = (last_end >= 0 && d < 0xFFFF) ? (uint16_t)d : (uint16_t)0xFFFF;
   }
-  __syncthreads();
+  if (ROWS) wave_lds_sync();
+  else __syncthreads();
   return L;
 }
 
@@ -1861,7 +1874,9 @@ __device__ __forceinline__ void set_rounds_v(const uint8_t* __restrict__ txt, co
     const uint32_t e1 = ffbl_hw(Te);
     // the third field ends inside the window (so do the others); short numbers; the token's
     // length; the line has an end (lst[L] != 0xFFFF)
-    bool ok = act && e1 <= 31u && qn != 0xFFFFu && (a1 - a0) == tlen && (s1 - s0) <= 9u && (e1 - e0) <= 9u;
+    // (tokens past 16 bytes: compared in full by set_row's hash, not by the 16-byte prefix)
+    bool ok = act && tlen <= 16u && e1 <= 31u && qn != 0xFFFFu && (a1 - a0) == tlen && (s1 - s0) <= 9u &&
+              (e1 - e0) <= 9u;
     const uint8_t* lb = &SV.buf[HB + q];  // the line's bytes (LDS)
     {
       uint32_t dif;
@@ -1982,6 +1997,275 @@ __global__ void __launch_bounds__(64) k_parse_set_v(
   const uint32_t u = blockIdx.x;
   load_sub(txt, nb, (int64_t)u * TW, V);
   parse_sub_v(txt, nb, u, V, S, runlo, runhi, R, LCS, LCE, TS, st);
+}
+
+// ---- k_parse_rv (round 6): the row parse in k_parse_set_v's shape -----------------------
+// Row columns (keys, rest spans, scores) for bedmap, closest-features and the row side of the
+// element operations. A workgroup of two waves owns one 8 KiB tile (the scout's row0 unit);
+// wave h parses sub-tile h (4 KiB) with k_parse_set_v's prologue and lean common path: on a
+// one-run sub-tile a line "<token> <start> <end>..." whose three fields end inside its first 32
+// bytes, the token the run's and both numbers <= 9 digits, is read from the whitespace
+// transitions, the token compared in SGPRs and the numbers converted by digits9. BED5 scores
+// then take parse_score_fast_ws (integers, "<int>.<frac>"); every other line takes
+// k_parse_n's per-line path (parse_line_fast_ws, then the full grammar) in its own lane. Same
+// outputs and error reports as k_parse_n. The only exchange between the waves: wave 0's line
+// count (wave 1's first row) and the keys on either side of the sub-tile edge (sort check).
+#define LCAP_R 512  // lines per 4 KiB sub-tile (lines averaging >= 8 bytes; more: redone with k_parse)
+// a 224-byte halo (+32) after the sub-tile, so that the lines crossing its end are staged for
+// the score path too (with k_parse_set_v's 32 bytes, one BED5 sub-tile in seven sent a lane to
+// the byte path)
+#define HA_R 224
+struct ParseLdsR {
+  __attribute__((aligned(16))) uint8_t buf[HB + TW + HA_R + 32];
+  uint32_t wsm[TW / 32 + (HA_R + 32) / 32 + 1];
+  uint16_t lst[LCAP_R + 1];
+};
+
+__device__ __forceinline__ int64_t wave_shr1_i64(int64_t v) {
+  return (int64_t)(((uint64_t)wave_shr1_v((uint32_t)((uint64_t)v >> 32)) << 32) | wave_shr1_v((uint32_t)v));
+}
+
+// the BED5 score after the end field ("<ws>id<ws>score", then whitespace or the line end) from
+// the whitespace window at the end field's end (p = q + e1): an integer of <= 9 digits by the
+// window's transitions and digits9; anything else parse_score_fast_ws, then the byte path
+__device__ __forceinline__ bool score_fast_v(const ParseLdsR& S, uint32_t q, uint32_t len, uint32_t e1, double& sc) {
+  const uint32_t p = q + e1, l2 = len - e1;
+  uint32_t WS;
+  {
+    const uint2 two = ldsu64(&S.wsm[p >> 5]);
+    WS = __builtin_amdgcn_alignbit(two.y, two.x, p & 31u);
+  }
+  WS |= l2 < 32u ? (~0u << (l2 & 31u)) : 0u;
+  const uint32_t NW = ~WS, NW1 = NW << 1;
+  uint32_t Ts = NW & ~NW1, Te = WS & NW1;
+  Ts &= Ts - 1;  // (the id's start)
+  const uint32_t c0 = ffbl_hw(Ts);
+  Te &= Te - 1;  // (the id's end)
+  const uint32_t c1 = ffbl_hw(Te);
+  bool ok = c1 <= 31u && (c1 - c0) <= 9u && (WS & 1u);
+  const uint32_t v = digits9(ldsu96(&S.buf[HB + p + (c1 & 31u) - 12]), (c1 - c0) & 15u, ok);
+  sc = (double)v;
+  return ok;
+}
+
+// one line on k_parse_n's per-line path (the run by position, parse_line_fast_ws, else the
+// full grammar); key: the row's start key (LLONG_MIN: not a row)
+template <bool REST, bool SCORE>
+__device__ __forceinline__ void row_line_general(const ParseLdsR& S, const TileText& T, const RunTable& R,
+                                                 uint32_t rl, uint32_t rh, int64_t t0, uint32_t q, int64_t ls,
+                                                 int64_t le, uint64_t r, int64_t* __restrict__ KS,
+                                                 int64_t* __restrict__ KE, uint64_t* __restrict__ rest_off,
+                                                 uint32_t* __restrict__ rest_len, double* __restrict__ score,
+                                                 bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap,
+                                                 int64_t& key, int64_t& mlen, bool& nonint) {
+  Fast F;
+  const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
+  const RunInfo& I = R.info[run];
+  const uint32_t len = (uint32_t)(le - ls);
+  double sc = 0;
+  bool isint = true;
+  // (scores are read up to the line's end: only lines ending inside the staged halo)
+  if (parse_line_fast_ws(S.buf, S.wsm, q, len, F, I.tlen <= 8) && F.toklen == I.tlen && F.tlo == I.tlo &&
+      F.thi == I.thi &&
+      (!SCORE || (le - t0 <= TW + HA_R && parse_score_fast_ws(S.buf, S.wsm, q, len, F.rest, sc, isint)))) {
+    nonint |= !isint;
+    emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
+    if (REST) {
+      rest_off[r] = (uint64_t)(ls + F.rest);
+      rest_len[r] = len - F.rest;
+    }
+    if (SCORE) score[r] = sc;
+    return;
+  }
+  Line Ln;
+  parse_line_slow(T, ls, le, SCORE ? BG_BED5 : BG_BED3, Ln);
+  if (Ln.err) {
+    if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
+    bg_report(st, r, Ln.err);
+    KS[r] = KE[r] = 0;
+  } else if (Ln.hash != I.hash) {  // a chromosome outside the run order: unsorted input
+    bg_report(st, r, ERR_UNSORTED);
+  } else {
+    emit_row(R, run, ls, r, Ln.start, Ln.end, KS, KE, st, key, mlen);
+    if (REST) {
+      rest_off[r] = (uint64_t)Ln.rest;
+      rest_len[r] = (uint32_t)(le - Ln.rest);
+    }
+    if (SCORE) {
+      score[r] = Ln.score;
+      if (Ln.scoreint <= 0) atomicOr(&st->flags, 1ULL);
+      if (Ln.scoreint < 0) big_push(st, big, bigcap, r, Ln.spos);
+    }
+  }
+}
+
+// the rounds of one sub-tile (64 lines per round, one per lane, in line order); kf / kl: the
+// keys of its first and last line (LLONG_MIN: not a row)
+template <bool REST, bool SCORE>
+__device__ __forceinline__ void row_rounds_v(const ParseLdsR& S, const TileText& T, const RunTable& R,
+                                             uint32_t rl, uint32_t rh, int64_t t0, uint32_t L, int64_t last_end,
+                                             uint64_t r0, uint64_t nrows, int64_t* __restrict__ KS,
+                                             int64_t* __restrict__ KE, uint64_t* __restrict__ rest_off,
+                                             uint32_t* __restrict__ rest_len, double* __restrict__ score,
+                                             bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap,
+                                             int64_t& kf, int64_t& kl, int64_t& mlen, bool& nonint) {
+  const int lane = threadIdx.x & 63;
+  const bool one = rl == rh;  // (wave-uniform)
+  // the run's token, mask, first line and key prefix in SGPRs (as set_rounds_v)
+  const RunInfo& I = R.info[rl];
+  const uint32_t tlen = sgpr(I.tlen);
+  const uint64_t tm = tlen >= 8 ? ~0ull : ((1ull << (8 * tlen)) - 1);
+  const uint64_t tm2 = tlen >= 16 ? ~0ull : (tlen <= 8 ? 0ull : ((1ull << (8 * (tlen - 8))) - 1));
+  const uint32_t tk0 = sgpr((uint32_t)I.tlo), tk1 = sgpr((uint32_t)(I.tlo >> 32));
+  const uint32_t tk2 = sgpr((uint32_t)I.thi), tk3 = sgpr((uint32_t)(I.thi >> 32));
+  const uint32_t tm0 = sgpr((uint32_t)tm), tm1 = sgpr((uint32_t)(tm >> 32)), tm2l = sgpr((uint32_t)tm2),
+                 tm2h = sgpr((uint32_t)(tm2 >> 32));
+  const int64_t pos0 = (int64_t)(((uint64_t)sgpr((uint32_t)((uint64_t)I.pos >> 32)) << 32) | sgpr((uint32_t)I.pos));
+  const int64_t gbase = (int64_t)sgpr((uint32_t)I.gid) << BG_KEY_SHIFT;
+  const bool tok16 = tlen > 8;
+  int64_t carry = LLONG_MIN;
+  kf = kl = LLONG_MIN;
+  const uint32_t rounds = (L + 63) / 64;
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t k = j * 64 + lane;
+    const bool act = k < L;
+    const uint32_t pr = ldsu32(&S.lst[act ? k : 0]);
+    const uint32_t q = pr & 0xFFFFu, qn = pr >> 16;
+    const int64_t ls = t0 + q;
+    const int64_t le = (k + 1 < L) ? t0 + qn - 1 : last_end;
+    const uint64_t r = r0 + k;
+    // le < 0 / r >= nrows: the unterminated last line (dropped like the reference)
+    const bool live = act && r < nrows && le >= 0;
+    const uint32_t len = live ? (uint32_t)(le - ls) : 0u;
+    int64_t key = LLONG_MIN;
+    bool ok = false;
+    uint32_t start = 0, end = 0, e1 = 0;
+    double sc = 0;
+    bool isint = true;
+    if (one) {
+      uint32_t WS;
+      {
+        const uint2 two = ldsu64(&S.wsm[q >> 5]);
+        WS = __builtin_amdgcn_alignbit(two.y, two.x, q & 31u);
+      }
+      WS |= len < 32u ? (~0u << (len & 31u)) : 0u;  // bytes past the line end act as whitespace
+      const uint32_t NW = ~WS, NW1 = NW << 1;
+      uint32_t Ts = NW & ~NW1, Te = WS & NW1;  // field starts, field ends
+      const uint32_t a0 = ffbl_hw(Ts);
+      Ts &= Ts - 1;
+      const uint32_t s0 = ffbl_hw(Ts);
+      Ts &= Ts - 1;
+      const uint32_t e0 = ffbl_hw(Ts);
+      const uint32_t a1 = ffbl_hw(Te);
+      Te &= Te - 1;
+      const uint32_t s1 = ffbl_hw(Te);
+      Te &= Te - 1;
+      e1 = ffbl_hw(Te);
+      ok = live && tlen <= 16u && e1 <= 31u && (a1 - a0) == tlen && (s1 - s0) <= 9u && (e1 - e0) <= 9u;
+      const uint8_t* lb = &S.buf[HB + q];
+      {
+        uint32_t dif;
+        if (tok16) {
+          const uint4 t = ldsu128(lb + (a0 & 31u));
+          dif = ((t.x ^ tk0) & tm0) | ((t.y ^ tk1) & tm1) | ((t.z ^ tk2) & tm2l) | ((t.w ^ tk3) & tm2h);
+        } else {
+          const uint2 t = ldsu64(lb + (a0 & 31u));
+          dif = ((t.x ^ tk0) & tm0) | ((t.y ^ tk1) & tm1);
+        }
+        ok = ok && dif == 0;
+      }
+      start = digits9(ldsu96(lb + (s1 & 31u) - 12), (s1 - s0) & 15u, ok);
+      end = digits9(ldsu96(lb + (e1 & 31u) - 12), (e1 - e0) & 15u, ok);
+      if (SCORE) ok = ok && le - t0 <= TW + HA_R && score_fast_v(S, q, len, e1, sc);
+    }
+    if (ok) {
+      if (start > end) bg_report(st, r, ERR_RANGE);
+      if (start == end) atomicOr(&st->flags, 2ULL);
+      mlen = max(mlen, (int64_t)end - (int64_t)start);
+      if (ls == pos0) R.row[rl] = r;
+      key = gbase | (int64_t)start;
+      KS[r] = key;
+      KE[r] = gbase | (int64_t)end;
+      if (REST) {
+        rest_off[r] = (uint64_t)(ls + e1);
+        rest_len[r] = len - e1;
+      }
+      if (SCORE) {
+        score[r] = sc;
+        nonint |= !isint;
+      }
+    } else if (live) {
+      row_line_general<REST, SCORE>(S, T, R, rl, rh, t0, q, ls, le, r, KS, KE, rest_off, rest_len, score, st,
+                                    big, bigcap, key, mlen, nonint);
+    }
+    // sort order: each line against the one before it (the lane before, or lane 63 of the
+    // previous round)
+    const int64_t pk = wave_shr1_i64(key);
+    const int64_t prev = lane ? pk : carry;
+    if (key != LLONG_MIN && prev != LLONG_MIN && key < prev) bg_report(st, r, ERR_UNSORTED);
+    if (j == 0) kf = (int64_t)wave_readlane((uint64_t)key, 0);
+    if (j + 1 == rounds) kl = (int64_t)wave_readlane((uint64_t)key, (int)(L - 1 - j * 64));
+    carry = (int64_t)wave_readlane((uint64_t)key, 63);
+  }
+}
+
+#ifndef BG_RV_WAVES
+#define BG_RV_WAVES 6
+#endif
+#ifndef BG_RV_WAVES5
+#define BG_RV_WAVES5 6
+#endif
+template <bool REST, bool SCORE>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SCORE ? BG_RV_WAVES5 : BG_RV_WAVES, 8))) k_parse_rv(
+    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
+    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
+    int64_t* __restrict__ KS, int64_t* __restrict__ KE, uint64_t* __restrict__ rest_off,
+    uint32_t* __restrict__ rest_len, double* __restrict__ score, bg_dstatus* st, uint64_t* __restrict__ big,
+    uint32_t bigcap) {
+  __shared__ ParseLdsR SS[2];
+  __shared__ uint32_t xl[2];
+  __shared__ int64_t xk[2][2];  // [wave][first line, last line] keys
+  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
+  const uint32_t u = 2 * blockIdx.x + h;  // sub-tile
+  const int64_t t0 = (int64_t)u * TW;
+  const bool inside = (uint64_t)t0 < nb;  // (the file's last tile may hold one sub-tile)
+  ParseLdsR& S = SS[h];
+  int64_t last_end = -1;
+  uint32_t L = 0;
+  if (inside) {
+    SubRegs V;
+    load_sub<HA_R>(txt, nb, t0, V);
+    L = prologue_v<ParseLdsR, LCAP_R, true, HA_R>(txt, nb, t0, V, S, last_end, st);
+  }
+  if (lane == 0) xl[h] = L;
+  __syncthreads();
+  const uint32_t L0 = xl[0];
+  if (L0 > LCAP_R || xl[1] > LCAP_R) return;  // (BG_ROW_OVERFLOW: the load is redone with k_parse)
+  // the first owned line's row: newlines before the tile (+1 when the tile opens mid-line);
+  // wave 1's follows wave 0's L0 lines
+  const int64_t tt = (int64_t)blockIdx.x * TT;
+  const bool has0 = tt == 0 || SS[0].buf[HB - 1] == '\n';
+  const uint64_t r0 = row0[blockIdx.x] + (has0 ? 0 : 1) + (h ? L0 : 0);
+  int64_t mlen = 0, kf = LLONG_MIN, kl = LLONG_MIN;
+  bool nonint = false;
+  if (L > 0) {
+    const TileText T{txt, S.buf, t0 - HB, t0 + TW + HA_R, nb};
+    row_rounds_v<REST, SCORE>(S, T, R, runlo[u], runhi[u], t0, L, last_end, r0, nrows, KS, KE, rest_off,
+                              rest_len, score, st, big, bigcap, kf, kl, mlen, nonint);
+  }
+  if (__ballot(nonint) && lane == 0) atomicOr(&st->flags, 1ULL);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mlen = max(mlen, (int64_t)__shfl_xor(mlen, d, 64));
+  if (lane == 0 && mlen > *(volatile long long*)&st->maxlen) atomicMax(&st->maxlen, (long long)mlen);
+  if (lane == 0) {
+    xk[h][0] = kf;
+    xk[h][1] = kl;
+  }
+  __syncthreads();
+  if (h == 1 && lane == 0 && L0 > 0 && L > 0) {  // wave 1's first line vs wave 0's last
+    const int64_t a = xk[0][1], b = xk[1][0];
+    if (a != LLONG_MIN && b != LLONG_MIN && b < a) bg_report(st, r0, ERR_UNSORTED);
+  }
 }
 
 
@@ -2484,8 +2768,15 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   }
   const uint32_t nr = (uint32_t)S.run_pos.size();
   if (S.ntiles == 0 || T->n == 0 || nr == 0) return 0;
+  // k_parse_rv (two waves per tile, run ranges per 4 KiB sub-tile) unless BEDGPU_ROW_V=0
+  // (k_parse_n) or the load is a redo with k_parse
+  static const bool rowv = [] {
+    const char* e = getenv("BEDGPU_ROW_V");
+    return !e || atoi(e) != 0;
+  }();
+  const bool rv = rowv && !c->row_wide;
   RunTable R;
-  int rc = upload_runs(c, T, S, gid, R);
+  int rc = upload_runs(c, T, S, gid, R, rv ? TW : TT);
   if (rc) return rc;
   // k_parse_n (whitespace-only tile front end, 128 threads) unless a load found a tile of very
   // short lines (BG_ROW_OVERFLOW) and is being redone with k_parse
@@ -2501,7 +2792,18 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     S.big = (uint64_t*)bg_alloc(c, 16ull * (S.bigcap ? S.bigcap : 1));
     if (!S.big) return BG_E_NOMEM;
   }
-  if (!c->row_wide)
+  const int kind = in.kind == BG_BED5_REST ? BG_BED5 : in.kind;
+  if (rv) {
+#define BG_ROWV(RE, SC)                                                                                    \
+  BG_LAUNCH(c, "k_parse", (k_parse_rv<RE, SC>), dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo, \
+            S.rhi, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st, S.big, S.bigcap)
+    const bool re = T->rest_off != nullptr, sc = kind == BG_BED5;
+    if (re && sc) BG_ROWV(true, true);
+    else if (re) BG_ROWV(true, false);
+    else if (sc) BG_ROWV(false, true);
+    else BG_ROWV(false, false);
+#undef BG_ROWV
+  } else if (!c->row_wide)
     BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
               S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
               S.big, S.bigcap);

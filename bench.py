@@ -605,9 +605,11 @@ def main():
             dist.barrier()
 
     # warmup; every warmup step profiles every kernel: the last (warm) one names the
-    # dominant kernel (the first carries code-object loading and first-touch costs)
+    # dominant kernel (the first carries code-object loading and first-touch costs — with
+    # --warmup 1 it named k_fmt_write, whose first launch faults its output pages in — so at
+    # least two untimed steps run)
     eng.prof_enable("*")
-    for w in range(max(args.warmup, 1)):
+    for w in range(max(args.warmup, 2)):
         step()
         last = eng.prof_read()
         eng.prof_enable("*")  # (clears the statistics)
