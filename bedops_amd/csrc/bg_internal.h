@@ -43,7 +43,6 @@ struct bg_dstatus {
   unsigned long long stop_row;   // bedmap: first row where the reference throws (~0: none)
   unsigned long long pad[2];
   unsigned long long nbig;       // BED5 scores left to the exact big-number conversion (k_score_big)
-  unsigned long long nrows;      // k_parse_n without a scout pass: the input's lines (its last tile's prefix)
 };
 
 // bedmap: map rows longer than thr, by length class (see bg_map_cands below)

@@ -453,6 +453,11 @@ __device__ __forceinline__ bool decimal_exact(uint64_t m, int pw, double& out) {
   return true;
 }
 
+// exact powers of ten (a table in constant memory: a local array indexed at run time is
+// placed in scratch)
+__constant__ double BG_P10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
 // strtod subset, correctly rounded where it accepts: [+-]digits[.digits][(e|E)[+-]digits]
 // with <= 19 significant digits m and value m * 10^p, |p| <= 22 and m <= 2^53 (Clinger's
 // fast path: one rounding of exact operands), p up to 37 when m * 10^(p-22) stays an exact
@@ -461,6 +466,10 @@ __device__ __forceinline__ bool decimal_exact(uint64_t m, int pw, double& out) {
 // (exact sums). Any other valid number (up to BG_SD_DIGITS significant digits, any
 // exponent) returns isint = -1: the caller lists it for k_score_big (bg_strtod.h). More
 // digits, or anything that is not a plain decimal number -> ERR_SCORE.
+// EXACT == false (k_parse_rv): what would take decimal_exact's 128-bit arithmetic is listed for
+// k_score_big instead (isint -1: the same correctly rounded value; the 128-bit division's
+// registers spilled in the row kernel's every wave)
+template <bool EXACT = true>
 __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64_t le,
                                             double& out, int& isint) {
   bool neg = false;
@@ -503,15 +512,14 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
   }
   int pw = ex - frac;  // value = m * 10^pw
   while (pw < 0 && m != 0 && m % 10 == 0) { m /= 10; ++pw; }  // trailing zeros
-  const double P10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                          1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  const double* const P10 = BG_P10;
   if (m == 0) {
     isint = 1;
     out = neg ? -0.0 : 0.0;
     return true;
   }
   if (m > (1ULL << 53) || pw < -22) {  // outside Clinger's fast path: exact 128-bit rounding
-    if (!decimal_exact(m, pw, out)) {  // beyond 128 bits: k_score_big
+    if (!EXACT || !decimal_exact(m, pw, out)) {  // beyond 128 bits: k_score_big
       isint = -1;
       out = 0;
       return true;
@@ -532,7 +540,7 @@ __device__ __forceinline__ bool parse_score(const TileText& T, int64_t& p, int64
         mm *= 10;
       }
       if (pp > 22) {  // not exact that way
-        if (!decimal_exact(m, pw, out)) {
+        if (!EXACT || !decimal_exact(m, pw, out)) {
           isint = -1;
           out = 0;
           return true;
@@ -571,6 +579,7 @@ struct Line {
 };
 
 // full grammar, byte by byte (fallback path and error reporting)
+template <bool EXACT = true>
 __device__ __forceinline__ void parse_line_slow(const TileText& T, int64_t ls, int64_t le, int kind,
                                              Line& L) {
   L.err = 0;
@@ -603,7 +612,7 @@ __device__ __forceinline__ void parse_line_slow(const TileText& T, int64_t ls, i
     while (p < le && bg_isws(T.at(p))) ++p;
     int isint = 1;
     L.spos = p;
-    if (!parse_score(T, p, le, L.score, isint)) { L.err = ERR_SCORE; return; }
+    if (!parse_score<EXACT>(T, p, le, L.score, isint)) { L.err = ERR_SCORE; return; }
     L.scoreint = isint;
   }
 }
@@ -749,7 +758,7 @@ __device__ __forceinline__ bool parse_line_fast(const uint8_t* buf, const uint32
   return true;
 }
 
-// parse_line_fast from the whitespace mask alone (k_parse_n: the tile is classified for
+// parse_line_fast from the whitespace mask alone (k_parse_rv: the tile is classified for
 // whitespace only, half the prologue's work): numbers end at whitespace and their bytes are
 // checked to be digits while they are converted (bgp_fields_ws / bgp_digits_rc); a line this
 // refuses takes the byte path, as in parse_line_fast
@@ -866,25 +875,6 @@ struct ParseLdsT {
   uint32_t shs[BG_NT / 64 + 1];
 };
 
-// k_parse_n's whitespace-only layout: no digit bitmap, and line starts for up to
-// LCAP_WS lines (8 KiB of lines averaging >= 8 bytes; a tile of shorter lines reports a
-// parse error and the load is redone with row columns, as any set-path refusal): 2.1 KiB
-// less LDS per workgroup, 13 instead of 11 workgroups per CU
-#define LCAP_WS 1024
-struct ParseBufWs {
-  __attribute__((aligned(16))) uint8_t buf[LBUF];
-  uint32_t wsm[TT / 32 + HA / 32 + 1];
-  uint32_t hnl;
-};
-struct ParseLdsWs {
-  ParseBufWs b[1];
-  uint16_t lst[LCAP_WS + 1];
-  uint32_t shs[BG_NT / 64 + 1];
-};
-__device__ __forceinline__ void clear_halo(ParseBufWs& B) {
-  if (threadIdx.x == 0) B.hnl = ~0u;
-  if (threadIdx.x < (HA + 32) / 32) B.wsm[TT / 32 + threadIdx.x] = 0;
-}
 // the halo words of B's bitmaps start empty (LDS atomics in prologue_core), hnl unset
 __device__ __forceinline__ void clear_halo(ParseBuf& B) {
   if (threadIdx.x == 0) B.hnl = ~0u;
@@ -1160,7 +1150,7 @@ __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64<0x1
 // A sub-tile with more than SCAP_W (4 KiB of rows shorter than 16 bytes, almost all
 // disjoint) sets BG_SET_OVERFLOW and bg_load re-reads that input with its row columns (BG_BED3).
 #define BG_SET_OVERFLOW 8ULL  // bg_dstatus.flags bit
-#define BG_ROW_OVERFLOW 16ULL  // k_parse_n: a tile of more than LCAP_WS lines
+#define BG_ROW_OVERFLOW 16ULL  // k_parse_rv: a sub-tile of more than LCAP_R lines
 
 __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
   v = max(v, dpp32<0x111, 0xF, true>(v));
@@ -1176,131 +1166,6 @@ __device__ __forceinline__ uint64_t wave_incl_max_v(uint64_t v) { return wave_in
 __device__ __forceinline__ uint32_t wave_shr1_v(uint32_t v) { return dpp32<0x138, 0xF, true>(v); }
 __device__ __forceinline__ uint64_t wave_shr1_v(uint64_t v) { return wave_shr1_u64(v); }
 
-
-// ---- the row parse's tile front end: NT-thread workgroups over 8 KiB tiles -----------------
-// each thread stages and classifies TT / NT tile bytes (k_parse_n: NT = 128, the ~340 lines of
-// a tile in rounds of 128)
-template <int NT>
-struct TileRegsN {
-  uint4 v[TT / NT / 16];  // this thread's TT / NT tile bytes
-  uint4 vh;               // halo piece (as TileRegs)
-};
-template <int NT>
-__device__ __forceinline__ void load_tile_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
-                                            TileRegsN<NT>& R) {
-  constexpr int BPT = TT / NT;
-  const int64_t b = t0 + (int64_t)threadIdx.x * BPT;
-#pragma unroll
-  for (int i = 0; i < BPT / 16; ++i) R.v[i] = load16(txt, b + 16 * i, nb);
-  if (threadIdx.x < (HA + 32) / 16) R.vh = load16(txt, t0 + TT + (int64_t)threadIdx.x * 16, nb);
-  else if (threadIdx.x == NT - 1) R.vh = load16(txt, t0 - HB, nb);
-}
-template <int NT>
-__device__ __forceinline__ void store_tile_n(uint8_t* buf, const TileRegsN<NT>& R) {
-  constexpr int BPT = TT / NT;
-#pragma unroll
-  for (int i = 0; i < BPT / 16; ++i) *reinterpret_cast<uint4*>(&buf[HB + threadIdx.x * BPT + 16 * i]) = R.v[i];
-  if (threadIdx.x < (HA + 32) / 16) *reinterpret_cast<uint4*>(&buf[HB + TT + threadIdx.x * 16]) = R.vh;
-  else if (threadIdx.x == NT - 1) *reinterpret_cast<uint4*>(&buf[0]) = R.vh;
-}
-// tile_line_starts for TT / NT bytes per thread (G 32-byte groups, lines in byte order)
-template <int NT>
-__device__ __forceinline__ uint32_t tile_line_starts_n(const TileRegsN<NT>& R, const uint8_t* buf, int64_t t0,
-                                                       uint16_t* ls, uint32_t cap, uint32_t* shs, bool& has0) {
-  constexpr int G = TT / NT / 32;
-  has0 = (t0 == 0) || buf[HB - 1] == '\n';
-  uint32_t nlg[G];
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) m |= bgp_group4(nl_mask4(w[k])) << (4 * k);
-    if (g == G - 1 && threadIdx.x == NT - 1) m &= 0x7FFFFFFFu;  // starts a line in the next tile
-    nlg[g] = m;
-    cnt += (uint32_t)__popc(m);
-  }
-  const uint32_t inc = wave_incl_scan(cnt, OpSum());
-  if (bg_lane() == 63) shs[bg_wave()] = inc;
-  __syncthreads();
-  uint32_t tot = 0, wpre = 0;
-#pragma unroll
-  for (int q = 0; q < NT / 64; ++q) {
-    const uint32_t x = shs[q];
-    if (q < bg_wave()) wpre += x;
-    tot += x;
-  }
-  uint32_t o = wpre + inc - cnt + (has0 ? 1u : 0u);
-  if (threadIdx.x == 0 && has0) ls[0] = 0;
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    for (uint32_t m = nlg[g]; m; m &= m - 1) {
-      if (o < cap) ls[o] = (uint16_t)(threadIdx.x * (TT / NT) + 32 * g + bgp_ctz(m) + 1);
-      ++o;
-    }
-  __syncthreads();
-  return tot + (has0 ? 1u : 0u);
-}
-// WSO: whitespace masks only (parse_line_fast_ws): one multiply per two dwords instead of
-// one per dword plus the digit classes
-// (OVF_FLAG: a tile of more than CAP lines sets BG_ROW_OVERFLOW instead of reporting a
-// parse error; bg_load then redoes the load with k_parse)
-template <int NT, bool WSO, typename LdsT, bool OVF_FLAG = false>
-__device__ __forceinline__ uint32_t tile_prologue_n(const uint8_t* __restrict__ txt, uint64_t nb, int64_t t0,
-                                                    LdsT& S, const TileRegsN<NT>& R, int64_t& last_end,
-                                                    bg_dstatus* st) {
-  constexpr uint32_t CAP = WSO ? LCAP_WS : LCAP;
-  auto& B = S.b[0];
-  clear_halo(B);
-  store_tile_n<NT>(B.buf, R);
-  __syncthreads();
-  constexpr int G = TT / NT / 32;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {  // classify this thread's bytes once (SWAR), publish the masks
-    const uint4 a = R.v[2 * g], b = R.v[2 * g + 1];
-    const uint32_t W[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    if constexpr (WSO) {
-      B.wsm[threadIdx.x * G + g] = bgp_ws8(W[0], W[1]) | (bgp_ws8(W[2], W[3]) << 8) |
-                                   (bgp_ws8(W[4], W[5]) << 16) | (bgp_ws8(W[6], W[7]) << 24);
-    } else {
-      uint32_t ws, dg;
-      bgp_classify8(W, ws, dg);
-      B.wsm[threadIdx.x * G + g] = ws;
-      B.dgm[threadIdx.x * G + g] = dg;
-    }
-  }
-  {  // the halo after the tile (as prologue_core)
-    constexpr uint32_t HD = (HA + 32) / 4;
-    static_assert(HD <= NT, "halo dwords per thread");
-    if (threadIdx.x < HD) {
-      const uint32_t x = reinterpret_cast<const uint32_t*>(&B.buf[HB + TT])[threadIdx.x];
-      uint32_t w4, d4;
-      bgp_classify(x, w4, d4);
-      const uint32_t sh = 4 * (threadIdx.x & 7);
-      if (w4) atomicOr(&B.wsm[TT / 32 + threadIdx.x / 8], w4 << sh);
-      if constexpr (!WSO)
-        if (d4) atomicOr(&B.dgm[TT / 32 + threadIdx.x / 8], d4 << sh);
-      const uint32_t m = nl_mask4(x);
-      if (m) atomicMin(&B.hnl, TT + 4 * threadIdx.x + (__ffs(m) - 1) / 8);
-    }
-  }
-  bool has0;
-  const uint32_t L = tile_line_starts_n<NT>(R, B.buf, t0, S.lst, CAP + 1, S.shs, has0);
-  if (L > CAP) {
-    if (threadIdx.x == 0) {
-      if (OVF_FLAG) atomicOr(&st->flags, BG_ROW_OVERFLOW);
-      else bg_report(st, 0, ERR_PARSE);
-    }
-    return L;
-  }
-  TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
-  last_end = L == 0 ? -1
-             : (B.buf[HB + TT - 1] == '\n') ? t0 + TT - 1
-             : (B.hnl != ~0u ? t0 + B.hnl : find_nl(T, t0 + TT + HA + 32));
-  return L;
-}
 
 // parse_score_fast from the whitespace mask alone: the score's bytes are checked to be
 // digits while they are converted (bgp_digits_rc)
@@ -1352,7 +1217,7 @@ __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const ui
   lds12_end(buf, q + HB + e1 + c1, d1, d2, d3);
   const uint64_t vf = bgp_digits_rc(d1, d2, d3, (int)nf, ok);
   if (!ok) return false;
-  const double P10[13] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12};
+  const double* const P10 = BG_P10;
   uint64_t m = vi * (uint64_t)P10[nf] + vf;
   int pw = -(int)nf;
   while (pw < 0 && m != 0 && m % 10 == 0) {
@@ -1367,110 +1232,6 @@ __device__ __forceinline__ bool parse_score_fast_ws(const uint8_t* buf, const ui
   score = (double)m / P10[-pw];
   isint = false;
   return true;
-}
-
-// Row parse (keys, rest spans, scores): NT threads per 8 KiB tile, the tile classified for
-// whitespace only (tile_prologue_n<NT, true>), fields and digits checked in
-// parse_line_fast_ws / parse_score_fast_ws. Lines the fast path refuses take parse_line_slow
-// in the same loop. Same outputs and error reports as k_parse. The tiles' first rows come
-// from the scout pass (row0).
-#ifndef BG_PN_WAVES
-#define BG_PN_WAVES 6  // k_parse_n's minimum waves per SIMD (6: <= 80 VGPRs)
-#endif
-template <int NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BG_PN_WAVES, 8))) k_parse_n(
-    const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, uint64_t* __restrict__ row0,
-    const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi,
-    int kind, RunTable R, int64_t* __restrict__ KS, int64_t* __restrict__ KE,
-    uint64_t* __restrict__ rest_off, uint32_t* __restrict__ rest_len, double* __restrict__ score,
-    bg_dstatus* st, uint64_t* __restrict__ big, uint32_t bigcap) {
-  __shared__ ParseLdsWs S;
-  constexpr uint32_t NR = LCAP_WS / NT;  // rounds of NT lines at most
-  __shared__ int64_t kfirst[NR][NT / 64], klast[NR][NT / 64];  // keys at the waves' edges
-  const int64_t t0 = (int64_t)blockIdx.x * TT;
-  int64_t last_end = -1;
-  uint32_t L;
-  {
-    TileRegsN<NT> TR;
-    load_tile_n<NT>(txt, nb, t0, TR);
-    L = tile_prologue_n<NT, true, ParseLdsWs, true>(txt, nb, t0, S, TR, last_end, st);
-  }
-  const auto& B = S.b[0];
-  const bool has0 = (t0 == 0) || B.buf[HB - 1] == '\n';
-  const uint64_t rt = row0[blockIdx.x];  // newlines before the tile
-  const uint64_t r0 = rt + (has0 ? 0 : 1);  // row of the first owned line
-  if (L > LCAP_WS) return;  // (BG_ROW_OVERFLOW: the load is redone with k_parse)
-  const uint32_t rl = runlo[blockIdx.x], rh = runhi[blockIdx.x];
-  const TileText T{txt, B.buf, t0 - HB, t0 + TT + HA, nb};
-  int64_t mlen = 0;
-  bool nonint = false;  // a decimal score on the fast path (st->flags bit 0, once per wave)
-  const uint32_t rounds = (L + NT - 1) / NT;
-  const int lane = bg_lane(), w = bg_wave();
-  for (uint32_t j = 0; j < rounds; ++j) {
-    const uint32_t k = j * NT + threadIdx.x;
-    int64_t key = LLONG_MIN;
-    const int64_t ls = k < L ? t0 + S.lst[k] : 0;
-    const uint64_t r = r0 + k;
-    const int64_t le = k >= L ? -1 : (k + 1 < L) ? t0 + S.lst[k + 1] - 1 : last_end;
-    if (k < L && r < nrows && le >= 0) {  // le < 0 / r >= nrows: the unterminated last line (dropped)
-      Fast F;
-      const uint32_t run = (rl == rh) ? rl : run_of(R, ls, rl, rh);
-      const RunInfo& I = R.info[run];
-      double sc = 0;
-      bool isint = true;
-      if (parse_line_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F, I.tlen <= 8) &&
-          F.toklen == I.tlen && F.tlo == I.tlo && F.thi == I.thi &&
-          (kind != BG_BED5 || parse_score_fast_ws(B.buf, B.wsm, S.lst[k], (uint32_t)(le - ls), F.rest, sc, isint))) {
-        nonint |= !isint;
-        emit_row(R, run, ls, r, F.start, F.end, KS, KE, st, key, mlen);
-        if (rest_off) {
-          rest_off[r] = (uint64_t)(ls + F.rest);
-          rest_len[r] = (uint32_t)(le - ls - F.rest);
-        }
-        if (score) score[r] = sc;
-      } else {  // the full grammar, byte by byte (decimal scores, odd spacing, errors)
-        Line Ln;
-        parse_line_slow(T, ls, le, kind, Ln);
-        if (Ln.err) {
-          if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
-          bg_report(st, r, Ln.err);
-          KS[r] = KE[r] = 0;
-        } else if (Ln.hash != I.hash) {  // a chromosome outside the run order: unsorted input
-          bg_report(st, r, ERR_UNSORTED);
-        } else {
-          emit_row(R, run, ls, r, Ln.start, Ln.end, KS, KE, st, key, mlen);
-          if (rest_off) {
-            rest_off[r] = (uint64_t)Ln.rest;
-            rest_len[r] = (uint32_t)(le - Ln.rest);
-          }
-          if (score) {
-            score[r] = Ln.score;
-            if (Ln.scoreint <= 0) atomicOr(&st->flags, 1ULL);
-            if (Ln.scoreint < 0) big_push(st, big, bigcap, r, Ln.spos);
-          }
-        }
-      }
-    }
-    // sort order inside the tile: each line against the one before it (the lane before, or
-    // across a wave edge after the loop)
-    const int64_t prev = __shfl_up(key, 1, 64);
-    if (lane > 0 && key != LLONG_MIN && prev != LLONG_MIN && key < prev) bg_report(st, r, ERR_UNSORTED);
-    if (lane == 0) kfirst[j][w] = key;
-    if (lane == 63) klast[j][w] = key;
-  }
-  if (__ballot(nonint) && lane == 0) atomicOr(&st->flags, 1ULL);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) mlen = max(mlen, (int64_t)__shfl_xor(mlen, d, 64));
-  if (bg_lane() == 0 && mlen > *(volatile long long*)&st->maxlen) atomicMax(&st->maxlen, (long long)mlen);
-  __syncthreads();
-  if (threadIdx.x < rounds * (NT / 64)) {  // the first line of each wave's round vs the line before it
-    const uint32_t j = threadIdx.x / (NT / 64), q = threadIdx.x % (NT / 64);
-    const uint32_t k = j * NT + q * 64;
-    if (k > 0 && k < L) {
-      const int64_t a = (q > 0) ? klast[j][q - 1] : klast[j - 1][NT / 64 - 1], b = kfirst[j][q];
-      if (a != LLONG_MIN && b != LLONG_MIN && b < a) bg_report(st, r0 + k, ERR_UNSORTED);
-    }
-  }
 }
 
 // ---- BG_BED3_SET: one wavefront per 4 KiB sub-tile -------------------------------------
@@ -1494,7 +1255,7 @@ __device__ __forceinline__ uint64_t wave_readlane(uint64_t v, int l) {
 }
 
 // the rounds of one sub-tile: 64 lines per round, one per lane, in line order (V as
-// k_parse_n's rows). kl: K (+1 form) of the sub-tile's largest row key.
+// k_parse_rv's rows). kl: K (+1 form) of the sub-tile's largest row key.
 template <typename V, typename LdsT>
 __device__ __forceinline__ void set_rounds_w(const LdsT& S, const TileText& T, const RunTable& R,
                                              uint32_t rl, uint32_t rh, int64_t t0, uint32_t L,
@@ -2007,8 +1768,10 @@ __global__ void __launch_bounds__(64) k_parse_set_v(
 // bytes, the token the run's and both numbers <= 9 digits, is read from the whitespace
 // transitions, the token compared in SGPRs and the numbers converted by digits9. BED5 scores
 // then take parse_score_fast_ws (integers, "<int>.<frac>"); every other line takes
-// k_parse_n's per-line path (parse_line_fast_ws, then the full grammar) in its own lane. Same
-// outputs and error reports as k_parse_n. The only exchange between the waves: wave 0's line
+// the per-line path (parse_line_fast_ws, then the full grammar) in its own lane. Same outputs
+// and error reports as k_parse (round 5's k_parse_n, 8 KiB tiles of 128 threads with a shared
+// front end, measured 15.8 / 10.5 / 3.1 ms against 12.0 / 8.9 / 2.3 ms for this kernel on the
+// closest, bedmap and element-of row files and was removed). The only exchange between the waves: wave 0's line
 // count (wave 1's first row) and the keys on either side of the sub-tile edge (sort check).
 #define LCAP_R 512  // lines per 4 KiB sub-tile (lines averaging >= 8 bytes; more: redone with k_parse)
 // a 224-byte halo (+32) after the sub-tile, so that the lines crossing its end are staged for
@@ -2048,7 +1811,7 @@ __device__ __forceinline__ bool score_fast_v(const ParseLdsR& S, uint32_t q, uin
   return ok;
 }
 
-// one line on k_parse_n's per-line path (the run by position, parse_line_fast_ws, else the
+// one line on the per-line path (the run by position, parse_line_fast_ws, else the
 // full grammar); key: the row's start key (LLONG_MIN: not a row)
 template <bool REST, bool SCORE>
 __device__ __forceinline__ void row_line_general(const ParseLdsR& S, const TileText& T, const RunTable& R,
@@ -2078,7 +1841,7 @@ __device__ __forceinline__ void row_line_general(const ParseLdsR& S, const TileT
     return;
   }
   Line Ln;
-  parse_line_slow(T, ls, le, SCORE ? BG_BED5 : BG_BED3, Ln);
+  parse_line_slow<false>(T, ls, le, SCORE ? BG_BED5 : BG_BED3, Ln);
   if (Ln.err) {
     if (Ln.err == ERR_BLANK) atomicAdd(&st->nblank, 1ULL);
     bg_report(st, r, Ln.err);
@@ -2209,14 +1972,11 @@ __device__ __forceinline__ void row_rounds_v(const ParseLdsR& S, const TileText&
   }
 }
 
-#ifndef BG_RV_WAVES
-#define BG_RV_WAVES 6
-#endif
-#ifndef BG_RV_WAVES5
-#define BG_RV_WAVES5 6
-#endif
+// (at least 6 waves per SIMD: <= 80 VGPRs. The BED5 variants then spill 28-40 bytes of values
+// only the byte path reloads; capped at 5 waves they spill nothing and measured slower, bedmap
+// 21.8 -> 22.1 ms, round 6)
 template <bool REST, bool SCORE>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SCORE ? BG_RV_WAVES5 : BG_RV_WAVES, 8))) k_parse_rv(
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(6, 8))) k_parse_rv(
     const uint8_t* __restrict__ txt, uint64_t nb, uint64_t nrows, const uint64_t* __restrict__ row0,
     const uint32_t* __restrict__ runlo, const uint32_t* __restrict__ runhi, RunTable R,
     int64_t* __restrict__ KS, int64_t* __restrict__ KE, uint64_t* __restrict__ rest_off,
@@ -2610,6 +2370,49 @@ static void release_state(bg_ctx* c, LoadState& S) {
   S = LoadState();
 }
 
+// work on the side stream (sstream) from the ctx stream's current position: side_begin
+// points c->stream at it, side_end records sjoin there and points c->stream back. Blocks
+// released meanwhile wait in c->deferred until side_join (the side stream may still use them).
+static int side_begin(bg_ctx* c, hipStream_t& main) {
+  if (!c->sstream) {
+    if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sfork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sjoin, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return bg_fail(c, BG_E_HIP, "side stream creation failed");
+    }
+  }
+  BG_HIP(c, hipEventRecord(c->sfork, c->stream));
+  BG_HIP(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
+  c->defer_release = true;
+  main = c->stream;
+  c->stream = c->sstream;
+  return 0;
+}
+static void side_end(bg_ctx* c, hipStream_t main) {
+  (void)hipEventRecord(c->sjoin, c->sstream);  // (on errors too: side_join waits for what was queued)
+  c->stream = main;
+}
+static int side_join(bg_ctx* c) {
+  if (!c->defer_release) return 0;
+  int rc = bg_hip_ok(c, hipStreamWaitEvent(c->stream, c->sjoin, 0));
+  c->defer_release = false;
+  for (auto& b : c->deferred) c->free_list.push_back(b);
+  c->deferred.clear();
+  return rc;
+}
+
+// the scout pass: k_scout + the row offsets' scan (run on the side stream beside the run
+// discovery and the previous input's parse, it measured no faster: bedmap 21.93 -> 22.23 ms,
+// the parse slowed by as much as the scout was hidden, round 6)
+static int scout_pass(bg_ctx* c, LoadState& S, uint64_t* ctr) {
+  const uint32_t nt = S.ntiles;
+  BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), S.txt, S.nb, nt,
+            S.cnt, S.fnl);
+  BG_HIP(c, hipGetLastError());
+  return bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
+}
+
 // phase 1 (no host round trip): text to HBM, scout, row offsets, chromosome-run records.
 // ctr[0] = rows, ctr[1] = boundary tiles (u32), ctr[2] = run records (u32)
 static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, uint64_t* ctr) {
@@ -2636,7 +2439,7 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   S.rc = (uint32_t)std::min<uint64_t>(REC_CAP, (uint64_t)nt * (TT / 6 + 2) + 16);
   const bool set = in.kind == BG_BED3_SET;  // no row numbers: no scout pass
   // row loads: the scout pass counts every tile's lines first (k_scout, a streaming read at
-  // ~6 TB/s) for the rows' numbers (a decoupled look-back inside k_parse_n instead measured
+  // ~6 TB/s) for the rows' numbers (a decoupled look-back inside round 5's row parse instead measured
   // 2x slower in round 5: bedmap 50M x 500M k_parse 11.4 -> 20.7 ms)
   const bool scout = !set;
   if (scout) {
@@ -2652,17 +2455,12 @@ static int scout_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S, u
   if (!S.fls || !S.fhash || !S.blist || !S.recs)
     return BG_E_NOMEM;
   if (scout) {
-    BG_LAUNCH(c, "k_scout", k_scout, dim3(bg_blocks(nt, SCOUT_TILES)), dim3(BG_NT), txt, S.nb, nt,
-              S.cnt, S.fnl);
-    BG_HIP(c, hipGetLastError());
-  }
-  BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, S.fnl,
-            S.fls, S.fhash);
-  BG_HIP(c, hipGetLastError());
-  if (scout) {
-    int rc = bg_scan_sum_u64(c, S.cnt, S.row0, nt, &ctr[0]);
+    int rc = scout_pass(c, S, ctr);
     if (rc) return rc;
   }
+  BG_LAUNCH(c, "k_tokhash", k_tokhash, dim3(bg_blocks(nt, 256)), dim3(256), txt, S.nb, nt, scout ? S.fnl : nullptr,
+            S.fls, S.fhash);
+  BG_HIP(c, hipGetLastError());
   uint32_t* nbound = reinterpret_cast<uint32_t*>(&ctr[1]);
   uint32_t* nrec = reinterpret_cast<uint32_t*>(&ctr[2]);
   BG_LAUNCH(c, "k_boundary", k_boundary, dim3(bg_blocks(nt, 256)), dim3(256), S.fls, S.fhash, nt,
@@ -2768,18 +2566,12 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
   }
   const uint32_t nr = (uint32_t)S.run_pos.size();
   if (S.ntiles == 0 || T->n == 0 || nr == 0) return 0;
-  // k_parse_rv (two waves per tile, run ranges per 4 KiB sub-tile) unless BEDGPU_ROW_V=0
-  // (k_parse_n) or the load is a redo with k_parse
-  static const bool rowv = [] {
-    const char* e = getenv("BEDGPU_ROW_V");
-    return !e || atoi(e) != 0;
-  }();
-  const bool rv = rowv && !c->row_wide;
+  // k_parse_rv (two waves per tile, run ranges per 4 KiB sub-tile) unless the load is a redo
+  // with k_parse (a sub-tile of more than LCAP_R lines: BG_ROW_OVERFLOW)
+  const bool rv = !c->row_wide;
   RunTable R;
   int rc = upload_runs(c, T, S, gid, R, rv ? TW : TT);
   if (rc) return rc;
-  // k_parse_n (whitespace-only tile front end, 128 threads) unless a load found a tile of very
-  // short lines (BG_ROW_OVERFLOW) and is being redone with k_parse
   // scores past the loader's fast paths (parse_score: isint -1) go to k_score_big (finish_one);
   // the list holds 2^20 (BEDGPU_BIGCAP) unless a load that overflowed it is being redone with
   // the count it found (c->big_need)
@@ -2803,14 +2595,10 @@ static int parse_one(bg_ctx* c, const bg_input& in, bg_table* T, LoadState& S,
     else if (sc) BG_ROWV(false, true);
     else BG_ROWV(false, false);
 #undef BG_ROWV
-  } else if (!c->row_wide)
-    BG_LAUNCH(c, "k_parse", k_parse_n<128>, dim3(S.ntiles), dim3(128), S.txt, S.nb, T->n, S.row0, S.rlo,
-              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
-              S.big, S.bigcap);
-  else
-    BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo,
-              S.rhi, in.kind == BG_BED5_REST ? BG_BED5 : in.kind, R, T->ks, T->ke, T->rest_off, T->rest_len, T->score, st,
-              S.big, S.bigcap);
+  } else {
+    BG_LAUNCH(c, "k_parse", k_parse, dim3(S.ntiles), dim3(BG_NT), S.txt, S.nb, T->n, S.row0, S.rlo, S.rhi, kind, R,
+              T->ks, T->ke, T->rest_off, T->rest_len, T->score, st, S.big, S.bigcap);
+  }
   BG_HIP(c, hipGetLastError());
   BG_LAUNCH(c, "k_check_bounds", k_check_bounds, dim3(bg_blocks(S.ntiles, 256)), dim3(256), T->ks,
             S.row0, S.ntiles, T->n, st);
@@ -2892,31 +2680,11 @@ static int parse_set_merge(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st)
 // the side stream from the ctx stream's current position: count passes (write == false) or
 // the deferred k_set_write (write == true)
 static int set_merge_side(bg_ctx* c, bg_table* T, LoadState& S, bg_dstatus* st, bool write) {
-  if (!c->sstream) {
-    if (hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sfork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sjoin, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      return bg_fail(c, BG_E_HIP, "side stream creation failed");
-    }
-  }
-  BG_HIP(c, hipEventRecord(c->sfork, c->stream));
-  BG_HIP(c, hipStreamWaitEvent(c->sstream, c->sfork, 0));
-  c->defer_release = true;  // until set_merge_join: blocks the side stream may still use
-  hipStream_t main = c->stream;
-  c->stream = c->sstream;
-  const int rc = write ? set_merge_write(c, T, S) : set_merge_count(c, S, st);
-  c->stream = main;
+  hipStream_t main;
+  int rc = side_begin(c, main);
   if (rc) return rc;
-  BG_HIP(c, hipEventRecord(c->sjoin, c->sstream));
-  return 0;
-}
-static int set_merge_join(bg_ctx* c) {
-  if (!c->defer_release) return 0;
-  int rc = bg_hip_ok(c, hipStreamWaitEvent(c->stream, c->sjoin, 0));
-  c->defer_release = false;
-  for (auto& b : c->deferred) c->free_list.push_back(b);
-  c->deferred.clear();
+  rc = write ? set_merge_write(c, T, S) : set_merge_count(c, S, st);
+  side_end(c, main);
   return rc;
 }
 
@@ -3100,7 +2868,7 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
   }
   if (!rc && pending >= 0) rc = set_merge_side(c, s->t[pending], st[pending], dst + pending, true);
   {
-    const int rj = set_merge_join(c);  // (on errors too: the side stream's blocks return to the pool)
+    const int rj = side_join(c);  // (on errors too: the side stream's blocks return to the pool)
     if (!rc) rc = rj;
   }
   HP("parse_q");
@@ -3125,7 +2893,7 @@ extern "C" int bg_load(bg_ctx* c, int n, const bg_input* inputs, bg_set** out) {
     if (inputs[i].kind == BG_BED3_SET && st[i].ntiles &&
         (hst[i].first_bad != ~0ULL || (hst[i].flags & BG_SET_OVERFLOW)))
       redo = setredo = true;
-  // a row input with a tile of more lines than k_parse_n holds: redone with k_parse
+  // a row input with a sub-tile of more lines than k_parse_rv holds: redone with k_parse
   for (int i = 0; i < n && !rc; ++i)
     if (inputs[i].kind != BG_BED3_SET && st[i].ntiles && (hst[i].flags & BG_ROW_OVERFLOW)) redo = wide = true;
   // a row input with more long scores than its k_score_big list holds: redone with room for all
