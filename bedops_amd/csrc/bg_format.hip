@@ -991,6 +991,18 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_count(FmtArgs A, uint64_t* __rest
   }
 }
 
+// the row stripes unrolled: their byte offsets (my[]) stay in registers (not unrolled, the
+// large render bodies left the loops rolled and my[] in scratch: 32 bytes per lane)
+#ifndef BG_FMT_UNROLL
+#define BG_FMT_UNROLL 1
+#endif
+#if BG_FMT_UNROLL
+#define FMT_UNROLL _Pragma("unroll")
+// (RES_MAP's render is too large to unroll; its loops stay rolled)
+#pragma clang diagnostic ignored "-Wpass-failed"
+#else
+#define FMT_UNROLL
+#endif
 template <int KIND>
 __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* __restrict__ toff,
                                                      char* __restrict__ out) {
@@ -1001,6 +1013,7 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   const uint64_t base = (uint64_t)blockIdx.x * FT_TILE + threadIdx.x;
   uint64_t my[FT_ROWS];
   uint64_t tot = 0;
+FMT_UNROLL
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     CountOut co;
@@ -1016,7 +1029,8 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   const uint64_t dst0 = toff[blockIdx.x];
   bool mismatch = false;  // a row rendered to another length than it was placed with
   if (tot > FT_LDS) {  // oversized tile (long names / rests): render straight to HBM
-    for (int k = 0; k < FT_ROWS; ++k) {
+  FMT_UNROLL
+  for (int k = 0; k < FT_ROWS; ++k) {
       const uint64_t row = base + (uint64_t)k * BG_NT;
       if (row >= A.n) continue;
       const uint64_t len = A.rowlen ? A.rowlen[row] : 0;
@@ -1031,6 +1045,7 @@ __global__ void __launch_bounds__(BG_NT) k_fmt_write(FmtArgs A, const uint64_t* 
   // stage with the same alignment mod 16 as the destination, so every aligned 16-byte
   // chunk of the output is one aligned 16-byte LDS read
   const uint32_t skew = (uint32_t)(dst0 & 15);
+FMT_UNROLL
   for (int k = 0; k < FT_ROWS; ++k) {
     const uint64_t row = base + (uint64_t)k * BG_NT;
     LdsOut o{buf + skew + my[k]};
