@@ -64,7 +64,7 @@ except OSError:
 
 # bg_prof labels -> kernel names as rocprofv3 reports them (profiles/pmc_traffic.json)
 PMC_NAME = {"k_components_count": "k_components<false>", "k_components_write": "k_components<true>",
-            "k_parse_set": "k_parse_set_v",
+            "k_parse_set": "k_parse_set_v", "k_parse": "k_parse_rv",
             "k_intersect_count": "k_mp_tile<0, false>", "k_intersect_write": "k_mp_tile<0, true, true>"}
 
 
@@ -713,9 +713,13 @@ def main():
             try:
                 tbl = json.load(open(pmc))
                 key = PMC_NAME.get(dominant, dominant)
-                ent = tbl.get(key) or max((v for k, v in tbl.items() if k.startswith(key + "<")),
-                                          key=lambda v: v.get("launches", 0), default={})
-                traffic = ent.get("bytes")
+                ent = tbl.get(key)
+                if ent:
+                    traffic = ent.get("bytes")
+                else:  # template instances (e.g. one k_parse_rv per file kind): launch-weighted mean
+                    vs = [v for k, v in tbl.items() if k.startswith(key + "<") and v.get("launches")]
+                    if vs:
+                        traffic = int(sum(v["bytes"] * v["launches"] for v in vs) / sum(v["launches"] for v in vs))
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
