@@ -1985,7 +1985,9 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(6, 8))
   __shared__ ParseLdsR SS[2];
   __shared__ uint32_t xl[2];
   __shared__ int64_t xk[2][2];  // [wave][first line, last line] keys
-  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
+  // (h through readfirstlane: the compiler does not know a wave's threads share threadIdx.x >> 6,
+  // and everything derived from it — the sub-tile, its runs, its row base — would take VGPRs)
+  const int lane = threadIdx.x & 63, h = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t u = 2 * blockIdx.x + h;  // sub-tile
   const int64_t t0 = (int64_t)u * TW;
   const bool inside = (uint64_t)t0 < nb;  // (the file's last tile may hold one sub-tile)
