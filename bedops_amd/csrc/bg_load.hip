@@ -1773,11 +1773,15 @@ __global__ void __launch_bounds__(64) k_parse_set_v(
 // front end, measured 15.8 / 10.5 / 3.1 ms against 12.0 / 8.9 / 2.3 ms for this kernel on the
 // closest, bedmap and element-of row files and was removed). The only exchange between the waves: wave 0's line
 // count (wave 1's first row) and the keys on either side of the sub-tile edge (sort check).
+#ifndef LCAP_R
 #define LCAP_R 512  // lines per 4 KiB sub-tile (lines averaging >= 8 bytes; more: redone with k_parse)
+#endif
 // a 224-byte halo (+32) after the sub-tile, so that the lines crossing its end are staged for
 // the score path too (with k_parse_set_v's 32 bytes, one BED5 sub-tile in seven sent a lane to
 // the byte path)
+#ifndef HA_R
 #define HA_R 224
+#endif
 struct ParseLdsR {
   __attribute__((aligned(16))) uint8_t buf[HB + TW + HA_R + 32];
   uint32_t wsm[TW / 32 + (HA_R + 32) / 32 + 1];
