@@ -1770,7 +1770,7 @@ __global__ void __launch_bounds__(64) k_parse_set_v(
 // then take parse_score_fast_ws (integers, "<int>.<frac>"); every other line takes
 // the per-line path (parse_line_fast_ws, then the full grammar) in its own lane. Same outputs
 // and error reports as k_parse (round 5's k_parse_n, 8 KiB tiles of 128 threads with a shared
-// front end, measured 15.8 / 10.5 / 3.1 ms against 12.0 / 8.9 / 2.3 ms for this kernel on the
+// front end, measured 15.8 / 10.5 / 3.1 ms against 11.8 / 8.2 / 2.1 ms for this kernel on the
 // closest, bedmap and element-of row files and was removed). The only exchange between the waves: wave 0's line
 // count (wave 1's first row) and the keys on either side of the sub-tile edge (sort check).
 #ifndef LCAP_R
