@@ -36,11 +36,13 @@
 #include "bg_internal.h"
 
 #ifndef CQ_DEF
-#define CQ_DEF 20  // ref rows per chunk (10M x 1B: 20 rows 17.55 ms against 24 rows 17.95, 16 rows 18.6, 28 rows 18.6,
+#define CQ_DEF 22  // ref rows per chunk (10M x 1B, round 6: 22 rows + 3 warm-up 16.5-16.7 ms, step 37.5-37.7; 20 + 4: 17.55; 24 + 4: 17.95; 16 or 28: 18.6;
                    // round 6: the 6.5K waves of 24-row chunks took 1.27 rounds of the 5 resident per SIMD;
                    // 3-8 warm-up rows, profiles/r04_closest_cq.txt)
 #endif
-#define CW_DEF 4   // speculative warm-up rows before a chunk
+#ifndef CW_DEF
+#define CW_DEF 3   // speculative warm-up rows before a chunk (2: the fix-up pass dominates, step 42.5 ms)
+#endif
 #define CBACK 4096 // at most this many candidates before the warm-up row are re-read
 #define CAP0 256   // initial capacity of the cache stack / kept list (x4 on overflow)
 #define FIX_ROUNDS 8
